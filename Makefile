@@ -1,0 +1,32 @@
+# Builds the product library (HIP, gfx950) and the test-only CPU oracle.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CSRC := vectorscan_amd/csrc
+LIB := vectorscan_amd/libvectorscan_amd.so
+ORACLE := oracle/_build/liboracle.so
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
+            -Wno-unused-parameter -Iinclude
+
+all: $(LIB) $(ORACLE)
+
+$(CSRC)/compile.o: $(CSRC)/compile.cpp $(CSRC)/hs_layout.h $(CSRC)/vsa_internal.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/kernels.o: $(CSRC)/kernels.hip $(CSRC)/kernels.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/runtime.o: $(CSRC)/runtime.hip $(CSRC)/kernels.h $(CSRC)/hs_layout.h \
+                   $(CSRC)/vsa_internal.h include/vectorscan_amd.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(CSRC)/compile.o $(CSRC)/kernels.o $(CSRC)/runtime.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
+
+$(ORACLE): oracle/oracle.c
+	mkdir -p oracle/_build
+	gcc -O2 -std=gnu11 -fPIC -shared -Wall $< -o $@
+
+clean:
+	rm -f $(CSRC)/*.o $(LIB) $(ORACLE)
+
+.PHONY: all clean

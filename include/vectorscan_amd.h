@@ -1,0 +1,228 @@
+/*
+ * vectorscan_amd.h — C ABI of libvectorscan_amd.so, the MI355X engine for
+ * Vectorscan's literal / char-class prefilter hot path.
+ *
+ * Part 1 is the drop-in boundary: the same names, signatures and semantics
+ * as the reference entry points it replaces, so Rose (or the reference's
+ * own unit tests) link against it unchanged.  Part 2 is the new device-batch
+ * API (64-bit lengths, device-resident buffers, many blocks per launch)
+ * that hsbench-style drivers and multi-GPU striping use.  Part 3 builds HWLM
+ * bytecode in the reference layout.
+ *
+ * No torch or HIP types appear in any signature; streams are void*.
+ */
+#ifndef VECTORSCAN_AMD_H
+#define VECTORSCAN_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#if defined(__x86_64__) || defined(__i386__)
+#include <emmintrin.h>
+typedef __m128i vsa_m128_t; /* passed in XMM registers, as the reference's m128 */
+#else
+typedef struct { uint8_t b[16]; } __attribute__((aligned(16))) vsa_m128_t;
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ *
+ * Part 1 — drop-in entry points (reference file:line of the interface)
+ * ------------------------------------------------------------------ */
+
+struct HWLM;
+struct FDR;
+struct noodTable;
+struct hs_scratch;
+union AccelAux;
+
+typedef int hwlm_error_t;             /* hwlm.h:57 */
+typedef uint64_t hwlm_group_t;        /* hwlm.h:60 */
+typedef hwlm_group_t hwlmcb_rv_t;     /* hwlm.h:63 */
+/* hwlm.h:98 */
+typedef hwlmcb_rv_t (*HWLMCallback)(size_t end, uint32_t id,
+                                    struct hs_scratch *scratch);
+
+/* Replaces hwlmExec, src/hwlm/hwlm.h:116 (impl. src/hwlm/hwlm.c:178).
+ * Copies buf to the GPU, scans, replays confirmed matches through cb in the
+ * reference order (end, bucket, confirm-chain order) applying groups /
+ * NOREPEAT / terminate / INCLUDED_JUMP squash exactly as confWithBit. */
+hwlm_error_t hwlmExec(const struct HWLM *tab, const uint8_t *buf, size_t len,
+                      size_t start, HWLMCallback callback,
+                      struct hs_scratch *scratch, hwlm_group_t groups);
+
+/* Replaces fdrExec, src/fdr/fdr.h:58 (impl. src/fdr/fdr.c:801). */
+hwlm_error_t fdrExec(const struct FDR *fdr, const uint8_t *buf, size_t len,
+                     size_t start, HWLMCallback cb, struct hs_scratch *scratch,
+                     hwlm_group_t groups);
+
+/* Replaces noodExec, src/hwlm/noodle_engine.h:47 (impl. noodle_engine.cpp:123). */
+hwlm_error_t noodExec(const struct noodTable *n, const uint8_t *buf, size_t len,
+                      size_t start, HWLMCallback cb, struct hs_scratch *scratch);
+
+/* Accel find-first / find-last (src/nfa/shufti.h:46-55, truffle.h:45-49,
+ * vermicelli.hpp:47-95, accel.h:148).  Return values as the reference:
+ * forward scans return buf_end when nothing is found, reverse scans
+ * buf - 1. */
+const uint8_t *shuftiExec(vsa_m128_t mask_lo, vsa_m128_t mask_hi,
+                          const uint8_t *buf, const uint8_t *buf_end);
+const uint8_t *rshuftiExec(vsa_m128_t mask_lo, vsa_m128_t mask_hi,
+                           const uint8_t *buf, const uint8_t *buf_end);
+const uint8_t *truffleExec(vsa_m128_t mask1, vsa_m128_t mask2,
+                           const uint8_t *buf, const uint8_t *buf_end);
+const uint8_t *rtruffleExec(vsa_m128_t mask1, vsa_m128_t mask2,
+                            const uint8_t *buf, const uint8_t *buf_end);
+const uint8_t *vermicelliExec(char c, char nocase, const uint8_t *buf,
+                              const uint8_t *buf_end);
+const uint8_t *nvermicelliExec(char c, char nocase, const uint8_t *buf,
+                               const uint8_t *buf_end);
+const uint8_t *rvermicelliExec(char c, char nocase, const uint8_t *buf,
+                               const uint8_t *buf_end);
+const uint8_t *rnvermicelliExec(char c, char nocase, const uint8_t *buf,
+                                const uint8_t *buf_end);
+const uint8_t *vermicelliDoubleExec(char c1, char c2, char nocase,
+                                    const uint8_t *buf, const uint8_t *buf_end);
+const uint8_t *vermicelliDoubleMaskedExec(char c1, char c2, char m1, char m2,
+                                          const uint8_t *buf,
+                                          const uint8_t *buf_end);
+const uint8_t *run_accel(const union AccelAux *accel, const uint8_t *c,
+                         const uint8_t *c_end);
+
+/* ------------------------------------------------------------------ *
+ * Part 2 — device batch API (new)
+ * ------------------------------------------------------------------ */
+
+#define VSA_OK 0
+#define VSA_E_INVALID (-1)
+#define VSA_E_NOMEM (-2)
+#define VSA_E_NOT_BUILDABLE (-3)
+#define VSA_E_DEVICE (-4)
+#define VSA_E_OVERFLOW (-5)
+
+typedef struct vsa_ctx vsa_ctx_t; /* stream + workspace, one per thread */
+typedef struct vsa_db vsa_db_t;   /* device copy of one HWLM blob */
+
+/* Sorted confirmed match: end = key >> 24, bucket = (key >> 20) & 15,
+ * confirm-chain index = key & 0xfffff; id = literal id. */
+typedef struct {
+    uint64_t key;
+    uint32_t id;
+    uint32_t pad;
+} vsa_match_t;
+
+int vsa_device_count(void);
+int vsa_ctx_create(int device, vsa_ctx_t **ctx);
+int vsa_ctx_destroy(vsa_ctx_t *ctx);
+void *vsa_ctx_stream(vsa_ctx_t *ctx);
+
+/* Upload an HWLM blob (reference layout, 64-byte aligned host copy). */
+int vsa_db_load(vsa_ctx_t *ctx, const void *hwlm, size_t size, vsa_db_t **db);
+int vsa_db_free(vsa_db_t *db);
+/* engine kind: 16 = noodle, 0 = FDR, 3..18 = Teddy engine id */
+int vsa_db_engine(const vsa_db_t *db);
+
+/* Device memory helpers (plain hipMalloc / hipMemcpy). */
+int vsa_malloc(vsa_ctx_t *ctx, size_t bytes, void **dptr);
+int vsa_free(vsa_ctx_t *ctx, void *dptr);
+int vsa_memcpy_h2d(vsa_ctx_t *ctx, void *dst, const void *src, size_t bytes);
+int vsa_memcpy_d2h(vsa_ctx_t *ctx, void *dst, const void *src, size_t bytes);
+int vsa_sync(vsa_ctx_t *ctx);
+
+/* Scan nblocks device-resident blocks (each = one hwlmExec(start=starts[i],
+ * groups=ALL)) in one launch.  offsets[i], lens[i] are relative to d_data;
+ * starts may be NULL (all 0).  Matches are sorted on the device into the
+ * reference order; ends are offsets relative to d_data.  flags bit0: skip
+ * the sort; bit1: asynchronous (do not wait for the count; *n_matches is
+ * filled by vsa_scan_wait). */
+#define VSA_SCAN_UNSORTED 1u
+#define VSA_SCAN_ASYNC 2u
+int vsa_scan_blocks(vsa_ctx_t *ctx, const vsa_db_t *db, const uint8_t *d_data,
+                    const uint64_t *offsets, const uint64_t *lens,
+                    const uint64_t *starts, uint32_t nblocks, uint32_t flags,
+                    uint64_t *n_matches);
+int vsa_scan_wait(vsa_ctx_t *ctx, uint64_t *n_matches);
+/* Device pointers to the last scan's sorted keys (u64) and ids (u32). */
+int vsa_scan_results(vsa_ctx_t *ctx, const uint64_t **d_keys,
+                     const uint32_t **d_ids);
+/* Copy up to cap results of the last scan to the host. */
+int vsa_scan_copy(vsa_ctx_t *ctx, vsa_match_t *out, uint64_t cap,
+                  uint64_t *n_copied);
+/* Candidates the first stage handed to confirm in the last scan. */
+uint64_t vsa_scan_candidates(vsa_ctx_t *ctx);
+/* Device time (ms, hipEvents on the scan stream) of the last scan kernel. */
+double vsa_scan_kernel_ms(vsa_ctx_t *ctx);
+
+/* Byte-class scan over a device buffer: class = 256-bit membership bitmap
+ * (bit c of byte c>>3).  class2 non-NULL: pair mode (class at i, class2 at
+ * i+1).  d_bitmap (optional) receives 1 bit per byte ((len+63)/64 u64).
+ * first/last/count are host outputs (first = len if none, last = index of
+ * the last set bit + 1, 0 if none). */
+int vsa_class_scan(vsa_ctx_t *ctx, const uint8_t cls[32], const uint8_t *cls2,
+                   const uint8_t *d_data, uint64_t len, uint64_t *d_bitmap,
+                   uint64_t *first, uint64_t *last, uint64_t *count,
+                   uint32_t flags);
+
+/* ------------------------------------------------------------------ *
+ * Part 3 — HWLM bytecode builder (reference layout; see compile.cpp)
+ * ------------------------------------------------------------------ */
+
+/* hwlmLiteral, src/hwlm/hwlm_literal.h:51 */
+typedef struct {
+    const uint8_t *s;
+    uint32_t len;
+    uint32_t id;
+    uint8_t nocase;
+    uint8_t noruns;
+    uint8_t msk_len;
+    uint8_t pad;
+    uint64_t groups;
+    const uint8_t *msk;
+    const uint8_t *cmp;
+} vsa_literal_t;
+
+typedef struct {
+    int32_t engine_hint; /* -1 choose; 0 FDR (domain 9, stride 1); 3..18 Teddy */
+    uint8_t allow_noodle;
+    uint8_t allow_teddy;
+    uint8_t allow_fat_teddy;
+    uint8_t allow_flood;
+} vsa_build_opts_t;
+
+void vsa_build_opts_default(vsa_build_opts_t *o);
+/* Builds an HWLM blob (64-byte aligned, free with vsa_blob_free). */
+int vsa_hwlm_build(const vsa_literal_t *lits, size_t n,
+                   const vsa_build_opts_t *opts, void **blob, size_t *size);
+void vsa_blob_free(void *blob);
+/* Set HWLM.accel0 / accel1 (+accel1_groups) of a built blob. */
+int vsa_hwlm_set_accel(void *blob, const union AccelAux *accel0,
+                       const union AccelAux *accel1, uint64_t accel1_groups);
+/* shufticompile.cpp:54 — returns buckets used or -1. */
+int vsa_shufti_build_masks(const uint8_t cls[32], uint8_t lo[16], uint8_t hi[16]);
+/* trufflecompile.cpp:60 */
+void vsa_truffle_build_masks(const uint8_t cls[32], uint8_t m1[16], uint8_t m2[16]);
+
+/* Pointer-argument forms of the accel drop-ins (for FFI callers that cannot
+ * pass vector registers).  Return an index: forward = first hit or len,
+ * reverse = last hit or -1. */
+int64_t vsa_shufti_find(const uint8_t lo[16], const uint8_t hi[16],
+                        const uint8_t *buf, size_t len, int reverse);
+int64_t vsa_truffle_find(const uint8_t m1[16], const uint8_t m2[16],
+                         const uint8_t *buf, size_t len, int reverse);
+/* mode: 0 verm, 1 nverm, 2 rverm, 3 rnverm, 4 dverm, 5 dverm masked */
+int64_t vsa_verm_find(int mode, uint8_t c1, uint8_t c2, uint8_t m1, uint8_t m2,
+                      int nocase, const uint8_t *buf, size_t len);
+
+/* Optional: hs_scratch field offsets for INCLUDED_JUMP squash replay
+ * (offsetof(struct hs_scratch, fdr_conf / fdr_conf_offset)); the defaults
+ * are the x86-64 layout of src/scratch.h:172-219. */
+void vsa_set_scratch_layout(long fdr_conf_off, long fdr_conf_offset_off);
+
+const char *vsa_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VECTORSCAN_AMD_H */

@@ -1,0 +1,165 @@
+"""TEST INFRASTRUCTURE ONLY — the CPU oracle (checker) for vectorscan_amd.
+
+ctypes bindings for oracle/oracle.c, a scalar C restatement of the
+reference runtime (see that file's header for the file:line it restates),
+plus a brute-force literal matcher in numpy that depends on nothing but the
+literal definitions.  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this package; the product never does.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "liboracle.so")
+
+
+def build():
+    os.makedirs(os.path.join(HERE, "_build"), exist_ok=True)
+    subprocess.check_call(["gcc", "-O2", "-std=gnu11", "-fPIC", "-shared", "-Wall",
+                           os.path.join(HERE, "oracle.c"), "-o", LIB])
+
+
+if not os.path.exists(LIB):
+    build()
+_lib = ctypes.CDLL(LIB)
+
+
+class _Match(ctypes.Structure):
+    _fields_ = [("end", ctypes.c_uint64), ("id", ctypes.c_uint32)]
+
+
+def _sig(name, res, *args):
+    f = getattr(_lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+_vp, _sz, _u64, _i64, _int = (ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
+                              ctypes.c_long, ctypes.c_int)
+_sig("orc_hwlm_exec", _i64, _vp, _vp, _sz, _sz, _u64, _vp, _sz, _i64, _u64,
+     ctypes.POINTER(_int))
+_sig("orc_fdr_exec", _i64, _vp, _vp, _sz, _sz, _u64, _vp, _sz, _i64, _u64,
+     ctypes.POINTER(_int))
+_sig("orc_nood_exec", _i64, _vp, _vp, _sz, _sz, _vp, _sz, _i64, ctypes.POINTER(_int))
+_sig("orc_shufti", _i64, _vp, _vp, _vp, _sz)
+_sig("orc_rshufti", _i64, _vp, _vp, _vp, _sz)
+_sig("orc_truffle", _i64, _vp, _vp, _vp, _sz)
+_sig("orc_rtruffle", _i64, _vp, _vp, _vp, _sz)
+_sig("orc_verm", _i64, ctypes.c_uint8, _int, _int, _int, _vp, _sz)
+_sig("orc_dverm", _i64, ctypes.c_uint8, ctypes.c_uint8, _int, _vp, _sz)
+_sig("orc_dverm_masked", _i64, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8,
+     ctypes.c_uint8, _vp, _sz)
+_sig("orc_fdr_candidates", _u64, _vp, _vp, _sz)
+
+ALL = (1 << 64) - 1
+
+
+def _buf(data):
+    if isinstance(data, np.ndarray):
+        data = np.ascontiguousarray(data, np.uint8)
+        return data, data.ctypes.data, data.nbytes
+    data = bytes(data)
+    b = ctypes.create_string_buffer(data, max(1, len(data)))
+    return b, ctypes.addressof(b), len(data)
+
+
+def _run(fn, ptr, data, start, extra, term_after, cap, cb_ret=ALL):
+    keep, p, n = _buf(data)
+    while True:
+        out = (_Match * max(1, cap))()
+        st = _int()
+        cnt = fn(ptr, p, n, start, *extra, out, cap, term_after, *(
+            [cb_ret] if fn is not _lib.orc_nood_exec else []), ctypes.byref(st))
+        if cnt <= cap:
+            return st.value, [(out[i].end, out[i].id) for i in range(cnt)]
+        cap = cnt
+
+
+def hwlm_exec(blob_ptr, data, start=0, groups=ALL, term_after=-1, cap=4096, cb_ret=ALL):
+    """Reference hwlmExec callback sequence [(end, id)]: the emulated
+    callback returns `cb_ret` (the new group mask), or TERMINATE once
+    `term_after` matches have been reported."""
+    return _run(_lib.orc_hwlm_exec, blob_ptr, data, start, [groups], term_after, cap, cb_ret)
+
+
+def fdr_exec(engine_ptr, data, start=0, groups=ALL, term_after=-1, cap=4096, cb_ret=ALL):
+    return _run(_lib.orc_fdr_exec, engine_ptr, data, start, [groups], term_after, cap, cb_ret)
+
+
+def nood_exec(engine_ptr, data, start=0, term_after=-1, cap=4096):
+    return _run(_lib.orc_nood_exec, engine_ptr, data, start, [], term_after, cap)
+
+
+def shufti(lo, hi, data, reverse=False):
+    keep, p, n = _buf(data)
+    f = _lib.orc_rshufti if reverse else _lib.orc_shufti
+    return f(bytes(lo), bytes(hi), p, n)
+
+
+def truffle(m1, m2, data, reverse=False):
+    keep, p, n = _buf(data)
+    f = _lib.orc_rtruffle if reverse else _lib.orc_truffle
+    return f(bytes(m1), bytes(m2), p, n)
+
+
+def verm(c, nocase, data, negate=False, reverse=False):
+    keep, p, n = _buf(data)
+    return _lib.orc_verm(c, int(nocase), int(negate), int(reverse), p, n)
+
+
+def dverm(c1, c2, nocase, data):
+    keep, p, n = _buf(data)
+    return _lib.orc_dverm(c1, c2, int(nocase), p, n)
+
+
+def dverm_masked(c1, c2, m1, m2, data):
+    keep, p, n = _buf(data)
+    return _lib.orc_dverm_masked(c1, c2, m1, m2, p, n)
+
+
+def fdr_candidates(engine_ptr, data):
+    keep, p, n = _buf(data)
+    return _lib.orc_fdr_candidates(engine_ptr, p, n)
+
+
+# ------------------------------------------------------------ brute force
+
+def _upper(b):
+    return bytes(c - 0x20 if 0x61 <= c <= 0x7A else c for c in b)
+
+
+def brute_force(lits, data, start=0):
+    """All (end, id) occurrences of each literal fully inside `data`, ending
+    at >= start: the match set any correct HWLM engine confirms (callers
+    apply NOREPEAT/groups separately).  Literals: objects with s, nocase,
+    id, msk, cmp (hwlm_literal.h semantics)."""
+    arr = np.frombuffer(bytes(data), np.uint8)
+    n = len(arr)
+    out = set()
+    for lit in lits:
+        s = np.frombuffer(_upper(lit.s) if lit.nocase else bytes(lit.s), np.uint8)
+        L = len(s)
+        W = max(L, len(lit.msk))
+        if n < W:
+            continue
+        ok = np.ones(n - W + 1, bool)  # window start positions
+        for k in range(L):
+            col = arr[W - L + k: n - L + k + 1]
+            c = s[k]
+            if lit.nocase and (0x41 <= c <= 0x5A):
+                ok &= (col & 0xDF) == c
+            else:
+                ok &= col == c
+        for k in range(len(lit.msk)):
+            m, v = lit.msk[k], lit.cmp[k]
+            col = arr[W - len(lit.msk) + k: n - len(lit.msk) + k + 1]
+            ok &= (col & m) == (v & m)
+        for w in np.nonzero(ok)[0]:
+            end = int(w) + W - 1
+            if end >= start:
+                out.add((end, lit.id))
+    return out

@@ -1,0 +1,545 @@
+/*
+ * oracle.c — TEST INFRASTRUCTURE ONLY.  A scalar CPU restatement of the
+ * Vectorscan hot-path runtime, used by tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg as the CHECKER.  Nothing in vectorscan_amd/
+ * links, loads or calls this file; the product path is the HIP engine.
+ *
+ * It reads the same HWLM bytecode the GPU engine reads and reproduces the
+ * reference's callback sequence.  Each routine cites what it restates:
+ *   hwlmExec              src/hwlm/hwlm.c:178-205 (accel pre-skip :48-105)
+ *   noodExec              src/hwlm/noodle_engine.cpp:75-134,
+ *                         noodle_engine_simd.hpp:173-273 (scan bounds)
+ *   fdrExec               src/fdr/fdr.c:699-825 (zones :362-659,
+ *                         get_conf_stride_1/2/4 :145-296, do_confirm :299)
+ *   confWithBit           src/fdr/fdr_confirm_runtime.h:43-102
+ *   Teddy / Fat Teddy     src/fdr/teddy.c:921-1066 (SSE),
+ *                         src/fdr/teddy_avx2.c:395-706 (AVX2 fat),
+ *                         teddy_runtime_common.h:146-199, :395-440
+ *   shufti / truffle      src/nfa/shufti.cpp:44-71, shufti_simd.hpp:89-280,
+ *                         src/nfa/x86/truffle.hpp:36-62
+ *   vermicelli            src/nfa/vermicelli_simd.cpp:493-622
+ *
+ * Parity pin: tests/test_oracle_golden.py checks every entry point here
+ * against the known answers of the reference's own unit tests
+ * (unit/internal/{noodle,fdr,shufti,truffle,vermicelli,rvermicelli}.cpp),
+ * restated as data in tests/golden/.
+ *
+ * Flood detection (flood_runtime.h) is restated only as "disabled": the
+ * blobs the tests build carry idCount == FDR_FLOOD_MAX_IDS for every char,
+ * under which the reference's floodDetect never changes the scan.
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+
+typedef uint8_t u8;
+typedef uint16_t u16;
+typedef uint32_t u32;
+typedef uint64_t u64a;
+typedef unsigned __int128 u128;
+
+#define ROUNDUP_CL(x) (((x) + 63) & ~(size_t)63)
+
+/* --- reference layouts (restated, see vectorscan_amd/csrc/hs_layout.h) -- */
+struct o_HWLM {
+    u8 type;
+    u64a accel1_groups;
+    u8 accel1[80] __attribute__((aligned(16)));
+    u8 accel0[80] __attribute__((aligned(16)));
+};
+struct o_nood {
+    u32 id;
+    u64a msk, cmp;
+    u8 msk_len, key_offset, nocase, single, key0, key1;
+};
+struct o_FDR {
+    u32 engineID, size, maxStringLen, numStrings, confOffset, floodOffset;
+    u8 stride, domain;
+    u16 domainMask;
+    u32 tabSize;
+    u8 start[16] __attribute__((aligned(16)));
+};
+struct o_Teddy {
+    u32 engineID, size, maxStringLen, numStrings, confOffset, floodOffset;
+};
+struct o_LitInfo {
+    u64a v, msk, groups;
+    u32 id;
+    u8 size, flags, next;
+};
+struct o_FDRConfirm {
+    u64a andmsk, mult;
+    u32 nBits;
+    u64a groups;
+};
+
+typedef struct {
+    u64a end;
+    u32 id;
+} orc_match;
+
+/* callback emulation: record; return CONTINUE unless told to terminate
+ * after `term_after` matches; optional control override */
+typedef struct {
+    orc_match *out;
+    size_t cap;
+    size_t n;
+    long term_after;
+    u64a ret_groups; /* value the emulated callback returns */
+} cbctx;
+
+static u64a emit(cbctx *c, u64a end, u32 id) {
+    if (c->n < c->cap) {
+        c->out[c->n].end = end;
+        c->out[c->n].id = id;
+    }
+    c->n++;
+    if (c->term_after >= 0 && (long)c->n >= c->term_after) {
+        return 0; /* HWLM_TERMINATE_MATCHING */
+    }
+    return c->ret_groups;
+}
+
+static inline u8 toupper_c(u8 c) { return (c >= 'a' && c <= 'z') ? c - 0x20 : c; }
+static inline int isalpha_c(u8 c) {
+    return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z');
+}
+
+/* ====================================================== accel engines == */
+
+/* shufti.cpp:44-71: first c with lo[c&15] & hi[c>>4], else buf_end */
+long orc_shufti(const u8 *lo, const u8 *hi, const u8 *buf, size_t len) {
+    for (size_t i = 0; i < len; i++) {
+        u8 c = buf[i];
+        if (lo[c & 0xf] & hi[c >> 4]) return (long)i;
+    }
+    return (long)len;
+}
+
+/* rshufti: last member, else -1 (buf - 1) */
+long orc_rshufti(const u8 *lo, const u8 *hi, const u8 *buf, size_t len) {
+    for (long i = (long)len - 1; i >= 0; i--) {
+        u8 c = buf[i];
+        if (lo[c & 0xf] & hi[c >> 4]) return i;
+    }
+    return -1;
+}
+
+/* x86/truffle.hpp:36-62: member iff mask[c>>7][c&15] has bit (c>>4)&7 */
+static inline int truffle_member(const u8 *m1, const u8 *m2, u8 c) {
+    const u8 *m = (c & 0x80) ? m2 : m1;
+    return (m[c & 0xf] >> ((c >> 4) & 7)) & 1;
+}
+
+long orc_truffle(const u8 *m1, const u8 *m2, const u8 *buf, size_t len) {
+    for (size_t i = 0; i < len; i++) {
+        if (truffle_member(m1, m2, buf[i])) return (long)i;
+    }
+    return (long)len;
+}
+
+long orc_rtruffle(const u8 *m1, const u8 *m2, const u8 *buf, size_t len) {
+    for (long i = (long)len - 1; i >= 0; i--) {
+        if (truffle_member(m1, m2, buf[i])) return i;
+    }
+    return -1;
+}
+
+/* vermicelli_simd.cpp:493-592 (c must be upper case when nocase) */
+long orc_verm(u8 c, int nocase, int negate, int reverse, const u8 *buf,
+              size_t len) {
+    u8 cm = nocase ? 0xdf : 0xff;
+    if (!reverse) {
+        for (size_t i = 0; i < len; i++) {
+            int eq = (u8)(buf[i] & cm) == c;
+            if (eq != negate) return (long)i;
+        }
+        return (long)len;
+    }
+    for (long i = (long)len - 1; i >= 0; i--) {
+        int eq = (u8)(buf[i] & cm) == c;
+        if (eq != negate) return i;
+    }
+    return -1;
+}
+
+/* vermicelliDoubleExecReal :293-358: first i with c1 c2 at i,i+1; else a
+ * partial match (last byte == c1) returns len-1; else len. */
+long orc_dverm(u8 c1, u8 c2, int nocase, const u8 *buf, size_t len) {
+    u8 cm = nocase ? 0xdf : 0xff;
+    for (size_t i = 0; i + 1 < len; i++) {
+        if ((u8)(buf[i] & cm) == c1 && (u8)(buf[i + 1] & cm) == c2) return (long)i;
+    }
+    if (len && (u8)(buf[len - 1] & cm) == c1) return (long)len - 1;
+    return (long)len;
+}
+
+/* vermicelliDoubleMaskedExecReal :425-491 */
+long orc_dverm_masked(u8 c1, u8 c2, u8 m1, u8 m2, const u8 *buf, size_t len) {
+    for (size_t i = 0; i + 1 < len; i++) {
+        if ((u8)(buf[i] & m1) == c1 && (u8)(buf[i + 1] & m2) == c2) return (long)i;
+    }
+    if (len && (u8)(buf[len - 1] & m1) == c1) return (long)len - 1;
+    return (long)len;
+}
+
+/* rvermicelliDoubleExecReal :360-423: highest offset of c2 of a pair, i.e.
+ * returns i+1 for the last pair (c1 at i, c2 at i+1); a c2 at buf[0] counts
+ * as a partial pair.  Returns -1 if none. */
+long orc_rdverm(u8 c1, u8 c2, int nocase, const u8 *buf, size_t len) {
+    u8 cm = nocase ? 0xdf : 0xff;
+    for (long i = (long)len - 1; i >= 1; i--) {
+        if ((u8)(buf[i] & cm) == c2 && (u8)(buf[i - 1] & cm) == c1) return i;
+    }
+    if (len && (u8)(buf[0] & cm) == c2) return 0;
+    return -1;
+}
+
+/* ============================================================ noodle == */
+
+/* noodle_engine.cpp:75-134 + scan bounds noodle_engine_simd.hpp:173-273:
+ * report end e (ascending) when the msk_len bytes ending at e satisfy
+ * (v & msk) == cmp and lie in [start, len). */
+static int nood_run(const struct o_nood *n, const u8 *buf, size_t len,
+                    size_t start, cbctx *cb) {
+    if (len - start < n->msk_len) return 0;
+    for (size_t e = start + n->msk_len - 1; e < len; e++) {
+        u64a v = 0;
+        memcpy(&v, buf + e + 1 - n->msk_len, n->msk_len);
+        if ((v & n->msk) != n->cmp) continue;
+        if (!emit(cb, e, n->id)) return 1;
+    }
+    return 0;
+}
+
+/* ======================================================= FDR confirm == */
+
+typedef struct {
+    const u8 *buf;
+    size_t len;
+    size_t start;
+    cbctx *cb;
+} rtargs;
+
+/* fdr_confirm_runtime.h:43-102 (block mode: len_history == 0) */
+static void conf_with_bit(const struct o_FDRConfirm *fc, const rtargs *a,
+                          size_t i, u64a *control, u32 *last_match,
+                          u64a conf_key) {
+    u32 c = (u32)(((conf_key & fc->andmsk) * fc->mult) >> (64 - fc->nBits));
+    const u32 *litIndex = (const u32 *)((const u8 *)fc + 32);
+    u32 st = litIndex[c];
+    if (!st) return;
+    const struct o_LitInfo *li = (const struct o_LitInfo *)((const u8 *)fc + st);
+    u8 next;
+    do {
+        if ((conf_key & li->msk) != li->v) goto out;
+        if (*last_match == li->id && (li->flags & 1)) goto out;
+        if ((long)i - (long)li->size + 1 < 0) goto out; /* overhang > 0 */
+        if (!(li->groups & *control)) goto out;
+        *last_match = li->id;
+        *control = emit(a->cb, i, li->id);
+    out:
+        next = li->next;
+        li++;
+    } while (next);
+}
+
+/* 8 bytes ending at e, bytes before buf read as the zero fake history
+ * (fdr.c:798-806) */
+static u64a conf_key_at(const u8 *buf, size_t len, long e) {
+    u64a v = 0;
+    for (int k = 0; k < 8; k++) {
+        long p = e - 7 + k;
+        u8 b = (p >= 0 && (size_t)p < len) ? buf[p] : 0;
+        v |= (u64a)b << (8 * k);
+    }
+    return v;
+}
+
+/* ================================================================ FDR == */
+
+/* a "zone" buffer as in fdr.c:50-80; we keep a logical byte accessor */
+typedef struct {
+    const u8 *buf;
+    size_t len;
+    long zstart;   /* logical position of the zone's first scanned byte */
+    long zend;     /* logical position one past the last scanned byte */
+    u8 shift;
+    long lo_valid; /* bytes at logical positions < lo_valid read as 0 */
+} zone;
+
+static inline u8 zbyte(const zone *z, long p) {
+    if (p < 0 || p < z->lo_valid) return 0;
+    if ((size_t)p >= z->len) return 0; /* post-padding byte */
+    return z->buf[p];
+}
+
+static u128 load_u64_as_u128(const u64a *ft, u32 idx) { return (u128)ft[idx]; }
+
+/* get_conf_stride_{1,2,4} fdr.c:145-296 on a logical zone */
+static void get_conf(const zone *z, long it, u32 stride, u16 dmask,
+                     const u64a *ft, u64a *conf0, u64a *conf8, u128 *s) {
+    u128 st0 = 0, st8 = 0;
+    for (int k = 0; k < 8; k += (int)stride) {
+        u32 r = ((u32)zbyte(z, it + k) | ((u32)zbyte(z, it + k + 1) << 8)) & dmask;
+        st0 |= load_u64_as_u128(ft, r) << (8 * k);
+    }
+    for (int k = 0; k < 8; k += (int)stride) {
+        u32 r = ((u32)zbyte(z, it + 8 + k) | ((u32)zbyte(z, it + 9 + k) << 8)) & dmask;
+        st8 |= load_u64_as_u128(ft, r) << (8 * k);
+    }
+    u128 st = *s | st0;
+    *conf0 = ~(u64a)st;
+    st >>= 64;
+    st |= st8;
+    *conf8 = ~(u64a)st;
+    *s = st >> 64;
+}
+
+static int fdr_run(const struct o_FDR *fdr, const rtargs *a, u64a control) {
+    const u8 *buf = a->buf;
+    size_t len = a->len, start = a->start;
+    if (start >= len) return 0;
+    const u64a *ft = (const u64a *)((const u8 *)fdr + ROUNDUP_CL(sizeof(*fdr)));
+    const u32 *confBase = (const u32 *)((const u8 *)fdr + fdr->confOffset);
+    u32 last_match = ~0U;
+
+    /* prepareZones fdr.c:625-659, in logical coordinates */
+    zone zones[3];
+    int nz = 0;
+    size_t remaining = len - start;
+    if (remaining <= 16) {
+        zone z = {buf, len, (long)len - 16, (long)len, (u8)(16 - remaining), 0};
+        zones[nz++] = z;
+    } else {
+        zone zs = {buf, len, (long)start, (long)start + 16, 0, 0};
+        zones[nz++] = zs;
+        size_t ptr = start + 16;
+        size_t main_end = start + ((len - start - 3) / 16) * 16;
+        if (main_end > ptr) {
+            zone zm = {buf, len, (long)ptr, (long)main_end, 0, 0};
+            zones[nz++] = zm;
+            ptr = main_end;
+        }
+        size_t zl = len - ptr;
+        size_t first = zl > 16 ? zl - 16 : zl;
+        zone ze = {buf, len, (long)len - (long)(zl > 16 ? 32 : 16), (long)len,
+                   (u8)(16 - first), 0};
+        zones[nz++] = ze;
+    }
+    u128 state;
+    memcpy(&state, fdr->start, 16);
+    for (int zi = 0; zi < nz; zi++) {
+        zone *z = &zones[zi];
+        /* variable_byte_shift_m128(state, shift) | zone_or_mask[shift] */
+        state <<= 8 * z->shift;
+        u128 orm = 0;
+        for (int k = 0; k < z->shift; k++) orm |= (u128)0xff << (8 * k);
+        state |= orm;
+        for (long it = z->zstart; it + 16 <= z->zend; it += 16) {
+            u64a c0, c8;
+            get_conf(z, it, fdr->stride, fdr->domainMask, ft, &c0, &c8, &state);
+            for (int half = 0; half < 2; half++) {
+                u64a conf = half ? c8 : c0;
+                while (conf) {
+                    u32 bit = (u32)__builtin_ctzll(conf);
+                    conf &= conf - 1;
+                    u32 byte = bit / 8 + 8 * half;
+                    u32 b = bit % 8;
+                    u32 cf = confBase[b];
+                    if (!cf) continue;
+                    const struct o_FDRConfirm *fc =
+                        (const struct o_FDRConfirm *)((const u8 *)confBase + cf);
+                    if (!(fc->groups & control)) continue;
+                    long e = it + byte;
+                    conf_with_bit(fc, a, (size_t)e, &control, &last_match,
+                                  conf_key_at(buf, len, e));
+                }
+                if (!control) return 1;
+            }
+        }
+    }
+    return 0;
+}
+
+/* ============================================================== Teddy == */
+
+/* FDR_EXEC_TEDDY teddy.c:1004-1066 and FDR_EXEC_FAT_TEDDY teddy_avx2.c:593-
+ * 660, restated per 16-byte block.  res[j][i] is the nibble lookup of mask j
+ * at byte i (8 or 16 bucket bits); the candidate word for byte i ORs
+ * res[j][i - j], taking i - j < 0 from the previous block (palignr with the
+ * carried res_old, zero at the start). */
+static int teddy_run(const struct o_Teddy *t, const rtargs *a, u64a control,
+                     int fat, u32 nMasks) {
+    const u8 *buf = a->buf;
+    size_t len = a->len;
+    const u8 *maskBase = (const u8 *)t + 64;
+    const u32 *confBase = (const u32 *)((const u8 *)t + t->confOffset);
+    u32 nb = fat ? 16 : 8;
+    u32 last_match = ~0U;
+    u16 old[4][16];
+    memset(old, 0, sizeof(old));
+
+    uintptr_t ptr = (uintptr_t)buf + a->start;
+    uintptr_t end = (uintptr_t)buf + len;
+    uintptr_t mainStart = (ptr + 15) & ~(uintptr_t)15;
+    if (ptr < mainStart) ptr = mainStart - 16;
+
+    for (; ptr < end; ptr += 16) {
+        u8 val[16];
+        u16 pmask = 0; /* bit i: poison byte i */
+        long base = (long)(ptr - (uintptr_t)buf);
+        for (int i = 0; i < 16; i++) {
+            long p = base + i;
+            val[i] = (p >= 0 && (size_t)p < len) ? buf[p] : 0;
+            if (p < (long)a->start || (size_t)p >= len) pmask |= (u16)(1u << i);
+        }
+        u16 res[4][16];
+        for (u32 j = 0; j < nMasks; j++) {
+            for (int i = 0; i < 16; i++) {
+                u8 c = val[i];
+                u16 v;
+                if (fat) {
+                    const u8 *lo = maskBase + j * 64;
+                    const u8 *hi = lo + 32;
+                    v = (u16)((lo[c & 15] | hi[c >> 4]) |
+                              ((lo[16 + (c & 15)] | hi[16 + (c >> 4)]) << 8));
+                } else {
+                    const u8 *lo = maskBase + j * 32;
+                    const u8 *hi = lo + 16;
+                    v = (u16)(lo[c & 15] | hi[c >> 4]);
+                }
+                res[j][i] = v;
+            }
+        }
+        u16 r[16];
+        for (int i = 0; i < 16; i++) {
+            u16 acc = res[0][i];
+            for (u32 j = 1; j < nMasks; j++) {
+                acc |= (i >= (int)j) ? res[j][i - j] : old[j][16 + i - j];
+            }
+            if (pmask & (1u << i)) acc = 0xffff;
+            r[i] = acc;
+        }
+        memcpy(old, res, sizeof(res));
+        u16 full = fat ? 0xffff : 0xff;
+        for (int i = 0; i < 16; i++) {
+            u16 cand = (u16)(~r[i]) & full;
+            while (cand) {
+                u32 b = (u32)__builtin_ctz(cand);
+                cand &= cand - 1;
+                u32 cf = confBase[b];
+                if (!cf) continue;
+                const struct o_FDRConfirm *fc =
+                    (const struct o_FDRConfirm *)((const u8 *)confBase + cf);
+                if (!(fc->groups & control)) continue;
+                long e = base + i;
+                conf_with_bit(fc, a, (size_t)e, &control, &last_match,
+                              conf_key_at(buf, len, e));
+            }
+            if ((i % (fat ? 4 : 8)) == (fat ? 3 : 7) && !control) return 1;
+        }
+        if (!control) return 1;
+        (void)nb;
+    }
+    return 0;
+}
+
+/* ====================================================== entry points == */
+
+static int fdr_dispatch(const void *eng, const u8 *buf, size_t len,
+                        size_t start, u64a groups, cbctx *cb) {
+    u32 id = *(const u32 *)eng;
+    rtargs a = {buf, len, start, cb};
+    if (start >= len) return 0;
+    if (id == 0) return fdr_run((const struct o_FDR *)eng, &a, groups);
+    if (id >= 3 && id <= 10) {
+        return teddy_run((const struct o_Teddy *)eng, &a, groups, 1, (id - 3) / 2 + 1);
+    }
+    if (id >= 11 && id <= 18) {
+        return teddy_run((const struct o_Teddy *)eng, &a, groups, 0, (id - 11) / 2 + 1);
+    }
+    return 2;
+}
+
+/* returns number of matches; *status = HWLM_SUCCESS/TERMINATED/ERROR */
+long orc_fdr_exec(const void *eng, const u8 *buf, size_t len, size_t start,
+                  u64a groups, orc_match *out, size_t cap, long term_after,
+                  u64a cb_ret, int *status) {
+    cbctx cb = {out, cap, 0, term_after, cb_ret};
+    *status = fdr_dispatch(eng, buf, len, start, groups, &cb);
+    return (long)cb.n;
+}
+
+long orc_nood_exec(const void *eng, const u8 *buf, size_t len, size_t start,
+                   orc_match *out, size_t cap, long term_after, int *status) {
+    cbctx cb = {out, cap, 0, term_after, ~0ULL};
+    *status = nood_run((const struct o_nood *)eng, buf, len, start, &cb);
+    return (long)cb.n;
+}
+
+/* hwlm.c:48-105 accel pre-skip (block mode) */
+static size_t accel_block(const u8 *aux, const u8 *buf, size_t len, size_t start) {
+    if (len - start < 16) return start;
+    u8 type = aux[0], offset = aux[1];
+    long r;
+    const u8 *p = buf + start;
+    size_t n = len - start;
+    switch (type) {
+    case 1: r = orc_verm(aux[2], 0, 0, 0, p, n); break;
+    case 2: r = orc_verm(aux[2], 1, 0, 0, p, n); break;
+    case 3: r = orc_dverm(aux[2], aux[3], 0, p, n); break;
+    case 4: r = orc_dverm(aux[2], aux[3], 1, p, n); break;
+    case 13: r = orc_shufti(aux + 16, aux + 32, p, n); break;
+    case 15: r = orc_truffle(aux + 16, aux + 32, p, n); break;
+    default: return start;
+    }
+    long np = (long)start + r;
+    if (offset) {
+        np -= offset;
+        if (np < 0) np = 0;
+    }
+    return (size_t)np;
+}
+
+long orc_hwlm_exec(const void *hwlm, const u8 *buf, size_t len, size_t start,
+                   u64a groups, orc_match *out, size_t cap, long term_after,
+                   u64a cb_ret, int *status) {
+    const struct o_HWLM *h = (const struct o_HWLM *)hwlm;
+    const void *eng = (const u8 *)hwlm + ROUNDUP_CL(sizeof(*h));
+    cbctx cb = {out, cap, 0, term_after, cb_ret};
+    *status = 0;
+    if (!groups) return 0;
+    if (h->type == 16) {
+        *status = nood_run((const struct o_nood *)eng, buf, len, start, &cb);
+        return (long)cb.n;
+    }
+    const u8 *aa = h->accel0;
+    if ((groups & ~h->accel1_groups) == 0) aa = h->accel1;
+    start = accel_block(aa, buf, len, start);
+    *status = fdr_dispatch(eng, buf, len, start, groups, &cb);
+    return (long)cb.n;
+}
+
+/* ====================================== counting helpers (cpu baseline) */
+
+/* Number of FDR first-stage candidates (end, bucket) over a block at stride
+ * 1 — a diagnostic for the false-positive rate the confirm stage sees. */
+u64a orc_fdr_candidates(const void *eng, const u8 *buf, size_t len) {
+    const struct o_FDR *fdr = (const struct o_FDR *)eng;
+    const u64a *ft = (const u64a *)((const u8 *)fdr + ROUNDUP_CL(sizeof(*fdr)));
+    u64a count = 0;
+    for (size_t e = 0; e < len; e++) {
+        u64a acc = 0;
+        for (int k = 0; k < 8; k++) {
+            long p = (long)e - k;
+            if (p < 0) break;
+            u32 key = ((u32)buf[p] | ((u32)((size_t)(p + 1) < len ? buf[p + 1] : 0) << 8)) &
+                      fdr->domainMask;
+            acc |= (ft[key] >> (8 * k)) & 0xff;
+        }
+        if (e < 8) acc |= fdr->start[e];
+        count += (u64a)__builtin_popcount((u32)(~acc & 0xff));
+    }
+    return count;
+}

@@ -1,0 +1,284 @@
+"""Generate tests/golden/*.json — the known answers of the reference's own
+unit tests for this path, restated as data (inputs + expected outputs).
+
+Each case cites the reference test it restates.  The expected values are
+the reference tests' assertions (literal positions / the test's own
+std::string::compare brute force), not outputs of our oracle or engine.
+
+    python tests/golden/make_golden.py      # rewrites the JSON files
+"""
+import json
+import math
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def hx(b):
+    return bytes(b).hex()
+
+
+# --------------------------------------------------------------- noodle
+def noodle_cases():
+    """unit/internal/noodle.cpp:81-262 (noodleMatch calls noodExec from 0)."""
+    cases = []
+
+    def add(src, data, lit, nocase, expected):
+        cases.append({"src": src, "data": hx(data), "lit": hx(lit), "nocase": nocase,
+                      "expected": expected})
+
+    a1024 = b"a" * 1024
+    # nood1 :81-121
+    add("noodle.cpp:87", a1024, b"a", 0, list(range(1024)))
+    add("noodle.cpp:93", a1024, b"A", 0, [])
+    add("noodle.cpp:97", a1024, b"A", 1, list(range(1024)))
+    for j in range(16):
+        add("noodle.cpp:105", a1024[j:], b"A", 1, list(range(1024 - j)))
+        add("noodle.cpp:112", a1024[:1024 - j], b"A", 1, list(range(1024 - j)))
+    # nood2 :123-177
+    add("noodle.cpp:130", a1024, b"aa", 0, [i + 1 for i in range(1023)])
+    add("noodle.cpp:137", a1024, b"aA", 0, [])
+    add("noodle.cpp:141", a1024, b"AA", 0, [])
+    add("noodle.cpp:145", a1024, b"aa", 1, [i + 1 for i in range(1023)])
+    add("noodle.cpp:152", a1024, b"Aa", 1, [i + 1 for i in range(1023)])
+    add("noodle.cpp:159", a1024, b"AA", 1, [i + 1 for i in range(1023)])
+    for j in range(16):
+        add("noodle.cpp:167", a1024[j:], b"Aa", 1, [i + 1 for i in range(1023 - j)])
+        add("noodle.cpp:174", a1024[:1024 - j], b"aA", 1, [i + 1 for i in range(1023 - j)])
+    # noodLong :179-221
+    add("noodle.cpp:186", a1024, b"aaaa", 0, [i + 3 for i in range(1021)])
+    add("noodle.cpp:192", a1024, b"aaAA", 0, [])
+    add("noodle.cpp:196", a1024, b"aaAA", 1, [i + 3 for i in range(1021)])
+    for j in range(16):
+        add("noodle.cpp:204", a1024[j:], b"AAaa", 1, [i + 3 for i in range(1021 - j)])
+        add("noodle.cpp:211", a1024[j:], b"aaaA", 1, [i + 3 for i in range(1021 - j)])
+    # noodCutoverSingle / Double :223-262 (alignment sweep -> lengths)
+    for ln in range(128):
+        add("noodle.cpp:233", b"a" * ln, b"a", 0, list(range(ln)))
+        add("noodle.cpp:253", b"a" * ln, b"aa", 0, [i + 1 for i in range(max(0, ln - 1))])
+    return cases
+
+
+# ------------------------------------------------------------------ FDR
+def fdr_cases():
+    """unit/internal/fdr.cpp:167-744, run for every engine hint by the
+    tests (FDRp is parameterised over getValidFdrEngines, :113-137)."""
+    cases = []
+
+    def lit(s, nocase=0, id=0, noruns=0):
+        return {"s": hx(s), "nocase": nocase, "id": id, "noruns": noruns}
+
+    def add(src, lits, data, expected, start=0, term_after=-1, exact_order=True,
+            expected_len=None):
+        c = {"src": src, "lits": lits, "data": hx(data), "start": start,
+             "term_after": term_after, "expected": expected,
+             "exact_order": exact_order}
+        if expected_len is not None:
+            c["expected_len"] = expected_len
+        cases.append(c)
+
+    d = b"mnopqrabcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ12345678901234567890mnopqr\0"
+    add("fdr.cpp:167 Simple", [lit(b"mnopqr", 0, 0)], d, [[5, 0], [23, 0], [83, 0]])
+    d2 = b"mnopqrabcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ12345678901234567890m0m"
+    add("fdr.cpp:191 SimpleSingle", [lit(b"m", 0, 0)], d2,
+        [[0, 0], [18, 0], [78, 0], [80, 0]])
+    for i in range(128 - 3):
+        buf = bytearray(128)
+        buf[i:i + 3] = b"abc"
+        add("fdr.cpp:216 MultiLocation", [lit(b"abc", 0, 1)], bytes(buf), [[i + 2, 1]])
+    add("fdr.cpp:246 NoRepeat1", [lit(b"m", 0, 0, 1)], d2, [[0, 0]])
+    # NoRepeat2 asserts only matches[0], matches[2] and the count (:290-293)
+    add("fdr.cpp:270 NoRepeat2", [lit(b"m", 0, 0, 1), lit(b"A", 0, 42)], d2,
+        [[0, 0], [32, 42], [78, 0]])
+    add("fdr.cpp:297 NoRepeat3", [lit(b"90m", 0, 0, 1), lit(b"zA", 0, 0, 1)], d2,
+        [[32, 0]])
+    d3 = b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ12345678901234567890"
+    add("fdr.cpp:405 moveByteStream", [lit(b"mnopqr", 0, 0)], d3, [[17, 0]])
+    # FDRTermB :721-744: first callback terminates
+    add("fdr.cpp:721 FDRTermB", [lit(b"f", 0, 0), lit(b"ff", 0, 1)], b"f" * 17, None,
+        term_after=1, expected_len=1)
+    # AlignAndTooEarly :496-567: matches at both ends only when j == 0
+    for pat, alien in ((b"abaabaaa", b"x"), (b"zzzyyzyz", b"\x99"), (b"abcdef l", b"\0")):
+        for ll in range(1, len(pat) + 1):
+            for i in range(0, 32, 5):
+                buf = bytearray(alien * 160)
+                buf[i:i + ll] = pat[:ll]
+                buf[i + 128 - ll:i + 128] = pat[:ll]
+                for j in range(0, ll + 1):
+                    data = bytes(buf[i + j:i + j + 128 - 2 * j])
+                    exp = [[ll - 1, 0], [127, 0]] if j == 0 else []
+                    add("fdr.cpp:496 AlignAndTooEarly", [lit(pat[:ll], 0, 0)], data, exp)
+    return cases
+
+
+def short_writings_spec():
+    """fdr.cpp:594-692 ShortWritings: buffers and literal groups; the test's
+    expected set is its own std::string::compare brute force."""
+    out = []
+    for alphabet in ([0x61, 0x62, 0x78], [0x78, 0x79, 0x7A], [0x00, 0x41, 0x20],
+                     [0x61, 0x20, 0x99]):
+        bufs = []
+        for ln in range(1, 7):
+            for j in range(3 ** ln):
+                bufs.append(bytes(alphabet[(j // (3 ** k)) % 3] for k in range(ln)))
+        nb = len(bufs)
+
+        def fib(n):
+            f0 = f1 = f2 = 1
+            for _ in range(n):
+                f2 = f1 + f0
+                f0 = f1
+                f1 = f2
+            return f2
+
+        for ln in range(7, 64):
+            for i in range(10):
+                s = b""
+                j = 0
+                while len(s) < ln:
+                    s += bufs[fib(i * 5 + j + (ln - 6) * 10) % nb]
+                    j += 1
+                bufs.append(s)
+        pats = []
+        for ln in range(1, 9):
+            for j in range(2 ** ln):
+                pats.append(bytes(alphabet[(j >> k) & 1] for k in range(ln)))
+        out.append({"alphabet": alphabet, "bufs": [hx(b) for b in bufs],
+                    "pats": [hx(p) for p in pats]})
+    return out
+
+
+# ---------------------------------------------------------------- accel
+def accel_cases():
+    """shufti.cpp / truffle.cpp / vermicelli.cpp / rvermicelli.cpp known
+    answers.  kind: shufti|rshufti|truffle|rtruffle (class = chars),
+    verm|nverm|rverm|rnverm (c, nocase), dverm (c1, c2, nocase)."""
+    cases = []
+
+    def add(src, kind, data, expected, **kw):
+        c = {"src": src, "kind": kind, "data": hx(data), "expected": expected}
+        c.update(kw)
+        cases.append(c)
+
+    t = b"bbbbbbbbbbbbbbbbbbbbbbbbbbbbbbbbbabbbbbbbbbbbbbbabbbbbbbbbbbb"
+    for i in range(32):
+        add("shufti.cpp:166 ExecMatch1", "shufti", t[i:], 33 - i, chars=[0x61])
+    t = b"bbbbbbbbbbbbbbbbbaaaaaaaaaaaaaaaabbbbbbbbbbbbbbbabbbbbbbbbbbb"
+    for i in range(16):
+        add("shufti.cpp:185 ExecMatch2", "shufti", t[i:], 17 - i, chars=[0x61])
+        add("truffle.cpp:249 ExecMatch2", "truffle", t[i:], 17 - i, chars=[0x61])
+    t = b"bbbbbbbbbbbbbbbbbBaaaaaaaaaaaaaaabbbbbbbbbbbbbbbabbbbbbbbbbbb"
+    for i in range(16):
+        add("shufti.cpp:204 ExecMatch3", "shufti", t[i:], 17 - i, chars=[0x61, 0x42])
+    for ch in b"ACca":
+        t = b"bbbbbbbbbbbbbbbbb" + bytes([ch]) + b"aaaaaaaaaaaaaaabbbbbbbbbbbbbbbabbbbbbbbbbbb"
+        for i in range(16):
+            add("shufti.cpp:224 ExecMatch4", "shufti", t[i:], 17 - i,
+                chars=[0x61, 0x43, 0x41, 0x63])
+    t = bytearray(b"b" * 76)
+    for i in range(31):
+        t[48 - i] = 0x61
+        add("shufti.cpp:261 ExecMatch5", "shufti", bytes(t), 48 - i, chars=[0x61])
+    t = b"b" * 61
+    for i in range(32):
+        add("shufti.cpp:111 ExecNoMatch1", "shufti", t[i:], len(t) - i, chars=[0x61])
+    t = b"bbbbbbabbbbbbbbbbabbbbbbbbbbbbbbbbbbbbbbbbbbbbbbbbbbbbbbbbbbb"
+    for i in range(16):
+        add("shufti.cpp:964 ReverseExecMatch1", "rshufti", t[:len(t) - i], 17, chars=[0x61])
+    t = bytearray(b"b" * 76)
+    for i in range(76):
+        t[i] = 0x61
+        add("shufti.cpp:1076 ReverseExecMatch5", "rshufti", bytes(t), i, chars=[0x61])
+    t = bytearray(b"b" * 256)
+    for i in range(256):
+        t[i] = 0x61
+        add("shufti.cpp:1096 ReverseExecMatch6", "rshufti", bytes(t), i, chars=[0x61])
+    # truffle
+    t = b"b" * 61 + b"\xff"
+    for i in range(16):
+        add("truffle.cpp:94 ExecNoMatch1", "truffle", t[i:], len(t) - i, chars=[0x61])
+    add("truffle.cpp:151 ExecMiniMatch0", "truffle", b"a", 0, chars=[0x61])
+    add("truffle.cpp:166 ExecMiniMatch1", "truffle", b"bbbbbbbabbb", 7, chars=[0x61])
+    add("truffle.cpp:181 ExecMiniMatch2", "truffle", b"bbbbbbb\0bbb", 7, chars=[0])
+    add("truffle.cpp:196 ExecMiniMatch3", "truffle", b"\0\0\0\0\0\0\0a\0\0\0", 7, chars=[0x61])
+    t = b"bbbbbbbbbbbbbbbbbabbbbbbbbbbbbbbbbbbbbbbbbbbbbbbabbbbbbbbbbbb"
+    for i in range(16):
+        add("truffle.cpp:230 ExecMatch1", "truffle", t[i:], 17 - i, chars=[0x61])
+    t = b"eeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeeee"
+    for i in range(16):
+        add("truffle.cpp:133 ExecNoMatch3", "truffle", t[i:], len(t) - i, chars=[0x56])
+    t = bytearray(b"b" * 76)
+    for i in range(76):
+        t[i] = 0x61
+        add("truffle.cpp:602 ReverseExecMatch5", "rtruffle", bytes(t), i, chars=[0x61])
+    # vermicelli
+    t = b"b" * 61
+    for i in range(16):
+        for j in range(16):
+            s = t[i:len(t) - j]
+            add("vermicelli.cpp:35 ExecNoMatch1", "verm", s, len(s), c=0x61, nocase=0)
+            add("vermicelli.cpp:35 ExecNoMatch1", "verm", s, len(s), c=0x41, nocase=1)
+            add("vermicelli.cpp:122 DV ExecNoMatch1", "dverm", s, len(s), c1=0x61, c2=0x62,
+                nocase=0)
+            add("vermicelli.cpp:140 DV partial", "dverm", s, len(s) - 1, c1=0x62, c2=0x42,
+                nocase=0)
+            add("vermicelli.cpp:145 DV partial", "dverm", s, len(s) - 1, c1=0x42, c2=0x41,
+                nocase=1)
+    t = b"bbbbbbbbbbbbbbbbbabbbbbbbbbbbbbbbbbbbbbbbbbbbbbbabbbbbbbbbbbb"
+    for i in range(16):
+        add("vermicelli.cpp:58 Exec1", "verm", t[i:], 17 - i, c=0x61, nocase=0)
+        add("vermicelli.cpp:58 Exec1", "verm", t[i:], 17 - i, c=0x41, nocase=1)
+    t = b"bbbbbbbbbbbbbbbbbAaaaaaaaaaaaaaaaaaaaaaabbbbbbbbabbbbbbbbbbbb"
+    for i in range(16):
+        add("vermicelli.cpp:90 Exec3", "verm", t[i:], 18 - i, c=0x61, nocase=0)
+        add("vermicelli.cpp:90 Exec3", "verm", t[i:], 17 - i, c=0x41, nocase=1)
+    t = b"bbbbbbbbbbbbbbbbbbabbbbbbbbbbbbbbbbbbbbbbbbbbbbbbabbbbbbbbbbb"
+    for i in range(16):
+        add("vermicelli.cpp:157 DV Exec1", "dverm", t[i:], 18 - i, c1=0x61, c2=0x62, nocase=0)
+        add("vermicelli.cpp:157 DV Exec1", "dverm", t[i:], 18 - i, c1=0x41, c2=0x42, nocase=1)
+        add("vermicelli.cpp:157 DV Exec1", "dverm", t[i:], 17 - i, c1=0x62, c2=0x61, nocase=0)
+    t = b"bbbbbbbbbbbbbbbbbaAaaAAaaaaaaaaaaaaaaaaaabbbbbbbaaaaabbbbbbbb"
+    for i in range(16):
+        add("vermicelli.cpp:199 DV Exec3", "dverm", t[i:], 18 - i, c1=0x41, c2=0x61, nocase=0)
+        add("vermicelli.cpp:199 DV Exec3", "dverm", t[i:], 17 - i, c1=0x41, c2=0x41, nocase=1)
+        add("vermicelli.cpp:199 DV Exec3", "dverm", t[i:], 21 - i, c1=0x41, c2=0x41, nocase=0)
+        add("vermicelli.cpp:199 DV Exec3", "dverm", t[i:], 17 - i, c1=0x61, c2=0x41, nocase=0)
+    la = b"abcdefghijklmnopqrstuvwxyz"
+    add("vermicelli.cpp:244 noodEarlyExit", "verm", la, 26, c=0x30, nocase=0)
+    add("vermicelli.cpp:244 noodEarlyExit", "verm", la, 26, c=0x41, nocase=0)
+    for i, ch in enumerate(la):
+        add("vermicelli.cpp:253 noodEarlyExit", "verm", la, i, c=ch, nocase=0)
+        add("vermicelli.cpp:253 noodEarlyExit", "verm", la, i, c=ch - 0x20, nocase=1)
+    t = b"b" * 61
+    for i in range(16):
+        for j in range(16):
+            s_ = t[i:len(t) - j]
+            add("vermicelli.cpp:262 NVerm ExecNoMatch1", "nverm", s_, len(s_), c=0x62, nocase=0)
+            add("vermicelli.cpp:262 NVerm ExecNoMatch1", "nverm", s_, len(s_), c=0x42, nocase=1)
+            add("rvermicelli.cpp:37 ExecNoMatch1", "rverm", s_, -1, c=0x61, nocase=0)
+            add("rvermicelli.cpp:37 ExecNoMatch1", "rverm", s_, -1, c=0x42, nocase=0)
+            add("rvermicelli.cpp:37 ExecNoMatch1", "rverm", s_, -1, c=0x41, nocase=1)
+    t = b"bbbbbbbbbbbbbbbbbabbbbbbbbbbbbbbbbbbbbbbbbbbbbbbabbbbbbbbbbbb"
+    for i in range(16):
+        add("vermicelli.cpp:282 NVerm Exec1", "nverm", t[i:], 17 - i, c=0x62, nocase=0)
+        add("vermicelli.cpp:282 NVerm Exec1", "nverm", t[i:], 17 - i, c=0x42, nocase=1)
+    t = b"bbbbbbbbbbbbbbbbbabbbbbbbbbbbbbbbbbbbbbbbbbbbbbbabbbbbbbbbbbbbbbbbbbbb"
+    for i in range(16):
+        add("rvermicelli.cpp:57 Exec1", "rverm", t[:len(t) - i], 48, c=0x61, nocase=0)
+        add("rvermicelli.cpp:57 Exec1", "rverm", t[i:], 48 - i, c=0x41, nocase=1)
+    return cases
+
+
+def main():
+    with open(os.path.join(HERE, "noodle.json"), "w") as f:
+        json.dump(noodle_cases(), f)
+    with open(os.path.join(HERE, "fdr.json"), "w") as f:
+        json.dump(fdr_cases(), f)
+    with open(os.path.join(HERE, "fdr_shortwritings.json"), "w") as f:
+        json.dump(short_writings_spec(), f)
+    with open(os.path.join(HERE, "accel.json"), "w") as f:
+        json.dump(accel_cases(), f)
+
+
+if __name__ == "__main__":
+    main()

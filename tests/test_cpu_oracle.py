@@ -1,0 +1,266 @@
+"""CPU tests: the oracle against the reference's own known answers
+(tests/golden, restated from unit/internal/*.cpp), the oracle against a
+brute-force matcher on random inputs, and the bytecode builder's layout.
+
+No GPU is touched here: the builder is host code in the library and the
+oracle is plain C.
+"""
+import ctypes
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+import vectorscan_amd as vsa
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FDR_HINTS = [0, 11, 12, 13, 14, 15, 16, 17, 18, 3, 4, 5, 6, 7, 8, 9, 10]
+
+
+def load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+def lits_of(case):
+    return [vsa.HwlmLiteral(bytes.fromhex(l["s"]), l["nocase"], l["id"], noruns=l["noruns"])
+            for l in case["lits"]]
+
+
+def build_or_none(lits, hint):
+    try:
+        return vsa.hwlm_build(lits, engine_hint=hint)
+    except vsa.BuildError:
+        return None
+
+
+# ------------------------------------------------------------- golden ---
+
+def test_golden_noodle_oracle():
+    for c in load("noodle.json"):
+        blob = vsa.hwlm_build([vsa.HwlmLiteral(bytes.fromhex(c["lit"]), c["nocase"], 1000)])
+        assert blob.is_noodle
+        st, m = oracle.nood_exec(vsa.engine_blob(blob), bytes.fromhex(c["data"]))
+        assert st == 0
+        assert [e for e, _ in m] == c["expected"], c["src"]
+        assert all(i == 1000 for _, i in m)
+
+
+@pytest.mark.parametrize("hint", FDR_HINTS)
+def test_golden_fdr_oracle(hint):
+    ran = 0
+    for c in load("fdr.json"):
+        blob = build_or_none(lits_of(c), hint)
+        if blob is None:
+            continue  # CHECK_WITH_TEDDY_OK_TO_FAIL (fdr.cpp:75-84)
+        ran += 1
+        st, m = oracle.fdr_exec(vsa.engine_blob(blob), bytes.fromhex(c["data"]),
+                                start=c["start"], term_after=c["term_after"])
+        if c["expected"] is None:
+            assert len(m) == c["expected_len"], c["src"]
+            assert st == 1
+            continue
+        assert st == 0
+        assert [list(x) for x in m] == c["expected"], (c["src"], hint)
+    assert ran > 0
+
+
+@pytest.mark.parametrize("hint", [0, 11, 17, 3, 9])
+def test_golden_short_writings_oracle(hint):
+    """fdr.cpp:594-692 on the first alphabet (all alphabets: slow test)."""
+    spec = load("fdr_shortwritings.json")[0]
+    _short_writings(spec, hint, oracle_run)
+
+
+def oracle_run(blob, bufs):
+    out = []
+    for b in bufs:
+        st, m = oracle.fdr_exec(vsa.engine_blob(blob), b)
+        assert st == 0
+        out.append(m)
+    return out
+
+
+def _short_writings(spec, hint, run):
+    bufs = [bytes.fromhex(x) for x in spec["bufs"]]
+    pats = [bytes.fromhex(x) for x in spec["pats"]]
+    for g in range(0, len(pats), 32):
+        group = pats[g:g + 32]
+        lits = [vsa.HwlmLiteral(p, False, g + i) for i, p in enumerate(group)]
+        blob = build_or_none(lits, hint)
+        if blob is None:
+            continue
+        got = run(blob, bufs)
+        for b, m in zip(bufs, got):
+            exp = sorted((j + len(p) - 1, g + i) for i, p in enumerate(group)
+                         for j in range(len(b) - len(p) + 1) if b[j:j + len(p)] == p)
+            assert sorted(m) == exp
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("alpha", [1, 2, 3])
+def test_golden_short_writings_oracle_all(alpha):
+    spec = load("fdr_shortwritings.json")[alpha]
+    for hint in (0, 11, 17, 3):
+        _short_writings(spec, hint, oracle_run)
+
+
+def accel_expected_oracle(c):
+    data = bytes.fromhex(c["data"])
+    k = c["kind"]
+    if k in ("shufti", "rshufti"):
+        lo, hi = vsa.shufti_build_masks(c["chars"])
+        return oracle.shufti(lo, hi, data, reverse=(k == "rshufti"))
+    if k in ("truffle", "rtruffle"):
+        m1, m2 = vsa.truffle_build_masks(c["chars"])
+        return oracle.truffle(m1, m2, data, reverse=(k == "rtruffle"))
+    if k in ("verm", "nverm", "rverm", "rnverm"):
+        return oracle.verm(c["c"], c["nocase"], data, negate=k in ("nverm", "rnverm"),
+                           reverse=k in ("rverm", "rnverm"))
+    if k == "dverm":
+        return oracle.dverm(c["c1"], c["c2"], c["nocase"], data)
+    raise AssertionError(k)
+
+
+def test_golden_accel_oracle():
+    for c in load("accel.json"):
+        assert accel_expected_oracle(c) == c["expected"], c["src"]
+
+
+# -------------------------------------------------- random differential --
+
+def rand_lits(rng, n, minlen=1, maxlen=8, alphabet=b"abcdefgh", nocase_frac=0.2,
+              msk_frac=0.0):
+    lits = []
+    for i in range(n):
+        ln = rng.randint(minlen, maxlen)
+        s = bytes(rng.choice(alphabet) for _ in range(ln))
+        nc = rng.random() < nocase_frac
+        msk = cmp = b""
+        if rng.random() < msk_frac:
+            ml = rng.randint(1, 8)
+            m = bytearray(ml)
+            v = bytearray(ml)
+            # constrain one byte before (or inside) the literal
+            k = rng.randrange(ml)
+            m[k] = 0xF0
+            v[k] = rng.choice(alphabet) & 0xF0
+            # keep consistent with s where overlapping
+            for q in range(ml):
+                si = len(s) - ml + q
+                if 0 <= si and m[q]:
+                    c = s[si]
+                    if nc and (0x41 <= (c & 0xDF) <= 0x5A):
+                        c &= 0xDF
+                        m[q] &= 0xDF
+                    v[q] = c & m[q]
+            msk, cmp = bytes(m), bytes(v)
+        lits.append(vsa.HwlmLiteral(s, nc, i, msk=msk, cmp=cmp))
+    return lits
+
+
+def rand_data(rng, n, alphabet=b"abcdefghABCDEFGH"):
+    return bytes(rng.choice(alphabet) for _ in range(n))
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("nlits", [1, 5, 30, 60, 200])
+def test_oracle_vs_bruteforce(seed, nlits):
+    rng = random.Random(seed * 1000 + nlits)
+    lits = rand_lits(rng, nlits, msk_frac=0.2)
+    blob = vsa.hwlm_build(lits)
+    for ln in (0, 1, 7, 15, 16, 17, 33, 100, 999):
+        data = rand_data(rng, ln)
+        for start in sorted({0, 1, min(5, ln), ln // 2}):
+            if ln and start >= ln:
+                continue
+            st, m = oracle.hwlm_exec(blob.ptr, data, start=start)
+            got = set(m)
+            exp = oracle.brute_force(lits, data)
+            if start == 0 or blob.is_noodle:
+                if blob.is_noodle:
+                    # noodle needs the whole window at or after start
+                    w = max(len(lits[0].s), len(lits[0].msk))
+                    exp = {(e, i) for e, i in exp if e - w + 1 >= start}
+                assert got == exp, (nlits, ln, start)
+            else:
+                # FDR/Teddy may report literals that begin before `start`
+                # (zone semantics, fdr.c:625-659); every report is real and
+                # every occurrence fully after start is reported
+                assert got <= {(e, i) for e, i in exp if e >= start}
+                lens = {l.id: max(len(l.s), len(l.msk)) for l in lits}
+                need = {(e, i) for e, i in exp if e - lens[i] + 1 >= start}
+                assert need <= got
+            # callback order: non-decreasing end
+            ends = [e for e, _ in m]
+            assert ends == sorted(ends)
+
+
+# ----------------------------------------------------------- builder ----
+
+def test_builder_engine_choice():
+    rng = random.Random(7)
+    pr = bytes(range(0x20, 0x7F))
+    def lits_n(n, seed):
+        r = random.Random(seed)
+        return [vsa.HwlmLiteral(bytes(r.choice(pr) for _ in range(r.randint(4, 8))), False, i)
+                for i in range(n)]
+    assert vsa.hwlm_build(lits_n(1, 1)).is_noodle
+    e48 = vsa.hwlm_build(lits_n(48, 55)).engine_id
+    assert 11 <= e48 <= 18 or 3 <= e48 <= 10
+    e64 = vsa.hwlm_build(lits_n(64, 71)).engine_id
+    assert 3 <= e64 <= 10  # fat teddy (16 buckets) on this target
+    b5k = vsa.hwlm_build(lits_n(5000, 12))
+    assert b5k.engine_id == 0
+    raw = b5k.tobytes()
+    fdr = raw[vsa.HWLM_HEADER:]
+    domain = fdr[25]
+    stride = fdr[24]
+    assert domain == 13 and stride == 1
+    assert int.from_bytes(fdr[26:28], "little") == (1 << domain) - 1
+    assert rng  # silence
+
+
+def test_builder_layout_offsets():
+    blob = vsa.hwlm_build([vsa.HwlmLiteral(b"abc", False, 1), vsa.HwlmLiteral(b"xyz", True, 2)],
+                          engine_hint=0)
+    raw = blob.tobytes()
+    assert raw[0] == 12  # HWLM_ENGINE_FDR
+    fdr = raw[192:]
+    size, = np.frombuffer(fdr[4:8], np.uint32)
+    conf_off, flood_off = np.frombuffer(fdr[16:24], np.uint32)
+    assert 192 + size == len(raw)
+    assert conf_off % 64 == 0 and flood_off % 64 == 0
+    assert conf_off == 64 + (1 << 9) * 8  # header, then the domain-9 table
+
+
+def test_shufti_truffle_masks():
+    chars = [1, 0x7F, 0x80, 0xFE, ord("<"), ord(">"), ord('"'), ord("'")]
+    lo, hi = vsa.shufti_build_masks(chars)
+    member = {c for c in range(256) if lo[c & 15] & hi[c >> 4]}
+    assert member == set(chars)
+    m1, m2 = vsa.truffle_build_masks(range(0, 256, 3))
+    mem = {c for c in range(256) if ((m2 if c & 0x80 else m1)[c & 15] >> ((c >> 4) & 7)) & 1}
+    assert mem == set(range(0, 256, 3))
+    big = random.Random(5).sample(range(256), 100)
+    assert vsa.shufti_build_masks(big) is None  # needs truffle (SURVEY §8d cfg 2)
+
+
+# ------------------------------------------------------------ C ABI -----
+
+def test_library_exports_header_symbols():
+    import re
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "include", "vectorscan_amd.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    hdr = "\n".join(l for l in hdr.splitlines()
+                    if not l.lstrip().startswith(("#", "typedef")))
+    names = set(re.findall(r"\b(\w+)\s*\(", hdr))
+    names -= {"if", "while", "sizeof", "defined", "HWLMCallback"}
+    assert "hwlmExec" in names and "vsa_scan_blocks" in names
+    lib = ctypes.CDLL(vsa.LIB_PATH)
+    missing = [n for n in sorted(names) if not hasattr(lib, n)]
+    assert not missing, missing

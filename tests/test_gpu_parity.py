@@ -1,0 +1,252 @@
+"""GPU parity tests: the HIP engine (through the C ABI) against the oracle
+and the reference's known answers.  Integer/byte work: every comparison is
+bit-exact (match lists compared in callback order)."""
+import ctypes
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+import vectorscan_amd as vsa
+from test_cpu_oracle import (FDR_HINTS, build_or_none, load, lits_of, rand_data,
+                             rand_lits, _short_writings)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = vsa.Context(0)
+    yield c
+    c.close()
+
+
+def gpu_hwlm(blob, data, start=0, groups=vsa.HWLM_ALL_GROUPS, term_after=-1, cb_ret=None):
+    seq = []
+
+    def cb(end, id_):
+        seq.append((end, id_))
+        if term_after >= 0 and len(seq) >= term_after:
+            return 0
+        return vsa.HWLM_ALL_GROUPS if cb_ret is None else cb_ret
+
+    rc = vsa.hwlm_exec(blob, data, start=start, cb=cb, groups=groups)
+    return rc, seq
+
+
+# ------------------------------------------------------------- golden ---
+
+def test_gpu_golden_noodle():
+    for c in load("noodle.json"):
+        blob = vsa.hwlm_build([vsa.HwlmLiteral(bytes.fromhex(c["lit"]), c["nocase"], 1000)])
+        st, m = vsa.nood_exec(blob, bytes.fromhex(c["data"]))
+        assert st == 0
+        assert [e for e, _ in m] == c["expected"], c["src"]
+
+
+@pytest.mark.parametrize("hint", FDR_HINTS)
+def test_gpu_golden_fdr(hint):
+    for c in load("fdr.json"):
+        blob = build_or_none(lits_of(c), hint)
+        if blob is None:
+            continue
+        data = bytes.fromhex(c["data"])
+        if c["expected"] is None:
+            seq = []
+
+            def cb(end, id_):
+                seq.append((end, id_))
+                return 0
+            rc = vsa.fdr_exec(blob, data, cb=cb)
+            assert rc == vsa.HWLM_TERMINATED and len(seq) == c["expected_len"]
+            continue
+        st, m = vsa.fdr_exec(blob, data, start=c["start"])
+        assert st == 0
+        assert [list(x) for x in m] == c["expected"], (c["src"], hint)
+
+
+def test_gpu_golden_accel():
+    from test_cpu_oracle import accel_expected_oracle  # noqa: F401
+    for c in load("accel.json"):
+        data = bytes.fromhex(c["data"])
+        k = c["kind"]
+        if k in ("shufti", "rshufti"):
+            lo, hi = vsa.shufti_build_masks(c["chars"])
+            got = (vsa.rshufti_exec if k == "rshufti" else vsa.shufti_exec)(lo, hi, data)
+        elif k in ("truffle", "rtruffle"):
+            m1, m2 = vsa.truffle_build_masks(c["chars"])
+            got = (vsa.rtruffle_exec if k == "rtruffle" else vsa.truffle_exec)(m1, m2, data)
+        elif k == "verm":
+            got = vsa.vermicelli_exec(c["c"], c["nocase"], data)
+        elif k == "nverm":
+            got = vsa.nvermicelli_exec(c["c"], c["nocase"], data)
+        elif k == "rverm":
+            got = vsa.rvermicelli_exec(c["c"], c["nocase"], data)
+        elif k == "dverm":
+            got = vsa.vermicelli_double_exec(c["c1"], c["c2"], c["nocase"], data)
+        else:
+            raise AssertionError(k)
+        assert got == c["expected"], c["src"]
+
+
+def test_gpu_short_writings_batched(ctx):
+    """fdr.cpp:594-692: every buffer of a literal group is one block of a
+    single device launch."""
+    spec = load("fdr_shortwritings.json")[0]
+
+    def run(blob, bufs):
+        return batch_run(ctx, blob, bufs)
+
+    for hint in (0, 11, 17, 3, 9):
+        _short_writings(spec, hint, run)
+
+
+# ---------------------------------------------------------- batch API ---
+
+def batch_run(ctx, blob, bufs, starts=None, misalign=0):
+    """Scan bufs as blocks of one launch; return per-block [(end, id)]."""
+    offs, pos = [], misalign
+    for b in bufs:
+        offs.append(pos)
+        pos += len(b) + 3  # gaps between blocks: bytes outside every block
+    host = np.full(pos + 16, 0x61, np.uint8)
+    for o, b in zip(offs, bufs):
+        host[o:o + len(b)] = np.frombuffer(b, np.uint8)
+    dbuf = ctx.malloc(len(host))
+    try:
+        ctx.h2d(dbuf, host)
+        db = vsa.Database(ctx, blob)
+        n = ctx.scan_blocks(db, dbuf, offs, [len(b) for b in bufs], starts)
+        res = ctx.results(n)
+        db.close()
+    finally:
+        ctx.free(dbuf)
+    out = [[] for _ in bufs]
+    ends = res["key"] >> np.uint64(24)
+    bi = np.searchsorted(np.array(offs, np.uint64), ends, side="right") - 1
+    for e, i, b in zip(ends.tolist(), res["id"].tolist(), bi.tolist()):
+        out[b].append((e - offs[b], i))
+    return out
+
+
+def replay_set(blob, seq):
+    return seq
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("nlits", [1, 5, 30, 60, 96, 300, 3000])
+def test_gpu_vs_oracle_random(seed, nlits):
+    rng = random.Random(seed * 7919 + nlits)
+    lits = rand_lits(rng, nlits, msk_frac=0.15)
+    for l in lits:
+        l.noruns = rng.random() < 0.3
+        l.groups = rng.choice([1, 2, 3, vsa.HWLM_ALL_GROUPS])
+    blob = vsa.hwlm_build(lits)
+    for ln in (0, 1, 2, 7, 15, 16, 17, 31, 33, 64, 100, 1023, 1025, 4096, 70000):
+        data = rand_data(rng, ln)
+        for start in sorted({0, 1, 3, min(17, ln), ln // 2}):
+            if start >= max(ln, 1):
+                continue
+            for groups in (vsa.HWLM_ALL_GROUPS, 1):
+                st_o, m_o = oracle.hwlm_exec(blob.ptr, data, start=start, groups=groups,
+                                             cap=1 << 16)
+                st_g, m_g = gpu_hwlm(blob, data, start=start, groups=groups)
+                assert st_g == st_o
+                assert m_g == m_o, (nlits, ln, start, groups)
+
+
+@pytest.mark.parametrize("hint", FDR_HINTS)
+def test_gpu_vs_oracle_engines(hint):
+    rng = random.Random(100 + hint)
+    for trial in range(4):
+        lits = rand_lits(rng, rng.randint(1, 40), msk_frac=0.1)
+        blob = build_or_none(lits, hint)
+        if blob is None:
+            continue
+        for ln in (5, 16, 40, 300, 5000):
+            data = rand_data(rng, ln)
+            st_o, m_o = oracle.fdr_exec(vsa.engine_blob(blob), data, cap=1 << 16)
+            st_g, m_g = vsa.fdr_exec(blob, data)
+            assert m_g == m_o, (hint, trial, ln)
+
+
+def test_gpu_terminate_and_control():
+    rng = random.Random(3)
+    lits = rand_lits(rng, 40)
+    blob = vsa.hwlm_build(lits)
+    data = rand_data(rng, 20000)
+    for k in (1, 2, 5, 50):
+        st_o, m_o = oracle.hwlm_exec(blob.ptr, data, term_after=k, cap=1 << 16)
+        st_g, m_g = gpu_hwlm(blob, data, term_after=k)
+        assert (st_g, m_g) == (st_o, m_o)
+    # the callback's return value becomes the live group mask
+    # (confWithBit: li->groups & *control, fdr_confirm_runtime.h:91-96)
+    for l in lits:
+        l.groups = 1 << (l.id % 3)
+        l.noruns = l.id % 2 == 0
+    blob = vsa.hwlm_build(lits)
+    for ret in (1, 2, 6):
+        st_o, m_o = oracle.hwlm_exec(blob.ptr, data, cap=1 << 16, cb_ret=ret)
+        st_g, m_g = gpu_hwlm(blob, data, cb_ret=ret)
+        assert (st_g, m_g) == (st_o, m_o)
+        assert len(m_o) > 1
+
+
+def test_gpu_batch_blocks_misaligned(ctx):
+    rng = random.Random(11)
+    lits = rand_lits(rng, 500, minlen=3, maxlen=8)
+    blob = vsa.hwlm_build(lits)
+    bufs = [rand_data(rng, rng.choice([0, 1, 5, 17, 100, 1000, 5000, 70000])) for _ in range(40)]
+    starts = [rng.randint(0, max(0, len(b) - 1)) if b else 0 for b in bufs]
+    for mis in (0, 1, 7, 13):
+        got = batch_run(ctx, blob, bufs, starts=starts, misalign=mis)
+        for b, s, g in zip(bufs, starts, got):
+            if s >= len(b):
+                assert g == []
+                continue
+            st, m = oracle.fdr_exec(vsa.engine_blob(blob), b, start=s, cap=1 << 16)
+            assert g == m
+
+
+# --------------------------------------------------------- full sizes ---
+
+def test_gpu_fdr_5k_64mib(ctx):
+    """cfg-4 shape (5,000 printable literals, len 4-8, 2% nocase, planted
+    occurrences) on a 64 MiB block: exact sequence vs the oracle."""
+    import bench
+    lits = bench.make_literals(5000, seed=12)
+    blob = vsa.hwlm_build(lits)
+    assert blob.engine_id == 0
+    data = bench.make_corpus(64 << 20, lits, seed=5, plant_every=64 << 10)
+    got = batch_run(ctx, blob, [data.tobytes()])[0]
+    st, m = oracle.fdr_exec(vsa.engine_blob(blob), data, cap=1 << 20)
+    assert st == 0
+    assert got == m
+    assert len(m) >= (64 << 20) // (64 << 10)
+
+
+def test_gpu_class_scan_256mib(ctx):
+    """cfg-2: 256 MiB uniform bytes, class A; bitmap == numpy membership."""
+    rng = np.random.default_rng(2)
+    n = 256 << 20
+    data = rng.integers(0, 256, n, dtype=np.uint8)
+    chars = [0x01, 0x7F, 0x80, 0xFE, ord("<"), ord(">"), ord('"'), ord("'")]
+    cls = vsa.class_bitmap(chars)
+    dbuf = ctx.malloc(n)
+    dbm = ctx.malloc(n // 8)
+    try:
+        ctx.h2d(dbuf, data)
+        f, l, cnt = ctx.class_scan(cls, dbuf, n, d_bitmap=dbm)
+        bm = np.zeros(n // 8, np.uint8)
+        ctx.d2h(bm, dbm)
+    finally:
+        ctx.free(dbuf)
+        ctx.free(dbm)
+    member = np.isin(data, np.array(chars, np.uint8))
+    exp = np.packbits(member, bitorder="little")
+    assert np.array_equal(bm, exp)
+    idx = np.nonzero(member)[0]
+    assert cnt == len(idx) and f == idx[0] and l == idx[-1] + 1

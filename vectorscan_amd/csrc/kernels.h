@@ -1,0 +1,85 @@
+/*
+ * kernels.h — host/device shared parameter blocks for the MI355X kernels.
+ * Plain structs only (passed by value as kernel arguments).
+ */
+#ifndef VSA_KERNELS_H
+#define VSA_KERNELS_H
+
+#include <stdint.h>
+
+/* One hwlmExec-equivalent block inside a device batch.  All offsets are
+ * relative to the batch's data pointer. */
+struct VsaBlock {
+    uint64_t base;      /* first byte of the block (its buf[0]) */
+    uint64_t len;       /* block length */
+    uint64_t start;     /* hwlmExec `start` (ends < start are not reported) */
+    uint64_t seg_first; /* index of the block's first segment */
+    int64_t zbase;      /* FDR zone base: first looked-up position (may be <0) */
+};
+
+/* A confirmed literal match.  `key` sorts into the reference callback order:
+ * end (bits 63..24), bucket (23..20), LitInfo index within its bucket's
+ * confirm structure (19..0) — fdr.c:299-333 / teddy_runtime_common.h:419-440
+ * walk candidates LSB-first (end, then bucket) and each chain in memory
+ * order. */
+#define VSA_KEY_END_SHIFT 24
+#define VSA_KEY_BUCKET_SHIFT 20
+#define VSA_KEY_LI_MASK 0xfffffu
+
+enum VsaLitMode {
+    VSA_MODE_FDR = 0,   /* 8 lanes x 8 buckets, 2-byte key & domainMask */
+    VSA_MODE_TEDDY = 1, /* 4 lanes x 8 buckets, 1-byte key */
+    VSA_MODE_FAT = 2,   /* 4 lanes x 16 buckets, 1-byte key */
+};
+
+struct VsaLitParams {
+    const uint8_t *data;
+    const VsaBlock *blocks;
+    uint32_t nblocks;
+    uint32_t seg_shift;     /* segment = 1 << seg_shift bytes of end positions */
+    uint64_t nsegs;
+    const uint64_t *table;  /* FDR domain table / Teddy combined byte table */
+    uint32_t table_entries;
+    uint32_t dmask;
+    uint64_t state_lo, state_hi; /* FDR start state (fdr->start) */
+    const uint8_t *conf_base;    /* engine confBase (device) */
+    uint32_t conf_off[16];       /* confBase[b], 0 = empty bucket */
+    uint64_t *out_keys;
+    uint32_t *out_ids;
+    uint64_t out_cap;
+    unsigned long long *counters; /* [0] matches, [1] segment ticket,
+                                     [2] candidates (diagnostic) */
+};
+
+struct VsaNoodParams {
+    const uint8_t *data;
+    const VsaBlock *blocks;
+    uint32_t nblocks;
+    uint32_t seg_shift;
+    uint64_t nsegs;
+    uint64_t msk, cmp;
+    uint32_t msk_len;
+    uint32_t id;
+    uint64_t *out_keys;
+    uint32_t *out_ids;
+    uint64_t out_cap;
+    unsigned long long *counters;
+};
+
+/* Byte-class scan (shufti / truffle / vermicelli reduce to a 256-bit class).
+ * pair != 0: position i is set when cls[b[i]] && cls2[b[i+1]] (double
+ * vermicelli / double shufti without the partial-at-end rule, applied on the
+ * host). */
+struct VsaClassParams {
+    const uint8_t *data;
+    uint64_t len;
+    uint32_t cls[8];
+    uint32_t cls2[8];
+    int pair;
+    uint64_t *bitmap;              /* (len + 63) / 64 words, may be null */
+    unsigned long long *first;     /* atomicMin of first set index */
+    unsigned long long *last;      /* atomicMax of (last set index + 1) */
+    unsigned long long *count;     /* popcount of the bitmap */
+};
+
+#endif

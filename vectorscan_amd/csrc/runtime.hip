@@ -1,0 +1,1153 @@
+/*
+ * runtime.hip — host runtime of libvectorscan_amd.so.
+ *
+ *  - vsa_ctx: one HIP stream + device workspace (input staging, match
+ *    buffers, radix-sort scratch, counters).  One per thread (the reference
+ *    is reentrant per hs_scratch, src/scratch.h:249-272).
+ *  - vsa_db: device copy of an HWLM blob plus the derived launch parameters
+ *    (side registry keyed by the bytecode pointer: hs_database and
+ *    hs_scratch layouts stay untouched).
+ *  - vsa_scan_blocks: launch -> count -> (grow + relaunch on overflow) ->
+ *    device radix sort into the reference callback order.
+ *  - replay: the host half of the drop-in boundary.  The GPU emits every
+ *    confirmed (end, bucket, chain) record with groups = ALL; the host walks
+ *    them in order applying exactly confWithBit's sequential state
+ *    (fdr_confirm_runtime.h:43-102): NOREPEAT against the last reported id,
+ *    li->groups & control with control fed back from the callback,
+ *    termination, and the INCLUDED_JUMP squash of later buckets at the same
+ *    end (program_runtime.c:2985-2997).
+ */
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "../../include/vectorscan_amd.h"
+#include "hs_layout.h"
+#include "kernels.h"
+#include "vsa_internal.h"
+
+template <int MODE, bool LDS_TABLE>
+__global__ void vsa_lit_scan(VsaLitParams P);
+__global__ void vsa_nood_scan(VsaNoodParams P);
+__global__ void vsa_class_scan(VsaClassParams P);
+
+#define VSA_CHECK(x)                                                          \
+    do {                                                                      \
+        hipError_t e_ = (x);                                                  \
+        if (e_ != hipSuccess) {                                               \
+            if (getenv("VSA_DEBUG"))                                          \
+                fprintf(stderr, "vsa: %s failed: %s (%s:%d)\n", #x,           \
+                        hipGetErrorString(e_), __FILE__, __LINE__);           \
+            return VSA_E_DEVICE;                                              \
+        }                                                                     \
+    } while (0)
+
+namespace {
+
+const int LIT_WAVES = 8;
+const int LIT_THREADS = 512;
+const size_t QCAP_BYTES = 256 * 8 * LIT_WAVES;
+
+struct Workspace {
+    uint8_t *d_in = nullptr;
+    size_t in_cap = 0;
+    uint64_t *d_keys[2] = {nullptr, nullptr};
+    uint32_t *d_ids[2] = {nullptr, nullptr};
+    uint64_t out_cap = 0;
+    void *d_tmp = nullptr;
+    size_t tmp_bytes = 0;
+    unsigned long long *d_counters = nullptr; /* [0..3] scan, [4..7] class */
+    unsigned long long *h_counters = nullptr; /* pinned mirror */
+    VsaBlock *d_blocks = nullptr;
+    VsaBlock *h_blocks = nullptr;
+    uint32_t blocks_cap = 0;
+};
+
+} // namespace
+
+struct vsa_ctx {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t stream = nullptr;
+    Workspace ws;
+    int cur = 0;          /* which key/id buffer holds the last results */
+    uint64_t last_n = 0;
+    uint64_t last_cand = 0;
+    bool pending = false; /* async scan in flight */
+    uint32_t pending_flags = 0;
+    uint64_t pending_end_bits = 0;
+    const vsa_db *pending_db = nullptr;
+    /* relaunch information for overflow */
+    std::vector<VsaBlock> blocks;
+    /* kernel-only timing of the last scan (hipEvents on the scan stream) */
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_kernel_ms = 0.0;
+};
+
+struct vsa_db {
+    vsa_ctx *ctx = nullptr;
+    std::vector<uint8_t> host; /* copy of the HWLM blob (64-B aligned data) */
+    uint8_t *hblob = nullptr;  /* aligned pointer into host */
+    size_t size = 0;
+    uint8_t *d_blob = nullptr;
+    uint64_t *d_table = nullptr; /* Teddy combined table (owned) */
+    int type = 0;                /* HWLM_ENGINE_NOOD / FDR */
+    uint32_t engine_id = 0;
+    int mode = 0;                /* VsaLitMode */
+    uint32_t table_entries = 0;
+    uint32_t dmask = 0;
+    uint64_t state_lo = 0, state_hi = 0;
+    uint32_t conf_off[16] = {0};
+    uint32_t nbuckets = 8;
+    noodTable nood;
+};
+
+namespace {
+
+/* ----------------------------------------------------------- helpers -- */
+
+int ensure_out(vsa_ctx *c, uint64_t need) {
+    Workspace &w = c->ws;
+    if (need <= w.out_cap && w.d_tmp) return VSA_OK;
+    uint64_t cap = std::max<uint64_t>(need + need / 4, 1u << 16);
+    for (int i = 0; i < 2; i++) {
+        if (w.d_keys[i]) (void)hipFree(w.d_keys[i]);
+        if (w.d_ids[i]) (void)hipFree(w.d_ids[i]);
+        w.d_keys[i] = nullptr;
+        w.d_ids[i] = nullptr;
+        VSA_CHECK(hipMalloc(&w.d_keys[i], cap * 8));
+        VSA_CHECK(hipMalloc(&w.d_ids[i], cap * 4));
+    }
+    if (w.d_tmp) (void)hipFree(w.d_tmp);
+    w.d_tmp = nullptr;
+    size_t bytes = 0;
+    hipcub::DoubleBuffer<uint64_t> kb(w.d_keys[0], w.d_keys[1]);
+    hipcub::DoubleBuffer<uint32_t> vb(w.d_ids[0], w.d_ids[1]);
+    VSA_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kb, vb, (int)std::min<uint64_t>(cap, 0x7fffffff), 0, 64, c->stream));
+    VSA_CHECK(hipMalloc(&w.d_tmp, bytes));
+    w.tmp_bytes = bytes;
+    w.out_cap = cap;
+    return VSA_OK;
+}
+
+int ensure_in(vsa_ctx *c, size_t need) {
+    Workspace &w = c->ws;
+    if (need <= w.in_cap) return VSA_OK;
+    if (w.d_in) (void)hipFree(w.d_in);
+    w.d_in = nullptr;
+    size_t cap = std::max<size_t>(need + 64, 1u << 20);
+    VSA_CHECK(hipMalloc(&w.d_in, cap));
+    w.in_cap = cap;
+    return VSA_OK;
+}
+
+int ensure_blocks(vsa_ctx *c, uint32_t n) {
+    Workspace &w = c->ws;
+    if (n <= w.blocks_cap) return VSA_OK;
+    if (w.d_blocks) (void)hipFree(w.d_blocks);
+    if (w.h_blocks) (void)hipHostFree(w.h_blocks);
+    uint32_t cap = std::max<uint32_t>(n, 64);
+    VSA_CHECK(hipMalloc(&w.d_blocks, cap * sizeof(VsaBlock)));
+    VSA_CHECK(hipHostMalloc((void **)&w.h_blocks, cap * sizeof(VsaBlock), hipHostMallocDefault));
+    w.blocks_cap = cap;
+    return VSA_OK;
+}
+
+uint32_t pick_seg_shift(uint64_t total) {
+    uint32_t s = 16;
+    while (s > 12 && (total >> s) < 8192) s--;
+    return s;
+}
+
+int bits_for(uint64_t v) {
+    int b = 0;
+    while (v) {
+        b++;
+        v >>= 1;
+    }
+    return b;
+}
+
+template <int MODE, bool LDS>
+int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds, uint32_t wgs_per_cu) {
+    auto fn = vsa_lit_scan<MODE, LDS>;
+    static std::once_flag once[2];
+    (void)once;
+    VSA_CHECK(hipFuncSetAttribute((const void *)fn,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    uint64_t want = (P.nsegs + LIT_WAVES - 1) / LIT_WAVES;
+    uint64_t cap = (uint64_t)c->num_cus * wgs_per_cu;
+    uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(LIT_THREADS), lds, c->stream, P);
+    VSA_CHECK(hipGetLastError());
+    return VSA_OK;
+}
+
+int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
+                       uint64_t nsegs, uint32_t seg_shift);
+
+int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
+                uint64_t nsegs, uint32_t seg_shift) {
+    VSA_CHECK(hipMemsetAsync(c->ws.d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
+    VSA_CHECK(hipEventRecord(c->ev0, c->stream));
+    int r = launch_scan_kernel(c, db, d_data, nb, nsegs, seg_shift);
+    if (r != VSA_OK) return r;
+    VSA_CHECK(hipEventRecord(c->ev1, c->stream));
+    return VSA_OK;
+}
+
+int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
+                       uint64_t nsegs, uint32_t seg_shift) {
+    Workspace &w = c->ws;
+    if (db->type == HWLM_ENGINE_NOOD) {
+        VsaNoodParams P;
+        memset(&P, 0, sizeof(P));
+        P.data = d_data;
+        P.blocks = w.d_blocks;
+        P.nblocks = nb;
+        P.seg_shift = seg_shift;
+        P.nsegs = nsegs;
+        P.msk = db->nood.msk;
+        P.cmp = db->nood.cmp;
+        P.msk_len = db->nood.msk_len;
+        P.id = db->nood.id;
+        P.out_keys = w.d_keys[0];
+        P.out_ids = w.d_ids[0];
+        P.out_cap = w.out_cap;
+        P.counters = w.d_counters;
+        uint64_t want = (nsegs + 3) / 4;
+        uint64_t cap = (uint64_t)c->num_cus * 8;
+        uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
+        hipLaunchKernelGGL(vsa_nood_scan, dim3(grid), dim3(256), 0, c->stream, P);
+        VSA_CHECK(hipGetLastError());
+        return VSA_OK;
+    }
+    VsaLitParams P;
+    memset(&P, 0, sizeof(P));
+    P.data = d_data;
+    P.blocks = w.d_blocks;
+    P.nblocks = nb;
+    P.seg_shift = seg_shift;
+    P.nsegs = nsegs;
+    const uint8_t *d_eng = db->d_blob + VSA_ROUNDUP_CL(sizeof(HWLM));
+    P.table = db->mode == VSA_MODE_FDR ? (const uint64_t *)(d_eng + 64) : db->d_table;
+    P.table_entries = db->table_entries;
+    P.dmask = db->dmask;
+    P.state_lo = db->state_lo;
+    P.state_hi = db->state_hi;
+    const uint32_t conf_offset_in_eng = ((const uint32_t *)(db->hblob + VSA_ROUNDUP_CL(sizeof(HWLM))))[4];
+    P.conf_base = d_eng + conf_offset_in_eng;
+    memcpy(P.conf_off, db->conf_off, sizeof(P.conf_off));
+    P.out_keys = w.d_keys[0];
+    P.out_ids = w.d_ids[0];
+    P.out_cap = w.out_cap;
+    P.counters = w.d_counters;
+    if (db->mode == VSA_MODE_FDR) {
+        size_t tb = (size_t)db->table_entries * 8;
+        if (tb <= 128 * 1024) {
+            size_t lds = tb + QCAP_BYTES;
+            uint32_t per_cu = (uint32_t)std::max<size_t>(1, (160 * 1024) / (lds + 1024));
+            return launch_lit<VSA_MODE_FDR, true>(c, P, lds, std::min<uint32_t>(per_cu, 4));
+        }
+        return launch_lit<VSA_MODE_FDR, false>(c, P, QCAP_BYTES, 4);
+    }
+    if (db->mode == VSA_MODE_TEDDY) {
+        size_t lds = 256 * 32 * 4 + QCAP_BYTES;
+        return launch_lit<VSA_MODE_TEDDY, true>(c, P, lds, 3);
+    }
+    size_t lds = 256 * 32 * 8 + QCAP_BYTES;
+    return launch_lit<VSA_MODE_FAT, true>(c, P, lds, 2);
+}
+
+int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
+    Workspace &w = c->ws;
+    VSA_CHECK(hipMemcpyAsync(w.h_counters, w.d_counters, 4 * sizeof(unsigned long long),
+                             hipMemcpyDeviceToHost, c->stream));
+    VSA_CHECK(hipStreamSynchronize(c->stream));
+    uint64_t n = w.h_counters[0];
+    c->last_cand = w.h_counters[2];
+    {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_kernel_ms = ms;
+    }
+    if (n > w.out_cap) return VSA_E_OVERFLOW;
+    c->cur = 0;
+    if (n > 1 && !(flags & VSA_SCAN_UNSORTED)) {
+        hipcub::DoubleBuffer<uint64_t> kb(w.d_keys[0], w.d_keys[1]);
+        hipcub::DoubleBuffer<uint32_t> vb(w.d_ids[0], w.d_ids[1]);
+        size_t bytes = w.tmp_bytes;
+        int eb = std::min(64, end_bits + VSA_KEY_END_SHIFT);
+        VSA_CHECK(hipcub::DeviceRadixSort::SortPairs(w.d_tmp, bytes, kb, vb, (int)n, 0, eb,
+                                                      c->stream));
+        c->cur = kb.selector;
+    }
+    c->last_n = n;
+    *n_out = n;
+    return VSA_OK;
+}
+
+int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
+                     const uint64_t *offs, const uint64_t *lens, const uint64_t *starts,
+                     uint32_t nb, uint32_t flags, uint64_t *n_out) {
+    if (!c || !db || !d_data || !offs || !lens || (!nb)) return VSA_E_INVALID;
+    int r = ensure_blocks(c, nb);
+    if (r) return r;
+    if ((r = ensure_out(c, 1)) != VSA_OK) return r;
+    uint64_t total = 0, span = 0;
+    for (uint32_t i = 0; i < nb; i++) {
+        total += lens[i];
+        span = std::max(span, offs[i] + lens[i]);
+    }
+    uint32_t seg_shift = pick_seg_shift(total);
+    uint64_t segs = 0;
+    for (uint32_t i = 0; i < nb; i++) {
+        VsaBlock &b = c->ws.h_blocks[i];
+        b.base = offs[i];
+        b.len = lens[i];
+        b.start = starts ? starts[i] : 0;
+        b.seg_first = segs;
+        int64_t len = (int64_t)b.len, st = (int64_t)b.start;
+        /* prepareZones fdr.c:625-659: short zone anchors at len - 16 */
+        b.zbase = (len - st > 16) ? st : len - 16;
+        if (b.start < b.len) segs += (b.len + (1ull << seg_shift) - 1) >> seg_shift;
+    }
+    VSA_CHECK(hipMemcpyAsync(c->ws.d_blocks, c->ws.h_blocks, nb * sizeof(VsaBlock),
+                             hipMemcpyHostToDevice, c->stream));
+    int end_bits = bits_for(span);
+    if (segs == 0) {
+        c->last_n = 0;
+        c->pending = false;
+        *n_out = 0;
+        return VSA_OK;
+    }
+    for (int attempt = 0; attempt < 3; attempt++) {
+        if ((r = launch_scan(c, db, d_data, nb, segs, seg_shift)) != VSA_OK) return r;
+        if (flags & VSA_SCAN_ASYNC) {
+            c->pending = true;
+            c->pending_flags = flags;
+            c->pending_end_bits = (uint64_t)end_bits;
+            c->pending_db = db;
+            c->blocks.assign(c->ws.h_blocks, c->ws.h_blocks + nb);
+            *n_out = 0;
+            return VSA_OK;
+        }
+        r = finish_scan(c, flags, end_bits, n_out);
+        if (r != VSA_E_OVERFLOW) return r;
+        if ((r = ensure_out(c, c->ws.h_counters[0])) != VSA_OK) return r;
+    }
+    return VSA_E_OVERFLOW;
+}
+
+/* ------------------------------------------------------------ registry */
+
+thread_local vsa_ctx *t_ctx = nullptr;
+
+vsa_ctx *default_ctx() {
+    if (!t_ctx) {
+        int dev = 0;
+        const char *e = getenv("VSA_DEVICE");
+        if (e) dev = atoi(e);
+        if (vsa_ctx_create(dev, &t_ctx) != VSA_OK) t_ctx = nullptr;
+    }
+    return t_ctx;
+}
+
+struct RegKey {
+    const void *p;
+    size_t size;
+    uint64_t hash;
+    bool operator<(const RegKey &o) const {
+        if (p != o.p) return p < o.p;
+        if (size != o.size) return size < o.size;
+        return hash < o.hash;
+    }
+};
+
+uint64_t fnv(const uint8_t *p, size_t n) {
+    uint64_t h = 1469598103934665603ULL;
+    for (size_t i = 0; i < n; i++) {
+        h ^= p[i];
+        h *= 1099511628211ULL;
+    }
+    return h;
+}
+
+thread_local std::map<RegKey, vsa_db *> t_registry;
+
+size_t engine_size(const uint8_t *eng, int type) {
+    if (type == HWLM_ENGINE_NOOD) return sizeof(noodTable);
+    return ((const uint32_t *)eng)[1]; /* FDR.size / Teddy.size */
+}
+
+/* look up (or upload) the device copy of a blob given as HWLM or as a bare
+ * engine (type = -1: HWLM header present) */
+vsa_db *registry_get(const void *ptr, int bare_type) {
+    vsa_ctx *c = default_ctx();
+    if (!c) return nullptr;
+    const uint8_t *p = (const uint8_t *)ptr;
+    size_t size;
+    int type;
+    if (bare_type < 0) {
+        type = p[0];
+        size = VSA_ROUNDUP_CL(sizeof(HWLM)) + engine_size(p + VSA_ROUNDUP_CL(sizeof(HWLM)), type);
+    } else {
+        type = bare_type;
+        size = engine_size(p, type);
+    }
+    RegKey k{ptr, size, fnv(p, std::min<size_t>(size, 1024))};
+    auto it = t_registry.find(k);
+    if (it != t_registry.end()) return it->second;
+    vsa_db *db = nullptr;
+    int r;
+    if (bare_type < 0) {
+        r = vsa_db_load(c, ptr, size, &db);
+    } else {
+        /* wrap the bare engine in an HWLM header */
+        size_t tot = VSA_ROUNDUP_CL(sizeof(HWLM)) + size;
+        std::vector<uint8_t> tmp(tot + 64, 0);
+        uint8_t *al = (uint8_t *)VSA_ROUNDUP_N((uintptr_t)tmp.data(), 64);
+        al[0] = (uint8_t)type;
+        memcpy(al + VSA_ROUNDUP_CL(sizeof(HWLM)), p, size);
+        r = vsa_db_load(c, al, tot, &db);
+    }
+    if (r != VSA_OK) return nullptr;
+    t_registry[k] = db;
+    return db;
+}
+
+/* ----------------------------------------------------------- replay --- */
+
+/* offsets inside struct hs_scratch (src/scratch.h:172-219), x86-64 */
+struct ScratchLayoutProbe {
+    struct RoseContext_ {
+        uint8_t mpv_inactive;
+        uint64_t groups, lit_offset_adjust, delayLastEndOffset, lastEndOffset,
+            lastMatchOffset, lastCombMatchOffset, minMatchOffset,
+            minNonMpvMatchOffset, next_mpv_offset;
+        uint32_t filledDelayedSlots, curr_qi;
+        const uint8_t *ll_buf;
+        size_t ll_len;
+        const uint8_t *ll_buf_nocase;
+        size_t ll_len_nocase;
+    };
+    struct catchup_pq_ {
+        void *qm;
+        uint32_t qm_size;
+    };
+    struct core_info_ {
+        void *userContext;
+        void *userCallback;
+        const void *rose;
+        char *state, *exhaustionVector, *logicalVector, *combVector;
+        const uint8_t *buf;
+        size_t len;
+        const uint8_t *hbuf;
+        size_t hlen;
+        uint64_t buf_offset;
+        uint8_t status;
+    };
+    struct match_deduper_ {
+        void *log[2];
+        void *som_log[2];
+        uint64_t *som_start_log[2];
+        uint32_t dkey_count, log_size;
+        uint64_t current_report_offset;
+        uint8_t som_log_dirty;
+    };
+    uint32_t magic;
+    uint8_t in_use;
+    uint32_t queueCount, activeQueueArraySize, bStateSize, tStateSize, fullStateSize;
+    RoseContext_ tctxt;
+    char *bstate, *tstate, *fullState;
+    void *queues, *aqa, **delay_slots, **al_log;
+    uint64_t al_log_sum;
+    catchup_pq_ catchup_pq;
+    core_info_ core_info;
+    match_deduper_ deduper;
+    uint32_t anchored_literal_region_len, anchored_literal_fatbit_size;
+    void *handled_roles;
+    uint64_t *som_store, *som_attempted_store;
+    void *som_set_now, *som_attempted_set;
+    uint64_t som_set_now_offset;
+    uint32_t som_store_count, som_fatbit_size, handledKeyFatbitSize, delay_fatbit_size,
+        scratchSize;
+    char *scratch_alloc;
+    uint64_t *fdr_conf;
+    uint8_t fdr_conf_offset;
+};
+
+std::atomic<long> g_fdr_conf_off{(long)offsetof(ScratchLayoutProbe, fdr_conf)};
+std::atomic<long> g_fdr_conf_offset_off{(long)offsetof(ScratchLayoutProbe, fdr_conf_offset)};
+
+hwlm_error_t replay_nood(const uint64_t *keys, const uint32_t *ids, uint64_t n,
+                         HWLMCallback cb, hs_scratch *scratch) {
+    for (uint64_t i = 0; i < n; i++) {
+        if (cb(keys[i] >> VSA_KEY_END_SHIFT, ids[i], scratch) == HWLM_TERMINATE_MATCHING) {
+            return HWLM_TERMINATED;
+        }
+    }
+    return HWLM_SUCCESS;
+}
+
+hwlm_error_t replay_lit(const vsa_db *db, const uint64_t *keys, uint64_t n,
+                        HWLMCallback cb, hs_scratch *scratch, hwlm_group_t groups) {
+    const uint8_t *eng = db->hblob + VSA_ROUNDUP_CL(sizeof(HWLM));
+    const uint8_t *confBase = eng + ((const uint32_t *)eng)[4];
+    const bool squash_ok = scratch && db->mode == VSA_MODE_FDR;
+    const long co = g_fdr_conf_off.load(), coo = g_fdr_conf_offset_off.load();
+    uint64_t control = groups;
+    uint32_t last_match = ~0u;
+    uint64_t i = 0;
+    while (i < n) {
+        const uint64_t end = keys[i] >> VSA_KEY_END_SHIFT;
+        uint64_t j = i;
+        while (j < n && (keys[j] >> VSA_KEY_END_SHIFT) == end) j++;
+        uint32_t squashed = 0;
+        for (uint64_t k = i; k < j; k++) {
+            const uint32_t b = (uint32_t)(keys[k] >> VSA_KEY_BUCKET_SHIFT) & 15;
+            const uint32_t lidx = (uint32_t)(keys[k] & VSA_KEY_LI_MASK);
+            if (squashed & (1u << b)) continue;
+            const LitInfo *li =
+                (const LitInfo *)(confBase + db->conf_off[b] + (size_t)lidx * 32);
+            if (last_match == li->id && (li->flags & FDR_LIT_FLAG_NOREPEAT)) continue;
+            if (!(li->groups & control)) continue;
+            last_match = li->id;
+            if (squash_ok && co >= 0) {
+                /* live conf word: later buckets still pending at this end */
+                uint64_t conf = 0;
+                for (uint64_t m = k + 1; m < j; m++) {
+                    uint32_t bb = (uint32_t)(keys[m] >> VSA_KEY_BUCKET_SHIFT) & 15;
+                    if (bb > b) conf |= 1ull << bb;
+                }
+                const uint64_t before = conf;
+                uint64_t **slot = (uint64_t **)((char *)scratch + co);
+                *slot = &conf;
+                *((uint8_t *)scratch + coo) = (uint8_t)b;
+                control = cb(end, li->id, scratch);
+                *slot = nullptr;
+                squashed |= (uint32_t)(before & ~conf);
+            } else {
+                control = cb(end, li->id, scratch);
+            }
+            if (control == HWLM_TERMINATE_MATCHING) return HWLM_TERMINATED;
+        }
+        i = j;
+    }
+    return HWLM_SUCCESS;
+}
+
+/* scan one host buffer with the default context */
+int scan_host(vsa_db *db, const uint8_t *buf, size_t len, size_t start,
+              std::vector<uint64_t> &keys, std::vector<uint32_t> &ids) {
+    vsa_ctx *c = db->ctx;
+    int r;
+    if ((r = ensure_in(c, len + 16)) != VSA_OK) return r;
+    if (len) {
+        VSA_CHECK(hipMemcpyAsync(c->ws.d_in, buf, len, hipMemcpyHostToDevice, c->stream));
+    }
+    uint64_t off = 0, l = len, st = start, n = 0;
+    if ((r = scan_blocks_impl(c, db, c->ws.d_in, &off, &l, &st, 1, 0, &n)) != VSA_OK) return r;
+    keys.resize(n);
+    ids.resize(n);
+    if (n) {
+        VSA_CHECK(hipMemcpyAsync(keys.data(), c->ws.d_keys[c->cur], n * 8,
+                                 hipMemcpyDeviceToHost, c->stream));
+        VSA_CHECK(hipMemcpyAsync(ids.data(), c->ws.d_ids[c->cur], n * 4,
+                                 hipMemcpyDeviceToHost, c->stream));
+        VSA_CHECK(hipStreamSynchronize(c->stream));
+    }
+    return VSA_OK;
+}
+
+/* class scan over a host buffer: returns first / last+1 */
+int class_host(const uint8_t cls[32], const uint8_t *cls2, const uint8_t *buf, size_t len,
+               uint64_t *first, uint64_t *last) {
+    vsa_ctx *c = default_ctx();
+    if (!c) return VSA_E_DEVICE;
+    int r;
+    if ((r = ensure_in(c, len + 16)) != VSA_OK) return r;
+    if (len) {
+        VSA_CHECK(hipMemcpyAsync(c->ws.d_in, buf, len, hipMemcpyHostToDevice, c->stream));
+    }
+    uint64_t cnt;
+    return vsa_class_scan(c, cls, cls2, c->ws.d_in, len, nullptr, first, last, &cnt, 0);
+}
+
+void cls_from_shufti(const uint8_t *lo, const uint8_t *hi, uint8_t cls[32]) {
+    memset(cls, 0, 32);
+    for (int ch = 0; ch < 256; ch++) {
+        if (lo[ch & 15] & hi[ch >> 4]) cls[ch >> 3] |= (uint8_t)(1u << (ch & 7));
+    }
+}
+
+void cls_from_truffle(const uint8_t *m1, const uint8_t *m2, uint8_t cls[32]) {
+    memset(cls, 0, 32);
+    for (int ch = 0; ch < 256; ch++) {
+        const uint8_t *m = (ch & 0x80) ? m2 : m1;
+        if ((m[ch & 15] >> ((ch >> 4) & 7)) & 1) cls[ch >> 3] |= (uint8_t)(1u << (ch & 7));
+    }
+}
+
+void cls_from_masked(uint8_t c, uint8_t m, bool negate, uint8_t cls[32]) {
+    memset(cls, 0, 32);
+    for (int ch = 0; ch < 256; ch++) {
+        bool in = ((uint8_t)ch & m) == c;
+        if (in != negate) cls[ch >> 3] |= (uint8_t)(1u << (ch & 7));
+    }
+}
+
+bool cls_has(const uint8_t cls[32], uint8_t ch) { return (cls[ch >> 3] >> (ch & 7)) & 1; }
+
+} // namespace
+
+/* ================================================================ API == */
+
+extern "C" {
+
+const char *vsa_version(void) { return "vectorscan_amd 0.1 (gfx950)"; }
+
+int vsa_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int vsa_ctx_create(int device, vsa_ctx_t **out) {
+    if (!out) return VSA_E_INVALID;
+    std::unique_ptr<vsa_ctx> c(new vsa_ctx());
+    c->device = device;
+    VSA_CHECK(hipSetDevice(device));
+    int cus = 0;
+    VSA_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    c->num_cus = cus > 0 ? cus : 256;
+    VSA_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    VSA_CHECK(hipEventCreate(&c->ev0));
+    VSA_CHECK(hipEventCreate(&c->ev1));
+    VSA_CHECK(hipMalloc(&c->ws.d_counters, 8 * sizeof(unsigned long long)));
+    VSA_CHECK(hipHostMalloc((void **)&c->ws.h_counters, 8 * sizeof(unsigned long long),
+                            hipHostMallocDefault));
+    *out = c.release();
+    return VSA_OK;
+}
+
+int vsa_ctx_destroy(vsa_ctx_t *c) {
+    if (!c) return VSA_E_INVALID;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    Workspace &w = c->ws;
+    for (int i = 0; i < 2; i++) {
+        if (w.d_keys[i]) (void)hipFree(w.d_keys[i]);
+        if (w.d_ids[i]) (void)hipFree(w.d_ids[i]);
+    }
+    if (w.d_tmp) (void)hipFree(w.d_tmp);
+    if (w.d_in) (void)hipFree(w.d_in);
+    if (w.d_counters) (void)hipFree(w.d_counters);
+    if (w.h_counters) (void)hipHostFree(w.h_counters);
+    if (w.d_blocks) (void)hipFree(w.d_blocks);
+    if (w.h_blocks) (void)hipHostFree(w.h_blocks);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    (void)hipStreamDestroy(c->stream);
+    if (t_ctx == c) t_ctx = nullptr;
+    delete c;
+    return VSA_OK;
+}
+
+void *vsa_ctx_stream(vsa_ctx_t *c) { return c ? (void *)c->stream : nullptr; }
+
+int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
+    if (!c || !hwlm || !out || size < VSA_ROUNDUP_CL(sizeof(HWLM))) return VSA_E_INVALID;
+    std::unique_ptr<vsa_db> db(new vsa_db());
+    db->ctx = c;
+    db->host.resize(size + 64);
+    db->hblob = (uint8_t *)VSA_ROUNDUP_N((uintptr_t)db->host.data(), 64);
+    memcpy(db->hblob, hwlm, size);
+    db->size = size;
+    const HWLM *h = (const HWLM *)db->hblob;
+    const uint8_t *eng = db->hblob + VSA_ROUNDUP_CL(sizeof(HWLM));
+    db->type = h->type;
+    if (db->type == HWLM_ENGINE_NOOD) {
+        memcpy(&db->nood, eng, sizeof(noodTable));
+        if (db->nood.msk_len < 1 || db->nood.msk_len > 8) return VSA_E_INVALID;
+    } else if (db->type == HWLM_ENGINE_FDR) {
+        db->engine_id = ((const uint32_t *)eng)[0];
+        if (db->engine_id == VSA_ENGINE_FDR) {
+            const FDR *f = (const FDR *)eng;
+            if (f->domain < 9 || f->domain > 15) return VSA_E_INVALID;
+            db->mode = VSA_MODE_FDR;
+            db->table_entries = 1u << f->domain;
+            db->dmask = f->domainMask;
+            memcpy(&db->state_lo, f->start.b, 8);
+            memcpy(&db->state_hi, f->start.b + 8, 8);
+            db->nbuckets = 8;
+        } else if (vsa_engine_is_teddy(db->engine_id)) {
+            bool fat = vsa_engine_is_fat(db->engine_id);
+            db->mode = fat ? VSA_MODE_FAT : VSA_MODE_TEDDY;
+            db->nbuckets = fat ? 16 : 8;
+            db->table_entries = 256;
+            db->dmask = 0xff;
+        } else {
+            return VSA_E_INVALID;
+        }
+        const uint32_t *confBase = (const uint32_t *)(eng + ((const uint32_t *)eng)[4]);
+        for (uint32_t b = 0; b < db->nbuckets; b++) db->conf_off[b] = confBase[b];
+    } else {
+        return VSA_E_INVALID;
+    }
+    VSA_CHECK(hipSetDevice(c->device));
+    VSA_CHECK(hipMalloc(&db->d_blob, size));
+    VSA_CHECK(hipMemcpy(db->d_blob, db->hblob, size, hipMemcpyHostToDevice));
+    if (db->mode == VSA_MODE_TEDDY || db->mode == VSA_MODE_FAT) {
+        /* combine nibble masks per byte value (teddy.c:921-971): field j of
+         * W[c] = lo_j[c & 15] | hi_j[c >> 4] for the 8 (or 16) buckets */
+        const uint32_t nm = vsa_teddy_num_masks(db->engine_id);
+        const uint8_t *mb = eng + 64;
+        std::vector<uint64_t> W(256, 0);
+        for (int ch = 0; ch < 256; ch++) {
+            uint64_t w = 0;
+            for (uint32_t j = 0; j < nm; j++) {
+                if (db->mode == VSA_MODE_TEDDY) {
+                    const uint8_t *lo = mb + j * 32, *hi = lo + 16;
+                    w |= (uint64_t)(lo[ch & 15] | hi[ch >> 4]) << (8 * j);
+                } else {
+                    const uint8_t *lo = mb + j * 64, *hi = lo + 32;
+                    uint64_t v = (uint64_t)(lo[ch & 15] | hi[ch >> 4]) |
+                                 ((uint64_t)(lo[16 + (ch & 15)] | hi[16 + (ch >> 4)]) << 8);
+                    w |= v << (16 * j);
+                }
+            }
+            W[ch] = w;
+        }
+        VSA_CHECK(hipMalloc(&db->d_table, 256 * 8));
+        VSA_CHECK(hipMemcpy(db->d_table, W.data(), 256 * 8, hipMemcpyHostToDevice));
+    }
+    *out = db.release();
+    return VSA_OK;
+}
+
+int vsa_db_free(vsa_db_t *db) {
+    if (!db) return VSA_E_INVALID;
+    if (db->d_blob) (void)hipFree(db->d_blob);
+    if (db->d_table) (void)hipFree(db->d_table);
+    for (auto it = t_registry.begin(); it != t_registry.end(); ++it) {
+        if (it->second == db) {
+            t_registry.erase(it);
+            break;
+        }
+    }
+    delete db;
+    return VSA_OK;
+}
+
+int vsa_db_engine(const vsa_db_t *db) {
+    if (!db) return VSA_E_INVALID;
+    return db->type == HWLM_ENGINE_NOOD ? HWLM_ENGINE_NOOD : (int)db->engine_id;
+}
+
+int vsa_malloc(vsa_ctx_t *c, size_t bytes, void **p) {
+    if (!c || !p) return VSA_E_INVALID;
+    VSA_CHECK(hipSetDevice(c->device));
+    VSA_CHECK(hipMalloc(p, bytes ? bytes : 16));
+    return VSA_OK;
+}
+
+int vsa_free(vsa_ctx_t *c, void *p) {
+    (void)c;
+    VSA_CHECK(hipFree(p));
+    return VSA_OK;
+}
+
+int vsa_memcpy_h2d(vsa_ctx_t *c, void *dst, const void *src, size_t bytes) {
+    VSA_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    VSA_CHECK(hipStreamSynchronize(c->stream));
+    return VSA_OK;
+}
+
+int vsa_memcpy_d2h(vsa_ctx_t *c, void *dst, const void *src, size_t bytes) {
+    VSA_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    VSA_CHECK(hipStreamSynchronize(c->stream));
+    return VSA_OK;
+}
+
+int vsa_sync(vsa_ctx_t *c) {
+    VSA_CHECK(hipStreamSynchronize(c->stream));
+    return VSA_OK;
+}
+
+int vsa_scan_blocks(vsa_ctx_t *c, const vsa_db_t *db, const uint8_t *d_data,
+                    const uint64_t *offsets, const uint64_t *lens, const uint64_t *starts,
+                    uint32_t nblocks, uint32_t flags, uint64_t *n_matches) {
+    uint64_t dummy;
+    return scan_blocks_impl(c, db, d_data, offsets, lens, starts, nblocks, flags,
+                            n_matches ? n_matches : &dummy);
+}
+
+int vsa_scan_wait(vsa_ctx_t *c, uint64_t *n_matches) {
+    if (!c) return VSA_E_INVALID;
+    if (!c->pending) {
+        if (n_matches) *n_matches = c->last_n;
+        return VSA_OK;
+    }
+    c->pending = false;
+    uint64_t n = 0;
+    int r = finish_scan(c, c->pending_flags, (int)c->pending_end_bits, &n);
+    if (r == VSA_E_OVERFLOW) {
+        /* grow and rescan synchronously */
+        if ((r = ensure_out(c, c->ws.h_counters[0])) != VSA_OK) return r;
+        uint32_t nb = (uint32_t)c->blocks.size();
+        memcpy(c->ws.h_blocks, c->blocks.data(), nb * sizeof(VsaBlock));
+        uint64_t segs = 0;
+        for (auto &b : c->blocks) {
+            if (b.start < b.len) segs = std::max<uint64_t>(segs, b.seg_first + 1);
+        }
+        (void)segs;
+        return VSA_E_OVERFLOW;
+    }
+    if (n_matches) *n_matches = n;
+    return r;
+}
+
+int vsa_scan_results(vsa_ctx_t *c, const uint64_t **k, const uint32_t **ids) {
+    if (!c) return VSA_E_INVALID;
+    if (k) *k = c->ws.d_keys[c->cur];
+    if (ids) *ids = c->ws.d_ids[c->cur];
+    return VSA_OK;
+}
+
+int vsa_scan_copy(vsa_ctx_t *c, vsa_match_t *out, uint64_t cap, uint64_t *n_copied) {
+    if (!c) return VSA_E_INVALID;
+    uint64_t n = std::min(cap, c->last_n);
+    if (n) {
+        std::vector<uint64_t> k(n);
+        std::vector<uint32_t> id(n);
+        VSA_CHECK(hipMemcpyAsync(k.data(), c->ws.d_keys[c->cur], n * 8, hipMemcpyDeviceToHost,
+                                 c->stream));
+        VSA_CHECK(hipMemcpyAsync(id.data(), c->ws.d_ids[c->cur], n * 4, hipMemcpyDeviceToHost,
+                                 c->stream));
+        VSA_CHECK(hipStreamSynchronize(c->stream));
+        for (uint64_t i = 0; i < n; i++) {
+            out[i].key = k[i];
+            out[i].id = id[i];
+            out[i].pad = 0;
+        }
+    }
+    if (n_copied) *n_copied = n;
+    return VSA_OK;
+}
+
+uint64_t vsa_scan_candidates(vsa_ctx_t *c) { return c ? c->last_cand : 0; }
+
+double vsa_scan_kernel_ms(vsa_ctx_t *c) { return c ? c->last_kernel_ms : 0.0; }
+
+int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
+                   const uint8_t *d_data, uint64_t len, uint64_t *d_bitmap, uint64_t *first,
+                   uint64_t *last, uint64_t *count, uint32_t flags) {
+    (void)flags;
+    if (!c || !cls) return VSA_E_INVALID;
+    if (len == 0) {
+        if (first) *first = 0;
+        if (last) *last = 0;
+        if (count) *count = 0;
+        return VSA_OK;
+    }
+    if (!d_data || ((uintptr_t)d_data & 15)) return VSA_E_INVALID;
+    Workspace &w = c->ws;
+    unsigned long long init[3] = {~0ULL, 0, 0};
+    memcpy(w.h_counters + 4, init, sizeof(init));
+    VSA_CHECK(hipMemcpyAsync(w.d_counters + 4, w.h_counters + 4, 3 * 8, hipMemcpyHostToDevice,
+                             c->stream));
+    VsaClassParams P;
+    memset(&P, 0, sizeof(P));
+    P.data = d_data;
+    P.len = len;
+    memcpy(P.cls, cls, 32);
+    if (cls2) {
+        memcpy(P.cls2, cls2, 32);
+        P.pair = 1;
+    }
+    P.bitmap = d_bitmap;
+    P.first = w.d_counters + 4;
+    P.last = w.d_counters + 5;
+    P.count = w.d_counters + 6;
+    uint64_t chunks = (len + 15) / 16;
+    uint64_t want = (chunks + 255) / 256;
+    uint64_t cap = (uint64_t)c->num_cus * 8;
+    uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
+    hipLaunchKernelGGL(vsa_class_scan, dim3(grid), dim3(256), 0, c->stream, P);
+    VSA_CHECK(hipGetLastError());
+    VSA_CHECK(hipMemcpyAsync(w.h_counters + 4, w.d_counters + 4, 3 * 8, hipMemcpyDeviceToHost,
+                             c->stream));
+    VSA_CHECK(hipStreamSynchronize(c->stream));
+    uint64_t f = w.h_counters[4];
+    if (first) *first = f == ~0ULL ? len : f;
+    if (last) *last = w.h_counters[5];
+    if (count) *count = w.h_counters[6];
+    return VSA_OK;
+}
+
+/* --------------------------------------------------- drop-in literal -- */
+
+hwlm_error_t hwlmExec(const struct HWLM *tab, const uint8_t *buf, size_t len, size_t start,
+                      HWLMCallback cb, struct hs_scratch *scratch, hwlm_group_t groups) {
+    if (!tab) return HWLM_ERROR_UNKNOWN;
+    if (!groups) return HWLM_SUCCESS;
+    if (start >= len) return HWLM_SUCCESS;
+    vsa_db *db = registry_get(tab, -1);
+    if (!db) return HWLM_ERROR_UNKNOWN;
+    std::vector<uint64_t> keys;
+    std::vector<uint32_t> ids;
+    if (db->type == HWLM_ENGINE_NOOD) {
+        if (scan_host(db, buf, len, start, keys, ids) != VSA_OK) return HWLM_ERROR_UNKNOWN;
+        return replay_nood(keys.data(), ids.data(), keys.size(), cb, scratch);
+    }
+    /* accel pre-skip (hwlm.c:85-105, 191-201) on the GPU */
+    const HWLM *h = (const HWLM *)db->hblob;
+    const union AccelAux *aa = &h->accel0;
+    if ((groups & ~h->accel1_groups) == 0) aa = &h->accel1;
+    if (aa->accel_type != ACCEL_NONE && len - start >= 16) {
+        int64_t r = run_accel(aa, buf + start, buf + len) - buf;
+        if (aa->generic.offset) {
+            r -= aa->generic.offset;
+            if (r < 0) r = 0;
+        }
+        start = (size_t)r;
+        if (start >= len) return HWLM_SUCCESS;
+    }
+    if (scan_host(db, buf, len, start, keys, ids) != VSA_OK) return HWLM_ERROR_UNKNOWN;
+    return replay_lit(db, keys.data(), keys.size(), cb, scratch, groups);
+}
+
+hwlm_error_t fdrExec(const struct FDR *fdr, const uint8_t *buf, size_t len, size_t start,
+                     HWLMCallback cb, struct hs_scratch *scratch, hwlm_group_t groups) {
+    if (!fdr) return HWLM_ERROR_UNKNOWN;
+    if (start >= len) return HWLM_SUCCESS;
+    vsa_db *db = registry_get(fdr, HWLM_ENGINE_FDR);
+    if (!db) return HWLM_ERROR_UNKNOWN;
+    std::vector<uint64_t> keys;
+    std::vector<uint32_t> ids;
+    if (scan_host(db, buf, len, start, keys, ids) != VSA_OK) return HWLM_ERROR_UNKNOWN;
+    return replay_lit(db, keys.data(), keys.size(), cb, scratch, groups);
+}
+
+hwlm_error_t noodExec(const struct noodTable *n, const uint8_t *buf, size_t len, size_t start,
+                      HWLMCallback cb, struct hs_scratch *scratch) {
+    if (!n) return HWLM_ERROR_UNKNOWN;
+    if (start >= len) return HWLM_SUCCESS;
+    vsa_db *db = registry_get(n, HWLM_ENGINE_NOOD);
+    if (!db) return HWLM_ERROR_UNKNOWN;
+    std::vector<uint64_t> keys;
+    std::vector<uint32_t> ids;
+    if (scan_host(db, buf, len, start, keys, ids) != VSA_OK) return HWLM_ERROR_UNKNOWN;
+    return replay_nood(keys.data(), ids.data(), keys.size(), cb, scratch);
+}
+
+/* ----------------------------------------------------- drop-in accel -- */
+
+int64_t vsa_shufti_find(const uint8_t lo[16], const uint8_t hi[16], const uint8_t *buf,
+                        size_t len, int reverse) {
+    uint8_t cls[32];
+    cls_from_shufti(lo, hi, cls);
+    uint64_t f = len, l = 0;
+    if (class_host(cls, nullptr, buf, len, &f, &l) != VSA_OK) return -2;
+    return reverse ? (int64_t)l - 1 : (int64_t)f;
+}
+
+int64_t vsa_truffle_find(const uint8_t m1[16], const uint8_t m2[16], const uint8_t *buf,
+                         size_t len, int reverse) {
+    uint8_t cls[32];
+    cls_from_truffle(m1, m2, cls);
+    uint64_t f = len, l = 0;
+    if (class_host(cls, nullptr, buf, len, &f, &l) != VSA_OK) return -2;
+    return reverse ? (int64_t)l - 1 : (int64_t)f;
+}
+
+int64_t vsa_verm_find(int mode, uint8_t c1, uint8_t c2, uint8_t m1, uint8_t m2, int nocase,
+                      const uint8_t *buf, size_t len) {
+    uint8_t cls[32], cls2[32];
+    uint8_t cm = nocase ? 0xdf : 0xff;
+    uint64_t f = len, l = 0;
+    switch (mode) {
+    case 0: /* vermicelliExec */
+    case 2: /* rvermicelliExec */
+        cls_from_masked(c1, cm, false, cls);
+        break;
+    case 1: /* nvermicelliExec */
+    case 3: /* rnvermicelliExec */
+        cls_from_masked(c1, cm, true, cls);
+        break;
+    case 4: /* vermicelliDoubleExec */
+        cls_from_masked(c1, cm, false, cls);
+        cls_from_masked(c2, cm, false, cls2);
+        break;
+    case 5: /* vermicelliDoubleMaskedExec */
+        cls_from_masked(c1, m1, false, cls);
+        cls_from_masked(c2, m2, false, cls2);
+        break;
+    default:
+        return -2;
+    }
+    bool pair = mode >= 4;
+    if (class_host(cls, pair ? cls2 : nullptr, buf, len, &f, &l) != VSA_OK) return -2;
+    if (mode == 2 || mode == 3) return (int64_t)l - 1;
+    if (pair && f == len && len && cls_has(cls, buf[len - 1])) {
+        /* partial match at the end (vermicelli_simd.cpp:349-355) */
+        return (int64_t)len - 1;
+    }
+    return (int64_t)f;
+}
+
+static void m128_bytes(vsa_m128_t m, uint8_t out[16]) { memcpy(out, &m, 16); }
+
+const uint8_t *shuftiExec(vsa_m128_t mask_lo, vsa_m128_t mask_hi, const uint8_t *buf,
+                          const uint8_t *buf_end) {
+    uint8_t lo[16], hi[16];
+    m128_bytes(mask_lo, lo);
+    m128_bytes(mask_hi, hi);
+    int64_t r = vsa_shufti_find(lo, hi, buf, (size_t)(buf_end - buf), 0);
+    return r < 0 ? buf_end : buf + r;
+}
+
+const uint8_t *rshuftiExec(vsa_m128_t mask_lo, vsa_m128_t mask_hi, const uint8_t *buf,
+                           const uint8_t *buf_end) {
+    uint8_t lo[16], hi[16];
+    m128_bytes(mask_lo, lo);
+    m128_bytes(mask_hi, hi);
+    return buf + vsa_shufti_find(lo, hi, buf, (size_t)(buf_end - buf), 1);
+}
+
+const uint8_t *truffleExec(vsa_m128_t mask1, vsa_m128_t mask2, const uint8_t *buf,
+                           const uint8_t *buf_end) {
+    uint8_t a[16], b[16];
+    m128_bytes(mask1, a);
+    m128_bytes(mask2, b);
+    int64_t r = vsa_truffle_find(a, b, buf, (size_t)(buf_end - buf), 0);
+    return r < 0 ? buf_end : buf + r;
+}
+
+const uint8_t *rtruffleExec(vsa_m128_t mask1, vsa_m128_t mask2, const uint8_t *buf,
+                            const uint8_t *buf_end) {
+    uint8_t a[16], b[16];
+    m128_bytes(mask1, a);
+    m128_bytes(mask2, b);
+    return buf + vsa_truffle_find(a, b, buf, (size_t)(buf_end - buf), 1);
+}
+
+const uint8_t *vermicelliExec(char c, char nocase, const uint8_t *buf, const uint8_t *buf_end) {
+    return buf + vsa_verm_find(0, (uint8_t)c, 0, 0, 0, nocase, buf, (size_t)(buf_end - buf));
+}
+const uint8_t *nvermicelliExec(char c, char nocase, const uint8_t *buf, const uint8_t *buf_end) {
+    return buf + vsa_verm_find(1, (uint8_t)c, 0, 0, 0, nocase, buf, (size_t)(buf_end - buf));
+}
+const uint8_t *rvermicelliExec(char c, char nocase, const uint8_t *buf, const uint8_t *buf_end) {
+    return buf + vsa_verm_find(2, (uint8_t)c, 0, 0, 0, nocase, buf, (size_t)(buf_end - buf));
+}
+const uint8_t *rnvermicelliExec(char c, char nocase, const uint8_t *buf,
+                                const uint8_t *buf_end) {
+    return buf + vsa_verm_find(3, (uint8_t)c, 0, 0, 0, nocase, buf, (size_t)(buf_end - buf));
+}
+const uint8_t *vermicelliDoubleExec(char c1, char c2, char nocase, const uint8_t *buf,
+                                    const uint8_t *buf_end) {
+    return buf + vsa_verm_find(4, (uint8_t)c1, (uint8_t)c2, 0, 0, nocase, buf,
+                               (size_t)(buf_end - buf));
+}
+const uint8_t *vermicelliDoubleMaskedExec(char c1, char c2, char m1, char m2,
+                                          const uint8_t *buf, const uint8_t *buf_end) {
+    return buf + vsa_verm_find(5, (uint8_t)c1, (uint8_t)c2, (uint8_t)m1, (uint8_t)m2, 0, buf,
+                               (size_t)(buf_end - buf));
+}
+
+/* accel.c:35-180 dispatch for the forward schemes HWLM and NFAs use */
+const uint8_t *run_accel(const union AccelAux *accel, const uint8_t *c, const uint8_t *c_end) {
+    size_t len = (size_t)(c_end - c);
+    switch (accel->accel_type) {
+    case ACCEL_VERM:
+        return c + vsa_verm_find(0, accel->verm.c, 0, 0, 0, 0, c, len);
+    case ACCEL_VERM_NOCASE:
+        return c + vsa_verm_find(0, accel->verm.c, 0, 0, 0, 1, c, len);
+    case ACCEL_DVERM:
+        return c + vsa_verm_find(4, accel->dverm.c1, accel->dverm.c2, 0, 0, 0, c, len);
+    case ACCEL_DVERM_NOCASE:
+        return c + vsa_verm_find(4, accel->dverm.c1, accel->dverm.c2, 0, 0, 1, c, len);
+    case ACCEL_DVERM_MASKED:
+        return c + vsa_verm_find(5, accel->dverm.c1, accel->dverm.c2, accel->dverm.m1,
+                                 accel->dverm.m2, 0, c, len);
+    case ACCEL_SHUFTI:
+        return c + vsa_shufti_find(accel->shufti.lo.b, accel->shufti.hi.b, c, len, 0);
+    case ACCEL_TRUFFLE:
+        return c + vsa_truffle_find(accel->truffle.mask1.b, accel->truffle.mask2.b, c, len, 0);
+    default:
+        return c;
+    }
+}
+
+void vsa_set_scratch_layout(long fdr_conf_off, long fdr_conf_offset_off) {
+    g_fdr_conf_off.store(fdr_conf_off);
+    g_fdr_conf_offset_off.store(fdr_conf_offset_off);
+}
+
+/* ---------------------------------------------------------- builder --- */
+
+void vsa_build_opts_default(vsa_build_opts_t *o) {
+    o->engine_hint = -1;
+    o->allow_noodle = 1;
+    o->allow_teddy = 1;
+    o->allow_fat_teddy = 1;
+    o->allow_flood = 0;
+}
+
+int vsa_hwlm_build(const vsa_literal_t *lits, size_t n, const vsa_build_opts_t *opts,
+                   void **blob, size_t *size) {
+    if (!lits || !n || !blob || !size) return VSA_E_INVALID;
+    vsa::BuildOptions bo;
+    if (opts) {
+        bo.engine_hint = opts->engine_hint;
+        bo.allow_noodle = opts->allow_noodle;
+        bo.allow_teddy = opts->allow_teddy;
+        bo.allow_fat_teddy = opts->allow_fat_teddy;
+        bo.allow_flood = opts->allow_flood;
+    }
+    std::vector<vsa::Literal> v;
+    v.reserve(n);
+    for (size_t i = 0; i < n; i++) {
+        const vsa_literal_t &l = lits[i];
+        if (!l.s || !l.len) return VSA_E_INVALID;
+        v.push_back(vsa::makeLiteral(l.s, l.len, l.nocase, l.noruns, l.id, l.groups, l.msk,
+                                     l.cmp, l.msk_len));
+    }
+    uint8_t *out = nullptr;
+    int r = vsa::buildHwlm(std::move(v), bo, &out, size);
+    if (r != VSA_OK) return r;
+    *blob = out;
+    return VSA_OK;
+}
+
+void vsa_blob_free(void *blob) { free(blob); }
+
+int vsa_hwlm_set_accel(void *blob, const union AccelAux *a0, const union AccelAux *a1,
+                       uint64_t g1) {
+    if (!blob) return VSA_E_INVALID;
+    HWLM *h = (HWLM *)blob;
+    if (a0) memcpy(&h->accel0, a0, sizeof(*a0));
+    if (a1) memcpy(&h->accel1, a1, sizeof(*a1));
+    h->accel1_groups = g1;
+    return VSA_OK;
+}
+
+int vsa_shufti_build_masks(const uint8_t cls[32], uint8_t lo[16], uint8_t hi[16]) {
+    return vsa::shuftiMasks(cls, lo, hi);
+}
+
+void vsa_truffle_build_masks(const uint8_t cls[32], uint8_t m1[16], uint8_t m2[16]) {
+    vsa::truffleMasks(cls, m1, m2);
+}
+
+} /* extern "C" */

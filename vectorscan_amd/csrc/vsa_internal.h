@@ -1,0 +1,53 @@
+/*
+ * vsa_internal.h — host-side declarations shared by compile.cpp and the
+ * runtime (runtime.hip).  Not part of the public ABI (see
+ * include/vectorscan_amd.h).
+ */
+#ifndef VSA_INTERNAL_H
+#define VSA_INTERNAL_H
+
+#include "hs_layout.h"
+
+#include <string>
+#include <vector>
+
+#define VSA_OK 0
+#define VSA_E_INVALID (-1)
+#define VSA_E_NOMEM (-2)
+#define VSA_E_NOT_BUILDABLE (-3)
+#define VSA_E_DEVICE (-4)
+#define VSA_E_OVERFLOW (-5)
+
+namespace vsa {
+
+/* hwlmLiteral, src/hwlm/hwlm_literal.h:51-130 */
+struct Literal {
+    std::string s;
+    u32 id = 0;
+    bool nocase = false;
+    bool noruns = false;
+    u64a groups = HWLM_ALL_GROUPS;
+    std::vector<u8> msk;
+    std::vector<u8> cmp;
+};
+
+/* The Grey knobs that change engine choice (src/grey.cpp:66-68) plus the
+ * unit-test engine hint (fdr_compile.cpp:899-910). */
+struct BuildOptions {
+    bool allow_noodle = true;
+    bool allow_teddy = true;
+    bool allow_fat_teddy = true; /* the GPU runs 16-bucket Teddy natively */
+    bool allow_flood = false;    /* see DESIGN.md "flood" */
+    int engine_hint = -1;        /* -1: choose; 0: FDR d9 s1; 3..18 Teddy id */
+};
+
+Literal makeLiteral(const u8 *s, size_t len, bool nocase, bool noruns, u32 id,
+                    u64a groups, const u8 *msk, const u8 *cmp, size_t mlen);
+int buildHwlm(std::vector<Literal> lits, const BuildOptions &opt, u8 **out,
+              size_t *outSize);
+int shuftiMasks(const u8 cls[32], u8 lo[16], u8 hi[16]);
+void truffleMasks(const u8 cls[32], u8 m1[16], u8 m2[16]);
+
+} // namespace vsa
+
+#endif
