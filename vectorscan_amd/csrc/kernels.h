@@ -14,7 +14,9 @@ struct VsaBlock {
     uint64_t len;       /* block length */
     uint64_t start;     /* hwlmExec `start` (ends < start are not reported) */
     uint64_t seg_first; /* index of the block's first segment */
-    int64_t zbase;      /* FDR zone base: first looked-up position (may be <0) */
+    int64_t zbase;      /* FDR: first looked-up position (start, or len - 16
+                           for a short zone; may be < 0).  The start state
+                           always applies from `start`. */
 };
 
 /* A confirmed literal match.  `key` sorts into the reference callback order:

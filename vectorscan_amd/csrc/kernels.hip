@@ -277,10 +277,13 @@ __device__ __forceinline__ void lit_iter(const VsaLitParams &P, const u8 *A,
 
     if (EDGE) {
         if constexpr (MODE == VSA_MODE_FDR) {
-            /* start state: byte i applies to end zbase + i (fdr.c:615-662) */
+            /* start state: byte i applies to end start + i.  The short zone
+             * shifts fdr->start by 16 - (len - start) bytes against a scan
+             * that begins at len - 16 (fdr.c:372-440, :712-720), which lands
+             * it on `start` as well. */
 #pragma unroll
             for (int j = 0; j < 16; j++) {
-                int64_t r = q0 + j - B.zbase;
+                int64_t r = q0 + j - (int64_t)B.start;
                 if (r >= 0 && r < 16) {
                     u64 st = r < 8 ? P.state_lo : P.state_hi;
                     u32 sb = (u32)(st >> (8 * (r & 7))) & 0xff;
@@ -510,7 +513,7 @@ vsa_lit_scan(VsaLitParams P) {
              * interior, ends outside the segment, or the FDR start state */
             int64_t qa = ib - blo, qb = ib + 16 * WAVE - blo; /* [qa, qb) */
             bool edge = (qa < zlo + 16) || (qa < 0) || (qb + 1 > (int64_t)B.len) ||
-                        (qa < s_lo) || (qb > s_hi) || (qa < (int64_t)B.start);
+                        (qa < s_lo) || (qb > s_hi) || (qa < (int64_t)B.start + 16);
             if (edge) {
                 lit_iter<MODE, true>(P, A, mis, tab, blk, B, ib, s_lo, s_hi, &carry,
                                      queue, &qn, cl, bucket_mask, dc, true);
