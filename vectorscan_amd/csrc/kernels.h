@@ -17,6 +17,8 @@ struct VsaBlock {
     int64_t zbase;      /* FDR: first looked-up position (start, or len - 16
                            for a short zone; may be < 0).  The start state
                            always applies from `start`. */
+    int64_t org;        /* aligned (1 KiB, relative to data & ~15) origin of
+                           the block's first segment */
 };
 
 /* A confirmed literal match.  `key` sorts into the reference callback order:
@@ -46,6 +48,13 @@ struct VsaLitParams {
     uint64_t state_lo, state_hi; /* FDR start state (fdr->start) */
     const uint8_t *conf_base;    /* engine confBase (device) */
     uint32_t conf_off[16];       /* confBase[b], 0 = empty bucket */
+    const uint32_t *slotmap;     /* per-bucket bitmap of litIndex[h] != 0 */
+    uint32_t slot_words;
+    uint32_t slot_off[16];       /* word offset per bucket, ~0 = no prefilter */
+    uint32_t qcap;               /* per-wave LDS confirm-queue entries */
+    uint32_t dbg;                /* debug: bit0 verify queued keys against HBM
+                                    (mismatches -> counters[3]); bit1 drop all
+                                    candidates (filter-only timing) */
     uint64_t *out_keys;
     uint32_t *out_ids;
     uint64_t out_cap;

@@ -39,7 +39,7 @@
 #include "kernels.h"
 
 #define WAVE 64
-#define LIT_WAVES 8
+#define LIT_WAVES 16
 #define LIT_THREADS (LIT_WAVES * WAVE)
 #define QCAP 256
 
@@ -49,11 +49,23 @@ typedef uint8_t u8;
 
 __device__ __forceinline__ u32 lane_id() { return __lane_id(); }
 
+/* the builtins return int: keep them unsigned so u64 assembly never
+ * sign-extends a low word */
+__device__ __forceinline__ u32 readlane_u32(u32 v, int src) {
+    return (u32)__builtin_amdgcn_readlane((int)v, src);
+}
+__device__ __forceinline__ u32 readfirstlane_u32(u32 v) {
+    return (u32)__builtin_amdgcn_readfirstlane((int)v);
+}
+
 __device__ __forceinline__ u32 shfl_u32(u32 v, int src) {
     return (u32)__shfl((int)v, src, WAVE);
 }
 __device__ __forceinline__ u32 shfl_up_u32(u32 v, unsigned d) {
     return (u32)__shfl_up((int)v, d, WAVE);
+}
+__device__ __forceinline__ u32 shfl_xor_u32(u32 v, int m) {
+    return (u32)__shfl_xor((int)v, m, WAVE);
 }
 __device__ __forceinline__ u32 shfl_down_u32(u32 v, unsigned d) {
     return (u32)__shfl_down((int)v, d, WAVE);
@@ -107,64 +119,104 @@ struct LitTraits<VSA_MODE_FAT> {
     typedef u64 S_t;
 };
 
+/* per-bucket confirm parameters staged in LDS (FDRConfirm, fdr_confirm.h:78) */
 struct ConfLds {
     u64 andmsk[16];
     u64 mult[16];
     u32 nbits[16];
     u32 off[16];
+    u32 slot_off[16]; /* word offset of the bucket's slot bitmap, ~0 = none */
 };
 
-/* Confirm one queued candidate (one per lane).  ent = aoff<<24 | blk<<4 | b */
-__device__ __forceinline__ void confirm_entry(const VsaLitParams &P,
-                                              const u8 *A, u32 mis, u64 ent,
-                                              const ConfLds &cl) {
-    u32 b = (u32)(ent & 15);
-    u32 blk = (u32)((ent >> 4) & 0xfffff);
-    int64_t aoff = (int64_t)(ent >> 24);
-    const VsaBlock &B = P.blocks[blk];
-    int64_t blo = (int64_t)B.base + mis;
-    int64_t e = aoff - blo; /* block-relative end */
-    /* 8 bytes ending at e; bytes before the block read as 0 (fdr.c:798) */
-    u64 key = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        int64_t p = aoff - 7 + k;
-        u64 byte = (p >= blo) ? (u64)A[p] : 0;
-        key |= byte << (8 * k);
-    }
-    u32 off = cl.off[b];
-    const u8 *fc = P.conf_base + off;
-    u32 nb = cl.nbits[b];
-    u32 c = (u32)(((key & cl.andmsk[b]) * cl.mult[b]) >> (64 - nb));
-    u32 st = *(const u32 *)(fc + 32 + 4 * (size_t)c);
+/* queue entry: meta = aoff << 24 | blk << 4 | bucket; key = 8 bytes ending
+ * at the candidate end (bytes before the block are 0, fdr.c:798-806) */
+struct QEnt {
+    u64 meta;
+    u64 key;
+};
+
+struct LitShared {
+    const void *tab;
+    QEnt *queue; /* this wave's QCAP entries */
+    u32 *qcount; /* this wave's counter (LDS) */
+    const u32 *slots;
+    u32 qcap;
+};
+
+__device__ __forceinline__ u32 conf_hash(u64 key, u64 andmsk, u64 mult, u32 nbits) {
+    return (u32)(((key & andmsk) * mult) >> (64 - nbits));
+}
+
+/* Exact confirm of one candidate (fdr_confirm_runtime.h:43-102 minus the
+ * sequential state, which the host replays): walk the LitInfo chain of
+ * litIndex[hash] and emit every literal with (key & msk) == v whose start
+ * lies inside the block. */
+__device__ __forceinline__ void confirm_one(const VsaLitParams &P, const ConfLds &cl,
+                                            u64 meta, u64 key, u32 mis) {
+    const u32 b = (u32)(meta & 15);
+    const u32 blk = (u32)((meta >> 4) & 0xfffff);
+    const u64 aoff = meta >> 24;
+    const u8 *fc = P.conf_base + cl.off[b];
+    const u32 c = conf_hash(key, cl.andmsk[b], cl.mult[b], cl.nbits[b]);
+    const u32 st = *((const u32 *)(fc + 32) + c);
     if (!st) return;
+    const u64 base = P.blocks[blk].base;
+    const int64_t e = (int64_t)(aoff - mis - base); /* block-relative end */
+    if (P.dbg & 1) {
+        const u8 *A = P.data - mis;
+        const int64_t blo = (int64_t)base + mis;
+        u64 k2 = 0;
+        for (int k = 0; k < 8; k++) {
+            int64_t p = (int64_t)aoff - 7 + k;
+            k2 |= (u64)(p >= blo ? A[p] : 0) << (8 * k);
+        }
+        if (k2 != key) atomicAdd(&P.counters[3], 1ULL);
+    }
     const u8 *li = fc + st;
-    u8 next;
+    u32 next;
     do {
-        const uint4 w0 = *(const uint4 *)li;       /* v, msk */
-        const uint4 w1 = *(const uint4 *)(li + 16); /* groups, id|size|flags|next */
-        u64 v = ((u64)w0.y << 32) | w0.x;
-        u64 msk = ((u64)w0.w << 32) | w0.z;
-        u32 id = w1.z;
-        u32 size = w1.w & 0xff;
-        next = (u8)(w1.w >> 16);
+        const uint4 w0 = *(const uint4 *)li;        /* v, msk */
+        const uint4 w1 = *(const uint4 *)(li + 16); /* groups | id,size,flags,next */
+        const u64 v = ((u64)w0.y << 32) | w0.x;
+        const u64 msk = ((u64)w0.w << 32) | w0.z;
+        const u32 size = w1.w & 0xff;
+        next = (w1.w >> 16) & 0xff;
         if ((key & msk) == v && e + 1 >= (int64_t)size) {
             unsigned long long slot = atomicAdd(&P.counters[0], 1ULL);
             if (slot < P.out_cap) {
-                u64 end_abs = (u64)B.base + (u64)e;
-                u64 lidx = ((u64)(li - fc) >> 5) & VSA_KEY_LI_MASK;
-                P.out_keys[slot] = (end_abs << VSA_KEY_END_SHIFT) |
+                const u64 lidx = ((u64)(li - fc) >> 5) & VSA_KEY_LI_MASK;
+                P.out_keys[slot] = ((base + (u64)e) << VSA_KEY_END_SHIFT) |
                                    ((u64)b << VSA_KEY_BUCKET_SHIFT) | lidx;
-                P.out_ids[slot] = id;
+                P.out_ids[slot] = w1.z;
             }
         }
         li += 32;
     } while (next);
 }
 
-template <int MODE>
+/* confirm 64 queued candidates per round while at least `keep` remain */
+__device__ __forceinline__ void drain_queue(const VsaLitParams &P, const ConfLds &cl,
+                                            const LitShared &L, u32 mis, u32 keep) {
+    const u32 lane = lane_id();
+    u32 qn = readfirstlane_u32(*L.qcount);
+    while (qn > keep) {
+        u32 take = qn - keep < (u32)WAVE ? qn - keep : (u32)WAVE;
+        if (lane < take) {
+            QEnt q = L.queue[qn - take + lane];
+            confirm_one(P, cl, q.meta, q.key, mis);
+        }
+        qn -= take;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) *L.qcount = qn;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int MODE, bool LDS_TABLE>
 __device__ __forceinline__ u64 lit_lookup(const void *tab, u32 key, u32 lane) {
     if constexpr (MODE == VSA_MODE_FDR) {
+        (void)lane;
         return ((const u64 *)tab)[key];
     } else if constexpr (MODE == VSA_MODE_TEDDY) {
         return ((const u32 *)tab)[(key << 5) | (lane & 31)];
@@ -173,8 +225,7 @@ __device__ __forceinline__ u64 lit_lookup(const void *tab, u32 key, u32 lane) {
     }
 }
 
-/* key for position j (0..15) of the lane's 16-byte chunk d[0..3], nx =
- * byte after the chunk */
+/* key of position j (0..15) of the lane's chunk d[0..3] (d[4] = next byte) */
 template <int MODE>
 __device__ __forceinline__ u32 lit_key(const u32 d[5], int j, u32 dmask) {
     if constexpr (LitTraits<MODE>::KEY16) {
@@ -182,206 +233,225 @@ __device__ __forceinline__ u32 lit_key(const u32 d[5], int j, u32 dmask) {
                         : d[j >> 2];
         return w & dmask;
     } else {
+        (void)dmask;
         return (d[j >> 2] >> (8 * (j & 3))) & 0xff;
     }
 }
 
-/* Process one 1 KiB iteration.  Returns S_out of lane 63 in *carry. */
-template <int MODE, bool EDGE>
-__device__ __forceinline__ void lit_iter(const VsaLitParams &P, const u8 *A,
-                                         u32 mis, const void *tab, u32 blk,
-                                         const VsaBlock &B, int64_t ib,
-                                         int64_t s_lo, int64_t s_hi,
-                                         u64 *carry, u64 *queue, u32 *qn,
-                                         const ConfLds &cl, u32 bucket_mask,
-                                         u32 d_next[4], bool have_next) {
+struct IterState {
+    u64 carry;  /* pending table contributions into the next chunk's first ends */
+    u64 pbytes; /* the 8 bytes before the next chunk (lane 63's d[2..3]) */
+    u32 ncand;  /* first-stage candidates so far (diagnostic, wave-uniform) */
+};
+
+struct SegCtx {
+    u32 blk;
+    int64_t blo, bhi; /* aoff of the block */
+    int64_t start, len, zbase;
+};
+
+/* One 1 KiB iteration at aoff `ib`: lane l owns bytes [ib + 16 l, +16).
+ * d = the lane's 16 bytes, nxt0 = first byte of the following chunk (for
+ * lane 63's last 2-byte key). */
+template <int MODE, bool LDS_TABLE, bool EDGE>
+__device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfLds &cl,
+                                              const LitShared &L, const SegCtx &S,
+                                              u32 mis, int64_t ib, uint4 chunk,
+                                              u32 nxt0, IterState in, u32 bucket_mask) {
     typedef LitTraits<MODE> T;
     typedef typename T::S_t S_t;
     const u32 lane = lane_id();
-    const int64_t blo = (int64_t)B.base + mis; /* aoff of block byte 0 */
-    const int64_t bhi = blo + (int64_t)B.len;
-    const int64_t p0 = ib + 16 * (int64_t)lane; /* aoff of lane's first byte */
-    const int64_t q0 = p0 - blo;                /* block-relative */
+    const int64_t p0 = ib + 16 * (int64_t)lane;
+    const int64_t q0 = p0 - S.blo;
 
-    u32 d[5];
-    d[0] = d_next[0];
-    d[1] = d_next[1];
-    d[2] = d_next[2];
-    d[3] = d_next[3];
-    (void)have_next;
-    /* byte after the chunk: lane+1's first byte; lane 63 loads it */
+    u32 d[5] = {chunk.x, chunk.y, chunk.z, chunk.w, 0};
     u32 nx = shfl_down_u32(d[0], 1);
-    if (lane == WAVE - 1) {
-        int64_t pn = p0 + 16;
-        nx = (pn < bhi) ? (u32)A[pn] : 0u;
-    }
+    if (lane == WAVE - 1) nx = nxt0;
     d[4] = nx & 0xff;
     if (EDGE) {
-        /* zero bytes outside the block */
 #pragma unroll
         for (int w = 0; w < 4; w++) {
             u32 m = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 int64_t p = p0 + 4 * w + k;
-                if (p >= blo && p < bhi) m |= 0xffu << (8 * k);
+                if (p >= S.blo && p < S.bhi) m |= 0xffu << (8 * k);
             }
             d[w] &= m;
         }
-        if (p0 + 16 < blo || p0 + 16 >= bhi) d[4] = 0;
+        if (p0 + 16 < S.blo || p0 + 16 >= S.bhi) d[4] = 0;
     }
 
     /* own contributions: running state over the lane's 16 positions */
     u32 c[T::CW];
 #pragma unroll
     for (int i = 0; i < T::CW; i++) c[i] = 0;
-    S_t S = 0;
+    S_t st = 0;
 #pragma unroll
     for (int j = 0; j < 16; j++) {
         u32 key = lit_key<MODE>(d, j, P.dmask);
-        S_t x = (S_t)lit_lookup<MODE>(tab, key, lane);
+        S_t x = (S_t)lit_lookup<MODE, LDS_TABLE>(L.tab, key, lane);
         if (EDGE) {
             int64_t q = q0 + j;
             bool valid;
             if constexpr (MODE == VSA_MODE_FDR) {
-                valid = q >= B.zbase && q < (int64_t)B.len;
+                valid = q >= S.zbase && q < S.len;
             } else {
-                valid = q >= 0 && q < (int64_t)B.len;
+                valid = q >= 0 && q < S.len;
             }
             if (!valid) x = 0;
         }
-        S |= x;
+        st |= x;
         if constexpr (T::LB == 8) {
-            /* insert low byte of S as byte (j&3) of c[j>>2] */
-            const u32 sel = 0x03020100u & ~(0xffu << (8 * (j & 3)));
-            c[j >> 2] = __builtin_amdgcn_perm((u32)S, c[j >> 2],
-                                              sel | (0x04u << (8 * (j & 3))));
+            const u32 sel = (0x03020100u & ~(0xffu << (8 * (j & 3)))) | (0x04u << (8 * (j & 3)));
+            c[j >> 2] = __builtin_amdgcn_perm((u32)st, c[j >> 2], sel);
         } else {
-            c[j >> 1] |= ((u32)S & 0xffffu) << (16 * (j & 1));
+            c[j >> 1] |= ((u32)st & 0xffffu) << (16 * (j & 1));
         }
-        S >>= T::LB;
+        st >>= T::LB;
     }
-    /* spill from the previous lane (lane 0: from the previous iteration) */
-    u64 s_out = (u64)S;
-    u32 in_lo = shfl_up_u32((u32)s_out, 1);
-    u32 in_hi = shfl_up_u32((u32)(s_out >> 32), 1);
-    u64 s_in = ((u64)in_hi << 32) | in_lo;
-    if (lane == 0) s_in = *carry;
-    {
-        u32 lo = (u32)shfl_u32((u32)s_out, WAVE - 1);
-        u32 hi = (u32)shfl_u32((u32)(s_out >> 32), WAVE - 1);
-        *carry = ((u64)hi << 32) | lo;
-    }
+    /* spill from the previous lane (lane 0: from the previous chunk) */
+    const u64 s_out = (u64)st;
+    u64 s_in = ((u64)shfl_up_u32((u32)(s_out >> 32), 1) << 32) | shfl_up_u32((u32)s_out, 1);
+    if (lane == 0) s_in = in.carry;
+    IterState out;
+    out.ncand = in.ncand;
+    out.carry = ((u64)readlane_u32((u32)(s_out >> 32), WAVE - 1) << 32) |
+                readlane_u32((u32)s_out, WAVE - 1);
+    out.pbytes = ((u64)readlane_u32(d[3], WAVE - 1) << 32) | readlane_u32(d[2], WAVE - 1);
     c[0] |= (u32)s_in;
     if constexpr (sizeof(S_t) == 8) c[1] |= (u32)(s_in >> 32);
-
     if (EDGE) {
         if constexpr (MODE == VSA_MODE_FDR) {
-            /* start state: byte i applies to end start + i.  The short zone
-             * shifts fdr->start by 16 - (len - start) bytes against a scan
-             * that begins at len - 16 (fdr.c:372-440, :712-720), which lands
-             * it on `start` as well. */
+            /* start state: byte i applies to end start + i (the short zone
+             * shifts fdr->start by 16 - (len - start) against a scan from
+             * len - 16, fdr.c:372-440 and :712-720, landing on start too) */
 #pragma unroll
             for (int j = 0; j < 16; j++) {
-                int64_t r = q0 + j - (int64_t)B.start;
+                int64_t r = q0 + j - S.start;
                 if (r >= 0 && r < 16) {
-                    u64 st = r < 8 ? P.state_lo : P.state_hi;
-                    u32 sb = (u32)(st >> (8 * (r & 7))) & 0xff;
-                    c[j >> 2] |= sb << (8 * (j & 3));
+                    u64 sv = r < 8 ? P.state_lo : P.state_hi;
+                    c[j >> 2] |= ((u32)(sv >> (8 * (r & 7))) & 0xff) << (8 * (j & 3));
                 }
             }
         }
-        /* report only ends in [max(start, s_lo), min(len, s_hi)) */
-        int64_t elo = s_lo > (int64_t)B.start ? s_lo : (int64_t)B.start;
-        int64_t ehi = s_hi < (int64_t)B.len ? s_hi : (int64_t)B.len;
+        /* only ends in [start, len) are reported */
 #pragma unroll
         for (int j = 0; j < 16; j++) {
             int64_t q = q0 + j;
-            if (q < elo || q >= ehi) {
+            if (q < S.start || q >= S.len) {
                 if constexpr (T::LB == 8) c[j >> 2] |= 0xffu << (8 * (j & 3));
                 else c[j >> 1] |= 0xffffu << (16 * (j & 1));
             }
         }
     }
 
-    /* candidate bits, empty buckets masked (do_confirm_fdr skips cf == 0) */
-    u32 n = 0;
+    /* candidate bits (do_confirm_fdr skips empty buckets, cf == 0) */
+    u32 any = 0;
 #pragma unroll
     for (int i = 0; i < T::CW; i++) {
         c[i] = ~c[i] & bucket_mask;
-        n += __popc(c[i]);
+        any |= c[i];
     }
-    if (!__any(n != 0)) return;
+    if (!__any(any != 0)) return out;
 
-    u32 total;
-    u32 pos = wave_excl_scan(n, &total);
-    /* make room: confirm 64 at a time while the queue would overflow */
-    while (*qn + total > QCAP) {
-        u32 avail = *qn < (u32)WAVE ? *qn : (u32)WAVE;
-        if (lane < avail) confirm_entry(P, A, mis, queue[*qn - avail + lane], cl);
-        *qn -= avail;
-        if (avail == 0) break;
+    /* bytes p0-8 .. p0+15 for the 8-byte confirm keys */
+    u32 pv2 = shfl_up_u32(d[2], 1), pv3 = shfl_up_u32(d[3], 1);
+    if (lane == 0) {
+        pv2 = (u32)in.pbytes;
+        pv3 = (u32)(in.pbytes >> 32);
     }
-    if (*qn + total <= QCAP) {
-        u32 w = *qn + pos;
+    const u64 W0 = ((u64)pv3 << 32) | pv2;
+    const u64 W1 = ((u64)d[1] << 32) | d[0];
+    const u64 W2 = ((u64)d[3] << 32) | d[2];
+    u32 ncand = 0;
 #pragma unroll
-        for (int i = 0; i < T::CW; i++) {
-            u32 bits = c[i];
-            while (bits) {
-                u32 bit = __ffs(bits) - 1;
-                bits &= bits - 1;
-                u32 jj, bk;
-                if constexpr (T::LB == 8) {
-                    jj = 4 * i + (bit >> 3);
-                    bk = bit & 7;
-                } else {
-                    jj = 2 * i + (bit >> 4);
-                    bk = bit & 15;
-                }
-                u64 aoff = (u64)(p0 + jj);
-                queue[w++] = (aoff << 24) | ((u64)blk << 4) | bk;
+    for (int i = 0; i < T::CW; i++) {
+        u32 bits = c[i];
+        while (bits) {
+            const u32 bit = __ffs(bits) - 1;
+            bits &= bits - 1;
+            u32 j, b;
+            if constexpr (T::LB == 8) {
+                j = 4 * i + (bit >> 3);
+                b = bit & 7;
+            } else {
+                j = 2 * i + (bit >> 4);
+                b = bit & 15;
             }
-        }
-        *qn += total;
-    } else {
-        /* pathological burst (> QCAP candidates in 1 KiB): confirm in place */
-#pragma unroll
-        for (int i = 0; i < T::CW; i++) {
-            u32 bits = c[i];
-            while (bits) {
-                u32 bit = __ffs(bits) - 1;
-                bits &= bits - 1;
-                u32 jj, bk;
-                if constexpr (T::LB == 8) {
-                    jj = 4 * i + (bit >> 3);
-                    bk = bit & 7;
-                } else {
-                    jj = 2 * i + (bit >> 4);
-                    bk = bit & 15;
-                }
-                u64 aoff = (u64)(p0 + jj);
-                confirm_entry(P, A, mis, (aoff << 24) | ((u64)blk << 4) | bk, cl);
+            ncand++;
+            /* key = bytes [j-7, j] = byte offset j+1 .. j+8 of W0:W1:W2 */
+            const u32 o = j + 1;
+            u64 key;
+            if (o < 8) key = (W0 >> (8 * o)) | (W1 << (64 - 8 * o));
+            else if (o == 8) key = W1;
+            else if (o < 16) key = (W1 >> (8 * (o - 8))) | (W2 << (64 - 8 * (o - 8)));
+            else key = W2;
+            /* LDS slot-bitmap prefilter: litIndex[hash] == 0 rejects */
+            const u32 so = cl.slot_off[b];
+            if (so != 0xffffffffu) {
+                const u32 h = conf_hash(key, cl.andmsk[b], cl.mult[b], cl.nbits[b]);
+                if (!((L.slots[so + (h >> 5)] >> (h & 31)) & 1u)) continue;
+            }
+            const u64 meta = ((u64)(p0 + j) << 24) | ((u64)S.blk << 4) | b;
+            const u32 slot = atomicAdd(L.qcount, 1u);
+            if (slot < L.qcap) {
+                L.queue[slot].meta = meta;
+                L.queue[slot].key = key;
+            } else {
+                confirm_one(P, cl, meta, key, mis);
             }
         }
     }
-    /* drain full rounds */
-    while (*qn >= (u32)WAVE) {
-        confirm_entry(P, A, mis, queue[*qn - WAVE + lane], cl);
-        *qn -= WAVE;
+    {
+        u32 tot = ncand;
+#pragma unroll
+        for (int dd = 32; dd >= 1; dd >>= 1) tot += shfl_xor_u32(tot, dd);
+        out.ncand += readfirstlane_u32(tot);
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    u32 qn = readfirstlane_u32(*L.qcount);
+    if (qn > L.qcap) {
+        if (lane == 0) *L.qcount = L.qcap;
+        qn = L.qcap;
+    }
+    if (qn >= (u32)WAVE) drain_queue(P, cl, L, mis, qn % WAVE);
+    return out;
 }
+
+__device__ __forceinline__ uint4 load_chunk(const u8 *A, int64_t p0, int64_t bhi) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    typedef u32 v4u __attribute__((ext_vector_type(4)));
+    if (p0 < bhi) {
+        v4u t = __builtin_nontemporal_load((const v4u *)(A + p0));
+        v = make_uint4(t.x, t.y, t.z, t.w);
+    }
+    return v;
+}
+
+/* unconditional 16-byte load (caller guarantees the address is valid) */
+__device__ __forceinline__ uint4 load_chunk_nc(const u8 *A, int64_t p0) {
+    typedef u32 v4u __attribute__((ext_vector_type(4)));
+    v4u t = __builtin_nontemporal_load((const v4u *)(A + p0));
+    return make_uint4(t.x, t.y, t.z, t.w);
+}
+
+#define LIT_DEPTH 4
 
 template <int MODE, bool LDS_TABLE>
 __global__ void __launch_bounds__(LIT_THREADS)
 vsa_lit_scan(VsaLitParams P) {
     typedef LitTraits<MODE> T;
+    typedef typename T::S_t S_t;
     extern __shared__ __align__(16) u8 smem[];
     __shared__ ConfLds cl;
+    __shared__ u32 qcounts[LIT_WAVES];
     const u32 tid = threadIdx.x;
     const u32 lane = lane_id();
     const u32 wave = tid / WAVE;
 
-    /* table -> LDS */
+    /* ---- stage tables into LDS ---- */
     u32 tab_bytes = 0;
     const void *tab;
     if constexpr (MODE == VSA_MODE_FDR) {
@@ -395,11 +465,10 @@ vsa_lit_scan(VsaLitParams P) {
             tab = P.table;
         }
     } else if constexpr (MODE == VSA_MODE_TEDDY) {
+        /* byte-combined masks, replicated 32x: lane group of 32 hits 32 banks */
         tab_bytes = 256 * 32 * 4;
         u32 *dst = (u32 *)smem;
-        for (u32 i = tid; i < 256 * 32; i += LIT_THREADS) {
-            dst[i] = (u32)P.table[i >> 5];
-        }
+        for (u32 i = tid; i < 256 * 32; i += LIT_THREADS) dst[i] = (u32)P.table[i >> 5];
         tab = smem;
     } else {
         tab_bytes = 256 * 32 * 8;
@@ -407,9 +476,13 @@ vsa_lit_scan(VsaLitParams P) {
         for (u32 i = tid; i < 256 * 32; i += LIT_THREADS) dst[i] = P.table[i >> 5];
         tab = smem;
     }
+    QEnt *queues = (QEnt *)(smem + ((tab_bytes + 15) & ~15u));
+    u32 *slots = (u32 *)(queues + (size_t)LIT_WAVES * P.qcap);
+    for (u32 i = tid; i < P.slot_words; i += LIT_THREADS) slots[i] = P.slotmap[i];
     if (tid < 16) {
         u32 off = P.conf_off[tid];
         cl.off[tid] = off;
+        cl.slot_off[tid] = P.slot_off[tid];
         if (off) {
             const u8 *fc = P.conf_base + off;
             cl.andmsk[tid] = *(const u64 *)fc;
@@ -419,12 +492,14 @@ vsa_lit_scan(VsaLitParams P) {
             cl.andmsk[tid] = 0;
             cl.mult[tid] = 0;
             cl.nbits[tid] = 1;
+            cl.slot_off[tid] = 0xffffffffu;
         }
     }
+    if (tid < LIT_WAVES) qcounts[tid] = 0;
     __syncthreads();
 
     u32 bucket_mask = 0;
-    {
+    if (!(P.dbg & 2)) {
         u32 present = 0;
         for (int b = 0; b < 16; b++) {
             if (P.conf_off[b]) present |= 1u << b;
@@ -436,99 +511,158 @@ vsa_lit_scan(VsaLitParams P) {
             bucket_mask = (present & 0xffff) | (present << 16);
         }
     }
+    LitShared L;
+    L.tab = tab;
+    L.queue = queues + (size_t)wave * P.qcap;
+    L.qcount = &qcounts[wave];
+    L.slots = slots;
+    L.qcap = P.qcap;
 
-    u64 *queue = (u64 *)(smem + ((tab_bytes + 15) & ~15u)) + wave * QCAP;
-    u32 qn = 0;
     const u32 mis = (u32)((uintptr_t)P.data & 15);
     const u8 *A = P.data - mis;
     const int64_t SEG = (int64_t)1 << P.seg_shift;
+    u32 ncand_total = 0;
 
     for (;;) {
         unsigned long long t = 0;
         if (lane == 0) t = atomicAdd(&P.counters[1], 1ULL);
-        u64 seg = ((u64)shfl_u32((u32)(t >> 32), 0) << 32) | shfl_u32((u32)t, 0);
+        const u64 seg = ((u64)readfirstlane_u32(shfl_u32((u32)(t >> 32), 0)) << 32) |
+                        readfirstlane_u32(shfl_u32((u32)t, 0));
         if (seg >= P.nsegs) break;
         u32 blk = 0;
         while (blk + 1 < P.nblocks && P.blocks[blk + 1].seg_first <= seg) blk++;
+        blk = readfirstlane_u32(blk);
         const VsaBlock B = P.blocks[blk];
-        const int64_t blo = (int64_t)B.base + mis;
-        const int64_t s_lo = (int64_t)(seg - B.seg_first) * SEG;
-        int64_t s_hi = s_lo + SEG;
-        if (s_hi > (int64_t)B.len) s_hi = (int64_t)B.len;
+        SegCtx S;
+        S.blk = blk;
+        S.blo = (int64_t)B.base + mis;
+        S.bhi = S.blo + (int64_t)B.len;
+        S.start = (int64_t)B.start;
+        S.len = (int64_t)B.len;
+        S.zbase = B.zbase;
+        const int64_t s_lo = B.org + (int64_t)(seg - B.seg_first) * SEG;
+        const int64_t s_hi = (s_lo + SEG < S.bhi) ? s_lo + SEG : S.bhi;
+        const u32 niters = (u32)((s_hi - s_lo + 1023) >> 10);
         const int64_t zlo = (MODE == VSA_MODE_FDR) ? B.zbase : 0;
-        int64_t ib = (blo + s_lo) & ~(int64_t)15;
 
-        /* prologue: spill into the first iteration from positions ib-7..ib-1
-         * (lanes 0..6 each look up one position) */
-        u64 carry = 0;
+        /* prologue 1: table spill from positions s_lo-NL+1 .. s_lo-1 */
+        IterState is;
+        is.ncand = ncand_total;
         {
-            typedef typename T::S_t S_t;
             S_t x = 0;
             if (lane < (u32)(T::NL - 1)) {
-                int64_t p = ib - (T::NL - 1) + (int64_t)lane; /* aoff */
-                int64_t q = p - blo;
+                const int64_t p = s_lo - (T::NL - 1) + (int64_t)lane;
+                const int64_t q = p - S.blo;
                 if (q >= zlo && q < (int64_t)B.len) {
+                    const u8 b0 = load_byte_masked(A, p, S.blo, S.bhi);
                     u32 key;
-                    u8 b0 = load_byte_masked(A, p, blo, blo + (int64_t)B.len);
                     if constexpr (T::KEY16) {
-                        u8 b1 = load_byte_masked(A, p + 1, blo, blo + (int64_t)B.len);
+                        const u8 b1 = load_byte_masked(A, p + 1, S.blo, S.bhi);
                         key = ((u32)b0 | ((u32)b1 << 8)) & P.dmask;
                     } else {
                         key = b0;
                     }
-                    x = (S_t)lit_lookup<MODE>(tab, key, lane);
-                    x >>= T::LB * (ib - p);
+                    x = (S_t)lit_lookup<MODE, LDS_TABLE>(tab, key, lane);
+                    x >>= T::LB * (s_lo - p);
                 }
             }
             u64 xv = (u64)x;
 #pragma unroll
-            for (int d = 1; d < 8; d <<= 1) {
-                u32 lo = shfl_down_u32((u32)xv, d);
-                u32 hi = shfl_down_u32((u32)(xv >> 32), d);
+            for (int dd = 1; dd < 8; dd <<= 1) {
+                const u32 lo = shfl_down_u32((u32)xv, dd);
+                const u32 hi = shfl_down_u32((u32)(xv >> 32), dd);
                 xv |= ((u64)hi << 32) | lo;
             }
-            carry = ((u64)shfl_u32((u32)(xv >> 32), 0) << 32) | shfl_u32((u32)xv, 0);
-        }
-
-        const int64_t it_end = blo + s_hi; /* aoff past the last end */
-        u32 dn[4] = {0, 0, 0, 0};
-        {
-            int64_t p0 = ib + 16 * (int64_t)lane;
-            if (p0 < blo + (int64_t)B.len) {
-                uint4 v = *(const uint4 *)(A + p0);
-                dn[0] = v.x; dn[1] = v.y; dn[2] = v.z; dn[3] = v.w;
+            is.carry = ((u64)shfl_u32((u32)(xv >> 32), 0) << 32) | shfl_u32((u32)xv, 0);
+            /* prologue 2: the 8 bytes before s_lo (keys of the first ends) */
+            u32 bb = 0;
+            if (lane < 8) bb = load_byte_masked(A, s_lo - 8 + (int64_t)lane, S.blo, S.bhi);
+            u64 pb = (u64)bb << (8 * (lane & 7));
+#pragma unroll
+            for (int dd = 1; dd < 8; dd <<= 1) {
+                const u32 lo = shfl_down_u32((u32)pb, dd);
+                const u32 hi = shfl_down_u32((u32)(pb >> 32), dd);
+                pb |= ((u64)hi << 32) | lo;
             }
+            is.pbytes = ((u64)shfl_u32((u32)(pb >> 32), 0) << 32) | shfl_u32((u32)pb, 0);
         }
-        for (; ib < it_end; ib += 16 * WAVE) {
-            u32 dc[4] = {dn[0], dn[1], dn[2], dn[3]};
-            /* prefetch next iteration */
-            {
-                int64_t p0n = ib + 16 * WAVE + 16 * (int64_t)lane;
-                if (ib + 16 * WAVE < it_end && p0n < blo + (int64_t)B.len) {
-                    uint4 v = *(const uint4 *)(A + p0n);
-                    dn[0] = v.x; dn[1] = v.y; dn[2] = v.z; dn[3] = v.w;
+        /* iterations [f0, f1) are interior ("fast"): no byte of the 1 KiB
+         * chunk or its successor byte lies outside the block, and the FDR
+         * start state / `start` cut-off are behind it.  The rest (at most a
+         * couple per block) run the checked path one at a time. */
+        const int64_t fast_lo = S.blo + S.start + 16;
+        u32 f0 = 0, f1 = niters;
+        if (s_lo < fast_lo) f0 = (u32)min((int64_t)niters, (fast_lo - s_lo + 1023) >> 10);
+        {
+            /* need ib + 1024 < bhi  <=>  it < (bhi - s_lo - 1024 + 1023) / 1024 rounded */
+            int64_t lim = S.bhi - s_lo - 1024; /* ib - s_lo must be < lim */
+            int64_t nf = lim <= 0 ? 0 : (lim + 1023) >> 10;
+            if (nf < (int64_t)f1) f1 = (u32)nf;
+        }
+        if (f1 < f0) f1 = f0;
+        for (u32 it = 0; it < f0; it++) {
+            const int64_t ib = s_lo + 1024 * (int64_t)it;
+            const uint4 cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
+            const u32 nxt0 = load_byte_masked(A, ib + 1024, S.blo, S.bhi);
+            is = lit_iter<MODE, LDS_TABLE, true>(P, cl, L, S, mis, ib, cur, nxt0, is,
+                                                 bucket_mask);
+        }
+        if (f0 < f1) {
+            /* main sweep: LIT_DEPTH chunks in flight per wave.  ring[k] is
+             * consumed and then refilled in place (no register rotation), so
+             * each step waits only for the load issued LIT_DEPTH-1 steps ago
+             * (the next chunk's first byte) */
+            const u32 nf = f1 - f0;
+            const int64_t fb = s_lo + 1024 * (int64_t)f0;
+            const u32 after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.blo, S.bhi);
+            uint4 ring[LIT_DEPTH];
+            /* every load is unconditional (an out-of-range prefetch re-reads
+             * the current chunk) so the wait counters stay exact */
+#pragma unroll
+            for (int k = 0; k < LIT_DEPTH; k++) {
+                const int64_t pk = ((u32)k < nf ? fb + 1024 * k : fb) + 16 * (int64_t)lane;
+                ring[k] = load_chunk_nc(A, pk);
+            }
+            const u32 ng = nf / LIT_DEPTH;
+            for (u32 g = 0; g < ng; g++) {
+#pragma unroll
+                for (int k = 0; k < LIT_DEPTH; k++) {
+                    const u32 it = g * LIT_DEPTH + k;
+                    const int64_t ib = fb + 1024 * (int64_t)it;
+                    const u32 nb = shfl_u32(ring[(k + 1) % LIT_DEPTH].x, 0);
+                    const u32 nxt0 = (it + 1 < nf) ? nb : after;
+                    is = lit_iter<MODE, LDS_TABLE, false>(P, cl, L, S, mis, ib, ring[k], nxt0,
+                                                          is, bucket_mask);
+                    const int64_t pn = (it + LIT_DEPTH < nf) ? ib + 1024 * LIT_DEPTH : ib;
+                    ring[k] = load_chunk_nc(A, pn + 16 * (int64_t)lane);
                 }
             }
-            /* edge iteration: touches positions outside the fully valid
-             * interior, ends outside the segment, or the FDR start state */
-            int64_t qa = ib - blo, qb = ib + 16 * WAVE - blo; /* [qa, qb) */
-            bool edge = (qa < zlo + 16) || (qa < 0) || (qb + 1 > (int64_t)B.len) ||
-                        (qa < s_lo) || (qb > s_hi) || (qa < (int64_t)B.start + 16);
-            if (edge) {
-                lit_iter<MODE, true>(P, A, mis, tab, blk, B, ib, s_lo, s_hi, &carry,
-                                     queue, &qn, cl, bucket_mask, dc, true);
-            } else {
-                lit_iter<MODE, false>(P, A, mis, tab, blk, B, ib, s_lo, s_hi, &carry,
-                                      queue, &qn, cl, bucket_mask, dc, true);
+            const u32 rem = nf - ng * LIT_DEPTH;
+#pragma unroll
+            for (int k = 0; k < LIT_DEPTH - 1; k++) {
+                if ((u32)k < rem) {
+                    const u32 it = ng * LIT_DEPTH + k;
+                    const int64_t ib = fb + 1024 * (int64_t)it;
+                    const u32 nb = shfl_u32(ring[(k + 1) % LIT_DEPTH].x, 0);
+                    const u32 nxt0 = (it + 1 < nf) ? nb : after;
+                    is = lit_iter<MODE, LDS_TABLE, false>(P, cl, L, S, mis, ib, ring[k], nxt0,
+                                                          is, bucket_mask);
+                }
             }
         }
+        for (u32 it = f1; it < niters; it++) {
+            const int64_t ib = s_lo + 1024 * (int64_t)it;
+            const uint4 cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
+            const u32 nxt0 = load_byte_masked(A, ib + 1024, S.blo, S.bhi);
+            is = lit_iter<MODE, LDS_TABLE, true>(P, cl, L, S, mis, ib, cur, nxt0, is,
+                                                 bucket_mask);
+        }
+        ncand_total = is.ncand;
     }
     /* drain the wave's queue */
-    while (qn) {
-        u32 avail = qn < (u32)WAVE ? qn : (u32)WAVE;
-        if (lane < avail) confirm_entry(P, A, mis, queue[qn - avail + lane], cl);
-        qn -= avail;
-    }
+    drain_queue(P, cl, L, mis, 0);
+    if (P.counters && lane_id() == 0 && ncand_total)
+        atomicAdd(&P.counters[2], (unsigned long long)ncand_total);
 }
 
 template __global__ void vsa_lit_scan<VSA_MODE_FDR, true>(VsaLitParams);
@@ -558,12 +692,11 @@ __global__ void __launch_bounds__(256) vsa_nood_scan(VsaNoodParams P) {
         const VsaBlock B = P.blocks[blk];
         const int64_t blo = (int64_t)B.base + mis;
         const int64_t bhi = blo + (int64_t)B.len;
-        const int64_t s_lo = (int64_t)(seg - B.seg_first) * SEG;
-        int64_t s_hi = s_lo + SEG;
-        if (s_hi > (int64_t)B.len) s_hi = (int64_t)B.len;
-        int64_t elo = (int64_t)B.start + ml - 1;
-        if (elo < s_lo) elo = s_lo;
-        for (int64_t ib = (blo + s_lo) & ~(int64_t)15; ib < blo + s_hi; ib += 16 * WAVE) {
+        /* same 1 KiB-aligned segment grid as vsa_lit_scan (VsaBlock.org) */
+        const int64_t s_lo = B.org + (int64_t)(seg - B.seg_first) * SEG;
+        const int64_t s_hi = (s_lo + SEG < bhi) ? s_lo + SEG : bhi;
+        const int64_t elo = (int64_t)B.start + ml - 1; /* block-relative */
+        for (int64_t ib = s_lo; ib < s_hi; ib += 16 * WAVE) {
             int64_t p0 = ib + 16 * (int64_t)lane;
             u32 d[4] = {0, 0, 0, 0};
             if (p0 < bhi) {
@@ -615,7 +748,7 @@ __global__ void __launch_bounds__(256) vsa_nood_scan(VsaNoodParams P) {
 #pragma unroll
             for (int j = 0; j < 16; j++) {
                 int64_t q = q0 + j;
-                if (q < elo || q >= s_hi) hits &= ~(1u << j);
+                if (q < elo || q >= (int64_t)B.len) hits &= ~(1u << j);
             }
             while (hits) {
                 u32 j = __ffs(hits) - 1;

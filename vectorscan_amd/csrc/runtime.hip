@@ -53,9 +53,10 @@ __global__ void vsa_class_scan(VsaClassParams P);
 
 namespace {
 
-const int LIT_WAVES = 8;
-const int LIT_THREADS = 512;
-const size_t QCAP_BYTES = 256 * 8 * LIT_WAVES;
+const int LIT_WAVES = 16;
+const int LIT_THREADS = 1024;
+const size_t LDS_BUDGET = 160 * 1024 - 2048; /* minus static LDS */
+const uint32_t SLOT_WORDS_MAX = 4096;        /* 16 KiB of slot bitmaps */
 
 struct Workspace {
     uint8_t *d_in = nullptr;
@@ -109,6 +110,9 @@ struct vsa_db {
     uint32_t conf_off[16] = {0};
     uint32_t nbuckets = 8;
     noodTable nood;
+    uint32_t *d_slots = nullptr; /* litIndex-occupancy bitmaps (prefilter) */
+    uint32_t slot_words = 0;
+    uint32_t slot_off[16];
 };
 
 namespace {
@@ -178,18 +182,26 @@ int bits_for(uint64_t v) {
 }
 
 template <int MODE, bool LDS>
-int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds, uint32_t wgs_per_cu) {
+int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds) {
     auto fn = vsa_lit_scan<MODE, LDS>;
-    static std::once_flag once[2];
-    (void)once;
     VSA_CHECK(hipFuncSetAttribute((const void *)fn,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     uint64_t want = (P.nsegs + LIT_WAVES - 1) / LIT_WAVES;
-    uint64_t cap = (uint64_t)c->num_cus * wgs_per_cu;
+    uint64_t cap = (uint64_t)c->num_cus; /* persistent: one 16-wave WG per CU */
     uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
     hipLaunchKernelGGL(fn, dim3(grid), dim3(LIT_THREADS), lds, c->stream, P);
     VSA_CHECK(hipGetLastError());
     return VSA_OK;
+}
+
+/* LDS plan: table + per-wave queues (QEnt 16 B) + slot bitmaps */
+size_t plan_lds(size_t tab, uint32_t slot_words, uint32_t *qcap) {
+    size_t rest = LDS_BUDGET > tab + slot_words * 4 ? LDS_BUDGET - tab - slot_words * 4 : 0;
+    uint32_t q = (uint32_t)std::min<size_t>(128, rest / (16 * LIT_WAVES));
+    q &= ~63u;
+    if (q < 64) q = 64;
+    *qcap = q;
+    return tab + (size_t)q * 16 * LIT_WAVES + (size_t)slot_words * 4;
 }
 
 int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
@@ -251,21 +263,28 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.out_ids = w.d_ids[0];
     P.out_cap = w.out_cap;
     P.counters = w.d_counters;
+    {
+        const char *e = getenv("VSA_DEBUG_FLAGS");
+        P.dbg = e ? (uint32_t)atoi(e) : 0u;
+    }
+    P.slotmap = db->d_slots;
+    P.slot_words = db->slot_words;
+    memcpy(P.slot_off, db->slot_off, sizeof(P.slot_off));
     if (db->mode == VSA_MODE_FDR) {
         size_t tb = (size_t)db->table_entries * 8;
         if (tb <= 128 * 1024) {
-            size_t lds = tb + QCAP_BYTES;
-            uint32_t per_cu = (uint32_t)std::max<size_t>(1, (160 * 1024) / (lds + 1024));
-            return launch_lit<VSA_MODE_FDR, true>(c, P, lds, std::min<uint32_t>(per_cu, 4));
+            size_t lds = plan_lds(tb, db->slot_words, &P.qcap);
+            if (lds <= LDS_BUDGET) return launch_lit<VSA_MODE_FDR, true>(c, P, lds);
         }
-        return launch_lit<VSA_MODE_FDR, false>(c, P, QCAP_BYTES, 4);
+        size_t lds = plan_lds(0, db->slot_words, &P.qcap);
+        return launch_lit<VSA_MODE_FDR, false>(c, P, lds);
     }
     if (db->mode == VSA_MODE_TEDDY) {
-        size_t lds = 256 * 32 * 4 + QCAP_BYTES;
-        return launch_lit<VSA_MODE_TEDDY, true>(c, P, lds, 3);
+        size_t lds = plan_lds(256 * 32 * 4, db->slot_words, &P.qcap);
+        return launch_lit<VSA_MODE_TEDDY, true>(c, P, lds);
     }
-    size_t lds = 256 * 32 * 8 + QCAP_BYTES;
-    return launch_lit<VSA_MODE_FAT, true>(c, P, lds, 2);
+    size_t lds = plan_lds(256 * 32 * 8, db->slot_words, &P.qcap);
+    return launch_lit<VSA_MODE_FAT, true>(c, P, lds);
 }
 
 int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
@@ -275,6 +294,10 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     VSA_CHECK(hipStreamSynchronize(c->stream));
     uint64_t n = w.h_counters[0];
     c->last_cand = w.h_counters[2];
+    if (getenv("VSA_DEBUG_FLAGS") && w.h_counters[3]) {
+        fprintf(stderr, "vsa: %llu queued confirm keys differ from HBM\n",
+                (unsigned long long)w.h_counters[3]);
+    }
     {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_kernel_ms = ms;
@@ -309,6 +332,7 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
     }
     uint32_t seg_shift = pick_seg_shift(total);
     uint64_t segs = 0;
+    const int64_t mis = (int64_t)((uintptr_t)d_data & 15);
     for (uint32_t i = 0; i < nb; i++) {
         VsaBlock &b = c->ws.h_blocks[i];
         b.base = offs[i];
@@ -318,7 +342,14 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         int64_t len = (int64_t)b.len, st = (int64_t)b.start;
         /* prepareZones fdr.c:625-659: short zone anchors at len - 16 */
         b.zbase = (len - st > 16) ? st : len - 16;
-        if (b.start < b.len) segs += (b.len + (1ull << seg_shift) - 1) >> seg_shift;
+        /* segments are 1 KiB-aligned (in data-aligned coordinates) and start
+         * just before `start`: earlier positions cannot reach ends >= start */
+        int64_t blo = (int64_t)b.base + mis;
+        b.org = (blo + std::max<int64_t>(0, st - 16)) & ~(int64_t)1023;
+        if (b.start < b.len) {
+            int64_t span = blo + len - b.org;
+            segs += (uint64_t)((span + (1ll << seg_shift) - 1) >> seg_shift);
+        }
     }
     VSA_CHECK(hipMemcpyAsync(c->ws.d_blocks, c->ws.h_blocks, nb * sizeof(VsaBlock),
                              hipMemcpyHostToDevice, c->stream));
@@ -666,6 +697,7 @@ void *vsa_ctx_stream(vsa_ctx_t *c) { return c ? (void *)c->stream : nullptr; }
 
 int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
     if (!c || !hwlm || !out || size < VSA_ROUNDUP_CL(sizeof(HWLM))) return VSA_E_INVALID;
+    VSA_CHECK(hipSetDevice(c->device));
     std::unique_ptr<vsa_db> db(new vsa_db());
     db->ctx = c;
     db->host.resize(size + 64);
@@ -700,6 +732,31 @@ int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
         }
         const uint32_t *confBase = (const uint32_t *)(eng + ((const uint32_t *)eng)[4]);
         for (uint32_t b = 0; b < db->nbuckets; b++) db->conf_off[b] = confBase[b];
+        /* prefilter bitmaps: bit h of bucket b = (litIndex_b[h] != 0) */
+        std::vector<uint32_t> slots;
+        for (uint32_t b = 0; b < 16; b++) db->slot_off[b] = 0xffffffffu;
+        const bool no_pf = getenv("VSA_NO_PREFILTER") != nullptr;
+        for (uint32_t b = 0; b < db->nbuckets && !no_pf; b++) {
+            if (!db->conf_off[b]) continue;
+            const uint8_t *fc = (const uint8_t *)confBase + db->conf_off[b];
+            const uint32_t nbits = *(const uint32_t *)(fc + 16);
+            if (nbits > 24) continue;
+            const uint32_t n = 1u << nbits;
+            const uint32_t words = (n + 31) / 32;
+            if (slots.size() + words > SLOT_WORDS_MAX) continue;
+            const uint32_t *li = (const uint32_t *)(fc + 32);
+            db->slot_off[b] = (uint32_t)slots.size();
+            slots.resize(slots.size() + words, 0);
+            for (uint32_t h = 0; h < n; h++) {
+                if (li[h]) slots[db->slot_off[b] + h / 32] |= 1u << (h % 32);
+            }
+        }
+        db->slot_words = (uint32_t)slots.size();
+        if (!slots.empty()) {
+            VSA_CHECK(hipMalloc(&db->d_slots, slots.size() * 4));
+            VSA_CHECK(hipMemcpy(db->d_slots, slots.data(), slots.size() * 4,
+                                hipMemcpyHostToDevice));
+        }
     } else {
         return VSA_E_INVALID;
     }
@@ -738,6 +795,7 @@ int vsa_db_free(vsa_db_t *db) {
     if (!db) return VSA_E_INVALID;
     if (db->d_blob) (void)hipFree(db->d_blob);
     if (db->d_table) (void)hipFree(db->d_table);
+    if (db->d_slots) (void)hipFree(db->d_slots);
     for (auto it = t_registry.begin(); it != t_registry.end(); ++it) {
         if (it->second == db) {
             t_registry.erase(it);
