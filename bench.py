@@ -162,6 +162,7 @@ def main():
     barrier()
     t1 = time.perf_counter()
     el = t1 - t0
+    ncand = int(ctx.candidates())  # of the last timed step
     if dist is not None:
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -225,7 +226,7 @@ def main():
                                    (args.lits, args.gib, args.blocks, blob.engine_id),
                        "global_bytes": world * n, "parallelism": "stripe%d" % world},
             "matches": total_matches,
-            "candidates": int(ctx.candidates()),
+            "confirm_candidates": ncand,
             "parity": parity,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

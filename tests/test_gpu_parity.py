@@ -250,3 +250,24 @@ def test_gpu_class_scan_256mib(ctx):
     assert np.array_equal(bm, exp)
     idx = np.nonzero(member)[0]
     assert cnt == len(idx) and f == idx[0] and l == idx[-1] + 1
+
+
+@pytest.mark.gpu
+def test_gpu_dropin_reused_address():
+    """A database freed and rebuilt at the same address (same size, other
+    content) must not be served from the drop-in's cached device copy."""
+    import ctypes
+    lits_a = [vsa.HwlmLiteral(s, False, i) for i, s in enumerate(
+        [b"abcdef", b"bcdefg", b"xyzw", b"hello", b"world"] * 20)]
+    lits_b = [vsa.HwlmLiteral(l.s, False, l.id + 1000) for l in lits_a]
+    a, b = vsa.hwlm_build(lits_a), vsa.hwlm_build(lits_b)
+    assert a.size == b.size and a.tobytes() != b.tobytes()
+    raw = ctypes.create_string_buffer(a.size + 64)
+    base = (ctypes.addressof(raw) + 63) & ~63
+    data = b"..abcdefg..hello world xyzw" * 50
+    shared = vsa.Blob(base, a.size, owned=False)
+    for blob in (a, b, a):
+        ctypes.memmove(base, blob.ptr, blob.size)
+        _, m_g = vsa.hwlm_exec(shared, data)
+        _, m_o = oracle.hwlm_exec(blob.ptr, data, cap=1 << 16)
+        assert m_g == m_o and m_g

@@ -160,9 +160,10 @@ class HwlmLiteral:
 class Blob:
     """An HWLM bytecode blob (reference layout) owned by the C library."""
 
-    def __init__(self, ptr, size):
+    def __init__(self, ptr, size, owned=True):
         self.ptr = ptr
         self.size = size
+        self.owned = owned  # False: a view of memory the caller owns
 
     def tobytes(self):
         return ctypes.string_at(self.ptr, self.size)
@@ -189,9 +190,9 @@ class Blob:
         _check(lib.vsa_hwlm_set_accel(self.ptr, a0, a1, accel1_groups))
 
     def __del__(self):
-        if getattr(self, "ptr", None):
+        if getattr(self, "ptr", None) and getattr(self, "owned", True):
             lib.vsa_blob_free(self.ptr)
-            self.ptr = None
+        self.ptr = None
 
 
 class BuildError(RuntimeError):

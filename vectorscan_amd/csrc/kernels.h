@@ -54,12 +54,15 @@ struct VsaLitParams {
     uint32_t qcap;               /* per-wave LDS confirm-queue entries */
     uint32_t dbg;                /* debug: bit0 verify queued keys against HBM
                                     (mismatches -> counters[3]); bit1 drop all
-                                    candidates (filter-only timing) */
+                                    candidates (filter-only timing); bit3 stop
+                                    after the candidate test; bit4 skip the
+                                    push; bit5 count first-stage candidates */
     uint64_t *out_keys;
     uint32_t *out_ids;
     uint64_t out_cap;
     unsigned long long *counters; /* [0] matches, [1] segment ticket,
-                                     [2] candidates (diagnostic) */
+                                     [2] candidates handed to confirm (after
+                                     the slot prefilter; diagnostic) */
 };
 
 struct VsaNoodParams {

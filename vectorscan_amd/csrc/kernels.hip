@@ -120,12 +120,19 @@ struct LitTraits<VSA_MODE_FAT> {
 };
 
 /* per-bucket confirm parameters staged in LDS (FDRConfirm, fdr_confirm.h:78) */
+struct PfRec {
+    u64 andmsk, mult;
+    u32 slot_off; /* word offset of the bucket's slot bitmap, ~0 = none */
+    u32 shift;    /* 64 - nBits */
+    u32 pad[2];
+};
+
 struct ConfLds {
     u64 andmsk[16];
     u64 mult[16];
     u32 nbits[16];
     u32 off[16];
-    u32 slot_off[16]; /* word offset of the bucket's slot bitmap, ~0 = none */
+    PfRec pf[16]; /* one 32-B record per bucket for the scanners' prefilter */
 };
 
 /* queue entry: meta = aoff << 24 | blk << 4 | bucket; key = 8 bytes ending
@@ -135,12 +142,30 @@ struct QEnt {
     u64 key;
 };
 
+/* Candidates go from each scanning wave to the workgroup's confirm wave
+ * through the scanning wave's own LDS ring of rsize (power of two) entries.
+ * The scanner owns *head (entries written, published after the entries),
+ * the confirm wave owns *tail (entries consumed).  LDS executes one wave's
+ * instructions in order, so a published head implies visible entries. */
 struct LitShared {
     const void *tab;
-    QEnt *queue; /* this wave's QCAP entries */
-    u32 *qcount; /* this wave's counter (LDS) */
+    QEnt *ring;      /* this wave's ring */
+    u32 *head_pub;   /* this wave's published head */
+    const u32 *tail; /* this wave's tail (written by the confirm wave) */
     const u32 *slots;
-    u32 qcap;
+    u32 rmask;
+};
+
+__device__ __forceinline__ u32 lds_ld32(const u32 *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st32(u32 *p, u32 v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+/* wave-uniform ring cursor of a scanning wave */
+struct RingCur {
+    u32 head, tail_cache;
 };
 
 __device__ __forceinline__ u32 conf_hash(u64 key, u64 andmsk, u64 mult, u32 nbits) {
@@ -194,25 +219,6 @@ __device__ __forceinline__ void confirm_one(const VsaLitParams &P, const ConfLds
     } while (next);
 }
 
-/* confirm 64 queued candidates per round while at least `keep` remain */
-__device__ __forceinline__ void drain_queue(const VsaLitParams &P, const ConfLds &cl,
-                                            const LitShared &L, u32 mis, u32 keep) {
-    const u32 lane = lane_id();
-    u32 qn = readfirstlane_u32(*L.qcount);
-    while (qn > keep) {
-        u32 take = qn - keep < (u32)WAVE ? qn - keep : (u32)WAVE;
-        if (lane < take) {
-            QEnt q = L.queue[qn - take + lane];
-            confirm_one(P, cl, q.meta, q.key, mis);
-        }
-        qn -= take;
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) *L.qcount = qn;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
 template <int MODE, bool LDS_TABLE>
 __device__ __forceinline__ u64 lit_lookup(const void *tab, u32 key, u32 lane) {
     if constexpr (MODE == VSA_MODE_FDR) {
@@ -242,6 +248,8 @@ struct IterState {
     u64 carry;  /* pending table contributions into the next chunk's first ends */
     u64 pbytes; /* the 8 bytes before the next chunk (lane 63's d[2..3]) */
     u32 ncand;  /* first-stage candidates so far (diagnostic, wave-uniform) */
+    u32 head;   /* ring entries written by this wave (wave-uniform) */
+    u32 tail_cache; /* last tail read from the confirm wave */
 };
 
 struct SegCtx {
@@ -316,6 +324,8 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     if (lane == 0) s_in = in.carry;
     IterState out;
     out.ncand = in.ncand;
+    out.head = in.head;
+    out.tail_cache = in.tail_cache;
     out.carry = ((u64)readlane_u32((u32)(s_out >> 32), WAVE - 1) << 32) |
                 readlane_u32((u32)s_out, WAVE - 1);
     out.pbytes = ((u64)readlane_u32(d[3], WAVE - 1) << 32) | readlane_u32(d[2], WAVE - 1);
@@ -354,6 +364,16 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
         any |= c[i];
     }
     if (!__any(any != 0)) return out;
+    if (P.dbg & 32) {
+        /* diagnostic first-stage candidate count */
+        u32 pc = 0;
+#pragma unroll
+        for (int i = 0; i < T::CW; i++) pc += __popc(c[i]);
+#pragma unroll
+        for (int dd = 32; dd >= 1; dd >>= 1) pc += shfl_xor_u32(pc, dd);
+        out.ncand += readfirstlane_u32(pc);
+    }
+    if (P.dbg & 8) return out;
 
     /* bytes p0-8 .. p0+15 for the 8-byte confirm keys */
     u32 pv2 = shfl_up_u32(d[2], 1), pv3 = shfl_up_u32(d[3], 1);
@@ -364,59 +384,73 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     const u64 W0 = ((u64)pv3 << 32) | pv2;
     const u64 W1 = ((u64)d[1] << 32) | d[0];
     const u64 W2 = ((u64)d[3] << 32) | d[2];
-    u32 ncand = 0;
+    /* Wave-uniform loop: each round every lane takes its lowest remaining
+     * candidate bit (over all conf words), so the rounds are the largest
+     * per-lane count, not words x bits.  The ring cursor is updated by every
+     * lane each round and stays wave-uniform. */
+    for (;;) {
+        u32 word = 0, bits = c[0];
 #pragma unroll
-    for (int i = 0; i < T::CW; i++) {
-        u32 bits = c[i];
-        while (bits) {
+        for (int k = 1; k < T::CW; k++) {
+            const bool take = bits == 0;
+            bits = take ? c[k] : bits;
+            word = take ? (u32)k : word;
+        }
+        const bool have = bits != 0;
+        if (!__any(have)) break;
+        bool push = false;
+        u64 key = 0, meta = 0;
+        if (have) {
             const u32 bit = __ffs(bits) - 1;
-            bits &= bits - 1;
+#pragma unroll
+            for (int k = 0; k < T::CW; k++)
+                if (word == (u32)k) c[k] &= c[k] - 1;
             u32 j, b;
             if constexpr (T::LB == 8) {
-                j = 4 * i + (bit >> 3);
+                j = 4 * word + (bit >> 3);
                 b = bit & 7;
             } else {
-                j = 2 * i + (bit >> 4);
+                j = 2 * word + (bit >> 4);
                 b = bit & 15;
             }
-            ncand++;
             /* key = bytes [j-7, j] = byte offset j+1 .. j+8 of W0:W1:W2 */
             const u32 o = j + 1;
-            u64 key;
             if (o < 8) key = (W0 >> (8 * o)) | (W1 << (64 - 8 * o));
             else if (o == 8) key = W1;
             else if (o < 16) key = (W1 >> (8 * (o - 8))) | (W2 << (64 - 8 * (o - 8)));
             else key = W2;
             /* LDS slot-bitmap prefilter: litIndex[hash] == 0 rejects */
-            const u32 so = cl.slot_off[b];
-            if (so != 0xffffffffu) {
-                const u32 h = conf_hash(key, cl.andmsk[b], cl.mult[b], cl.nbits[b]);
-                if (!((L.slots[so + (h >> 5)] >> (h & 31)) & 1u)) continue;
+            const PfRec pf = cl.pf[b];
+            push = true;
+            if (pf.slot_off != 0xffffffffu) {
+                const u32 h = (u32)(((key & pf.andmsk) * pf.mult) >> pf.shift);
+                push = (L.slots[pf.slot_off + (h >> 5)] >> (h & 31)) & 1u;
             }
-            const u64 meta = ((u64)(p0 + j) << 24) | ((u64)S.blk << 4) | b;
-            const u32 slot = atomicAdd(L.qcount, 1u);
-            if (slot < L.qcap) {
-                L.queue[slot].meta = meta;
-                L.queue[slot].key = key;
-            } else {
-                confirm_one(P, cl, meta, key, mis);
+            if (P.dbg & 16) push = false;
+            meta = ((u64)(p0 + j) << 24) | ((u64)S.blk << 4) | b;
+        }
+        const u64 pm = __ballot(push);
+        if (pm == 0) continue;
+        const u32 n = (u32)__popcll(pm);
+        /* room for n entries (the confirm wave frees them in order) */
+        if (out.head + n - out.tail_cache > L.rmask + 1) {
+            for (;;) {
+                out.tail_cache = readfirstlane_u32(lds_ld32(L.tail));
+                if (out.head + n - out.tail_cache <= L.rmask + 1) break;
+                __builtin_amdgcn_s_sleep(2);
             }
         }
+        if (push) {
+            const u32 r = __builtin_amdgcn_mbcnt_hi((u32)(pm >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((u32)pm, 0));
+            QEnt *q = &L.ring[(out.head + r) & L.rmask];
+            q->meta = meta;
+            q->key = key;
+        }
+        out.head += n;
+        asm volatile("" ::: "memory"); /* entries before the head (LDS order) */
+        if (lane == 0) lds_st32(L.head_pub, out.head);
     }
-    {
-        u32 tot = ncand;
-#pragma unroll
-        for (int dd = 32; dd >= 1; dd >>= 1) tot += shfl_xor_u32(tot, dd);
-        out.ncand += readfirstlane_u32(tot);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    u32 qn = readfirstlane_u32(*L.qcount);
-    if (qn > L.qcap) {
-        if (lane == 0) *L.qcount = L.qcap;
-        qn = L.qcap;
-    }
-    if (qn >= (u32)WAVE) drain_queue(P, cl, L, mis, qn % WAVE);
     return out;
 }
 
@@ -439,6 +473,57 @@ __device__ __forceinline__ uint4 load_chunk_nc(const u8 *A, int64_t p0) {
 
 #define LIT_DEPTH 4
 
+/* The workgroup's confirm wave: gathers up to 64 entries per round from the
+ * scanning waves' rings (each consumed in order) and runs the exact
+ * confirm.  Its global-memory latency never stalls a scanning wave.  Exits
+ * once every scanning wave has finished (q_done, read before the heads) and
+ * every ring is empty. */
+#define LIT_SCANNERS (LIT_WAVES - 1)
+__device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLds &cl,
+                                             const QEnt *rings, u32 rsize, const u32 *heads,
+                                             u32 *tails, const u32 *q_done, u32 mis) {
+    const u32 lane = lane_id();
+    u32 rr = 0; /* round-robin start */
+    u32 consumed = 0;
+    for (;;) {
+        const bool all_done = lds_ld32(q_done) == LIT_SCANNERS;
+        asm volatile("" ::: "memory");
+        u32 filled = 0;
+        u64 meta = 0, key = 0;
+        bool mine = false;
+        for (u32 i = 0; i < LIT_SCANNERS && filled < (u32)WAVE; i++) {
+            u32 w = rr + i;
+            if (w >= LIT_SCANNERS) w -= LIT_SCANNERS;
+            const u32 h = readfirstlane_u32(lds_ld32(&heads[w]));
+            const u32 t = readfirstlane_u32(lds_ld32(&tails[w]));
+            asm volatile("" ::: "memory");
+            const u32 avail = h - t;
+            if (!avail) continue;
+            const u32 take = min(avail, (u32)WAVE - filled);
+            if (lane >= filled && lane < filled + take) {
+                const QEnt e = rings[(size_t)w * rsize + ((t + lane - filled) & (rsize - 1))];
+                meta = e.meta;
+                key = e.key;
+                mine = true;
+            }
+            filled += take;
+            asm volatile("" ::: "memory");
+            if (lane == 0) lds_st32(&tails[w], t + take);
+        }
+        rr = rr + 1 == LIT_SCANNERS ? 0 : rr + 1;
+        consumed += filled;
+        if (filled == 0) {
+            if (all_done) break;
+            __builtin_amdgcn_s_sleep(4);
+            continue;
+        }
+        if (mine) confirm_one(P, cl, meta, key, mis);
+    }
+    /* confirm-stage candidates (first-stage count instead under dbg & 32) */
+    if (P.counters && lane == 0 && consumed && !(P.dbg & 32))
+        atomicAdd(&P.counters[2], (unsigned long long)consumed);
+}
+
 template <int MODE, bool LDS_TABLE>
 __global__ void __launch_bounds__(LIT_THREADS)
 vsa_lit_scan(VsaLitParams P) {
@@ -446,7 +531,7 @@ vsa_lit_scan(VsaLitParams P) {
     typedef typename T::S_t S_t;
     extern __shared__ __align__(16) u8 smem[];
     __shared__ ConfLds cl;
-    __shared__ u32 qcounts[LIT_WAVES];
+    __shared__ u32 q_heads[LIT_WAVES], q_tails[LIT_WAVES], q_done;
     const u32 tid = threadIdx.x;
     const u32 lane = lane_id();
     const u32 wave = tid / WAVE;
@@ -476,27 +561,42 @@ vsa_lit_scan(VsaLitParams P) {
         for (u32 i = tid; i < 256 * 32; i += LIT_THREADS) dst[i] = P.table[i >> 5];
         tab = smem;
     }
-    QEnt *queues = (QEnt *)(smem + ((tab_bytes + 15) & ~15u));
-    u32 *slots = (u32 *)(queues + (size_t)LIT_WAVES * P.qcap);
+    QEnt *rings = (QEnt *)(smem + ((tab_bytes + 15) & ~15u));
+    u32 *slots = (u32 *)(rings + (size_t)LIT_SCANNERS * P.qcap);
     for (u32 i = tid; i < P.slot_words; i += LIT_THREADS) slots[i] = P.slotmap[i];
     if (tid < 16) {
-        u32 off = P.conf_off[tid];
+        const u32 off = P.conf_off[tid];
         cl.off[tid] = off;
-        cl.slot_off[tid] = P.slot_off[tid];
+        PfRec pf;
+        pf.slot_off = P.slot_off[tid];
+        pf.pad[0] = pf.pad[1] = 0;
         if (off) {
             const u8 *fc = P.conf_base + off;
-            cl.andmsk[tid] = *(const u64 *)fc;
-            cl.mult[tid] = *(const u64 *)(fc + 8);
+            cl.andmsk[tid] = pf.andmsk = *(const u64 *)fc;
+            cl.mult[tid] = pf.mult = *(const u64 *)(fc + 8);
             cl.nbits[tid] = *(const u32 *)(fc + 16);
+            pf.shift = 64 - cl.nbits[tid];
         } else {
-            cl.andmsk[tid] = 0;
-            cl.mult[tid] = 0;
+            cl.andmsk[tid] = pf.andmsk = 0;
+            cl.mult[tid] = pf.mult = 0;
             cl.nbits[tid] = 1;
-            cl.slot_off[tid] = 0xffffffffu;
+            pf.shift = 63;
+            pf.slot_off = 0xffffffffu;
         }
+        cl.pf[tid] = pf;
     }
-    if (tid < LIT_WAVES) qcounts[tid] = 0;
+    if (tid < LIT_WAVES) {
+        q_heads[tid] = 0;
+        q_tails[tid] = 0;
+    }
+    if (tid == 0) q_done = 0;
     __syncthreads();
+
+    const u32 mis = (u32)((uintptr_t)P.data & 15);
+    if (wave == LIT_WAVES - 1) {
+        confirm_wave(P, cl, rings, P.qcap, q_heads, q_tails, &q_done, mis);
+        return;
+    }
 
     u32 bucket_mask = 0;
     if (!(P.dbg & 2)) {
@@ -513,15 +613,16 @@ vsa_lit_scan(VsaLitParams P) {
     }
     LitShared L;
     L.tab = tab;
-    L.queue = queues + (size_t)wave * P.qcap;
-    L.qcount = &qcounts[wave];
+    L.ring = rings + (size_t)wave * P.qcap;
+    L.head_pub = &q_heads[wave];
+    L.tail = &q_tails[wave];
     L.slots = slots;
-    L.qcap = P.qcap;
+    L.rmask = P.qcap - 1;
 
-    const u32 mis = (u32)((uintptr_t)P.data & 15);
     const u8 *A = P.data - mis;
     const int64_t SEG = (int64_t)1 << P.seg_shift;
     u32 ncand_total = 0;
+    u32 ring_head = 0, ring_tail_cache = 0;
 
     for (;;) {
         unsigned long long t = 0;
@@ -548,6 +649,8 @@ vsa_lit_scan(VsaLitParams P) {
         /* prologue 1: table spill from positions s_lo-NL+1 .. s_lo-1 */
         IterState is;
         is.ncand = ncand_total;
+        is.head = ring_head;
+        is.tail_cache = ring_tail_cache;
         {
             S_t x = 0;
             if (lane < (u32)(T::NL - 1)) {
@@ -658,9 +761,11 @@ vsa_lit_scan(VsaLitParams P) {
                                                  bucket_mask);
         }
         ncand_total = is.ncand;
+        ring_head = is.head;
+        ring_tail_cache = is.tail_cache;
     }
-    /* drain the wave's queue */
-    drain_queue(P, cl, L, mis, 0);
+    /* every push of this wave precedes this (LDS order) */
+    if (lane == 0) __hip_atomic_fetch_add(&q_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (P.counters && lane_id() == 0 && ncand_total)
         atomicAdd(&P.counters[2], (unsigned long long)ncand_total);
 }

@@ -195,13 +195,16 @@ int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds) {
 }
 
 /* LDS plan: table + per-wave queues (QEnt 16 B) + slot bitmaps */
+/* dynamic LDS = table + one confirm ring per scanning wave (power of two,
+ * 64..1024 entries of 16 B) + slot bitmaps */
 size_t plan_lds(size_t tab, uint32_t slot_words, uint32_t *qcap) {
+    const size_t scanners = LIT_WAVES - 1;
+    tab = (tab + 15) & ~(size_t)15;
     size_t rest = LDS_BUDGET > tab + slot_words * 4 ? LDS_BUDGET - tab - slot_words * 4 : 0;
-    uint32_t q = (uint32_t)std::min<size_t>(128, rest / (16 * LIT_WAVES));
-    q &= ~63u;
-    if (q < 64) q = 64;
+    uint32_t q = 64;
+    while (q < 1024 && (size_t)(2 * q) * 16 * scanners <= rest) q *= 2;
     *qcap = q;
-    return tab + (size_t)q * 16 * LIT_WAVES + (size_t)slot_words * 4;
+    return tab + (size_t)q * 16 * scanners + (size_t)slot_words * 4;
 }
 
 int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
@@ -392,25 +395,18 @@ vsa_ctx *default_ctx() {
     return t_ctx;
 }
 
+/* Keyed by (pointer, size); every lookup also compares the whole blob with
+ * the cached host copy, so a database freed and re-allocated at the same
+ * address is never served from a stale device copy (memcmp runs at memory
+ * speed, ~20 us for a 0.4 MB FDR blob). */
 struct RegKey {
     const void *p;
     size_t size;
-    uint64_t hash;
     bool operator<(const RegKey &o) const {
         if (p != o.p) return p < o.p;
-        if (size != o.size) return size < o.size;
-        return hash < o.hash;
+        return size < o.size;
     }
 };
-
-uint64_t fnv(const uint8_t *p, size_t n) {
-    uint64_t h = 1469598103934665603ULL;
-    for (size_t i = 0; i < n; i++) {
-        h ^= p[i];
-        h *= 1099511628211ULL;
-    }
-    return h;
-}
 
 thread_local std::map<RegKey, vsa_db *> t_registry;
 
@@ -434,9 +430,14 @@ vsa_db *registry_get(const void *ptr, int bare_type) {
         type = bare_type;
         size = engine_size(p, type);
     }
-    RegKey k{ptr, size, fnv(p, std::min<size_t>(size, 1024))};
+    RegKey k{ptr, size};
     auto it = t_registry.find(k);
-    if (it != t_registry.end()) return it->second;
+    if (it != t_registry.end()) {
+        vsa_db *old = it->second;
+        const uint8_t *cached = old->hblob + (bare_type < 0 ? 0 : VSA_ROUNDUP_CL(sizeof(HWLM)));
+        if (memcmp(cached, p, size) == 0) return old;
+        vsa_db_free(old); /* erases the registry entry */
+    }
     vsa_db *db = nullptr;
     int r;
     if (bare_type < 0) {
