@@ -10,8 +10,10 @@ resident in HBM before the timed region.
 
 Multi-GPU: one process per GPU (torch.distributed, RCCL); every rank scans
 its own 4 GiB stripe of an N x 4 GiB corpus (weak scaling, no data-path
-collective); the timed region is bracketed by barrier + synchronize and the
-max over ranks is reported.
+collective in the scan); each step ends with the RCCL gather of the ranks'
+sorted match records to rank 0 (where the sequential host replay runs,
+vectorscan_amd/stripe.py).  The timed region is bracketed by barrier +
+synchronize and the max over ranks is reported.
 
 Extra JSON fields: roofline (kernel-only HBM GB/s from hipEvents vs the 8 TB/s
 MI355X peak), cpu_baseline (the scalar oracle on a bounded sample of the
@@ -114,6 +116,7 @@ def main():
 
     import torch
     import vectorscan_amd as vsa
+    from vectorscan_amd import stripe
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -140,8 +143,26 @@ def main():
     lens = [bl] * (args.blocks - 1) + [n - bl * (args.blocks - 1)]
     dptr = data.data_ptr()
 
+    # N > 1: the step ends with the RCCL gather of every rank's sorted match
+    # records to rank 0 (device to device, over xGMI), where the host replay
+    # would run; the scan itself has no data-path collective.
+    gcap = 1 << 21
+    gkeys = torch.zeros(gcap, dtype=torch.int64, device=dev) if dist is not None else None
+    gids = torch.zeros(gcap, dtype=torch.int32, device=dev) if dist is not None else None
+    gathered = [0]
+
     def step():
-        return ctx.scan_blocks(db, dptr, offs, lens)
+        n_local = ctx.scan_blocks(db, dptr, offs, lens)
+        if dist is None:
+            return n_local
+        if n_local > gcap:
+            raise RuntimeError("bench: %d matches exceed the gather buffer" % n_local)
+        ctx.results_to_device(gkeys.data_ptr(), gids.data_ptr(), gcap)
+        ctx.sync()
+        got = stripe.gather_to_root(dist, gkeys, gids, n_local)
+        if got is not None:
+            gathered[0] = int(got[0].shape[0])
+        return n_local
 
     for _ in range(args.warmup):
         step()
@@ -226,6 +247,7 @@ def main():
                                    (args.lits, args.gib, args.blocks, blob.engine_id),
                        "global_bytes": world * n, "parallelism": "stripe%d" % world},
             "matches": total_matches,
+            "gathered_to_rank0": gathered[0] if dist is not None else None,
             "confirm_candidates": ncand,
             "parity": parity,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

@@ -149,7 +149,13 @@ int vsa_scan_results(vsa_ctx_t *ctx, const uint64_t **d_keys,
 /* Copy up to cap results of the last scan to the host. */
 int vsa_scan_copy(vsa_ctx_t *ctx, vsa_match_t *out, uint64_t cap,
                   uint64_t *n_copied);
-/* Candidates the first stage handed to confirm in the last scan. */
+/* Device-to-device copy (on the context's stream, not waited for) of up to
+ * cap results of the last scan into caller-owned device buffers (either may
+ * be NULL), e.g. tensors handed to an RCCL gather. */
+int vsa_scan_copy_device(vsa_ctx_t *ctx, uint64_t *d_keys, uint32_t *d_ids, uint64_t cap,
+                         uint64_t *n_copied);
+/* Candidates handed to the confirm stage (after the LDS slot prefilter) in
+ * the last scan. */
 uint64_t vsa_scan_candidates(vsa_ctx_t *ctx);
 /* Device time (ms, hipEvents on the scan stream) of the last scan kernel. */
 double vsa_scan_kernel_ms(vsa_ctx_t *ctx);

@@ -1,0 +1,134 @@
+"""Multi-rank striping of one block (vectorscan_amd/stripe.py), world size 2
+over gloo on CPU.  Each rank's window is scanned by the test-only oracle in
+place of the device (the device path is covered by test_gpu_parity); the
+gathered union must equal the single-block scan."""
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+import vectorscan_amd as vsa
+from vectorscan_amd import stripe as st
+from test_cpu_oracle import rand_lits
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _case(seed, nlits, length):
+    rng = random.Random(seed)
+    lits = rand_lits(rng, nlits, minlen=1, maxlen=8, msk_frac=0.1)
+    for l in lits:
+        l.noruns = False  # NOREPEAT is sequential host state, replayed after the gather
+    blob = vsa.hwlm_build(lits)
+    r = np.random.default_rng(seed)
+    data = bytes(r.choice(np.frombuffer(b"abcdefghABCD", np.uint8), length))
+    return blob, data
+
+
+def _worker(rank, world, port, seed, nlits, length, start, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        blob, data = _case(seed, nlits, length)
+        plan = st.plan_block_stripes(len(data), start, world, min_stripe=64)
+        s = plan[rank]
+        win = data[s.wlo:s.wlo + s.wlen]
+        _, m = oracle.hwlm_exec(blob.ptr, win, start=s.wstart, cap=1 << 20) if s.wlen else (0, [])
+        ends = [e for e, _ in m]
+        ids = [i for _, i in m]
+        e, i = st.localize(s, ends, ids)
+        ge, gi = st.gather_matches(dist, e, i)
+        if rank == 0:
+            q.put(list(zip(ge.tolist(), gi.tolist())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("seed,nlits,length,start", [
+    (1, 40, 5000, 0),      # Teddy
+    (2, 300, 20000, 0),    # FDR
+    (3, 300, 20000, 333),  # FDR, start inside rank 0's stripe
+    (4, 5, 3000, 2900),    # start inside rank 1's stripe
+    (5, 20, 40, 0),        # too short to split: rank 0 scans it whole
+])
+def test_striped_block_equals_single_scan(seed, nlits, length, start):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, seed, nlits, length, start, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    blob, data = _case(seed, nlits, length)
+    _, want = oracle.hwlm_exec(blob.ptr, data, start=start, cap=1 << 20)
+    assert got == want
+    assert len(want) > 0 or length < 64
+
+
+def test_plan_covers_every_end_once():
+    for length, start, world in [(10 ** 6, 0, 8), (10 ** 6, 12345, 8), (100, 0, 4),
+                                 (1 << 20, (1 << 20) - 5, 2)]:
+        plan = st.plan_block_stripes(length, start, world, min_stripe=64)
+        owned = []
+        for s in plan:
+            assert s.wlo + s.wlen <= length
+            if s.own_hi > s.own_lo:
+                assert s.wlo <= max(0, s.own_lo - st.HALO) or s.wlo == 0
+                assert s.wlo + s.wlen == s.own_hi
+                owned.append((s.own_lo, s.own_hi))
+        assert owned[0][0] == start
+        assert owned[-1][1] == length
+        for (a, b), (c, d) in zip(owned, owned[1:]):
+            assert b == c
+
+
+def _gather_worker(rank, world, port, q):
+    import torch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = [5, 0, 3][rank]
+        keys = torch.arange(8, dtype=torch.int64) + 100 * rank
+        ids = torch.arange(8, dtype=torch.int32) + 10 * rank
+        got = st.gather_to_root(dist, keys, ids, n)
+        if rank == 0:
+            q.put((got[0].tolist(), got[1].tolist()))
+        else:
+            assert got is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_to_root_world3():
+    """bench.py's per-step gather (uneven counts, one empty rank)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    keys, ids = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert keys == [0, 1, 2, 3, 4, 200, 201, 202]
+    assert ids == [0, 1, 2, 3, 4, 20, 21, 22]

@@ -125,6 +125,8 @@ _sig("vsa_scan_results", ctypes.c_int, ctypes.c_void_p,
      ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p))
 _sig("vsa_scan_copy", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_uint64, _u64p)
+_sig("vsa_scan_copy_device", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+     ctypes.c_uint64, _u64p)
 _sig("vsa_scan_candidates", ctypes.c_uint64, ctypes.c_void_p)
 _sig("vsa_scan_kernel_ms", ctypes.c_double, ctypes.c_void_p)
 _sig("vsa_class_scan", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -443,6 +445,13 @@ class Context:
         got = ctypes.c_uint64()
         _check(lib.vsa_scan_copy(self.ptr, out.ctypes.data, n, ctypes.byref(got)))
         return out[: got.value]
+
+    def results_to_device(self, d_keys, d_ids, cap):
+        """Copy up to cap results of the last scan into caller device buffers
+        (stream-ordered on this context's stream); returns the count."""
+        got = ctypes.c_uint64()
+        _check(lib.vsa_scan_copy_device(self.ptr, d_keys, d_ids, cap, ctypes.byref(got)))
+        return got.value
 
     def candidates(self):
         return lib.vsa_scan_candidates(self.ptr)

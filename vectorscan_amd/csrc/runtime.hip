@@ -903,6 +903,22 @@ int vsa_scan_copy(vsa_ctx_t *c, vsa_match_t *out, uint64_t cap, uint64_t *n_copi
     return VSA_OK;
 }
 
+int vsa_scan_copy_device(vsa_ctx_t *c, uint64_t *d_keys, uint32_t *d_ids, uint64_t cap,
+                         uint64_t *n_copied) {
+    if (!c) return VSA_E_INVALID;
+    const uint64_t n = std::min(cap, c->last_n);
+    if (n) {
+        if (d_keys)
+            VSA_CHECK(hipMemcpyAsync(d_keys, c->ws.d_keys[c->cur], n * 8,
+                                     hipMemcpyDeviceToDevice, c->stream));
+        if (d_ids)
+            VSA_CHECK(hipMemcpyAsync(d_ids, c->ws.d_ids[c->cur], n * 4,
+                                     hipMemcpyDeviceToDevice, c->stream));
+    }
+    if (n_copied) *n_copied = n;
+    return VSA_OK;
+}
+
 uint64_t vsa_scan_candidates(vsa_ctx_t *c) { return c ? c->last_cand : 0; }
 
 double vsa_scan_kernel_ms(vsa_ctx_t *c) { return c ? c->last_kernel_ms : 0.0; }

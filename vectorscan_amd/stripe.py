@@ -1,0 +1,128 @@
+"""Striping one hwlmExec block across ranks.
+
+HWLM literals are at most 8 bytes (hwlm.h:75, HWLM_MASKLEN 8), so a match
+ending at e depends only on bytes [e-7, e].  Rank r owns the end positions
+[lo_r, hi_r) of the block and scans the window [lo_r - 7, hi_r) as its own
+block (start 0, or the block's `start` mapped into the window); matches that
+end in the 7-byte halo belong to rank r-1 and are dropped.  Every owned end
+sees the same bytes, the same first-stage lookups (the window's lookups begin
+at or before lo_r - 7 >= the block's start) and the same confirm key as in
+the one-GPU scan, so the union over ranks is exactly the single-block match
+set, already in rank = end order.  No data-path collective: the only
+exchange is gathering the (small) match lists to rank 0, which then runs the
+sequential host replay (NOREPEAT, groups, terminate) in global order.
+
+The gathers use torch.distributed (RCCL over xGMI with backend "nccl" and
+device tensors; gloo with CPU tensors in the tests): one all_gather of the
+per-rank counts, then the records padded to the largest count
+(gather_matches: all_gather of host lists; gather_to_root: dist.gather of
+device tensors to one rank, used by bench.py).
+"""
+from dataclasses import dataclass
+
+import numpy as np
+
+HALO = 7  # max literal length (8) - 1
+
+
+@dataclass
+class Stripe:
+    rank: int
+    wlo: int     # window start (block-relative)
+    wlen: int    # window length
+    wstart: int  # hwlmExec start inside the window
+    own_lo: int  # first owned end (block-relative)
+    own_hi: int  # one past the last owned end
+
+
+def plan_block_stripes(length, start, world, min_stripe=1 << 16):
+    """Split one block of `length` bytes (hwlmExec start `start`) into
+    `world` stripes.  Blocks too short to split (or with a short first zone,
+    fdr.c:712-720) go to rank 0 whole.  Returns one Stripe per rank (empty
+    stripes have own_lo == own_hi)."""
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    out = []
+    if length - start <= max(16, min_stripe) or world == 1:
+        for r in range(world):
+            if r == 0:
+                out.append(Stripe(0, 0, length, start, start, length))
+            else:
+                out.append(Stripe(r, length, 0, 0, length, length))
+        return out
+    span = length - start
+    cuts = [start + (span * r) // world for r in range(world + 1)]
+    for r in range(world):
+        lo, hi = cuts[r], cuts[r + 1]
+        wlo = 0 if r == 0 else max(0, lo - HALO)
+        wstart = start if r == 0 else max(start - wlo, 0)
+        out.append(Stripe(r, wlo, hi - wlo, wstart, lo, hi))
+    return out
+
+
+def localize(stripe, ends, ids):
+    """Window-relative results -> block-relative, halo ends dropped."""
+    ends = np.asarray(ends, np.int64) + stripe.wlo
+    ids = np.asarray(ids, np.int64)
+    keep = (ends >= stripe.own_lo) & (ends < stripe.own_hi)
+    return ends[keep], ids[keep]
+
+
+def gather_matches(dist, ends, ids, device=None):
+    """all_gather the per-rank (end, id) lists; every rank gets the merged,
+    end-ordered list (ranks own increasing end ranges).  `dist` is
+    torch.distributed; `device` the tensor device for the collective
+    (a cuda device for RCCL, None = CPU for gloo)."""
+    import torch
+    world = dist.get_world_size()
+    n = torch.tensor([len(ends)], dtype=torch.int64, device=device)
+    counts = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(counts, n)
+    counts = [int(c.item()) for c in counts]
+    m = max(counts) if counts else 0
+    rec = torch.zeros((max(m, 1), 2), dtype=torch.int64, device=device)
+    if len(ends):
+        rec[:len(ends), 0] = torch.as_tensor(np.asarray(ends, np.int64), device=device)
+        rec[:len(ends), 1] = torch.as_tensor(np.asarray(ids, np.int64), device=device)
+    bufs = [torch.zeros_like(rec) for _ in range(world)]
+    dist.all_gather(bufs, rec)
+    parts = [b[:c].cpu().numpy() for b, c in zip(bufs, counts)]
+    allrec = np.concatenate(parts) if parts else np.zeros((0, 2), np.int64)
+    return allrec[:, 0], allrec[:, 1]
+
+
+def scan_block_striped(ctx, db, d_window, stripe):
+    """Scan this rank's window (device buffer holding the window bytes) and
+    return block-relative (ends, ids) of its owned ends, in reference order
+    (end, bucket, chain) before replay."""
+    if stripe.wlen == 0:
+        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+    n = ctx.scan_blocks(db, d_window, [0], [stripe.wlen], [stripe.wstart])
+    res = ctx.results(n)
+    ends = (res["key"] >> np.uint64(24)).astype(np.int64)
+    return localize(stripe, ends, res["id"])
+
+
+def gather_to_root(dist, keys, ids, n, root=0):
+    """Gather the first n rows of this rank's (keys, ids) tensors to `root`
+    (one all_gather of the counts, one gather per array, padded to the
+    largest count).  Returns (keys, ids) concatenated in rank order on root,
+    None elsewhere.  Works on device tensors with the nccl (RCCL) backend
+    and on CPU tensors with gloo."""
+    import torch
+    world = dist.get_world_size()
+    rank = dist.get_rank()
+    cnt = torch.tensor([n], dtype=torch.int64, device=keys.device)
+    counts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt)
+    counts = [int(c.item()) for c in counts]
+    m = max(max(counts), 1)
+    out = []
+    for t in (keys, ids):
+        send = t[:m] if t.shape[0] >= m else torch.cat(
+            [t, torch.zeros(m - t.shape[0], dtype=t.dtype, device=t.device)])
+        recv = [torch.empty_like(send) for _ in range(world)] if rank == root else None
+        dist.gather(send.contiguous(), recv, dst=root)
+        if rank == root:
+            out.append(torch.cat([r[:c] for r, c in zip(recv, counts)]))
+    return tuple(out) if rank == root else None
