@@ -51,6 +51,8 @@ struct VsaLitParams {
     const uint32_t *slotmap;     /* per-bucket bitmap of litIndex[h] != 0 */
     uint32_t slot_words;
     uint32_t slot_off[16];       /* word offset per bucket, ~0 = no prefilter */
+    uint64_t pf_mult;            /* FDRConfirm.mult shared by the prefiltered
+                                    buckets (fdr_confirm_compile.cpp) */
     uint32_t qcap;               /* per-wave LDS confirm-queue entries */
     uint32_t dbg;                /* debug: bit0 verify queued keys against HBM
                                     (mismatches -> counters[3]); bit1 drop all

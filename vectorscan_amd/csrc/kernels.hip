@@ -64,6 +64,15 @@ __device__ __forceinline__ u32 shfl_u32(u32 v, int src) {
 __device__ __forceinline__ u32 shfl_up_u32(u32 v, unsigned d) {
     return (u32)__shfl_up((int)v, d, WAVE);
 }
+/* whole-wave shift by one lane through DPP (no LDS traffic): up1 gives lane
+ * l the value of lane l-1 (lane 0 gets 0), down1 that of lane l+1 (lane 63
+ * gets 0) */
+__device__ __forceinline__ u32 lane_up1(u32 v) {
+    return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ u32 lane_down1(u32 v) {
+    return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+}
 __device__ __forceinline__ u32 shfl_xor_u32(u32 v, int m) {
     return (u32)__shfl_xor((int)v, m, WAVE);
 }
@@ -121,10 +130,9 @@ struct LitTraits<VSA_MODE_FAT> {
 
 /* per-bucket confirm parameters staged in LDS (FDRConfirm, fdr_confirm.h:78) */
 struct PfRec {
-    u64 andmsk, mult;
+    u64 andmsk;
     u32 slot_off; /* word offset of the bucket's slot bitmap, ~0 = none */
     u32 shift;    /* 64 - nBits */
-    u32 pad[2];
 };
 
 struct ConfLds {
@@ -273,7 +281,7 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     const int64_t q0 = p0 - S.blo;
 
     u32 d[5] = {chunk.x, chunk.y, chunk.z, chunk.w, 0};
-    u32 nx = shfl_down_u32(d[0], 1);
+    u32 nx = lane_down1(d[0]);
     if (lane == WAVE - 1) nx = nxt0;
     d[4] = nx & 0xff;
     if (EDGE) {
@@ -320,7 +328,7 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     }
     /* spill from the previous lane (lane 0: from the previous chunk) */
     const u64 s_out = (u64)st;
-    u64 s_in = ((u64)shfl_up_u32((u32)(s_out >> 32), 1) << 32) | shfl_up_u32((u32)s_out, 1);
+    u64 s_in = ((u64)lane_up1((u32)(s_out >> 32)) << 32) | lane_up1((u32)s_out);
     if (lane == 0) s_in = in.carry;
     IterState out;
     out.ncand = in.ncand;
@@ -376,7 +384,7 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     if (P.dbg & 8) return out;
 
     /* bytes p0-8 .. p0+15 for the 8-byte confirm keys */
-    u32 pv2 = shfl_up_u32(d[2], 1), pv3 = shfl_up_u32(d[3], 1);
+    u32 pv2 = lane_up1(d[2]), pv3 = lane_up1(d[3]);
     if (lane == 0) {
         pv2 = (u32)in.pbytes;
         pv3 = (u32)(in.pbytes >> 32);
@@ -423,7 +431,7 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
             const PfRec pf = cl.pf[b];
             push = true;
             if (pf.slot_off != 0xffffffffu) {
-                const u32 h = (u32)(((key & pf.andmsk) * pf.mult) >> pf.shift);
+                const u32 h = (u32)(((key & pf.andmsk) * P.pf_mult) >> pf.shift);
                 push = (L.slots[pf.slot_off + (h >> 5)] >> (h & 31)) & 1u;
             }
             if (P.dbg & 16) push = false;
@@ -569,16 +577,17 @@ vsa_lit_scan(VsaLitParams P) {
         cl.off[tid] = off;
         PfRec pf;
         pf.slot_off = P.slot_off[tid];
-        pf.pad[0] = pf.pad[1] = 0;
         if (off) {
             const u8 *fc = P.conf_base + off;
             cl.andmsk[tid] = pf.andmsk = *(const u64 *)fc;
-            cl.mult[tid] = pf.mult = *(const u64 *)(fc + 8);
+            cl.mult[tid] = *(const u64 *)(fc + 8);
             cl.nbits[tid] = *(const u32 *)(fc + 16);
             pf.shift = 64 - cl.nbits[tid];
+            /* the prefilter hashes with the kernel-wide multiplier */
+            if (cl.mult[tid] != P.pf_mult) pf.slot_off = 0xffffffffu;
         } else {
             cl.andmsk[tid] = pf.andmsk = 0;
-            cl.mult[tid] = pf.mult = 0;
+            cl.mult[tid] = 0;
             cl.nbits[tid] = 1;
             pf.shift = 63;
             pf.slot_off = 0xffffffffu;
@@ -732,7 +741,7 @@ vsa_lit_scan(VsaLitParams P) {
                 for (int k = 0; k < LIT_DEPTH; k++) {
                     const u32 it = g * LIT_DEPTH + k;
                     const int64_t ib = fb + 1024 * (int64_t)it;
-                    const u32 nb = shfl_u32(ring[(k + 1) % LIT_DEPTH].x, 0);
+                    const u32 nb = readlane_u32(ring[(k + 1) % LIT_DEPTH].x, 0);
                     const u32 nxt0 = (it + 1 < nf) ? nb : after;
                     is = lit_iter<MODE, LDS_TABLE, false>(P, cl, L, S, mis, ib, ring[k], nxt0,
                                                           is, bucket_mask);
@@ -746,7 +755,7 @@ vsa_lit_scan(VsaLitParams P) {
                 if ((u32)k < rem) {
                     const u32 it = ng * LIT_DEPTH + k;
                     const int64_t ib = fb + 1024 * (int64_t)it;
-                    const u32 nb = shfl_u32(ring[(k + 1) % LIT_DEPTH].x, 0);
+                    const u32 nb = readlane_u32(ring[(k + 1) % LIT_DEPTH].x, 0);
                     const u32 nxt0 = (it + 1 < nf) ? nb : after;
                     is = lit_iter<MODE, LDS_TABLE, false>(P, cl, L, S, mis, ib, ring[k], nxt0,
                                                           is, bucket_mask);
@@ -822,7 +831,7 @@ __global__ void __launch_bounds__(256) vsa_nood_scan(VsaNoodParams P) {
                     d[w] &= m;
                 }
             }
-            u32 pv2 = shfl_up_u32(d[2], 1), pv3 = shfl_up_u32(d[3], 1);
+            u32 pv2 = lane_up1(d[2]), pv3 = lane_up1(d[3]);
             if (lane == 0) {
                 /* 8 bytes before the iteration */
                 pv2 = 0; pv3 = 0;
@@ -911,7 +920,7 @@ __global__ void __launch_bounds__(256) vsa_class_scan(VsaClassParams P) {
         }
         if (P.pair) {
             /* c1 at i and c2 at i+1: next lane's first c2 bit */
-            u32 nb = shfl_down_u32(bits2, 1) & 1u;
+            u32 nb = lane_down1(bits2) & 1u;
             if (lane == WAVE - 1) {
                 u64 pn = p0 + 16;
                 nb = 0;

@@ -113,6 +113,7 @@ struct vsa_db {
     uint32_t *d_slots = nullptr; /* litIndex-occupancy bitmaps (prefilter) */
     uint32_t slot_words = 0;
     uint32_t slot_off[16];
+    uint64_t pf_mult = 0;
 };
 
 namespace {
@@ -273,6 +274,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.slotmap = db->d_slots;
     P.slot_words = db->slot_words;
     memcpy(P.slot_off, db->slot_off, sizeof(P.slot_off));
+    P.pf_mult = db->pf_mult;
     if (db->mode == VSA_MODE_FDR) {
         size_t tb = (size_t)db->table_entries * 8;
         if (tb <= 128 * 1024) {
@@ -737,10 +739,14 @@ int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
         std::vector<uint32_t> slots;
         for (uint32_t b = 0; b < 16; b++) db->slot_off[b] = 0xffffffffu;
         const bool no_pf = getenv("VSA_NO_PREFILTER") != nullptr;
+        db->pf_mult = 0;
         for (uint32_t b = 0; b < db->nbuckets && !no_pf; b++) {
             if (!db->conf_off[b]) continue;
             const uint8_t *fc = (const uint8_t *)confBase + db->conf_off[b];
             const uint32_t nbits = *(const uint32_t *)(fc + 16);
+            const uint64_t mult = *(const uint64_t *)(fc + 8);
+            if (!db->pf_mult) db->pf_mult = mult;
+            if (mult != db->pf_mult) continue; /* kernel hashes with one multiplier */
             if (nbits > 24) continue;
             const uint32_t n = 1u << nbits;
             const uint32_t words = (n + 31) / 32;
