@@ -1,0 +1,160 @@
+#!/usr/bin/env python3
+"""Measured lines for BASELINE.json configs 1-3 on one MI355X (bench.py is
+config 4, the headline).  One JSON line per workload:
+
+  cfg1  noodle "abcde" (caseful / nocase) — 1 GiB printable corpus
+  cfg2  shufti class A (8 chars, 3.1 %), truffle class B (100 random bytes),
+        no-match class — 256 MiB of uniform bytes 0x00-0xFF, seed 2;
+        output = 1 bit per byte bitmap + first / last / count
+  cfg3  Teddy 48 literals (8 buckets) and 64 literals (Fat Teddy), len 4-8
+        printable, seed 7+n — 1 GiB printable, seed 3, planted every 4 KiB
+
+value = input bytes / kernel time (hipEvents on the scan stream); each line
+also carries wall time per call (launch + count read-back + sort) and a
+parity check against the oracle / numpy on a bounded sample.
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0
+
+
+def lits_printable(n, seed, minlen=4, maxlen=8):
+    import vectorscan_amd as vsa
+    r = random.Random(seed)
+    out = []
+    for i in range(n):
+        ln = r.randint(minlen, maxlen)
+        out.append(vsa.HwlmLiteral(bytes(r.randint(0x20, 0x7E) for _ in range(ln)), False, i))
+    return out
+
+
+def timed(fn, steps, warmup, ctx):
+    for _ in range(warmup):
+        fn()
+    ks, t0 = [], time.perf_counter()
+    for _ in range(steps):
+        fn()
+        ks.append(ctx.kernel_ms())
+    wall = (time.perf_counter() - t0) / steps * 1e3
+    return float(np.mean(ks)), wall
+
+
+def line(name, nbytes, kms, wall, out_bytes, parity, extra):
+    ach = (nbytes + out_bytes) / (kms * 1e-3) / 1e9
+    d = {"workload": name, "value": round(nbytes / (kms * 1e-3) / 1e9, 2), "unit": "GB/s",
+         "kernel_ms": round(kms, 4), "wall_ms_per_call": round(wall, 4),
+         "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)},
+         "parity": parity}
+    d.update(extra)
+    print(json.dumps(d), flush=True)
+
+
+def cfg_literal(ctx, torch, name, lits, n, plant_every, seed, steps, warmup, sample):
+    import bench
+    import oracle
+    import vectorscan_amd as vsa
+    blob = vsa.hwlm_build(lits)
+    db = vsa.Database(ctx, blob)
+    data = bench.make_corpus_device(torch, n, lits, seed=seed, plant_every=plant_every,
+                                    device=torch.device("cuda", 0))
+    torch.cuda.synchronize()
+    dptr = data.data_ptr()
+    nm = [0]
+
+    def step():
+        nm[0] = ctx.scan_blocks(db, dptr, [0], [n])
+
+    kms, wall = timed(step, steps, warmup, ctx)
+    host = data[:sample].cpu().numpy()
+    k = ctx.scan_blocks(db, dptr, [0], [sample])
+    res = ctx.results(k)
+    got = list(zip((res["key"] >> np.uint64(24)).tolist(), res["id"].tolist()))
+    if blob.is_noodle:
+        _, want = oracle.nood_exec(vsa.engine_blob(blob), host, cap=1 << 22)
+    else:
+        _, want = oracle.fdr_exec(vsa.engine_blob(blob), host, cap=1 << 22)
+    line(name, n, kms, wall, 16 * nm[0], got == want,
+         {"engine_id": blob.engine_id, "matches": nm[0], "sample_bytes": sample})
+    db.close()
+    del data
+
+
+def cfg_class(ctx, torch, steps, warmup):
+    import vectorscan_amd as vsa
+    n = 256 << 20
+    g = torch.Generator(device="cuda")
+    g.manual_seed(2)
+    data = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    bitmap = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda")
+    host = data.cpu().numpy()
+    classA = b"\x01\x7f\x80\xfe<>\"'"
+    rb = random.Random(5)
+    classB = bytes(rb.sample(range(256), 100))
+    for name, chars, kind in (("cfg2 shufti class A (8 chars)", classA, "shufti"),
+                              ("cfg2 truffle class B (100 bytes)", classB, "truffle"),
+                              ("cfg2 shufti no-match", b"", "shufti")):
+        if kind == "shufti" and chars:
+            lo, hi = vsa.shufti_build_masks(chars)
+            cls = vsa.class_bitmap(chars)
+        elif kind == "shufti":
+            cls = np.zeros(32, np.uint8)
+        else:
+            m1, m2 = vsa.truffle_build_masks(chars)
+            cls = vsa.class_bitmap(chars)
+        res = [None]
+
+        def step():
+            res[0] = ctx.class_scan(cls, data.data_ptr(), n, bitmap.data_ptr())
+
+        kms, wall = timed(step, steps, warmup, ctx)
+        f, l, c = res[0]
+        member = np.zeros(256, bool)
+        member[list(chars)] = True
+        hits = member[host]
+        idx = np.flatnonzero(hits)
+        want_bm = np.packbits(hits, bitorder="little").view(np.int64)
+        ok = (c == len(idx) and f == (idx[0] if len(idx) else n) and
+              l == (idx[-1] + 1 if len(idx) else 0) and
+              np.array_equal(bitmap.cpu().numpy()[:len(want_bm)], want_bm))
+        line(name, n, kms, wall, n // 8, bool(ok), {"hits": int(c)})
+    del data, bitmap
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--only", default="1,2,3")
+    args = ap.parse_args()
+    import torch
+    import vectorscan_amd as vsa
+    ctx = vsa.Context(0)
+    only = set(args.only.split(","))
+    if "1" in only:
+        for nc in (False, True):
+            lits = [vsa.HwlmLiteral(b"abcde", nc, 0)]
+            cfg_literal(ctx, torch, "cfg1 noodle 'abcde'%s 1 GiB" % (" nocase" if nc else ""),
+                        lits, 1 << 30, 4096, 1, args.steps, args.warmup, 16 << 20)
+    if "2" in only:
+        cfg_class(ctx, torch, args.steps, args.warmup)
+    if "3" in only:
+        for nl in (48, 64):
+            cfg_literal(ctx, torch, "cfg3 teddy %d literals 1 GiB" % nl,
+                        lits_printable(nl, 7 + nl), 1 << 30, 4096, 3, args.steps,
+                        args.warmup, 64 << 20)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -34,6 +34,7 @@ enum VsaLitMode {
     VSA_MODE_FDR = 0,   /* 8 lanes x 8 buckets, 2-byte key & domainMask */
     VSA_MODE_TEDDY = 1, /* 4 lanes x 8 buckets, 1-byte key */
     VSA_MODE_FAT = 2,   /* 4 lanes x 16 buckets, 1-byte key */
+    VSA_MODE_NOOD = 3,  /* noodle: masked compare of the <= 8 bytes ending at e */
 };
 
 struct VsaLitParams {
@@ -51,6 +52,8 @@ struct VsaLitParams {
     const uint32_t *slotmap;     /* per-bucket bitmap of litIndex[h] != 0 */
     uint32_t slot_words;
     uint32_t slot_off[16];       /* word offset per bucket, ~0 = no prefilter */
+    uint64_t nood_msk, nood_cmp; /* noodle msk / cmp << 8 * (8 - msk_len) */
+    uint32_t nood_len, nood_id;  /* noodTable msk_len, id */
     uint64_t pf_mult;            /* FDRConfirm.mult shared by the prefiltered
                                     buckets (fdr_confirm_compile.cpp) */
     uint32_t qcap;               /* per-wave LDS confirm-queue entries */
@@ -67,20 +70,6 @@ struct VsaLitParams {
                                      the slot prefilter; diagnostic) */
 };
 
-struct VsaNoodParams {
-    const uint8_t *data;
-    const VsaBlock *blocks;
-    uint32_t nblocks;
-    uint32_t seg_shift;
-    uint64_t nsegs;
-    uint64_t msk, cmp;
-    uint32_t msk_len;
-    uint32_t id;
-    uint64_t *out_keys;
-    uint32_t *out_ids;
-    uint64_t out_cap;
-    unsigned long long *counters;
-};
 
 /* Byte-class scan (shufti / truffle / vermicelli reduce to a 256-bit class).
  * pair != 0: position i is set when cls[b[i]] && cls2[b[i+1]] (double
@@ -93,9 +82,10 @@ struct VsaClassParams {
     uint32_t cls2[8];
     int pair;
     uint64_t *bitmap;              /* (len + 63) / 64 words, may be null */
-    unsigned long long *first;     /* atomicMin of first set index */
-    unsigned long long *last;      /* atomicMax of (last set index + 1) */
-    unsigned long long *count;     /* popcount of the bitmap */
+    unsigned long long *first;     /* [slots] atomicMin of first set index */
+    unsigned long long *last;      /* [slots] atomicMax of (last set index + 1) */
+    unsigned long long *count;     /* [slots] popcount of the bitmap */
+    uint32_t slots;                /* workgroup b updates slot b % slots */
 };
 
 #endif

@@ -6,7 +6,8 @@
  *                      (teddy.c:921-1066, teddy_avx2.c:395-706): first-stage
  *                      filter + exact confirm (fdr_confirm_runtime.h:43-102)
  *                      in one pass.
- *  vsa_nood_scan       noodle (noodle_engine.cpp:75-134).
+ *                      Noodle (noodle_engine.cpp:75-134) is a fourth mode
+ *                      of the same kernel (masked compare, no table).
  *  vsa_class_scan      shufti / truffle / vermicelli reduced to a 256-bit
  *                      byte class (shufti_simd.hpp:89-280, x86/truffle.hpp,
  *                      vermicelli_simd.cpp) -> 1 bit/byte bitmap + first/last.
@@ -116,6 +117,14 @@ struct LitTraits<VSA_MODE_TEDDY> {
     static constexpr int LB = 8;
     static constexpr int NL = 4;
     static constexpr int CW = 4;
+    static constexpr bool KEY16 = false;
+    typedef u32 S_t;
+};
+template <>
+struct LitTraits<VSA_MODE_NOOD> {
+    static constexpr int LB = 8;
+    static constexpr int NL = 1; /* no look-back state */
+    static constexpr int CW = 1;
     static constexpr bool KEY16 = false;
     typedef u32 S_t;
 };
@@ -265,6 +274,34 @@ struct SegCtx {
     int64_t blo, bhi; /* aoff of the block */
     int64_t start, len, zbase;
 };
+
+/* Append one entry per lane with push set to the wave's ring (wave-uniform
+ * call).  The ring cursor in `st` is updated identically by every lane. */
+template <typename ST>
+__device__ __forceinline__ void ring_push(const LitShared &L, ST &st, bool push, u64 meta,
+                                          u64 key) {
+    const u64 pm = __ballot(push);
+    if (pm == 0) return;
+    const u32 n = (u32)__popcll(pm);
+    /* room for n entries (the confirm wave frees them in order) */
+    if (st.head + n - st.tail_cache > L.rmask + 1) {
+        for (;;) {
+            st.tail_cache = readfirstlane_u32(lds_ld32(L.tail));
+            if (st.head + n - st.tail_cache <= L.rmask + 1) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    if (push) {
+        const u32 r = __builtin_amdgcn_mbcnt_hi((u32)(pm >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((u32)pm, 0));
+        QEnt *q = &L.ring[(st.head + r) & L.rmask];
+        q->meta = meta;
+        q->key = key;
+    }
+    st.head += n;
+    asm volatile("" ::: "memory"); /* entries before the head (LDS order) */
+    if (lane_id() == 0) lds_st32(L.head_pub, st.head);
+}
 
 /* One 1 KiB iteration at aoff `ib`: lane l owns bytes [ib + 16 l, +16).
  * d = the lane's 16 bytes, nxt0 = first byte of the following chunk (for
@@ -437,29 +474,95 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
             if (P.dbg & 16) push = false;
             meta = ((u64)(p0 + j) << 24) | ((u64)S.blk << 4) | b;
         }
-        const u64 pm = __ballot(push);
-        if (pm == 0) continue;
-        const u32 n = (u32)__popcll(pm);
-        /* room for n entries (the confirm wave frees them in order) */
-        if (out.head + n - out.tail_cache > L.rmask + 1) {
-            for (;;) {
-                out.tail_cache = readfirstlane_u32(lds_ld32(L.tail));
-                if (out.head + n - out.tail_cache <= L.rmask + 1) break;
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        if (push) {
-            const u32 r = __builtin_amdgcn_mbcnt_hi((u32)(pm >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((u32)pm, 0));
-            QEnt *q = &L.ring[(out.head + r) & L.rmask];
-            q->meta = meta;
-            q->key = key;
-        }
-        out.head += n;
-        asm volatile("" ::: "memory"); /* entries before the head (LDS order) */
-        if (lane == 0) lds_st32(L.head_pub, out.head);
+        ring_push(L, out, push, meta, key);
     }
     return out;
+}
+
+/* Noodle (noodle_engine.cpp:75-134, noodle_engine_simd.hpp:173-226): end e
+ * is a match when the msk_len bytes ending at e, masked, equal cmp and the
+ * literal starts at or after `start`.  P.nood_msk / nood_cmp are the
+ * reference msk / cmp shifted to the top of a u64, compared against the 8
+ * bytes ending at e (bytes outside the block read as 0, never matched since
+ * those ends are cut). */
+template <bool EDGE>
+__device__ __forceinline__ IterState nood_iter(const VsaLitParams &P, const LitShared &L,
+                                               const SegCtx &S, int64_t ib, uint4 chunk,
+                                               IterState in) {
+    const u32 lane = lane_id();
+    const int64_t p0 = ib + 16 * (int64_t)lane;
+    const int64_t q0 = p0 - S.blo;
+    u32 d[4] = {chunk.x, chunk.y, chunk.z, chunk.w};
+    if (EDGE) {
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            u32 m = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                int64_t p = p0 + 4 * w + k;
+                if (p >= S.blo && p < S.bhi) m |= 0xffu << (8 * k);
+            }
+            d[w] &= m;
+        }
+    }
+    u32 pv2 = lane_up1(d[2]), pv3 = lane_up1(d[3]);
+    if (lane == 0) {
+        pv2 = (u32)in.pbytes;
+        pv3 = (u32)(in.pbytes >> 32);
+    }
+    IterState out = in;
+    out.pbytes = ((u64)readlane_u32(d[3], WAVE - 1) << 32) | readlane_u32(d[2], WAVE - 1);
+    const u32 w[6] = {pv2, pv3, d[0], d[1], d[2], d[3]};
+    const u32 mlo = (u32)P.nood_msk, mhi = (u32)(P.nood_msk >> 32);
+    const u32 clo = (u32)P.nood_cmp, chi = (u32)(P.nood_cmp >> 32);
+    u32 hits = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int bo = j + 1; /* 8 bytes ending at p0 + j start at w byte j + 1 */
+        u32 lo, hi;
+        if (bo & 3) {
+            lo = __builtin_amdgcn_alignbyte(w[(bo >> 2) + 1], w[bo >> 2], bo & 3);
+            hi = __builtin_amdgcn_alignbyte(w[(bo >> 2) + 2], w[(bo >> 2) + 1], bo & 3);
+        } else {
+            lo = w[bo >> 2];
+            hi = w[(bo >> 2) + 1];
+        }
+        if (((lo & mlo) == clo) & ((hi & mhi) == chi)) hits |= 1u << j;
+    }
+    if (EDGE) {
+        const int64_t elo = S.start + (int64_t)P.nood_len - 1;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const int64_t q = q0 + j;
+            if (q < elo || q >= S.len) hits &= ~(1u << j);
+        }
+    }
+    if (!__any(hits != 0)) return out;
+    for (;;) {
+        const bool have = hits != 0;
+        if (!__any(have)) break;
+        u64 meta = 0;
+        if (have) {
+            const u32 j = __ffs(hits) - 1;
+            hits &= hits - 1;
+            meta = ((u64)(p0 + j) << 24) | ((u64)S.blk << 4);
+        }
+        ring_push(L, out, have, meta, 0);
+    }
+    return out;
+}
+
+template <int MODE, bool LDS_TABLE, bool EDGE>
+__device__ __forceinline__ IterState scan_iter(const VsaLitParams &P, const ConfLds &cl,
+                                               const LitShared &L, const SegCtx &S,
+                                               u32 mis, int64_t ib, uint4 chunk,
+                                               u32 nxt0, IterState in, u32 bucket_mask) {
+    if constexpr (MODE == VSA_MODE_NOOD) {
+        return nood_iter<EDGE>(P, L, S, ib, chunk, in);
+    } else {
+        return lit_iter<MODE, LDS_TABLE, EDGE>(P, cl, L, S, mis, ib, chunk, nxt0, in,
+                                               bucket_mask);
+    }
 }
 
 __device__ __forceinline__ uint4 load_chunk(const u8 *A, int64_t p0, int64_t bhi) {
@@ -487,6 +590,7 @@ __device__ __forceinline__ uint4 load_chunk_nc(const u8 *A, int64_t p0) {
  * once every scanning wave has finished (q_done, read before the heads) and
  * every ring is empty. */
 #define LIT_SCANNERS (LIT_WAVES - 1)
+template <int MODE>
 __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLds &cl,
                                              const QEnt *rings, u32 rsize, const u32 *heads,
                                              u32 *tails, const u32 *q_done, u32 mis) {
@@ -525,7 +629,18 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
             __builtin_amdgcn_s_sleep(4);
             continue;
         }
-        if (mine) confirm_one(P, cl, meta, key, mis);
+        if (mine) {
+            if constexpr (MODE == VSA_MODE_NOOD) {
+                /* noodle hits are final: emit (end, id) */
+                const unsigned long long slot = atomicAdd(&P.counters[0], 1ULL);
+                if (slot < P.out_cap) {
+                    P.out_keys[slot] = ((meta >> 24) - mis) << VSA_KEY_END_SHIFT;
+                    P.out_ids[slot] = P.nood_id;
+                }
+            } else {
+                confirm_one(P, cl, meta, key, mis);
+            }
+        }
     }
     /* confirm-stage candidates (first-stage count instead under dbg & 32) */
     if (P.counters && lane == 0 && consumed && !(P.dbg & 32))
@@ -563,6 +678,8 @@ vsa_lit_scan(VsaLitParams P) {
         u32 *dst = (u32 *)smem;
         for (u32 i = tid; i < 256 * 32; i += LIT_THREADS) dst[i] = (u32)P.table[i >> 5];
         tab = smem;
+    } else if constexpr (MODE == VSA_MODE_NOOD) {
+        tab = nullptr;
     } else {
         tab_bytes = 256 * 32 * 8;
         u64 *dst = (u64 *)smem;
@@ -603,7 +720,7 @@ vsa_lit_scan(VsaLitParams P) {
 
     const u32 mis = (u32)((uintptr_t)P.data & 15);
     if (wave == LIT_WAVES - 1) {
-        confirm_wave(P, cl, rings, P.qcap, q_heads, q_tails, &q_done, mis);
+        confirm_wave<MODE>(P, cl, rings, P.qcap, q_heads, q_tails, &q_done, mis);
         return;
     }
 
@@ -716,7 +833,7 @@ vsa_lit_scan(VsaLitParams P) {
             const int64_t ib = s_lo + 1024 * (int64_t)it;
             const uint4 cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
             const u32 nxt0 = load_byte_masked(A, ib + 1024, S.blo, S.bhi);
-            is = lit_iter<MODE, LDS_TABLE, true>(P, cl, L, S, mis, ib, cur, nxt0, is,
+            is = scan_iter<MODE, LDS_TABLE, true>(P, cl, L, S, mis, ib, cur, nxt0, is,
                                                  bucket_mask);
         }
         if (f0 < f1) {
@@ -743,7 +860,7 @@ vsa_lit_scan(VsaLitParams P) {
                     const int64_t ib = fb + 1024 * (int64_t)it;
                     const u32 nb = readlane_u32(ring[(k + 1) % LIT_DEPTH].x, 0);
                     const u32 nxt0 = (it + 1 < nf) ? nb : after;
-                    is = lit_iter<MODE, LDS_TABLE, false>(P, cl, L, S, mis, ib, ring[k], nxt0,
+                    is = scan_iter<MODE, LDS_TABLE, false>(P, cl, L, S, mis, ib, ring[k], nxt0,
                                                           is, bucket_mask);
                     const int64_t pn = (it + LIT_DEPTH < nf) ? ib + 1024 * LIT_DEPTH : ib;
                     ring[k] = load_chunk_nc(A, pn + 16 * (int64_t)lane);
@@ -757,7 +874,7 @@ vsa_lit_scan(VsaLitParams P) {
                     const int64_t ib = fb + 1024 * (int64_t)it;
                     const u32 nb = readlane_u32(ring[(k + 1) % LIT_DEPTH].x, 0);
                     const u32 nxt0 = (it + 1 < nf) ? nb : after;
-                    is = lit_iter<MODE, LDS_TABLE, false>(P, cl, L, S, mis, ib, ring[k], nxt0,
+                    is = scan_iter<MODE, LDS_TABLE, false>(P, cl, L, S, mis, ib, ring[k], nxt0,
                                                           is, bucket_mask);
                 }
             }
@@ -766,7 +883,7 @@ vsa_lit_scan(VsaLitParams P) {
             const int64_t ib = s_lo + 1024 * (int64_t)it;
             const uint4 cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
             const u32 nxt0 = load_byte_masked(A, ib + 1024, S.blo, S.bhi);
-            is = lit_iter<MODE, LDS_TABLE, true>(P, cl, L, S, mis, ib, cur, nxt0, is,
+            is = scan_iter<MODE, LDS_TABLE, true>(P, cl, L, S, mis, ib, cur, nxt0, is,
                                                  bucket_mask);
         }
         ncand_total = is.ncand;
@@ -783,100 +900,7 @@ template __global__ void vsa_lit_scan<VSA_MODE_FDR, true>(VsaLitParams);
 template __global__ void vsa_lit_scan<VSA_MODE_FDR, false>(VsaLitParams);
 template __global__ void vsa_lit_scan<VSA_MODE_TEDDY, true>(VsaLitParams);
 template __global__ void vsa_lit_scan<VSA_MODE_FAT, true>(VsaLitParams);
-
-/* ========================================================== noodle === */
-
-/* Each lane owns 16 end positions; the 7 bytes before its chunk come from
- * lane-1 (shuffle).  Report e when (u64 of msk_len bytes ending at e & msk)
- * == cmp, with the whole window inside [start, len) (noodle_engine_simd.hpp
- * scanSingleMain/scanDoubleMain bounds). */
-__global__ void __launch_bounds__(256) vsa_nood_scan(VsaNoodParams P) {
-    const u32 lane = lane_id();
-    const u32 mis = (u32)((uintptr_t)P.data & 15);
-    const u8 *A = P.data - mis;
-    const int64_t SEG = (int64_t)1 << P.seg_shift;
-    const u32 ml = P.msk_len;
-    for (;;) {
-        unsigned long long t = 0;
-        if (lane == 0) t = atomicAdd(&P.counters[1], 1ULL);
-        u64 seg = ((u64)shfl_u32((u32)(t >> 32), 0) << 32) | shfl_u32((u32)t, 0);
-        if (seg >= P.nsegs) break;
-        u32 blk = 0;
-        while (blk + 1 < P.nblocks && P.blocks[blk + 1].seg_first <= seg) blk++;
-        const VsaBlock B = P.blocks[blk];
-        const int64_t blo = (int64_t)B.base + mis;
-        const int64_t bhi = blo + (int64_t)B.len;
-        /* same 1 KiB-aligned segment grid as vsa_lit_scan (VsaBlock.org) */
-        const int64_t s_lo = B.org + (int64_t)(seg - B.seg_first) * SEG;
-        const int64_t s_hi = (s_lo + SEG < bhi) ? s_lo + SEG : bhi;
-        const int64_t elo = (int64_t)B.start + ml - 1; /* block-relative */
-        for (int64_t ib = s_lo; ib < s_hi; ib += 16 * WAVE) {
-            int64_t p0 = ib + 16 * (int64_t)lane;
-            u32 d[4] = {0, 0, 0, 0};
-            if (p0 < bhi) {
-                uint4 v = *(const uint4 *)(A + p0);
-                d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-            }
-            /* zero bytes outside the block */
-            bool edge = (ib < blo) || (ib + 16 * WAVE > bhi);
-            if (edge) {
-#pragma unroll
-                for (int w = 0; w < 4; w++) {
-                    u32 m = 0;
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        int64_t p = p0 + 4 * w + k;
-                        if (p >= blo && p < bhi) m |= 0xffu << (8 * k);
-                    }
-                    d[w] &= m;
-                }
-            }
-            u32 pv2 = lane_up1(d[2]), pv3 = lane_up1(d[3]);
-            if (lane == 0) {
-                /* 8 bytes before the iteration */
-                pv2 = 0; pv3 = 0;
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    u32 b = load_byte_masked(A, p0 - 8 + k, blo, bhi);
-                    if (k < 4) pv2 |= b << (8 * k); else pv3 |= b << (8 * (k - 4));
-                }
-            }
-            u32 w[6] = {pv2, pv3, d[0], d[1], d[2], d[3]};
-            u32 hits = 0;
-#pragma unroll
-            for (int j = 0; j < 16; j++) {
-                /* 8 bytes ending at p0 + j: bytes [p0+j-7, p0+j] */
-                const int bo = 8 + j - 7; /* byte offset in w[] */
-                u32 lo, hi;
-                if (bo & 3) {
-                    lo = __builtin_amdgcn_alignbyte(w[(bo >> 2) + 1], w[bo >> 2], bo & 3);
-                    hi = __builtin_amdgcn_alignbyte(w[(bo >> 2) + 2], w[(bo >> 2) + 1], bo & 3);
-                } else {
-                    lo = w[bo >> 2];
-                    hi = w[(bo >> 2) + 1];
-                }
-                u64 v = (((u64)hi << 32) | lo) >> (8 * (8 - ml));
-                if ((v & P.msk) == P.cmp) hits |= 1u << j;
-            }
-            int64_t q0 = p0 - blo;
-#pragma unroll
-            for (int j = 0; j < 16; j++) {
-                int64_t q = q0 + j;
-                if (q < elo || q >= (int64_t)B.len) hits &= ~(1u << j);
-            }
-            while (hits) {
-                u32 j = __ffs(hits) - 1;
-                hits &= hits - 1;
-                unsigned long long slot = atomicAdd(&P.counters[0], 1ULL);
-                if (slot < P.out_cap) {
-                    u64 end_abs = (u64)B.base + (u64)(q0 + j);
-                    P.out_keys[slot] = end_abs << VSA_KEY_END_SHIFT;
-                    P.out_ids[slot] = P.id;
-                }
-            }
-        }
-    }
-}
+template __global__ void vsa_lit_scan<VSA_MODE_NOOD, false>(VsaLitParams);
 
 /* ======================================================= class scan === */
 
@@ -963,9 +987,10 @@ __global__ void __launch_bounds__(256) vsa_class_scan(VsaClassParams P) {
         cnt += ((u64)chi << 32) | clo;
     }
     if (lane == 0) {
-        if (first != ~0ULL) atomicMin(P.first, first);
-        if (last) atomicMax(P.last, last);
-        if (cnt) atomicAdd(P.count, cnt);
+        const u32 sl = blockIdx.x % P.slots;
+        if (first != ~0ULL) atomicMin(P.first + sl, first);
+        if (last) atomicMax(P.last + sl, last);
+        if (cnt) atomicAdd(P.count + sl, cnt);
     }
 }
 

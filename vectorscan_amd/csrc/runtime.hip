@@ -37,7 +37,6 @@
 
 template <int MODE, bool LDS_TABLE>
 __global__ void vsa_lit_scan(VsaLitParams P);
-__global__ void vsa_nood_scan(VsaNoodParams P);
 __global__ void vsa_class_scan(VsaClassParams P);
 
 #define VSA_CHECK(x)                                                          \
@@ -58,6 +57,10 @@ const int LIT_THREADS = 1024;
 const size_t LDS_BUDGET = 160 * 1024 - 2048; /* minus static LDS */
 const uint32_t SLOT_WORDS_MAX = 4096;        /* 16 KiB of slot bitmaps */
 
+constexpr int CLASS_SLOTS = 64;
+constexpr int CLASS_BASE = 8;
+constexpr int N_COUNTERS = CLASS_BASE + 3 * CLASS_SLOTS;
+
 struct Workspace {
     uint8_t *d_in = nullptr;
     size_t in_cap = 0;
@@ -66,7 +69,10 @@ struct Workspace {
     uint64_t out_cap = 0;
     void *d_tmp = nullptr;
     size_t tmp_bytes = 0;
-    unsigned long long *d_counters = nullptr; /* [0..3] scan, [4..7] class */
+    /* [0..7] scan counters; [8..199] class-scan partials: first / last /
+     * count in CLASS_SLOTS slots each (spread so that workgroups' atomics hit
+     * different addresses) */
+    unsigned long long *d_counters = nullptr;
     unsigned long long *h_counters = nullptr; /* pinned mirror */
     VsaBlock *d_blocks = nullptr;
     VsaBlock *h_blocks = nullptr;
@@ -225,27 +231,29 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
                        uint64_t nsegs, uint32_t seg_shift) {
     Workspace &w = c->ws;
     if (db->type == HWLM_ENGINE_NOOD) {
-        VsaNoodParams P;
+        VsaLitParams P;
         memset(&P, 0, sizeof(P));
         P.data = d_data;
         P.blocks = w.d_blocks;
         P.nblocks = nb;
         P.seg_shift = seg_shift;
         P.nsegs = nsegs;
-        P.msk = db->nood.msk;
-        P.cmp = db->nood.cmp;
-        P.msk_len = db->nood.msk_len;
-        P.id = db->nood.id;
+        const uint32_t ml = db->nood.msk_len; /* 1..8 */
+        P.nood_msk = db->nood.msk << (8 * (8 - ml));
+        P.nood_cmp = db->nood.cmp << (8 * (8 - ml));
+        P.nood_len = ml;
+        P.nood_id = db->nood.id;
         P.out_keys = w.d_keys[0];
         P.out_ids = w.d_ids[0];
         P.out_cap = w.out_cap;
         P.counters = w.d_counters;
-        uint64_t want = (nsegs + 3) / 4;
-        uint64_t cap = (uint64_t)c->num_cus * 8;
-        uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
-        hipLaunchKernelGGL(vsa_nood_scan, dim3(grid), dim3(256), 0, c->stream, P);
-        VSA_CHECK(hipGetLastError());
-        return VSA_OK;
+        {
+            const char *e = getenv("VSA_DEBUG_FLAGS");
+            P.dbg = e ? (uint32_t)atoi(e) : 0u;
+        }
+        for (int b = 0; b < 16; b++) P.slot_off[b] = 0xffffffffu;
+        size_t lds = plan_lds(0, 0, &P.qcap);
+        return launch_lit<VSA_MODE_NOOD, false>(c, P, lds);
     }
     VsaLitParams P;
     memset(&P, 0, sizeof(P));
@@ -666,8 +674,8 @@ int vsa_ctx_create(int device, vsa_ctx_t **out) {
     VSA_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     VSA_CHECK(hipEventCreate(&c->ev0));
     VSA_CHECK(hipEventCreate(&c->ev1));
-    VSA_CHECK(hipMalloc(&c->ws.d_counters, 8 * sizeof(unsigned long long)));
-    VSA_CHECK(hipHostMalloc((void **)&c->ws.h_counters, 8 * sizeof(unsigned long long),
+    VSA_CHECK(hipMalloc(&c->ws.d_counters, N_COUNTERS * sizeof(unsigned long long)));
+    VSA_CHECK(hipHostMalloc((void **)&c->ws.h_counters, N_COUNTERS * sizeof(unsigned long long),
                             hipHostMallocDefault));
     *out = c.release();
     return VSA_OK;
@@ -942,10 +950,9 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
     }
     if (!d_data || ((uintptr_t)d_data & 15)) return VSA_E_INVALID;
     Workspace &w = c->ws;
-    unsigned long long init[3] = {~0ULL, 0, 0};
-    memcpy(w.h_counters + 4, init, sizeof(init));
-    VSA_CHECK(hipMemcpyAsync(w.d_counters + 4, w.h_counters + 4, 3 * 8, hipMemcpyHostToDevice,
-                             c->stream));
+    unsigned long long *part = w.d_counters + CLASS_BASE;
+    VSA_CHECK(hipMemsetAsync(part, 0xff, CLASS_SLOTS * 8, c->stream));
+    VSA_CHECK(hipMemsetAsync(part + CLASS_SLOTS, 0, 2 * CLASS_SLOTS * 8, c->stream));
     VsaClassParams P;
     memset(&P, 0, sizeof(P));
     P.data = d_data;
@@ -956,22 +963,35 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
         P.pair = 1;
     }
     P.bitmap = d_bitmap;
-    P.first = w.d_counters + 4;
-    P.last = w.d_counters + 5;
-    P.count = w.d_counters + 6;
+    P.first = part;
+    P.last = part + CLASS_SLOTS;
+    P.count = part + 2 * CLASS_SLOTS;
+    P.slots = CLASS_SLOTS;
     uint64_t chunks = (len + 15) / 16;
     uint64_t want = (chunks + 255) / 256;
     uint64_t cap = (uint64_t)c->num_cus * 8;
     uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
+    VSA_CHECK(hipEventRecord(c->ev0, c->stream));
     hipLaunchKernelGGL(vsa_class_scan, dim3(grid), dim3(256), 0, c->stream, P);
     VSA_CHECK(hipGetLastError());
-    VSA_CHECK(hipMemcpyAsync(w.h_counters + 4, w.d_counters + 4, 3 * 8, hipMemcpyDeviceToHost,
-                             c->stream));
+    VSA_CHECK(hipEventRecord(c->ev1, c->stream));
+    VSA_CHECK(hipMemcpyAsync(w.h_counters + CLASS_BASE, part, 3 * CLASS_SLOTS * 8,
+                             hipMemcpyDeviceToHost, c->stream));
     VSA_CHECK(hipStreamSynchronize(c->stream));
-    uint64_t f = w.h_counters[4];
+    {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_kernel_ms = ms;
+    }
+    const unsigned long long *h = w.h_counters + CLASS_BASE;
+    uint64_t f = ~0ULL, l = 0, n = 0;
+    for (int i = 0; i < CLASS_SLOTS; i++) {
+        f = std::min<uint64_t>(f, h[i]);
+        l = std::max<uint64_t>(l, h[CLASS_SLOTS + i]);
+        n += h[2 * CLASS_SLOTS + i];
+    }
     if (first) *first = f == ~0ULL ? len : f;
-    if (last) *last = w.h_counters[5];
-    if (count) *count = w.h_counters[6];
+    if (last) *last = l;
+    if (count) *count = n;
     return VSA_OK;
 }
 
