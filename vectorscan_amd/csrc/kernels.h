@@ -41,7 +41,10 @@ struct VsaLitParams {
     const uint8_t *data;
     const VsaBlock *blocks;
     uint32_t nblocks;
-    uint32_t seg_shift;     /* segment = 1 << seg_shift bytes of end positions */
+    uint32_t seg_bytes;     /* segment size (multiple of 1 KiB) */
+    uint32_t dynamic;       /* 1: segments by atomic ticket per region */
+    uint32_t nregions;      /* ticket regions (counters[16 + 16 r], one
+                               128-B line each), <= 8 */
     uint64_t nsegs;
     const uint64_t *table;  /* FDR domain table / Teddy combined byte table */
     uint32_t table_entries;
@@ -65,7 +68,7 @@ struct VsaLitParams {
     uint64_t *out_keys;
     uint32_t *out_ids;
     uint64_t out_cap;
-    unsigned long long *counters; /* [0] matches, [1] segment ticket,
+    unsigned long long *counters; /* [0] matches, [16 + 16 r] region tickets,
                                      [2] candidates handed to confirm (after
                                      the slot prefilter; diagnostic) */
 };
@@ -85,7 +88,8 @@ struct VsaClassParams {
     unsigned long long *first;     /* [slots] atomicMin of first set index */
     unsigned long long *last;      /* [slots] atomicMax of (last set index + 1) */
     unsigned long long *count;     /* [slots] popcount of the bitmap */
-    uint32_t slots;                /* workgroup b updates slot b % slots */
+    uint32_t slots;                /* workgroup b updates slot b % slots, at
+                                      u64 index 16 * slot (one line each) */
 };
 
 #endif

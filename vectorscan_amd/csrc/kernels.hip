@@ -12,11 +12,13 @@
  *                      byte class (shufti_simd.hpp:89-280, x86/truffle.hpp,
  *                      vermicelli_simd.cpp) -> 1 bit/byte bitmap + first/last.
  *
- * Work decomposition (all kernels): the batch is a list of blocks (each one
- * hwlmExec call); a block is cut into segments of 2^seg_shift end positions;
- * one wave64 owns one segment at a time (dynamic ticket), sweeping it in
- * 1 KiB iterations: lane l loads 16 bytes at iteration_base + 16 l with one
- * global_load_dwordx4 (fully coalesced), so HBM is read exactly once.
+ * Work decomposition (literal scan): the batch is a list of blocks (each one
+ * hwlmExec call); a block is cut into segments of seg_bytes end positions
+ * (host-sized so every scanning wave gets the same number of segments);
+ * scanning wave g owns segments g, g + G, ... (static, G = all scanning
+ * waves), sweeping each in 1 KiB iterations: lane l loads 16 bytes at
+ * iteration_base + 16 l with one global_load_dwordx4 (fully coalesced), so
+ * HBM is read once plus a 1 KiB-aligned halo per segment.
  *
  * FDR / Teddy filter (the reference's stride-1 shift-or, restated per lane):
  * for end e, conf(e) = OR_k field_k(T[key(e-k)]); a zero bit b means
@@ -746,19 +748,46 @@ vsa_lit_scan(VsaLitParams P) {
     L.rmask = P.qcap - 1;
 
     const u8 *A = P.data - mis;
-    const int64_t SEG = (int64_t)1 << P.seg_shift;
+    const int64_t SEG = (int64_t)P.seg_bytes;
     u32 ncand_total = 0;
     u32 ring_head = 0, ring_tail_cache = 0;
 
-    for (;;) {
-        unsigned long long t = 0;
-        if (lane == 0) t = atomicAdd(&P.counters[1], 1ULL);
-        const u64 seg = ((u64)readfirstlane_u32(shfl_u32((u32)(t >> 32), 0)) << 32) |
-                        readfirstlane_u32(shfl_u32((u32)t, 0));
-        if (seg >= P.nsegs) break;
-        u32 blk = 0;
-        while (blk + 1 < P.nblocks && P.blocks[blk + 1].seg_first <= seg) blk++;
-        blk = readfirstlane_u32(blk);
+    /* Segment scheduling.  The segments are split into NREG contiguous
+     * regions; workgroup b works in region b % NREG first (workgroups are
+     * dispatched round-robin over the 8 XCDs, so a region streams through
+     * one XCD's L2 and the segments in flight stay adjacent in memory), taking
+     * segments by atomic ticket from the region's own counter, then moves on
+     * to the next regions when its own is exhausted (balancing across CUs).
+     * One ticket address per region keeps the atomics from serializing the
+     * grid (a single-address ticket capped streaming at ~4.4 TB/s,
+     * tools/probe_stream.hip).  P.dynamic == 0: plain static assignment
+     * (wave g takes g, g + G, ...). */
+    const u64 G = (u64)gridDim.x * LIT_SCANNERS;
+    const u32 nreg = P.dynamic ? P.nregions : 1u;
+    u32 reg_i = 0; /* regions tried so far */
+    u32 reg = blockIdx.x % nreg;
+    auto region_lo = [&](u32 r) { return P.nsegs * r / nreg; };
+    auto next_seg = [&](u64 cur, bool first) -> u64 {
+        if (!P.dynamic) return first ? (u64)blockIdx.x * LIT_SCANNERS + wave : cur + G;
+        for (;;) {
+            unsigned long long t = 0;
+            if (lane == 0) t = atomicAdd(&P.counters[16 + 16 * reg], 1ULL);
+            t = ((u64)readlane_u32((u32)(t >> 32), 0) << 32) | readlane_u32((u32)t, 0);
+            const u64 sg = region_lo(reg) + t;
+            if (sg < region_lo(reg + 1)) return sg;
+            if (++reg_i == nreg) return P.nsegs; /* every region drained */
+            reg = (reg + 1) % nreg;
+        }
+    };
+    for (u64 seg = next_seg(0, true); seg < P.nsegs; seg = next_seg(seg, false)) {
+        /* block of the segment: last block with seg_first <= seg */
+        u32 lo = 0, hi = P.nblocks - 1;
+        while (lo < hi) {
+            const u32 mid = (lo + hi + 1) >> 1;
+            if (P.blocks[mid].seg_first <= seg) lo = mid;
+            else hi = mid - 1;
+        }
+        const u32 blk = readfirstlane_u32(lo);
         const VsaBlock B = P.blocks[blk];
         SegCtx S;
         S.blk = blk;
@@ -772,6 +801,35 @@ vsa_lit_scan(VsaLitParams P) {
         const u32 niters = (u32)((s_hi - s_lo + 1023) >> 10);
         const int64_t zlo = (MODE == VSA_MODE_FDR) ? B.zbase : 0;
 
+        /* iterations [f0, f1) are interior ("fast"): no byte of the 1 KiB
+         * chunk or its successor byte lies outside the block, and the FDR
+         * start state / `start` cut-off are behind it.  The rest (at most a
+         * couple per block) run the checked path one at a time. */
+        const int64_t fast_lo = S.blo + S.start + 16;
+        u32 f0 = 0, f1 = niters;
+        if (s_lo < fast_lo) f0 = (u32)min((int64_t)niters, (fast_lo - s_lo + 1023) >> 10);
+        {
+            /* need ib + 1024 < bhi  <=>  it < (bhi - s_lo - 1024 + 1023) / 1024 rounded */
+            int64_t lim = S.bhi - s_lo - 1024; /* ib - s_lo must be < lim */
+            int64_t nf = lim <= 0 ? 0 : (lim + 1023) >> 10;
+            if (nf < (int64_t)f1) f1 = (u32)nf;
+        }
+        if (f1 < f0) f1 = f0;
+        const u32 nf = f1 - f0;
+        const int64_t fb = s_lo + 1024 * (int64_t)f0;
+        uint4 ring[LIT_DEPTH];
+        u32 after = 0;
+        /* issue the sweep's first loads before the prologue's dependent
+         * byte loads, so one memory latency covers both */
+        const bool early = (f0 == 0) && (nf > 0);
+        if (early) {
+#pragma unroll
+            for (int k = 0; k < LIT_DEPTH; k++) {
+                const int64_t pk = ((u32)k < nf ? fb + 1024 * k : fb) + 16 * (int64_t)lane;
+                ring[k] = load_chunk_nc(A, pk);
+            }
+            after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.blo, S.bhi);
+        }
         /* prologue 1: table spill from positions s_lo-NL+1 .. s_lo-1 */
         IterState is;
         is.ncand = ncand_total;
@@ -815,20 +873,6 @@ vsa_lit_scan(VsaLitParams P) {
             }
             is.pbytes = ((u64)shfl_u32((u32)(pb >> 32), 0) << 32) | shfl_u32((u32)pb, 0);
         }
-        /* iterations [f0, f1) are interior ("fast"): no byte of the 1 KiB
-         * chunk or its successor byte lies outside the block, and the FDR
-         * start state / `start` cut-off are behind it.  The rest (at most a
-         * couple per block) run the checked path one at a time. */
-        const int64_t fast_lo = S.blo + S.start + 16;
-        u32 f0 = 0, f1 = niters;
-        if (s_lo < fast_lo) f0 = (u32)min((int64_t)niters, (fast_lo - s_lo + 1023) >> 10);
-        {
-            /* need ib + 1024 < bhi  <=>  it < (bhi - s_lo - 1024 + 1023) / 1024 rounded */
-            int64_t lim = S.bhi - s_lo - 1024; /* ib - s_lo must be < lim */
-            int64_t nf = lim <= 0 ? 0 : (lim + 1023) >> 10;
-            if (nf < (int64_t)f1) f1 = (u32)nf;
-        }
-        if (f1 < f0) f1 = f0;
         for (u32 it = 0; it < f0; it++) {
             const int64_t ib = s_lo + 1024 * (int64_t)it;
             const uint4 cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
@@ -836,21 +880,20 @@ vsa_lit_scan(VsaLitParams P) {
             is = scan_iter<MODE, LDS_TABLE, true>(P, cl, L, S, mis, ib, cur, nxt0, is,
                                                  bucket_mask);
         }
-        if (f0 < f1) {
+        if (nf > 0) {
             /* main sweep: LIT_DEPTH chunks in flight per wave.  ring[k] is
              * consumed and then refilled in place (no register rotation), so
              * each step waits only for the load issued LIT_DEPTH-1 steps ago
-             * (the next chunk's first byte) */
-            const u32 nf = f1 - f0;
-            const int64_t fb = s_lo + 1024 * (int64_t)f0;
-            const u32 after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.blo, S.bhi);
-            uint4 ring[LIT_DEPTH];
-            /* every load is unconditional (an out-of-range prefetch re-reads
-             * the current chunk) so the wait counters stay exact */
+             * (the next chunk's first byte).  Every load is unconditional (an
+             * out-of-range prefetch re-reads the current chunk) so the wait
+             * counters stay exact. */
+            if (!early) {
 #pragma unroll
-            for (int k = 0; k < LIT_DEPTH; k++) {
-                const int64_t pk = ((u32)k < nf ? fb + 1024 * k : fb) + 16 * (int64_t)lane;
-                ring[k] = load_chunk_nc(A, pk);
+                for (int k = 0; k < LIT_DEPTH; k++) {
+                    const int64_t pk = ((u32)k < nf ? fb + 1024 * k : fb) + 16 * (int64_t)lane;
+                    ring[k] = load_chunk_nc(A, pk);
+                }
+                after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.blo, S.bhi);
             }
             const u32 ng = nf / LIT_DEPTH;
             for (u32 g = 0; g < ng; g++) {
@@ -987,7 +1030,7 @@ __global__ void __launch_bounds__(256) vsa_class_scan(VsaClassParams P) {
         cnt += ((u64)chi << 32) | clo;
     }
     if (lane == 0) {
-        const u32 sl = blockIdx.x % P.slots;
+        const u32 sl = 16 * (blockIdx.x % P.slots); /* one 128-B line per slot */
         if (first != ~0ULL) atomicMin(P.first + sl, first);
         if (last) atomicMax(P.last + sl, last);
         if (cnt) atomicAdd(P.count + sl, cnt);

@@ -57,9 +57,12 @@ const int LIT_THREADS = 1024;
 const size_t LDS_BUDGET = 160 * 1024 - 2048; /* minus static LDS */
 const uint32_t SLOT_WORDS_MAX = 4096;        /* 16 KiB of slot bitmaps */
 
+/* d_counters layout (u64): [0..7] scan counters, [16 + 16 r] region
+ * tickets (one 128-B line each), [CLASS_BASE + 16 s + {0,1,2}] class-scan
+ * first / last / count partials of slot s (one line per slot) */
 constexpr int CLASS_SLOTS = 64;
-constexpr int CLASS_BASE = 8;
-constexpr int N_COUNTERS = CLASS_BASE + 3 * CLASS_SLOTS;
+constexpr int CLASS_BASE = 256;
+constexpr int N_COUNTERS = CLASS_BASE + 16 * CLASS_SLOTS;
 
 struct Workspace {
     uint8_t *d_in = nullptr;
@@ -69,10 +72,7 @@ struct Workspace {
     uint64_t out_cap = 0;
     void *d_tmp = nullptr;
     size_t tmp_bytes = 0;
-    /* [0..7] scan counters; [8..199] class-scan partials: first / last /
-     * count in CLASS_SLOTS slots each (spread so that workgroups' atomics hit
-     * different addresses) */
-    unsigned long long *d_counters = nullptr;
+    unsigned long long *d_counters = nullptr; /* layout above */
     unsigned long long *h_counters = nullptr; /* pinned mirror */
     VsaBlock *d_blocks = nullptr;
     VsaBlock *h_blocks = nullptr;
@@ -173,10 +173,29 @@ int ensure_blocks(vsa_ctx *c, uint32_t n) {
     return VSA_OK;
 }
 
-uint32_t pick_seg_shift(uint64_t total) {
-    uint32_t s = 16;
-    while (s > 12 && (total >> s) < 8192) s--;
-    return s;
+/* Segment size (bytes, multiple of 1 KiB) for the literal-scan kernel's
+ * static assignment: at most 64 KiB, at least 4 KiB, and sized so the
+ * segment count is just under a multiple of the scanning-wave count
+ * (every wave gets k or k-1 segments, no long tail).  spans[] are the
+ * per-block byte spans from their 1 KiB-aligned origins. */
+uint64_t pick_seg_bytes(const std::vector<int64_t> &spans, uint64_t waves) {
+    auto count = [&](uint64_t seg) {
+        uint64_t n = 0;
+        for (int64_t sp : spans) n += (uint64_t)((sp + (int64_t)seg - 1) / (int64_t)seg);
+        return n;
+    };
+    uint64_t total = 0;
+    for (int64_t sp : spans) total += (uint64_t)sp;
+    uint64_t seg = 64 << 10;
+    while (seg > (4u << 10) && count(seg) < 2 * waves) seg >>= 1;
+    const uint64_t k = (count(seg) + waves - 1) / waves; /* rounds per wave */
+    if (k >= 2) {
+        uint64_t bal = (total + k * waves - 1) / (k * waves);
+        bal = (bal + 1023) & ~(uint64_t)1023;
+        while (count(bal) > k * waves) bal += 1024; /* per-block rounding */
+        if (bal <= seg) seg = bal;
+    }
+    return seg;
 }
 
 int bits_for(uint64_t v) {
@@ -215,20 +234,20 @@ size_t plan_lds(size_t tab, uint32_t slot_words, uint32_t *qcap) {
 }
 
 int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
-                       uint64_t nsegs, uint32_t seg_shift);
+                       uint64_t nsegs, uint32_t seg_bytes);
 
 int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
-                uint64_t nsegs, uint32_t seg_shift) {
-    VSA_CHECK(hipMemsetAsync(c->ws.d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
+                uint64_t nsegs, uint32_t seg_bytes) {
+    VSA_CHECK(hipMemsetAsync(c->ws.d_counters, 0, 144 * sizeof(unsigned long long), c->stream));
     VSA_CHECK(hipEventRecord(c->ev0, c->stream));
-    int r = launch_scan_kernel(c, db, d_data, nb, nsegs, seg_shift);
+    int r = launch_scan_kernel(c, db, d_data, nb, nsegs, seg_bytes);
     if (r != VSA_OK) return r;
     VSA_CHECK(hipEventRecord(c->ev1, c->stream));
     return VSA_OK;
 }
 
 int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
-                       uint64_t nsegs, uint32_t seg_shift) {
+                       uint64_t nsegs, uint32_t seg_bytes) {
     Workspace &w = c->ws;
     if (db->type == HWLM_ENGINE_NOOD) {
         VsaLitParams P;
@@ -236,7 +255,10 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         P.data = d_data;
         P.blocks = w.d_blocks;
         P.nblocks = nb;
-        P.seg_shift = seg_shift;
+        P.seg_bytes = seg_bytes;
+    P.dynamic = getenv("VSA_STATIC_SEGS") ? 0u : 1u;
+    P.nregions = 8;
+    if (const char *e = getenv("VSA_REGIONS")) P.nregions = (uint32_t)std::min(8, std::max(1, atoi(e)));
         P.nsegs = nsegs;
         const uint32_t ml = db->nood.msk_len; /* 1..8 */
         P.nood_msk = db->nood.msk << (8 * (8 - ml));
@@ -260,7 +282,10 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.data = d_data;
     P.blocks = w.d_blocks;
     P.nblocks = nb;
-    P.seg_shift = seg_shift;
+    P.seg_bytes = seg_bytes;
+    P.dynamic = getenv("VSA_STATIC_SEGS") ? 0u : 1u;
+    P.nregions = 8;
+    if (const char *e = getenv("VSA_REGIONS")) P.nregions = (uint32_t)std::min(8, std::max(1, atoi(e)));
     P.nsegs = nsegs;
     const uint8_t *d_eng = db->d_blob + VSA_ROUNDUP_CL(sizeof(HWLM));
     P.table = db->mode == VSA_MODE_FDR ? (const uint64_t *)(d_eng + 64) : db->d_table;
@@ -343,9 +368,19 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         total += lens[i];
         span = std::max(span, offs[i] + lens[i]);
     }
-    uint32_t seg_shift = pick_seg_shift(total);
-    uint64_t segs = 0;
     const int64_t mis = (int64_t)((uintptr_t)d_data & 15);
+    std::vector<int64_t> spans;
+    spans.reserve(nb);
+    for (uint32_t i = 0; i < nb; i++) {
+        const int64_t len = (int64_t)lens[i], st = starts ? (int64_t)starts[i] : 0;
+        const int64_t blo = (int64_t)offs[i] + mis;
+        const int64_t org = (blo + std::max<int64_t>(0, st - 16)) & ~(int64_t)1023;
+        if (st < len) spans.push_back(blo + len - org);
+    }
+    const uint64_t waves = (uint64_t)c->num_cus * (LIT_WAVES - 1);
+    uint64_t seg_bytes = spans.empty() ? (64u << 10) : pick_seg_bytes(spans, waves);
+    if (const char *e = getenv("VSA_SEG_KB")) seg_bytes = (uint64_t)std::max(1, atoi(e)) << 10;
+    uint64_t segs = 0;
     for (uint32_t i = 0; i < nb; i++) {
         VsaBlock &b = c->ws.h_blocks[i];
         b.base = offs[i];
@@ -361,7 +396,7 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         b.org = (blo + std::max<int64_t>(0, st - 16)) & ~(int64_t)1023;
         if (b.start < b.len) {
             int64_t span = blo + len - b.org;
-            segs += (uint64_t)((span + (1ll << seg_shift) - 1) >> seg_shift);
+            segs += (uint64_t)((span + (int64_t)seg_bytes - 1) / (int64_t)seg_bytes);
         }
     }
     VSA_CHECK(hipMemcpyAsync(c->ws.d_blocks, c->ws.h_blocks, nb * sizeof(VsaBlock),
@@ -374,7 +409,7 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         return VSA_OK;
     }
     for (int attempt = 0; attempt < 3; attempt++) {
-        if ((r = launch_scan(c, db, d_data, nb, segs, seg_shift)) != VSA_OK) return r;
+        if ((r = launch_scan(c, db, d_data, nb, segs, (uint32_t)seg_bytes)) != VSA_OK) return r;
         if (flags & VSA_SCAN_ASYNC) {
             c->pending = true;
             c->pending_flags = flags;
@@ -951,8 +986,13 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
     if (!d_data || ((uintptr_t)d_data & 15)) return VSA_E_INVALID;
     Workspace &w = c->ws;
     unsigned long long *part = w.d_counters + CLASS_BASE;
-    VSA_CHECK(hipMemsetAsync(part, 0xff, CLASS_SLOTS * 8, c->stream));
-    VSA_CHECK(hipMemsetAsync(part + CLASS_SLOTS, 0, 2 * CLASS_SLOTS * 8, c->stream));
+    for (int i = 0; i < CLASS_SLOTS; i++) {
+        w.h_counters[CLASS_BASE + 16 * i] = ~0ULL;
+        w.h_counters[CLASS_BASE + 16 * i + 1] = 0;
+        w.h_counters[CLASS_BASE + 16 * i + 2] = 0;
+    }
+    VSA_CHECK(hipMemcpyAsync(part, w.h_counters + CLASS_BASE, 16 * CLASS_SLOTS * 8,
+                             hipMemcpyHostToDevice, c->stream));
     VsaClassParams P;
     memset(&P, 0, sizeof(P));
     P.data = d_data;
@@ -964,8 +1004,8 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
     }
     P.bitmap = d_bitmap;
     P.first = part;
-    P.last = part + CLASS_SLOTS;
-    P.count = part + 2 * CLASS_SLOTS;
+    P.last = part + 1;
+    P.count = part + 2;
     P.slots = CLASS_SLOTS;
     uint64_t chunks = (len + 15) / 16;
     uint64_t want = (chunks + 255) / 256;
@@ -975,7 +1015,7 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
     hipLaunchKernelGGL(vsa_class_scan, dim3(grid), dim3(256), 0, c->stream, P);
     VSA_CHECK(hipGetLastError());
     VSA_CHECK(hipEventRecord(c->ev1, c->stream));
-    VSA_CHECK(hipMemcpyAsync(w.h_counters + CLASS_BASE, part, 3 * CLASS_SLOTS * 8,
+    VSA_CHECK(hipMemcpyAsync(w.h_counters + CLASS_BASE, part, 16 * CLASS_SLOTS * 8,
                              hipMemcpyDeviceToHost, c->stream));
     VSA_CHECK(hipStreamSynchronize(c->stream));
     {
@@ -985,9 +1025,9 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
     const unsigned long long *h = w.h_counters + CLASS_BASE;
     uint64_t f = ~0ULL, l = 0, n = 0;
     for (int i = 0; i < CLASS_SLOTS; i++) {
-        f = std::min<uint64_t>(f, h[i]);
-        l = std::max<uint64_t>(l, h[CLASS_SLOTS + i]);
-        n += h[2 * CLASS_SLOTS + i];
+        f = std::min<uint64_t>(f, h[16 * i]);
+        l = std::max<uint64_t>(l, h[16 * i + 1]);
+        n += h[16 * i + 2];
     }
     if (first) *first = f == ~0ULL ? len : f;
     if (last) *last = l;
