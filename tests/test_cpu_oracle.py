@@ -264,3 +264,27 @@ def test_library_exports_header_symbols():
     lib = ctypes.CDLL(vsa.LIB_PATH)
     missing = [n for n in sorted(names) if not hasattr(lib, n)]
     assert not missing, missing
+
+
+@pytest.mark.parametrize("nlits,lo", [(300, 6), (200, 8), (1000, 4)])
+def test_oracle_vs_bruteforce_long_literals(nlits, lo):
+    """Stride 2 / 4 FDR engines (long literal sets, fdr_compile.cpp
+    chooseEngine) against brute force."""
+    rng = random.Random(nlits * 31 + lo)
+    lits = rand_lits(rng, nlits, minlen=lo, maxlen=8, nocase_frac=0.1)
+    blob = vsa.hwlm_build(lits)
+    assert blob.engine_id == 0
+    for ln in (0, 5, 16, 17, 40, 300, 5000):
+        data = rand_data(rng, ln, alphabet=b"abcdefgh")
+        for start in sorted({0, 1, 3, ln // 2}):
+            if ln and start >= ln:
+                continue
+            st, m = oracle.hwlm_exec(blob.ptr, data, start=start, cap=1 << 16)
+            got = set(m)
+            exp = oracle.brute_force(lits, data)
+            if start == 0:
+                assert got == exp, (nlits, ln)
+            else:
+                assert got <= {(e, i) for e, i in exp if e >= start}
+                lens = {l.id: len(l.s) for l in lits}
+                assert {(e, i) for e, i in exp if e - lens[i] + 1 >= start} <= got

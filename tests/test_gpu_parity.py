@@ -271,3 +271,22 @@ def test_gpu_dropin_reused_address():
         _, m_g = vsa.hwlm_exec(shared, data)
         _, m_o = oracle.hwlm_exec(blob.ptr, data, cap=1 << 16)
         assert m_g == m_o and m_g
+
+
+@pytest.mark.parametrize("nlits,lo", [(300, 6), (200, 8), (1000, 4), (2000, 7)])
+def test_gpu_fdr_long_literal_strides(nlits, lo):
+    """Stride 2 / 4 FDR bytecode: the device first stage is rebuilt as a
+    stride-1 table from the confirm records; matches must equal the
+    oracle's (which follows the bytecode's own stride)."""
+    rng = random.Random(nlits * 31 + lo)
+    lits = rand_lits(rng, nlits, minlen=lo, maxlen=8, nocase_frac=0.1, msk_frac=0.1)
+    blob = vsa.hwlm_build(lits)
+    assert blob.engine_id == 0
+    for ln in (5, 16, 17, 40, 300, 5000, 70000):
+        data = rand_data(rng, ln, alphabet=b"abcdefghAB")
+        for start in sorted({0, 1, 3, 9, ln // 2}):
+            if start >= ln:
+                continue
+            st_o, m_o = oracle.hwlm_exec(blob.ptr, data, start=start, cap=1 << 18)
+            st_g, m_g = gpu_hwlm(blob, data, start=start)
+            assert m_g == m_o, (nlits, lo, ln, start)

@@ -106,7 +106,7 @@ struct vsa_db {
     uint8_t *hblob = nullptr;  /* aligned pointer into host */
     size_t size = 0;
     uint8_t *d_blob = nullptr;
-    uint64_t *d_table = nullptr; /* Teddy combined table (owned) */
+    uint64_t *d_table = nullptr; /* derived FDR table / Teddy combined table */
     int type = 0;                /* HWLM_ENGINE_NOOD / FDR */
     uint32_t engine_id = 0;
     int mode = 0;                /* VsaLitMode */
@@ -288,7 +288,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     if (const char *e = getenv("VSA_REGIONS")) P.nregions = (uint32_t)std::min(8, std::max(1, atoi(e)));
     P.nsegs = nsegs;
     const uint8_t *d_eng = db->d_blob + VSA_ROUNDUP_CL(sizeof(HWLM));
-    P.table = db->mode == VSA_MODE_FDR ? (const uint64_t *)(d_eng + 64) : db->d_table;
+    P.table = db->d_table; /* derived FDR table / combined Teddy table */
     P.table_entries = db->table_entries;
     P.dmask = db->dmask;
     P.state_lo = db->state_lo;
@@ -741,6 +741,81 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
 
 void *vsa_ctx_stream(vsa_ctx_t *c) { return c ? (void *)c->stream : nullptr; }
 
+/* ------------------------------------------- derived FDR first stage -- */
+
+/* The device first stage for an FDR engine is a stride-1 shift-or table
+ * rebuilt from the engine's own confirm records (every LitInfo's v / msk,
+ * fdr_confirm.h:57-65), in the reference's bucket layout: bit (k * 8 + b)
+ * of T[key] is 0 when some literal of bucket b is consistent with the two
+ * bytes (key & 0xff, key >> 8) sitting k bytes before its end
+ * (getMultiEntriesAtPosition, fdr_compile.cpp:520-600, restated over the
+ * 8-byte confirm window; the byte after the end is a don't-care).  Every
+ * literal the confirm accepts is consistent at every window, so the set of
+ * confirmed matches is exactly the reference's, for any stride / domain of
+ * the bytecode, while a wider domain (14 bits: the whole first byte and 6
+ * bits of the second) cuts false candidates. */
+static void derive_fdr_table(const uint8_t *eng, const uint32_t conf_off[8], uint32_t bits,
+                             std::vector<uint64_t> &T) {
+    const uint32_t n = 1u << bits;
+    const uint32_t hi_bits = bits - 8;            /* bits of the second byte */
+    const uint32_t hi_mask = (1u << hi_bits) - 1;
+    T.assign(n, ~0ULL);
+    uint64_t always = 0; /* (k, b) columns open for every key */
+    const uint8_t *confBase = eng + ((const uint32_t *)eng)[4];
+    for (uint32_t b = 0; b < 8; b++) {
+        if (!conf_off[b]) continue;
+        const uint8_t *fc = confBase + conf_off[b];
+        const FDRConfirm *cf = (const FDRConfirm *)fc;
+        const uint32_t *li = (const uint32_t *)(fc + sizeof(FDRConfirm));
+        std::vector<uint32_t> offs;
+        for (uint32_t h = 0; h < (1u << cf->nBits); h++) {
+            uint32_t o = li[h];
+            if (!o) continue;
+            for (;;) {
+                offs.push_back(o);
+                const LitInfo *L = (const LitInfo *)(fc + o);
+                if (!L->next) break;
+                o += sizeof(LitInfo);
+            }
+        }
+        std::sort(offs.begin(), offs.end());
+        offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
+        for (uint32_t o : offs) {
+            const LitInfo *L = (const LitInfo *)(fc + o);
+            for (uint32_t k = 0; k < 8; k++) {
+                const uint64_t bit = 1ULL << (k * 8 + b);
+                /* first key byte: k bytes before the end (byte 7 - k of v) */
+                const uint8_t m0 = (uint8_t)(L->msk >> (8 * (7 - k)));
+                const uint8_t v0 = (uint8_t)(L->v >> (8 * (7 - k))) & m0;
+                /* second key byte: k - 1 before the end (k = 0: past it) */
+                uint32_t m1 = 0, v1 = 0;
+                if (k >= 1) {
+                    m1 = (uint8_t)(L->msk >> (8 * (8 - k))) & hi_mask;
+                    v1 = (uint8_t)(L->v >> (8 * (8 - k))) & m1;
+                }
+                if (!m0 && !m1) {
+                    always |= bit;
+                    continue;
+                }
+                /* enumerate the free bits of both bytes */
+                const uint32_t f0 = 0xffu & ~m0, f1 = hi_mask & ~m1;
+                uint32_t x0 = 0;
+                do {
+                    uint32_t x1 = 0;
+                    do {
+                        T[(v0 | x0) | ((v1 | x1) << 8)] &= ~bit;
+                        x1 = (x1 - f1) & f1;
+                    } while (x1);
+                    x0 = (x0 - f0) & f0;
+                } while (x0);
+            }
+        }
+    }
+    if (always) {
+        for (auto &t : T) t &= ~always;
+    }
+}
+
 int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
     if (!c || !hwlm || !out || size < VSA_ROUNDUP_CL(sizeof(HWLM))) return VSA_E_INVALID;
     VSA_CHECK(hipSetDevice(c->device));
@@ -813,6 +888,20 @@ int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
     VSA_CHECK(hipSetDevice(c->device));
     VSA_CHECK(hipMalloc(&db->d_blob, size));
     VSA_CHECK(hipMemcpy(db->d_blob, db->hblob, size, hipMemcpyHostToDevice));
+    if (db->mode == VSA_MODE_FDR) {
+        /* derived stride-1 first stage: domain 14 when it fits in LDS beside
+         * the rings and slot bitmaps, else 13 (see derive_fdr_table) */
+        uint32_t qc = 0;
+        uint32_t bits = 14;
+        if (getenv("VSA_FDR_DOMAIN")) bits = (uint32_t)std::min(15, std::max(9, atoi(getenv("VSA_FDR_DOMAIN"))));
+        else if (plan_lds((size_t)8 << 14, db->slot_words, &qc) > LDS_BUDGET) bits = 13;
+        std::vector<uint64_t> T;
+        derive_fdr_table(eng, db->conf_off, bits, T);
+        db->table_entries = 1u << bits;
+        db->dmask = (1u << bits) - 1;
+        VSA_CHECK(hipMalloc(&db->d_table, T.size() * 8));
+        VSA_CHECK(hipMemcpy(db->d_table, T.data(), T.size() * 8, hipMemcpyHostToDevice));
+    }
     if (db->mode == VSA_MODE_TEDDY || db->mode == VSA_MODE_FAT) {
         /* combine nibble masks per byte value (teddy.c:921-971): field j of
          * W[c] = lo_j[c & 15] | hi_j[c >> 4] for the 8 (or 16) buckets */
