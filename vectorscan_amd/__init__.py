@@ -44,7 +44,7 @@ ENGINE_NOOD = 16
 HWLM_HEADER = 192  # ROUNDUP_CL(sizeof(struct HWLM))
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                        "libvectorscan_amd.so")
+                        os.environ.get("VSA_LIB_VARIANT", "libvectorscan_amd.so"))
 if not os.path.exists(LIB_PATH):
     raise ImportError(
         "vectorscan_amd: %s is missing — build it with `make` (or "

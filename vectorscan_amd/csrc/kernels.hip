@@ -254,9 +254,10 @@ __device__ __forceinline__ u64 lit_lookup(const void *tab, u32 key, u32 lane) {
 template <int MODE>
 __device__ __forceinline__ u32 lit_key(const u32 d[5], int j, u32 dmask) {
     if constexpr (LitTraits<MODE>::KEY16) {
-        u32 w = (j & 3) ? __builtin_amdgcn_alignbyte(d[(j >> 2) + 1], d[j >> 2], j & 3)
-                        : d[j >> 2];
-        return w & dmask;
+        /* dmask = 2^bits - 1 (fdr_compile.cpp:185-187, and the derived
+         * table): one bit-field extract while the key sits in one dword */
+        if ((j & 3) != 3) return __builtin_amdgcn_ubfe(d[j >> 2], 8 * (j & 3), 32 - __clz(dmask));
+        return __builtin_amdgcn_alignbyte(d[(j >> 2) + 1], d[j >> 2], 3) & dmask;
     } else {
         (void)dmask;
         return (d[j >> 2] >> (8 * (j & 3))) & 0xff;
@@ -821,7 +822,10 @@ vsa_lit_scan(VsaLitParams P) {
         u32 after = 0;
         /* issue the sweep's first loads before the prologue's dependent
          * byte loads, so one memory latency covers both */
-        const bool early = (f0 == 0) && (nf > 0);
+#ifndef LIT_EARLY
+#define LIT_EARLY 0
+#endif
+        const bool early = LIT_EARLY && (f0 == 0) && (nf > 0);
         if (early) {
 #pragma unroll
             for (int k = 0; k < LIT_DEPTH; k++) {
