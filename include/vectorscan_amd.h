@@ -70,6 +70,13 @@ const uint8_t *shuftiExec(vsa_m128_t mask_lo, vsa_m128_t mask_hi,
                           const uint8_t *buf, const uint8_t *buf_end);
 const uint8_t *rshuftiExec(vsa_m128_t mask_lo, vsa_m128_t mask_hi,
                            const uint8_t *buf, const uint8_t *buf_end);
+/* shufti.h:52-55; masks from shuftiBuildDoubleMasks (bit clear = member).
+ * Reproduces the reference's per-block results for VECTORSIZE set by
+ * vsa_set_accel_vector_size (default 64, the AVX-512 build), including the
+ * matches at the last byte of each 16-byte lane it reports. */
+const uint8_t *shuftiDoubleExec(vsa_m128_t mask1_lo, vsa_m128_t mask1_hi,
+                                vsa_m128_t mask2_lo, vsa_m128_t mask2_hi,
+                                const uint8_t *buf, const uint8_t *buf_end);
 const uint8_t *truffleExec(vsa_m128_t mask1, vsa_m128_t mask2,
                            const uint8_t *buf, const uint8_t *buf_end);
 const uint8_t *rtruffleExec(vsa_m128_t mask1, vsa_m128_t mask2,
@@ -216,6 +223,19 @@ int64_t vsa_shufti_find(const uint8_t lo[16], const uint8_t hi[16],
                         const uint8_t *buf, size_t len, int reverse);
 int64_t vsa_truffle_find(const uint8_t m1[16], const uint8_t m2[16],
                          const uint8_t *buf, size_t len, int reverse);
+/* shuftiDoubleExec by pointer: first match index or len (-2 on error). */
+int64_t vsa_shufti_double_find(const uint8_t lo1[16], const uint8_t hi1[16],
+                               const uint8_t lo2[16], const uint8_t hi2[16],
+                               const uint8_t *buf, size_t len);
+/* VECTORSIZE of the reference build whose shuftiDoubleExec is emulated
+ * (16 SSE, 32 AVX2, 64 AVX-512; default 64). */
+void vsa_set_accel_vector_size(uint32_t vsize);
+/* shufticompile.cpp:135 shuftiBuildDoubleMasks: onechar = 256-bit class
+ * (may be NULL), pairs = npairs (first, second) bytes.  0 ok, -1 = more
+ * than 8 buckets needed. */
+int vsa_shufti_build_double_masks(const uint8_t onechar[32], const uint8_t *pairs,
+                                  size_t npairs, uint8_t lo1[16], uint8_t hi1[16],
+                                  uint8_t lo2[16], uint8_t hi2[16]);
 /* mode: 0 verm, 1 nverm, 2 rverm, 3 rnverm, 4 dverm, 5 dverm masked */
 int64_t vsa_verm_find(int mode, uint8_t c1, uint8_t c2, uint8_t m1, uint8_t m2,
                       int nocase, const uint8_t *buf, size_t len);

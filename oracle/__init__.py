@@ -48,6 +48,7 @@ _sig("orc_nood_exec", _i64, _vp, _vp, _sz, _sz, _vp, _sz, _i64, ctypes.POINTER(_
 _sig("orc_shufti", _i64, _vp, _vp, _vp, _sz)
 _sig("orc_rshufti", _i64, _vp, _vp, _vp, _sz)
 _sig("orc_truffle", _i64, _vp, _vp, _vp, _sz)
+_sig("orc_shufti_double", _i64, _vp, _vp, _vp, _vp, _vp, _sz, _i64, _i64)
 _sig("orc_rtruffle", _i64, _vp, _vp, _vp, _sz)
 _sig("orc_verm", _i64, ctypes.c_uint8, _int, _int, _int, _vp, _sz)
 _sig("orc_dverm", _i64, ctypes.c_uint8, ctypes.c_uint8, _int, _vp, _sz)
@@ -98,6 +99,14 @@ def shufti(lo, hi, data, reverse=False):
     keep, p, n = _buf(data)
     f = _lib.orc_rshufti if reverse else _lib.orc_shufti
     return f(bytes(lo), bytes(hi), p, n)
+
+
+def shufti_double(lo1, hi1, lo2, hi2, data, vector_size=64, mis=0):
+    """shuftiDoubleExec with VECTORSIZE `vector_size` on a buffer whose
+    address is `mis` mod vector_size; returns the first match index or len."""
+    keep, p, n = _buf(data)
+    return _lib.orc_shufti_double(bytes(lo1), bytes(hi1), bytes(lo2), bytes(hi2), p, n,
+                                  vector_size, mis)
 
 
 def truffle(m1, m2, data, reverse=False):

@@ -125,6 +125,62 @@ long orc_rshufti(const u8 *lo, const u8 *hi, const u8 *buf, size_t len) {
     return -1;
 }
 
+/* shuftiDoubleExec (shufti_simd.hpp:195-258, x86/shufti.hpp:49-79) with
+ * vector width S (VECTORSIZE: 16 SSE, 32 AVX2, 64 AVX-512) and the buffer's
+ * address mod S (`mis`).  blockDoubleMask: c = c1 | (c2 shifted down one
+ * byte within each 128-bit lane); byte i matches when c != 0xff, i.e. some
+ * bucket is clear in both c1[i] and c2[i+1] -- at the last byte of every
+ * 16-byte lane the shifted-in c2 is 0, so c1 alone decides there.  Blocks:
+ * an unaligned head block at buf (when buf is not S-aligned and len >= S),
+ * S-aligned blocks while a whole block fits, then a tail block ending at
+ * buf_end (or, when len < S, the buffer zero-padded to S bytes, results
+ * >= len dropped).  Returns the first match, or len. */
+static long dshufti_block(const u8 *n1, const u8 *n2, const u8 *buf, size_t len, long b0,
+                          long S) {
+    for (long k = 0; k < S; k++) {
+        long i = b0 + k;
+        u8 x = (i >= 0 && (size_t)i < len) ? buf[i] : 0;
+        u8 m2;
+        if ((k & 15) == 15) {
+            m2 = 0xff;
+        } else {
+            long j = i + 1;
+            u8 y = (j >= 0 && (size_t)j < len) ? buf[j] : 0;
+            m2 = n2[y];
+        }
+        if (n1[x] & m2) return i;
+    }
+    return -1;
+}
+
+long orc_shufti_double(const u8 *lo1, const u8 *hi1, const u8 *lo2, const u8 *hi2,
+                       const u8 *buf, size_t len, long S, long mis) {
+    u8 n1[256], n2[256];
+    for (int c = 0; c < 256; c++) {
+        n1[c] = (u8)~(lo1[c & 15] | hi1[c >> 4]);
+        n2[c] = (u8)~(lo2[c & 15] | hi2[c >> 4]);
+    }
+    long d = 0, r;
+    if ((long)len >= S) {
+        if (mis % S) {
+            if ((r = dshufti_block(n1, n2, buf, len, 0, S)) >= 0) return r;
+            d = S - mis % S;
+        }
+        for (; d + S <= (long)len; d += S) {
+            if ((r = dshufti_block(n1, n2, buf, len, d, S)) >= 0) return r;
+        }
+    }
+    if (d != (long)len) {
+        if ((long)len < S) {
+            r = dshufti_block(n1, n2, buf, len, 0, S);
+        } else {
+            r = dshufti_block(n1, n2, buf, len, (long)len - S, S);
+        }
+        if (r >= 0 && r < (long)len) return r;
+    }
+    return (long)len;
+}
+
 /* x86/truffle.hpp:36-62: member iff mask[c>>7][c&15] has bit (c>>4)&7 */
 static inline int truffle_member(const u8 *m1, const u8 *m2, u8 c) {
     const u8 *m = (c & 0x80) ? m2 : m1;

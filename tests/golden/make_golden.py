@@ -269,6 +269,110 @@ def accel_cases():
     return cases
 
 
+def dshufti_cases():
+    """shufti.cpp:280-890 (DoubleShufti): mask-builder checks and
+    shuftiDoubleExec known answers.  Positions are relative to the test's
+    char array t; the scan covers t[start:end].  expect kinds:
+      eq       rv == t + value
+      ge       rv >= t + value
+      ge_end16 rv >= (addr(t) + end) & ~15   (depends on t's alignment)
+    """
+    build, ex = [], []
+    o = ord
+
+    def b(src, pairs, onechar=(), ok=True, checks=(), exact=None):
+        build.append({"src": src, "pairs": [[o(x), o(y)] for x, y in pairs],
+                      "onechar": [o(c) for c in onechar], "ok": ok,
+                      "checks": [[o(a), o(c), rel] for a, c, rel in checks],
+                      "exact": exact})
+
+    # BuildMask1 :280-320 (exact masks)
+    ex1 = {"lo1": [254 if i == o("a") % 16 else 255 for i in range(16)],
+           "hi1": [254 if i == o("a") >> 4 else 255 for i in range(16)],
+           "lo2": [254 if i == o("B") % 16 else 255 for i in range(16)],
+           "hi2": [254 if i == o("B") >> 4 else 255 for i in range(16)]}
+    b("shufti.cpp:280 BuildMask1", [("a", "B")], exact=ex1)
+    b("shufti.cpp:322 BuildMask2", [("a", "z"), ("B", "z")],
+      checks=[("a", "z", "ne"), ("B", "z", "ne")])
+    b("shufti.cpp:348 BuildMask4", [("a", "z"), ("B", "z"), ("A", "z"), ("b", "z")],
+      checks=[(c, "z", "ne") for c in "aAbB"])
+    b("shufti.cpp:376 BuildMask5", [("a", "z")], onechar="X",
+      checks=[("a", "z", "ne")] + [(c, "X", "eq") for c in "aAbB"])
+    six = [(c, d) for d in "zyx" for c in "aBAb"]
+    b("shufti.cpp:407 BuildMask6", six, checks=[(c, d, "ne") for c, d in six])
+    b("shufti.cpp:459 BuildMask7", [(chr(x), chr(x + 1)) for x in range(o("a"), o("x"), 2)],
+      ok=False)
+
+    def e(src, pairs, data, start, end, kind, value, onechar=()):
+        ex.append({"src": src, "pairs": [[o(x), o(y)] for x, y in pairs],
+                   "onechar": [o(c) for c in onechar], "data": hx(data), "start": start,
+                   "end": end, "kind": kind, "value": value})
+
+    allb = b"b" * 61
+    alle = b"e" * 61
+    for i in range(16):
+        e("shufti.cpp:482 ExecNoMatch1", [("a", "b")], allb, i, 61, "ge_end16", 0)
+        e("shufti.cpp:503 ExecNoMatch1b", [("b", "a")], allb, i, 61, "ge", i + 15)
+        e("shufti.cpp:524 ExecNoMatch2", [("a", "b"), ("B", "b")], allb, i, 61, "ge_end16", 0)
+        e("shufti.cpp:546 ExecNoMatch2b", [("b", "a"), ("b", "B")], allb, i, 61, "ge", i + 15)
+        e("shufti.cpp:568 ExecNoMatch3", [("V", "e")], alle, i, 61, "ge_end16", 0)
+        e("shufti.cpp:589 ExecNoMatch3b", [("e", "V")], alle, i, 61, "ge", i + 15)
+    t = b"bbbbbbbbbbbbbbbbbabbbbbbbbbbbbbbbbb"
+    for i in range(16):
+        e("shufti.cpp:610 ExecMatchShort1", [("a", "b")], t, i, len(t), "eq", 17)
+    t = b"bbbbbbbbbbbbbbbbbabbbbbbbbbbbbbbbbbbbbbbbbbbbbbbabbbbbbbbbbbb"
+    for i in range(16):
+        e("shufti.cpp:632 ExecMatch1", [("a", "b")], t, i, len(t), "eq", 17)
+    t = b"bbbbbbbbbbbbbbbbbaaaaaaaaaaaaaaaabbbbbbbbbbbbbbbabbbbbbbbbbbb"
+    for i in range(16):
+        e("shufti.cpp:654 ExecMatch2", [("a", "a")], t, i, len(t), "eq", 17)
+    t = b"bbbbbbbbbbbbbbbbbBaaaaaaaaaaaaaaaabbbbbbbbbbbbbbbabbbbbbbbbbbb"
+    for i in range(16):
+        e("shufti.cpp:676 ExecMatch3", [("B", "a"), ("a", "a")], t, i, len(t), "eq", 17)
+    p4 = [("A", "a"), ("a", "a"), ("C", "a"), ("c", "a")]
+    p4b = [("a", "A"), ("a", "a"), ("a", "C"), ("a", "c")]
+    for c in "ACca":
+        t = b"b" * 17 + c.encode() + b"a" * 15 + b"b" * 15 + b"a" + b"b" * 11
+        tb = b"b" * 17 + b"a" + c.encode() + b"a" * 14 + b"b" * 15 + b"a" + b"b" * 11
+        for i in range(16):
+            e("shufti.cpp:699 ExecMatch4", p4, t, i, len(t), "eq", 17)
+            e("shufti.cpp:742 ExecMatch4b", p4b, tb, i, len(tb), "eq", 17)
+    t = bytearray(b"b" * 76)
+    for i in range(31):
+        t[48 - i] = o("a")
+        t[48 - i + 1] = o("A")
+        e("shufti.cpp:785 ExecMatch5", [("a", "A")], bytes(t), 0, 76, "eq", 48 - i)
+    t = bytearray(b"b" * 76)
+    for i in range(31):
+        t[48 - i] = o("a")
+        e("shufti.cpp:808 ExecMatchMixed1", [], bytes(t), 0, 76, "eq", 48 - i, onechar="a")
+    t = bytearray(b"b" * 76)
+    for i in range(31):
+        t[48 - i] = o("a")
+        e("shufti.cpp:832 ExecMatchMixed2", [("x", "y")], bytes(t), 0, 76, "eq", 48 - i,
+          onechar="a")
+    t2 = bytearray(b"b" * 76)
+    for i in range(31):
+        t2[48 - i] = o("x")
+        t2[48 - i + 1] = o("y")
+        e("shufti.cpp:832 ExecMatchMixed2", [("x", "y")], bytes(t2), 0, 76, "eq", 48 - i,
+          onechar="a")
+    # Mixed3 :867-890 (len 420; t[len - i] written inside / just past the buffer)
+    L = 420
+    t = bytearray(b"b" * (L + 1))
+    for i in range(1, 400):
+        t[L - i] = o("a")
+        e("shufti.cpp:867 ExecMatchMixed3", [("x", "y")], bytes(t[:L]), 0, L, "eq", L - i,
+          onechar="a")
+    t = bytearray(b"b" * (L + 2))
+    for i in range(0, 400):
+        t[L - i] = o("x")
+        t[L - i + 1] = o("y")
+        e("shufti.cpp:867 ExecMatchMixed3", [("x", "y")], bytes(t[:L]), 0, L, "eq", L - i,
+          onechar="a")
+    return {"build": build, "exec": ex}
+
+
 def main():
     with open(os.path.join(HERE, "noodle.json"), "w") as f:
         json.dump(noodle_cases(), f)
@@ -278,6 +382,8 @@ def main():
         json.dump(short_writings_spec(), f)
     with open(os.path.join(HERE, "accel.json"), "w") as f:
         json.dump(accel_cases(), f)
+    with open(os.path.join(HERE, "dshufti.json"), "w") as f:
+        json.dump(dshufti_cases(), f)
 
 
 if __name__ == "__main__":

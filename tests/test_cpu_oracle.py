@@ -288,3 +288,62 @@ def test_oracle_vs_bruteforce_long_literals(nlits, lo):
                 assert got <= {(e, i) for e, i in exp if e >= start}
                 lens = {l.id: len(l.s) for l in lits}
                 assert {(e, i) for e, i in exp if e - lens[i] + 1 >= start} <= got
+
+
+# ------------------------------------------------------ double shufti ----
+
+def placed(data, mis, align=64):
+    """Copy data to host memory whose address is `mis` mod `align`;
+    returns (keepalive, address)."""
+    import ctypes
+    buf = ctypes.create_string_buffer(len(data) + 2 * align)
+    addr = ctypes.addressof(buf)
+    addr += (mis - addr) % align
+    ctypes.memmove(addr, bytes(data), len(data))
+    return buf, addr
+
+
+def dshufti_expect_ok(c, r, base_mis):
+    """r = result index relative to the scanned buffer t[start:end]."""
+    base = 4096 + base_mis
+    rv = base + c["start"] + r
+    if c["kind"] == "eq":
+        return rv == base + c["value"]
+    if c["kind"] == "ge":
+        return rv >= base + c["value"]
+    assert c["kind"] == "ge_end16"
+    return rv >= (base + c["end"]) & ~15
+
+
+def dshufti_masks(c):
+    return vsa.shufti_build_double_masks([tuple(p) for p in c["pairs"]], bytes(c["onechar"]))
+
+
+def test_golden_dshufti_build():
+    spec = load("dshufti.json")
+    for c in spec["build"]:
+        m = dshufti_masks(c)
+        assert (m is not None) == c["ok"], c["src"]
+        if m is None:
+            continue
+        lo1, hi1, lo2, hi2 = m
+        if c["exact"]:
+            assert list(lo1) == c["exact"]["lo1"] and list(hi1) == c["exact"]["hi1"]
+            assert list(lo2) == c["exact"]["lo2"] and list(hi2) == c["exact"]["hi2"]
+        for a, b, rel in c["checks"]:
+            v = lo1[a % 16] | hi1[a >> 4] | lo2[b % 16] | hi2[b >> 4]
+            assert (v != 0xFF) if rel == "ne" else (v == 0xFF), (c["src"], chr(a), chr(b))
+
+
+@pytest.mark.parametrize("vsize", [16, 32, 64])
+def test_golden_dshufti_oracle(vsize):
+    """shufti.cpp:482-890 known answers hold for the restated
+    shuftiDoubleExec at every alignment of the test array."""
+    spec = load("dshufti.json")
+    for c in spec["exec"]:
+        m = dshufti_masks(c)
+        data = bytes.fromhex(c["data"])[c["start"]:c["end"]]
+        for base_mis in (0, 1, 5, 8, 15, 16, 33, 63):
+            mis = (base_mis + c["start"]) % vsize
+            r = oracle.shufti_double(*m, data, vector_size=vsize, mis=mis)
+            assert dshufti_expect_ok(c, r, base_mis), (c["src"], vsize, base_mis, r)

@@ -290,3 +290,51 @@ def test_gpu_fdr_long_literal_strides(nlits, lo):
             st_o, m_o = oracle.hwlm_exec(blob.ptr, data, start=start, cap=1 << 18)
             st_g, m_g = gpu_hwlm(blob, data, start=start)
             assert m_g == m_o, (nlits, lo, ln, start)
+
+
+@pytest.mark.parametrize("vsize", [16, 32, 64])
+def test_gpu_golden_dshufti(vsize):
+    """shuftiDoubleExec drop-in: the reference's known answers (shufti.cpp:
+    482-890) and exact agreement with the oracle at several alignments."""
+    from test_cpu_oracle import dshufti_expect_ok, dshufti_masks, placed
+    vsa.set_accel_vector_size(vsize)
+    try:
+        spec = load("dshufti.json")
+        for c in spec["exec"][::3]:
+            m = dshufti_masks(c)
+            full = bytes.fromhex(c["data"])
+            for base_mis in (0, 3, 16, 47):
+                keep, addr = placed(full, base_mis)
+                p = addr + c["start"]
+                n = c["end"] - c["start"]
+                r = vsa.shufti_double_find(*m, p, n)
+                want = oracle.shufti_double(*m, full[c["start"]:c["end"]], vector_size=vsize,
+                                            mis=p % vsize)
+                assert r == want, (c["src"], vsize, base_mis)
+                assert dshufti_expect_ok(c, r, base_mis), (c["src"], vsize, base_mis)
+    finally:
+        vsa.set_accel_vector_size(64)
+
+
+def test_gpu_dshufti_random():
+    """Random byte pairs / one-byte literals: lane-end artifacts, short and
+    long buffers, every alignment mod 64 — device == oracle."""
+    from test_cpu_oracle import placed
+    rng = random.Random(77)
+    for trial in range(24):
+        alpha = bytes(rng.sample(range(256), rng.randint(2, 12)))
+        pairs = [(rng.choice(alpha), rng.choice(alpha)) for _ in range(rng.randint(0, 5))]
+        one = bytes(rng.sample(alpha, rng.randint(0, 2)))
+        m = vsa.shufti_build_double_masks(pairs, one)
+        if m is None or (not pairs and not one):
+            continue
+        for vsize in (16, 32, 64):
+            vsa.set_accel_vector_size(vsize)
+            for n in (1, 7, 15, 16, 17, 31, 33, 63, 64, 65, 100, 200, 1000):
+                data = bytes(rng.choice(alpha + b"..") for _ in range(n))
+                mis = rng.randrange(64)
+                keep, addr = placed(data, mis)
+                r = vsa.shufti_double_find(*m, addr, n)
+                want = oracle.shufti_double(*m, data, vector_size=vsize, mis=addr % vsize)
+                assert r == want, (trial, vsize, n, mis)
+    vsa.set_accel_vector_size(64)

@@ -93,6 +93,11 @@ _sig("noodExec", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t
      ctypes.c_size_t, HWLMCallback, ctypes.c_void_p)
 _sig("vsa_shufti_find", ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
+_sig("vsa_shufti_double_find", ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+_sig("vsa_set_accel_vector_size", None, ctypes.c_uint32)
+_sig("vsa_shufti_build_double_masks", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+     ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p)
 _sig("vsa_truffle_find", ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
 _sig("vsa_verm_find", ctypes.c_int64, ctypes.c_int, ctypes.c_uint8, ctypes.c_uint8,
@@ -305,6 +310,30 @@ def shufti_exec(lo, hi, data):
     """shuftiExec: index of the first byte in the class, or len(data)."""
     keep, ptr, n = _as_buf(data)
     return lib.vsa_shufti_find(_m16(lo), _m16(hi), ptr, n, 0)
+
+
+def shufti_double_find(lo1, hi1, lo2, hi2, ptr, n):
+    """shuftiDoubleExec on host memory at address `ptr` (its alignment
+    matters, as in the reference): first match index or n."""
+    return lib.vsa_shufti_double_find(_m16(lo1), _m16(hi1), _m16(lo2), _m16(hi2), ptr, n)
+
+
+def set_accel_vector_size(vsize):
+    """VECTORSIZE of the reference build emulated by shuftiDoubleExec."""
+    lib.vsa_set_accel_vector_size(vsize)
+
+
+def shufti_build_double_masks(pairs, onechar=b""):
+    """shuftiBuildDoubleMasks (shufticompile.cpp:135): (lo1, hi1, lo2, hi2)
+    or None when more than 8 buckets are needed."""
+    cls = class_bitmap(onechar)
+    pr = np.array([b for p in pairs for b in p], np.uint8)
+    out = [np.zeros(16, np.uint8) for _ in range(4)]
+    r = lib.vsa_shufti_build_double_masks(cls.ctypes.data, pr.ctypes.data if len(pr) else None,
+                                          len(pairs), *[o.ctypes.data for o in out])
+    if r < 0:
+        return None
+    return tuple(o.tobytes() for o in out)
 
 
 def rshufti_exec(lo, hi, data):

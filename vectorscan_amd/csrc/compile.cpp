@@ -1023,6 +1023,58 @@ int shuftiMasks(const u8 cls[32], u8 lo[16], u8 hi[16]) {
     return (int)bit;
 }
 
+/* shufticompile.cpp:135-209 (shuftiBuildDoubleMasks): one-byte literals
+ * (second byte wildcard) and two-byte literals -> bucketed nibble masks,
+ * bit clear = member.  Literals sharing three of their four nibble sets are
+ * merged (four passes, std::map order), at most 8 buckets; false = too many.
+ * pairs: npairs (first, second) byte pairs in flat_set (sorted) order. */
+bool shuftiDoubleMasks(const u8 onechar[32], const u8 *pairs, size_t npairs, u8 lo1[16],
+                       u8 hi1[16], u8 lo2[16], u8 hi2[16]) {
+    typedef std::array<u16, 4> NM;
+    std::vector<std::pair<u8, u8>> tw;
+    for (size_t i = 0; i < npairs; i++) tw.emplace_back(pairs[2 * i], pairs[2 * i + 1]);
+    std::sort(tw.begin(), tw.end());
+    tw.erase(std::unique(tw.begin(), tw.end()), tw.end());
+    std::vector<NM> nm;
+    for (auto &p : tw) {
+        nm.push_back({{(u16)(1U << (p.first & 0xf)), (u16)(1U << (p.first >> 4)),
+                       (u16)(1U << (p.second & 0xf)), (u16)(1U << (p.second >> 4))}});
+    }
+    for (u32 c = 0; c < 256; c++) {
+        if (onechar && (onechar[c >> 3] & (1U << (c & 7)))) {
+            nm.push_back({{(u16)(1U << (c & 0xf)), (u16)(1U << (c >> 4)), 0xffff, 0xffff}});
+        }
+    }
+    for (u32 i = 0; i < 4; i++) {
+        std::map<NM, NM> merged;
+        for (const auto &a : nm) {
+            NM key = a;
+            key[i] = 0;
+            auto it = merged.find(key);
+            if (it == merged.end()) {
+                merged[key] = a;
+            } else {
+                for (int k = 0; k < 4; k++) it->second[k] |= a[k];
+            }
+        }
+        nm.clear();
+        for (auto &e : merged) nm.push_back(e.second);
+    }
+    if (nm.size() > 8) return false;
+    u8 *out[4] = {lo1, hi1, lo2, hi2};
+    for (int k = 0; k < 4; k++) memset(out[k], 0xff, 16);
+    u32 bucket = 0;
+    for (const auto &a : nm) {
+        for (int k = 0; k < 4; k++) {
+            for (u32 n = 0; n < 16; n++) {
+                if (a[k] & (1U << n)) out[k][n] &= (u8)~(1U << bucket);
+            }
+        }
+        bucket++;
+    }
+    return true;
+}
+
 /* trufflecompile.cpp:60-75 */
 void truffleMasks(const u8 cls[32], u8 m1[16], u8 m2[16]) {
     memset(m1, 0, 16);

@@ -92,4 +92,17 @@ struct VsaClassParams {
                                       u64 index 16 * slot (one line each) */
 };
 
+/* Double shufti (shuftiDoubleExec): bucketed byte-pair test with the
+ * reference's per-block lane artifacts (see orc_shufti_double / kernel).
+ * first[0..2] receive atomicMin of the first match of the head, aligned and
+ * tail stages (initialised to ~0). */
+struct VsaPairParams {
+    const uint8_t *data;
+    uint64_t len;
+    uint8_t n1[256], n2[256]; /* bucket sets: ~(lo[c & 15] | hi[c >> 4]) */
+    uint32_t vsize;           /* VECTORSIZE S (16, 32, 64) */
+    uint32_t mis;             /* buffer address mod S */
+    unsigned long long *first; /* [3], one 128-B line apart (stride 16) */
+};
+
 #endif

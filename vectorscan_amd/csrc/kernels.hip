@@ -1042,3 +1042,58 @@ __global__ void __launch_bounds__(256) vsa_class_scan(VsaClassParams P) {
 }
 
 /* bitmap words are written as u16 lanes; the host sees little-endian u64 */
+
+/* ===================================================== double shufti === */
+
+/* shuftiDoubleExec (shufti_simd.hpp:195-258, x86/shufti.hpp:49-79): byte i
+ * matches when some bucket is set in both n1[b[i]] and n2[b[i+1]], except at
+ * the last byte of each 16-byte lane of the block being scanned, where the
+ * reference's in-lane byte shift feeds 0 (all buckets) for b[i+1].  The
+ * three scan stages (unaligned head block, S-aligned blocks, tail block)
+ * place those lane ends differently, so each position is tested once per
+ * stage it belongs to and the host takes the first stage with a match. */
+__global__ void __launch_bounds__(256) vsa_pair_scan(VsaPairParams P) {
+    __shared__ u8 n1[256], n2[256];
+    const u32 tid = threadIdx.x;
+    n1[tid] = P.n1[tid];
+    n2[tid] = P.n2[tid];
+    __syncthreads();
+    const int64_t len = (int64_t)P.len, S = P.vsize, mis = P.mis % P.vsize;
+    /* stage geometry (shuftiDoubleExecReal) */
+    const bool longbuf = len >= S;
+    const bool head = longbuf && mis != 0;
+    const int64_t d0 = longbuf ? (mis ? S - mis : 0) : 0;
+    const int64_t d_end = longbuf ? d0 + ((len - d0) / S) * S : 0;
+    const bool tail = (longbuf ? d_end : 0) != len;
+    const int64_t t0 = longbuf ? len - S : 0; /* tail block start */
+    unsigned long long fh = ~0ULL, fa = ~0ULL, ft = ~0ULL;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + tid; i < len; i += stride) {
+        const u8 a = n1[P.data[i]];
+        if (!a) continue;
+        const u8 nb = (i + 1 < len) ? n2[P.data[i + 1]] : n2[0];
+        if (head && i < S) {
+            if ((((i & 15) == 15) ? a : (a & nb)) && (u64)i < fh) fh = (u64)i;
+        }
+        if (i >= d0 && i < d_end) {
+            if (((((i + mis) & 15) == 15) ? a : (a & nb)) && (u64)i < fa) fa = (u64)i;
+        }
+        if (tail && i >= t0) {
+            if (((((i - t0) & 15) == 15) ? a : (a & nb)) && (u64)i < ft) ft = (u64)i;
+        }
+    }
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) {
+        u64 o = ((u64)shfl_down_u32((u32)(fh >> 32), dd) << 32) | shfl_down_u32((u32)fh, dd);
+        if (o < fh) fh = o;
+        o = ((u64)shfl_down_u32((u32)(fa >> 32), dd) << 32) | shfl_down_u32((u32)fa, dd);
+        if (o < fa) fa = o;
+        o = ((u64)shfl_down_u32((u32)(ft >> 32), dd) << 32) | shfl_down_u32((u32)ft, dd);
+        if (o < ft) ft = o;
+    }
+    if (lane_id() == 0) {
+        if (fh != ~0ULL) atomicMin(P.first, fh);
+        if (fa != ~0ULL) atomicMin(P.first + 16, fa);
+        if (ft != ~0ULL) atomicMin(P.first + 32, ft);
+    }
+}

@@ -38,6 +38,7 @@
 template <int MODE, bool LDS_TABLE>
 __global__ void vsa_lit_scan(VsaLitParams P);
 __global__ void vsa_class_scan(VsaClassParams P);
+__global__ void vsa_pair_scan(VsaPairParams P);
 
 #define VSA_CHECK(x)                                                          \
     do {                                                                      \
@@ -58,9 +59,11 @@ const size_t LDS_BUDGET = 160 * 1024 - 2048; /* minus static LDS */
 const uint32_t SLOT_WORDS_MAX = 4096;        /* 16 KiB of slot bitmaps */
 
 /* d_counters layout (u64): [0..7] scan counters, [16 + 16 r] region
- * tickets (one 128-B line each), [CLASS_BASE + 16 s + {0,1,2}] class-scan
+ * tickets (one 128-B line each), [PAIR_BASE + 16 k] double-shufti stage
+ * results, [CLASS_BASE + 16 s + {0,1,2}] class-scan
  * first / last / count partials of slot s (one line per slot) */
 constexpr int CLASS_SLOTS = 64;
+constexpr int PAIR_BASE = 160; /* double-shufti stage results, 16 apart */
 constexpr int CLASS_BASE = 256;
 constexpr int N_COUNTERS = CLASS_BASE + 16 * CLASS_SLOTS;
 
@@ -363,11 +366,8 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
     int r = ensure_blocks(c, nb);
     if (r) return r;
     if ((r = ensure_out(c, 1)) != VSA_OK) return r;
-    uint64_t total = 0, span = 0;
-    for (uint32_t i = 0; i < nb; i++) {
-        total += lens[i];
-        span = std::max(span, offs[i] + lens[i]);
-    }
+    uint64_t span = 0;
+    for (uint32_t i = 0; i < nb; i++) span = std::max(span, offs[i] + lens[i]);
     const int64_t mis = (int64_t)((uintptr_t)d_data & 15);
     std::vector<int64_t> spans;
     spans.reserve(nb);
@@ -657,6 +657,45 @@ int class_host(const uint8_t cls[32], const uint8_t *cls2, const uint8_t *buf, s
     }
     uint64_t cnt;
     return vsa_class_scan(c, cls, cls2, c->ws.d_in, len, nullptr, first, last, &cnt, 0);
+}
+
+/* shuftiDoubleExec on the device (VsaPairParams); `vsize` = the reference
+ * build's VECTORSIZE, the buffer's host address fixes the block alignment. */
+int64_t pair_host(const uint8_t *lo1, const uint8_t *hi1, const uint8_t *lo2,
+                  const uint8_t *hi2, const uint8_t *buf, size_t len, uint32_t vsize) {
+    vsa_ctx *c = default_ctx();
+    if (!c) return -2;
+    if (!len) return 0;
+    if (ensure_in(c, len + 16) != VSA_OK) return -2;
+    Workspace &w = c->ws;
+    if (hipMemcpyAsync(w.d_in, buf, len, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return -2;
+    unsigned long long *first = w.d_counters + PAIR_BASE;
+    if (hipMemsetAsync(first, 0xff, 48 * 8, c->stream) != hipSuccess) return -2;
+    VsaPairParams P;
+    memset(&P, 0, sizeof(P));
+    P.data = w.d_in;
+    P.len = len;
+    for (int ch = 0; ch < 256; ch++) {
+        P.n1[ch] = (uint8_t)~(lo1[ch & 15] | hi1[ch >> 4]);
+        P.n2[ch] = (uint8_t)~(lo2[ch & 15] | hi2[ch >> 4]);
+    }
+    P.vsize = vsize;
+    P.mis = (uint32_t)((uintptr_t)buf % vsize);
+    P.first = first;
+    uint64_t want = (len + 255) / 256;
+    uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * 4));
+    hipLaunchKernelGGL(vsa_pair_scan, dim3(grid), dim3(256), 0, c->stream, P);
+    if (hipGetLastError() != hipSuccess) return -2;
+    if (hipMemcpyAsync(w.h_counters + PAIR_BASE, first, 48 * 8, hipMemcpyDeviceToHost,
+                       c->stream) != hipSuccess)
+        return -2;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return -2;
+    const unsigned long long *h = w.h_counters + PAIR_BASE;
+    if (h[0] != ~0ULL) return (int64_t)h[0];
+    if (h[16] != ~0ULL) return (int64_t)h[16];
+    if (h[32] != ~0ULL && h[32] < len) return (int64_t)h[32];
+    return (int64_t)len;
 }
 
 void cls_from_shufti(const uint8_t *lo, const uint8_t *hi, uint8_t cls[32]) {
@@ -1244,6 +1283,36 @@ const uint8_t *shuftiExec(vsa_m128_t mask_lo, vsa_m128_t mask_hi, const uint8_t 
     m128_bytes(mask_hi, hi);
     int64_t r = vsa_shufti_find(lo, hi, buf, (size_t)(buf_end - buf), 0);
     return r < 0 ? buf_end : buf + r;
+}
+
+static uint32_t g_vector_size = 64; /* reference VECTORSIZE emulated by shuftiDoubleExec */
+
+void vsa_set_accel_vector_size(uint32_t vsize) {
+    if (vsize == 16 || vsize == 32 || vsize == 64) g_vector_size = vsize;
+}
+
+int64_t vsa_shufti_double_find(const uint8_t lo1[16], const uint8_t hi1[16],
+                               const uint8_t lo2[16], const uint8_t hi2[16],
+                               const uint8_t *buf, size_t len) {
+    return pair_host(lo1, hi1, lo2, hi2, buf, len, g_vector_size);
+}
+
+const uint8_t *shuftiDoubleExec(vsa_m128_t mask1_lo, vsa_m128_t mask1_hi, vsa_m128_t mask2_lo,
+                                vsa_m128_t mask2_hi, const uint8_t *buf,
+                                const uint8_t *buf_end) {
+    uint8_t lo1[16], hi1[16], lo2[16], hi2[16];
+    m128_bytes(mask1_lo, lo1);
+    m128_bytes(mask1_hi, hi1);
+    m128_bytes(mask2_lo, lo2);
+    m128_bytes(mask2_hi, hi2);
+    int64_t r = vsa_shufti_double_find(lo1, hi1, lo2, hi2, buf, (size_t)(buf_end - buf));
+    return r < 0 ? buf_end : buf + r;
+}
+
+int vsa_shufti_build_double_masks(const uint8_t onechar[32], const uint8_t *pairs,
+                                  size_t npairs, uint8_t lo1[16], uint8_t hi1[16],
+                                  uint8_t lo2[16], uint8_t hi2[16]) {
+    return vsa::shuftiDoubleMasks(onechar, pairs, npairs, lo1, hi1, lo2, hi2) ? 0 : -1;
 }
 
 const uint8_t *rshuftiExec(vsa_m128_t mask_lo, vsa_m128_t mask_hi, const uint8_t *buf,

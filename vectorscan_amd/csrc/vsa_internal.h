@@ -46,6 +46,8 @@ Literal makeLiteral(const u8 *s, size_t len, bool nocase, bool noruns, u32 id,
 int buildHwlm(std::vector<Literal> lits, const BuildOptions &opt, u8 **out,
               size_t *outSize);
 int shuftiMasks(const u8 cls[32], u8 lo[16], u8 hi[16]);
+bool shuftiDoubleMasks(const u8 onechar[32], const u8 *pairs, size_t npairs, u8 lo1[16],
+                       u8 hi1[16], u8 lo2[16], u8 hi2[16]);
 void truffleMasks(const u8 cls[32], u8 m1[16], u8 m2[16]);
 
 } // namespace vsa
