@@ -91,6 +91,8 @@ const uint8_t *rnvermicelliExec(char c, char nocase, const uint8_t *buf,
                                 const uint8_t *buf_end);
 const uint8_t *vermicelliDoubleExec(char c1, char c2, char nocase,
                                     const uint8_t *buf, const uint8_t *buf_end);
+const uint8_t *rvermicelliDoubleExec(char c1, char c2, char nocase, const uint8_t *buf,
+                                     const uint8_t *buf_end);
 const uint8_t *vermicelliDoubleMaskedExec(char c1, char c2, char m1, char m2,
                                           const uint8_t *buf,
                                           const uint8_t *buf_end);
@@ -236,7 +238,8 @@ void vsa_set_accel_vector_size(uint32_t vsize);
 int vsa_shufti_build_double_masks(const uint8_t onechar[32], const uint8_t *pairs,
                                   size_t npairs, uint8_t lo1[16], uint8_t hi1[16],
                                   uint8_t lo2[16], uint8_t hi2[16]);
-/* mode: 0 verm, 1 nverm, 2 rverm, 3 rnverm, 4 dverm, 5 dverm masked */
+/* mode: 0 verm, 1 nverm, 2 rverm, 3 rnverm, 4 dverm, 5 dverm masked,
+ * 6 rdverm (reverse double: index of c2 of the last pair, or -1) */
 int64_t vsa_verm_find(int mode, uint8_t c1, uint8_t c2, uint8_t m1, uint8_t m2,
                       int nocase, const uint8_t *buf, size_t len);
 

@@ -52,6 +52,7 @@ _sig("orc_shufti_double", _i64, _vp, _vp, _vp, _vp, _vp, _sz, _i64, _i64)
 _sig("orc_rtruffle", _i64, _vp, _vp, _vp, _sz)
 _sig("orc_verm", _i64, ctypes.c_uint8, _int, _int, _int, _vp, _sz)
 _sig("orc_dverm", _i64, ctypes.c_uint8, ctypes.c_uint8, _int, _vp, _sz)
+_sig("orc_rdverm", _i64, ctypes.c_uint8, ctypes.c_uint8, _int, _vp, _sz)
 _sig("orc_dverm_masked", _i64, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8,
      ctypes.c_uint8, _vp, _sz)
 _sig("orc_fdr_candidates", _u64, _vp, _vp, _sz)
@@ -123,6 +124,11 @@ def verm(c, nocase, data, negate=False, reverse=False):
 def dverm(c1, c2, nocase, data):
     keep, p, n = _buf(data)
     return _lib.orc_dverm(c1, c2, int(nocase), p, n)
+
+
+def rdverm(c1, c2, nocase, data):
+    keep, p, n = _buf(data)
+    return _lib.orc_rdverm(c1, c2, int(nocase), p, n)
 
 
 def dverm_masked(c1, c2, m1, m2, data):

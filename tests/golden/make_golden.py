@@ -152,7 +152,7 @@ def short_writings_spec():
 def accel_cases():
     """shufti.cpp / truffle.cpp / vermicelli.cpp / rvermicelli.cpp known
     answers.  kind: shufti|rshufti|truffle|rtruffle (class = chars),
-    verm|nverm|rverm|rnverm (c, nocase), dverm (c1, c2, nocase)."""
+    verm|nverm|rverm|rnverm (c, nocase), dverm|rdverm (c1, c2, nocase)."""
     cases = []
 
     def add(src, kind, data, expected, **kw):
@@ -266,6 +266,70 @@ def accel_cases():
     for i in range(16):
         add("rvermicelli.cpp:57 Exec1", "rverm", t[:len(t) - i], 48, c=0x61, nocase=0)
         add("rvermicelli.cpp:57 Exec1", "rverm", t[i:], 48 - i, c=0x41, nocase=1)
+    # rvermicelli.cpp:117-200 (RNVermicelli); expected index relative to the
+    # scanned slice, -1 = none (buf - 1)
+    t = b"b" * 61
+    for i in range(16):
+        for j in range(16):
+            s_ = t[i:len(t) - j]
+            add("rvermicelli.cpp:117 RNV ExecNoMatch1", "rnverm", s_, -1, c=0x62, nocase=0)
+            add("rvermicelli.cpp:117 RNV ExecNoMatch1", "rnverm", s_, -1, c=0x42, nocase=1)
+    for src, t in (("rvermicelli.cpp:137 RNV Exec1",
+                    b"bbbbbbbbbbbbbbbbbabbbbbbbbbbbbbbbbbbbbbbbbbbbbbbabbbbbbbbbbbbbbbbbbbbb"),
+                   ("rvermicelli.cpp:153 RNV Exec2",
+                    b"bbbbbbbbbbbbbbbbbabbbbbbbbaaaaaaaaaaaaaaaaaaaaaaabbbbbbbbbbbbbbbbbbbbb")):
+        for i in range(16):
+            add(src, "rnverm", t[:len(t) - i], 48, c=0x62, nocase=0)
+            add(src, "rnverm", t[i:len(t) - i], 48 - i, c=0x42, nocase=1)
+    t = b"bbbbbbbbbbbbbbbbbabbbbbbbbaaaaaaaaaaaaaaaaaaaaaaAbbbbbbbbbbbbbbbbbbbbbb"
+    for i in range(16):
+        add("rvermicelli.cpp:169 RNV Exec3", "rnverm", t[i:], 48 - i, c=0x62, nocase=0)
+        add("rvermicelli.cpp:169 RNV Exec3", "rnverm", t[i:], 48 - i, c=0x42, nocase=1)
+    t = bytearray(b"b" * 73)
+    for i in range(31):
+        t[16 + i] = 0x61
+        add("rvermicelli.cpp:185 RNV Exec4", "rnverm", bytes(t), 16 + i, c=0x62, nocase=0)
+        add("rvermicelli.cpp:185 RNV Exec4", "rnverm", bytes(t), 16 + i, c=0x42, nocase=1)
+    # rvermicelli.cpp:203-311 (RDoubleVermicelli): position of c2 of the last
+    # pair (a c2 at buf[0] counts), -1 = none
+    t = b"bbbbbbbbbbbbbbbbbbabbbbbbbbbbbbbbbbbbbbbbbbbbbbbbabbbbbbbbbbbbbbbbbbbbb"
+    for i in range(16):
+        add("rvermicelli.cpp:203 RDV Exec1", "rdverm", t[:len(t) - i], 50, c1=0x61, c2=0x62,
+            nocase=0)
+        add("rvermicelli.cpp:203 RDV Exec1", "rdverm", t[i:], 50 - i, c1=0x41, c2=0x42, nocase=1)
+        add("rvermicelli.cpp:203 RDV Exec1", "rdverm", t[i:], 49 - i, c1=0x62, c2=0x61, nocase=0)
+        add("rvermicelli.cpp:203 RDV Exec1", "rdverm", t[i:], 49 - i, c1=0x42, c2=0x41, nocase=1)
+    t = b"bbbbbbbbbbbbbbbbbaaaaaaaaaaaaaaaaaaaaaaaabbbbbbbaaaaabbbbbbbbbbbbbbbbbb"
+    for i in range(16):
+        add("rvermicelli.cpp:229 RDV Exec2", "rdverm", t[:len(t) - i], 52, c1=0x61, c2=0x61,
+            nocase=0)
+        add("rvermicelli.cpp:229 RDV Exec2", "rdverm", t[:len(t) - i], 52, c1=0x41, c2=0x41,
+            nocase=1)
+    t = b"bbbbbbbbbbbbbbbbbaAaaAAaaaaaaaaaaaaaaaaaabbbbbbbaaaaabbbbbbbbbbbbbbbbbb"
+    for i in range(16):
+        sl = t[:len(t) - i]
+        add("rvermicelli.cpp:245 RDV Exec3", "rdverm", sl, 23, c1=0x41, c2=0x61, nocase=0)
+        add("rvermicelli.cpp:245 RDV Exec3", "rdverm", sl, 52, c1=0x41, c2=0x41, nocase=1)
+        add("rvermicelli.cpp:245 RDV Exec3", "rdverm", sl, 22, c1=0x41, c2=0x41, nocase=0)
+        add("rvermicelli.cpp:245 RDV Exec3", "rdverm", sl, 21, c1=0x61, c2=0x41, nocase=0)
+    t = bytearray(b"b" * 93)
+    for i in range(31):
+        t[32 + i] = 0x61
+        t[32 + i - 1] = 0x61
+        add("rvermicelli.cpp:272 RDV Exec4", "rdverm", bytes(t), 32 + i, c1=0x61, c2=0x61,
+            nocase=0)
+        add("rvermicelli.cpp:272 RDV Exec4", "rdverm", bytes(t), 32 + i, c1=0x41, c2=0x41,
+            nocase=1)
+    t = bytearray(b"b" * 61)
+    L = len(t)
+    for i in range(16):
+        for j in range(1, 17):
+            t[L - i - j] = 0x61
+            add("rvermicelli.cpp:288 RDV Exec5", "rdverm", bytes(t[:L - i]), L - i - j,
+                c1=0x62, c2=0x61, nocase=0)
+            add("rvermicelli.cpp:288 RDV Exec5", "rdverm", bytes(t[:L - i]), L - i - j,
+                c1=0x42, c2=0x41, nocase=1)
+            t[L - i - j] = 0x62
     return cases
 
 

@@ -122,6 +122,8 @@ def accel_expected_oracle(c):
                            reverse=k in ("rverm", "rnverm"))
     if k == "dverm":
         return oracle.dverm(c["c1"], c["c2"], c["nocase"], data)
+    if k == "rdverm":
+        return oracle.rdverm(c["c1"], c["c2"], c["nocase"], data)
     raise AssertionError(k)
 
 

@@ -85,8 +85,12 @@ def test_gpu_golden_accel():
             got = vsa.nvermicelli_exec(c["c"], c["nocase"], data)
         elif k == "rverm":
             got = vsa.rvermicelli_exec(c["c"], c["nocase"], data)
+        elif k == "rnverm":
+            got = vsa.rnvermicelli_exec(c["c"], c["nocase"], data)
         elif k == "dverm":
             got = vsa.vermicelli_double_exec(c["c1"], c["c2"], c["nocase"], data)
+        elif k == "rdverm":
+            got = vsa.rvermicelli_double_exec(c["c1"], c["c2"], c["nocase"], data)
         else:
             raise AssertionError(k)
         assert got == c["expected"], c["src"]

@@ -381,6 +381,12 @@ def vermicelli_double_exec(c1, c2, nocase, data):
     return lib.vsa_verm_find(4, _ch(c1), _ch(c2), 0, 0, int(nocase), ptr, n)
 
 
+def rvermicelli_double_exec(c1, c2, nocase, data):
+    """rvermicelliDoubleExec: index of c2 of the last (c1, c2) pair, or -1."""
+    keep, ptr, n = _as_buf(data)
+    return lib.vsa_verm_find(6, _ch(c1), _ch(c2), 0, 0, int(nocase), ptr, n)
+
+
 def vermicelli_double_masked_exec(c1, c2, m1, m2, data):
     keep, ptr, n = _as_buf(data)
     return lib.vsa_verm_find(5, _ch(c1), _ch(c2), _ch(m1), _ch(m2), 0, ptr, n)

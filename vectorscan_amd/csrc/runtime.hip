@@ -1261,12 +1261,24 @@ int64_t vsa_verm_find(int mode, uint8_t c1, uint8_t c2, uint8_t m1, uint8_t m2, 
         cls_from_masked(c1, m1, false, cls);
         cls_from_masked(c2, m2, false, cls2);
         break;
+    case 6: /* rvermicelliDoubleExec */
+        cls_from_masked(c1, cm, false, cls);
+        cls_from_masked(c2, cm, false, cls2);
+        break;
     default:
         return -2;
     }
     bool pair = mode >= 4;
     if (class_host(cls, pair ? cls2 : nullptr, buf, len, &f, &l) != VSA_OK) return -2;
     if (mode == 2 || mode == 3) return (int64_t)l - 1;
+    if (mode == 6) {
+        /* vermicelli_simd.cpp:360-423: position of c2 in the last pair (the
+         * pair bitmap marks c1's position, so that is `last`); a c2 at
+         * buf[0] is a partial pair; else buf - 1 */
+        if (l) return (int64_t)l;
+        if (len && cls_has(cls2, buf[0])) return 0;
+        return -1;
+    }
     if (pair && f == len && len && cls_has(cls, buf[len - 1])) {
         /* partial match at the end (vermicelli_simd.cpp:349-355) */
         return (int64_t)len - 1;
@@ -1358,6 +1370,12 @@ const uint8_t *vermicelliDoubleExec(char c1, char c2, char nocase, const uint8_t
     return buf + vsa_verm_find(4, (uint8_t)c1, (uint8_t)c2, 0, 0, nocase, buf,
                                (size_t)(buf_end - buf));
 }
+const uint8_t *rvermicelliDoubleExec(char c1, char c2, char nocase, const uint8_t *buf,
+                                     const uint8_t *buf_end) {
+    return buf + vsa_verm_find(6, (uint8_t)c1, (uint8_t)c2, 0, 0, nocase, buf,
+                               (size_t)(buf_end - buf));
+}
+
 const uint8_t *vermicelliDoubleMaskedExec(char c1, char c2, char m1, char m2,
                                           const uint8_t *buf, const uint8_t *buf_end) {
     return buf + vsa_verm_find(5, (uint8_t)c1, (uint8_t)c2, (uint8_t)m1, (uint8_t)m2, 0, buf,
