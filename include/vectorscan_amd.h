@@ -62,6 +62,24 @@ hwlm_error_t fdrExec(const struct FDR *fdr, const uint8_t *buf, size_t len,
 hwlm_error_t noodExec(const struct noodTable *n, const uint8_t *buf, size_t len,
                       size_t start, HWLMCallback cb, struct hs_scratch *scratch);
 
+/* Streaming (history + current buffer; ends relative to buf, literals may
+ * begin up to hlen bytes into the history).  The 16 bytes before hbuf + hlen
+ * must be readable, as the reference requires (fdr.c:835-841).
+ * hwlmExecStreaming (hwlm.h:137, hwlm.c:207) reads buf / hbuf / hlen from
+ * scratch->core_info (scratch.h:91-110; offsets: vsa_set_scratch_core_info).
+ * fdrExecStreaming (fdr.h:75, fdr.c:827), noodExecStreaming
+ * (noodle_engine.h:52, noodle_engine.cpp:136). */
+hwlm_error_t hwlmExecStreaming(const struct HWLM *tab, size_t len, size_t start,
+                               HWLMCallback callback, struct hs_scratch *scratch,
+                               hwlm_group_t groups);
+hwlm_error_t fdrExecStreaming(const struct FDR *fdr, const uint8_t *hbuf, size_t hlen,
+                              const uint8_t *buf, size_t len, size_t start,
+                              HWLMCallback cb, struct hs_scratch *scratch,
+                              hwlm_group_t groups);
+hwlm_error_t noodExecStreaming(const struct noodTable *n, const uint8_t *hbuf, size_t hlen,
+                               const uint8_t *buf, size_t len, HWLMCallback cb,
+                               struct hs_scratch *scratch);
+
 /* Accel find-first / find-last (src/nfa/shufti.h:46-55, truffle.h:45-49,
  * vermicelli.hpp:47-95, accel.h:148).  Return values as the reference:
  * forward scans return buf_end when nothing is found, reverse scans
@@ -151,6 +169,15 @@ int vsa_scan_blocks(vsa_ctx_t *ctx, const vsa_db_t *db, const uint8_t *d_data,
                     const uint64_t *offsets, const uint64_t *lens,
                     const uint64_t *starts, uint32_t nblocks, uint32_t flags,
                     uint64_t *n_matches);
+/* As vsa_scan_blocks, each block a streaming call: hlens[i] bytes of
+ * history sit immediately before offsets[i] in d_data (at least 16 bytes
+ * before each block with hlens[i] > 0 must be readable); hlens[i] = 0 is a
+ * block-mode scan.  A stream cut into consecutive chunks is scanned as one
+ * launch this way. */
+int vsa_scan_blocks_stream(vsa_ctx_t *ctx, const vsa_db_t *db, const uint8_t *d_data,
+                           const uint64_t *offsets, const uint64_t *lens,
+                           const uint64_t *starts, const uint64_t *hlens, uint32_t nblocks,
+                           uint32_t flags, uint64_t *n_matches);
 int vsa_scan_wait(vsa_ctx_t *ctx, uint64_t *n_matches);
 /* Device pointers to the last scan's sorted keys (u64) and ids (u32). */
 int vsa_scan_results(vsa_ctx_t *ctx, const uint64_t **d_keys,
@@ -247,6 +274,11 @@ int64_t vsa_verm_find(int mode, uint8_t c1, uint8_t c2, uint8_t m1, uint8_t m2,
  * (offsetof(struct hs_scratch, fdr_conf / fdr_conf_offset)); the defaults
  * are the x86-64 layout of src/scratch.h:172-219. */
 void vsa_set_scratch_layout(long fdr_conf_off, long fdr_conf_offset_off);
+
+/* Optional: offsets of core_info.buf / hbuf / hlen inside hs_scratch for
+ * hwlmExecStreaming (defaults: x86-64 layout of scratch.h:91-191). */
+void vsa_set_scratch_core_info(long buf_off, long hbuf_off, long hlen_off);
+void vsa_get_scratch_core_info(long *buf_off, long *hbuf_off, long *hlen_off);
 
 const char *vsa_version(void);
 

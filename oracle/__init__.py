@@ -56,6 +56,12 @@ _sig("orc_rdverm", _i64, ctypes.c_uint8, ctypes.c_uint8, _int, _vp, _sz)
 _sig("orc_dverm_masked", _i64, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8,
      ctypes.c_uint8, _vp, _sz)
 _sig("orc_fdr_candidates", _u64, _vp, _vp, _sz)
+_sig("orc_hwlm_exec_stream", _i64, _vp, _vp, _sz, _vp, _sz, _sz, _u64, _vp, _sz, _i64, _u64,
+     ctypes.POINTER(_int))
+_sig("orc_fdr_exec_stream", _i64, _vp, _vp, _sz, _vp, _sz, _sz, _u64, _vp, _sz, _i64, _u64,
+     ctypes.POINTER(_int))
+_sig("orc_nood_exec_stream", _i64, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _i64,
+     ctypes.POINTER(_int))
 
 ALL = (1 << 64) - 1
 
@@ -90,6 +96,56 @@ def hwlm_exec(blob_ptr, data, start=0, groups=ALL, term_after=-1, cap=4096, cb_r
 
 def fdr_exec(engine_ptr, data, start=0, groups=ALL, term_after=-1, cap=4096, cb_ret=ALL):
     return _run(_lib.orc_fdr_exec, engine_ptr, data, start, [groups], term_after, cap, cb_ret)
+
+
+# the 16 bytes before the end of a short history, as the reference's
+# unit/internal/fdr.cpp safeExecStreaming provides them
+HIST_FILLER = b"0123456789abcdef"
+
+
+def history_buffer(hist, filler=HIST_FILLER):
+    """(keepalive, hend address, hlen): `hist` preceded by filler so the 16
+    bytes before hend are readable, as streaming callers guarantee."""
+    hist = bytes(hist)
+    raw = (bytes(filler) + hist) if len(hist) < 16 else hist
+    b = ctypes.create_string_buffer(raw, max(1, len(raw)))
+    return b, ctypes.addressof(b) + len(raw), len(hist)
+
+
+def _run_stream(fn, ptr, hist, data, start, groups, term_after, cap, cb_ret, filler):
+    hk, hend, hlen = history_buffer(hist, filler)
+    keep, p, n = _buf(data)
+    while True:
+        out = (_Match * max(1, cap))()
+        st = _int()
+        if fn is _lib.orc_nood_exec_stream:
+            cnt = fn(ptr, hend, hlen, p, n, out, cap, term_after, ctypes.byref(st))
+        else:
+            cnt = fn(ptr, hend, hlen, p, n, start, groups, out, cap, term_after, cb_ret,
+                     ctypes.byref(st))
+        if cnt <= cap:
+            return st.value, [(out[i].end, out[i].id) for i in range(cnt)]
+        cap = cnt
+
+
+def hwlm_exec_stream(blob_ptr, hist, data, start=0, groups=ALL, term_after=-1, cap=4096,
+                     cb_ret=ALL, filler=HIST_FILLER):
+    """hwlmExecStreaming (hwlm.c:207) over history `hist` + `data`."""
+    return _run_stream(_lib.orc_hwlm_exec_stream, blob_ptr, hist, data, start, groups,
+                       term_after, cap, cb_ret, filler)
+
+
+def fdr_exec_stream(engine_ptr, hist, data, start=0, groups=ALL, term_after=-1, cap=4096,
+                    cb_ret=ALL, filler=HIST_FILLER):
+    """fdrExecStreaming (fdr.c:827)."""
+    return _run_stream(_lib.orc_fdr_exec_stream, engine_ptr, hist, data, start, groups,
+                       term_after, cap, cb_ret, filler)
+
+
+def nood_exec_stream(engine_ptr, hist, data, term_after=-1, cap=4096, filler=HIST_FILLER):
+    """noodExecStreaming (noodle_engine.cpp:136)."""
+    return _run_stream(_lib.orc_nood_exec_stream, engine_ptr, hist, data, 0, 0, term_after,
+                       cap, 0, filler)
 
 
 def nood_exec(engine_ptr, data, start=0, term_after=-1, cap=4096):

@@ -275,7 +275,21 @@ typedef struct {
     size_t len;
     size_t start;
     cbctx *cb;
+    /* streaming (fdrExecStreaming fdr.c:827-855): hend = hbuf + hlen, the
+     * 16 bytes before it are readable (garbage before the real history, as
+     * the reference guarantees); hlen bounds the confirm overhang */
+    const u8 *hend;
+    size_t hlen;
+    int stream;
 } rtargs;
+
+/* byte at logical position p (0 = buf[0]): history bytes when streaming,
+ * the zero fake history (fdr.c:798-806) in block mode, 0 past the end */
+static inline u8 rbyte(const rtargs *a, long p) {
+    if (p >= 0) return (size_t)p < a->len ? a->buf[p] : 0;
+    if (a->stream && p >= -16) return a->hend[p];
+    return 0;
+}
 
 /* fdr_confirm_runtime.h:43-102 (block mode: len_history == 0) */
 static void conf_with_bit(const struct o_FDRConfirm *fc, const rtargs *a,
@@ -290,7 +304,8 @@ static void conf_with_bit(const struct o_FDRConfirm *fc, const rtargs *a,
     do {
         if ((conf_key & li->msk) != li->v) goto out;
         if (*last_match == li->id && (li->flags & 1)) goto out;
-        if ((long)i - (long)li->size + 1 < 0) goto out; /* overhang > 0 */
+        /* overhang into the history beyond len_history (fdr_confirm_runtime.h:79-88) */
+        if ((long)i - (long)li->size + 1 < -(long)a->hlen) goto out;
         if (!(li->groups & *control)) goto out;
         *last_match = li->id;
         *control = emit(a->cb, i, li->id);
@@ -300,15 +315,11 @@ static void conf_with_bit(const struct o_FDRConfirm *fc, const rtargs *a,
     } while (next);
 }
 
-/* 8 bytes ending at e, bytes before buf read as the zero fake history
- * (fdr.c:798-806) */
-static u64a conf_key_at(const u8 *buf, size_t len, long e) {
+/* 8 bytes ending at e: history bytes (streaming, fdr.c zone history and
+ * teddy_runtime_common.h:395-416 histBytes) or the zero fake history */
+static u64a conf_key_at(const rtargs *a, long e) {
     u64a v = 0;
-    for (int k = 0; k < 8; k++) {
-        long p = e - 7 + k;
-        u8 b = (p >= 0 && (size_t)p < len) ? buf[p] : 0;
-        v |= (u64a)b << (8 * k);
-    }
+    for (int k = 0; k < 8; k++) v |= (u64a)rbyte(a, e - 7 + k) << (8 * k);
     return v;
 }
 
@@ -316,19 +327,15 @@ static u64a conf_key_at(const u8 *buf, size_t len, long e) {
 
 /* a "zone" buffer as in fdr.c:50-80; we keep a logical byte accessor */
 typedef struct {
-    const u8 *buf;
-    size_t len;
+    const rtargs *a;
     long zstart;   /* logical position of the zone's first scanned byte */
     long zend;     /* logical position one past the last scanned byte */
     u8 shift;
-    long lo_valid; /* bytes at logical positions < lo_valid read as 0 */
 } zone;
 
-static inline u8 zbyte(const zone *z, long p) {
-    if (p < 0 || p < z->lo_valid) return 0;
-    if ((size_t)p >= z->len) return 0; /* post-padding byte */
-    return z->buf[p];
-}
+/* zones see history before buf (createStartZone / createShortZone copy it,
+ * fdr.c:380-560) and a zero post-padding byte */
+static inline u8 zbyte(const zone *z, long p) { return rbyte(z->a, p); }
 
 static u128 load_u64_as_u128(const u64a *ft, u32 idx) { return (u128)ft[idx]; }
 
@@ -353,7 +360,6 @@ static void get_conf(const zone *z, long it, u32 stride, u16 dmask,
 }
 
 static int fdr_run(const struct o_FDR *fdr, const rtargs *a, u64a control) {
-    const u8 *buf = a->buf;
     size_t len = a->len, start = a->start;
     if (start >= len) return 0;
     const u64a *ft = (const u64a *)((const u8 *)fdr + ROUNDUP_CL(sizeof(*fdr)));
@@ -365,26 +371,33 @@ static int fdr_run(const struct o_FDR *fdr, const rtargs *a, u64a control) {
     int nz = 0;
     size_t remaining = len - start;
     if (remaining <= 16) {
-        zone z = {buf, len, (long)len - 16, (long)len, (u8)(16 - remaining), 0};
+        zone z = {a, (long)len - 16, (long)len, (u8)(16 - remaining)};
         zones[nz++] = z;
     } else {
-        zone zs = {buf, len, (long)start, (long)start + 16, 0, 0};
+        zone zs = {a, (long)start, (long)start + 16, 0};
         zones[nz++] = zs;
         size_t ptr = start + 16;
         size_t main_end = start + ((len - start - 3) / 16) * 16;
         if (main_end > ptr) {
-            zone zm = {buf, len, (long)ptr, (long)main_end, 0, 0};
+            zone zm = {a, (long)ptr, (long)main_end, 0};
             zones[nz++] = zm;
             ptr = main_end;
         }
         size_t zl = len - ptr;
         size_t first = zl > 16 ? zl - 16 : zl;
-        zone ze = {buf, len, (long)len - (long)(zl > 16 ? 32 : 16), (long)len,
-                   (u8)(16 - first), 0};
+        zone ze = {a, (long)len - (long)(zl > 16 ? 32 : 16), (long)len, (u8)(16 - first)};
         zones[nz++] = ze;
     }
+    /* getInitState fdr.c:129-142: with history, the table entry of the
+     * byte pair before the scan start, moved on one byte; else fdr->start */
     u128 state;
-    memcpy(&state, fdr->start, 16);
+    if (a->hlen) {
+        long b = (long)start - 1;
+        u32 key = ((u32)rbyte(a, b) | ((u32)rbyte(a, b + 1) << 8)) & fdr->domainMask;
+        state = load_u64_as_u128(ft, key) >> 8;
+    } else {
+        memcpy(&state, fdr->start, 16);
+    }
     for (int zi = 0; zi < nz; zi++) {
         zone *z = &zones[zi];
         /* variable_byte_shift_m128(state, shift) | zone_or_mask[shift] */
@@ -409,7 +422,7 @@ static int fdr_run(const struct o_FDR *fdr, const rtargs *a, u64a control) {
                     if (!(fc->groups & control)) continue;
                     long e = it + byte;
                     conf_with_bit(fc, a, (size_t)e, &control, &last_match,
-                                  conf_key_at(buf, len, e));
+                                  conf_key_at(a, e));
                 }
                 if (!control) return 1;
             }
@@ -445,9 +458,13 @@ static int teddy_run(const struct o_Teddy *t, const rtargs *a, u64a control,
         u8 val[16];
         u16 pmask = 0; /* bit i: poison byte i */
         long base = (long)(ptr - (uintptr_t)buf);
+        /* vectoredLoad128 teddy_runtime_common.h:146-200: up to
+         * min(len_history, nMasks - 1) history bytes before buf */
+        long need = (long)(a->hlen < nMasks - 1 ? a->hlen : nMasks - 1);
         for (int i = 0; i < 16; i++) {
             long p = base + i;
-            val[i] = (p >= 0 && (size_t)p < len) ? buf[p] : 0;
+            val[i] = (p >= 0 && (size_t)p < len) ? buf[p]
+                     : (p < 0 && p >= -need) ? rbyte(a, p) : 0;
             if (p < (long)a->start || (size_t)p >= len) pmask |= (u16)(1u << i);
         }
         u16 res[4][16];
@@ -491,7 +508,7 @@ static int teddy_run(const struct o_Teddy *t, const rtargs *a, u64a control,
                 if (!(fc->groups & control)) continue;
                 long e = base + i;
                 conf_with_bit(fc, a, (size_t)e, &control, &last_match,
-                              conf_key_at(buf, len, e));
+                              conf_key_at(a, e));
             }
             if ((i % (fat ? 4 : 8)) == (fat ? 3 : 7) && !control) return 1;
         }
@@ -503,11 +520,10 @@ static int teddy_run(const struct o_Teddy *t, const rtargs *a, u64a control,
 
 /* ====================================================== entry points == */
 
-static int fdr_dispatch(const void *eng, const u8 *buf, size_t len,
-                        size_t start, u64a groups, cbctx *cb) {
+static int fdr_dispatch_a(const void *eng, rtargs a, u64a groups) {
     u32 id = *(const u32 *)eng;
-    rtargs a = {buf, len, start, cb};
-    if (start >= len) return 0;
+    size_t start = a.start;
+    if (start >= a.len) return 0;
     if (id == 0) return fdr_run((const struct o_FDR *)eng, &a, groups);
     if (id >= 3 && id <= 10) {
         return teddy_run((const struct o_Teddy *)eng, &a, groups, 1, (id - 3) / 2 + 1);
@@ -516,6 +532,55 @@ static int fdr_dispatch(const void *eng, const u8 *buf, size_t len,
         return teddy_run((const struct o_Teddy *)eng, &a, groups, 0, (id - 11) / 2 + 1);
     }
     return 2;
+}
+
+static int fdr_dispatch(const void *eng, const u8 *buf, size_t len,
+                        size_t start, u64a groups, cbctx *cb) {
+    rtargs a = {buf, len, start, cb, NULL, 0, 0};
+    return fdr_dispatch_a(eng, a, groups);
+}
+
+/* fdrExecStreaming fdr.c:827-855 */
+long orc_fdr_exec_stream(const void *eng, const u8 *hend, size_t hlen, const u8 *buf,
+                         size_t len, size_t start, u64a groups, orc_match *out, size_t cap,
+                         long term_after, u64a cb_ret, int *status) {
+    cbctx cb = {out, cap, 0, term_after, cb_ret};
+    rtargs a = {buf, len, start, &cb, hend, hlen, 1};
+    *status = fdr_dispatch_a(eng, a, groups);
+    return (long)cb.n;
+}
+
+/* noodExecStreaming noodle_engine.cpp:136-185: literals straddling the
+ * history (at most msk_len - 1 bytes of each side, scanned byte by byte),
+ * then a block scan of buf from 0 */
+long orc_nood_exec_stream(const void *eng, const u8 *hend, size_t hlen, const u8 *buf,
+                          size_t len, orc_match *out, size_t cap, long term_after,
+                          int *status) {
+    const struct o_nood *n = (const struct o_nood *)eng;
+    cbctx cb = {out, cap, 0, term_after, ~0ULL};
+    *status = 0;
+    if (len + hlen < n->msk_len) return 0;
+    if (hlen && n->msk_len > 1) {
+        u8 temp[24]; /* HWLM_LITERAL_MAX_LEN * 2, + slack for the 8-byte loads */
+        memset(temp, 0, sizeof(temp));
+        size_t tl1 = n->msk_len - 1 < hlen ? n->msk_len - 1 : hlen;
+        size_t tl2 = n->msk_len - 1 < len ? n->msk_len - 1 : len;
+        memcpy(temp, hend - tl1, tl1);
+        memcpy(temp + tl1, buf, tl2);
+        for (size_t i = 0; i + n->msk_len <= tl1 + tl2; i++) {
+            u64a v;
+            memcpy(&v, temp + i, 8);
+            if ((v & n->msk) == n->cmp) {
+                size_t m_end = i + n->msk_len - 1 - tl1;
+                if (!emit(&cb, m_end, n->id)) {
+                    *status = 1;
+                    return (long)cb.n;
+                }
+            }
+        }
+    }
+    *status = nood_run(n, buf, len, 0, &cb);
+    return (long)cb.n;
 }
 
 /* returns number of matches; *status = HWLM_SUCCESS/TERMINATED/ERROR */
@@ -575,6 +640,66 @@ long orc_hwlm_exec(const void *hwlm, const u8 *buf, size_t len, size_t start,
     start = accel_block(aa, buf, len, start);
     *status = fdr_dispatch(eng, buf, len, start, groups, &cb);
     return (long)cb.n;
+}
+
+/* run_hwlm_accel hwlm.c:48-80: offset of the accel hit in [p, p + n) */
+static size_t hwlm_accel_run(const u8 *aux, const u8 *p, size_t n) {
+    switch (aux[0]) {
+    case 1: return (size_t)orc_verm(aux[2], 0, 0, 0, p, n);
+    case 2: return (size_t)orc_verm(aux[2], 1, 0, 0, p, n);
+    case 3: return (size_t)orc_dverm(aux[2], aux[3], 0, p, n);
+    case 4: return (size_t)orc_dverm(aux[2], aux[3], 1, p, n);
+    case 13: return (size_t)orc_shufti(aux + 16, aux + 32, p, n);
+    case 15: return (size_t)orc_truffle(aux + 16, aux + 32, p, n);
+    default: return 0;
+    }
+}
+
+/* do_accel_streaming hwlm.c:114-175 */
+static size_t accel_stream(const u8 *aux, const u8 *hbuf, size_t hlen, const u8 *buf,
+                           size_t len, size_t start) {
+    if (aux[0] == 0 || len - start < 16) return start;
+    const u8 offset = aux[1];
+    if (!start && hlen) {
+        size_t p1 = 0;
+        if (hlen >= 16) p1 = hwlm_accel_run(aux, hbuf, hlen);
+        int inaccurate = aux[0] == 3 || aux[0] == 4; /* DVERM (nocase) */
+        if ((hlen <= 16 || inaccurate) && p1 != hlen && hlen - p1 <= 16) {
+            u8 temp[17];
+            size_t tlen = hlen - p1;
+            memcpy(temp, hbuf + p1, tlen);
+            memset(temp + tlen, 0, 17 - tlen);
+            if (len) temp[tlen] = buf[0];
+            if (hwlm_accel_run(aux, temp, 17) >= tlen) p1 = hlen;
+        }
+        if (p1 != hlen) return start; /* bailing in history */
+    }
+    size_t found = start + hwlm_accel_run(aux, buf + start, len - start);
+    if (found >= start + offset) start = found - offset;
+    return start;
+}
+
+/* hwlmExecStreaming hwlm.c:207-247 (hbuf = hend - hlen) */
+long orc_hwlm_exec_stream(const void *hwlm, const u8 *hend, size_t hlen, const u8 *buf,
+                          size_t len, size_t start, u64a groups, orc_match *out, size_t cap,
+                          long term_after, u64a cb_ret, int *status) {
+    const struct o_HWLM *h = (const struct o_HWLM *)hwlm;
+    const void *eng = (const u8 *)hwlm + ROUNDUP_CL(sizeof(*h));
+    *status = 0;
+    if (!groups) return 0;
+    if (h->type == 16) {
+        if (start) {
+            cbctx cb = {out, cap, 0, term_after, cb_ret};
+            *status = nood_run((const struct o_nood *)eng, buf, len, start, &cb);
+            return (long)cb.n;
+        }
+        return orc_nood_exec_stream(eng, hend, hlen, buf, len, out, cap, term_after, status);
+    }
+    const u8 *aa = h->accel0;
+    if ((groups & ~h->accel1_groups) == 0) aa = h->accel1;
+    start = accel_stream(aa, hend - hlen, hlen, buf, len, start);
+    return orc_fdr_exec_stream(eng, hend, hlen, buf, len, start, groups, out, cap, term_after,
+                               cb_ret, status);
 }
 
 /* ====================================== counting helpers (cpu baseline) */

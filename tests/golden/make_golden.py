@@ -437,6 +437,38 @@ def dshufti_cases():
     return {"build": build, "exec": ex}
 
 
+def fdr_stream_cases():
+    """unit/internal/fdr.cpp streaming known answers (safeExecStreaming
+    :323-337 places a short history after '0123456789abcdef' filler so that
+    16 bytes before its end are readable).  Ends are relative to buf."""
+    cases = []
+
+    def lit(s, nocase=0, id=0, noruns=0):
+        return {"s": hx(s), "nocase": nocase, "id": id, "noruns": noruns}
+
+    def add(src, lits, hist, data, expected, start=0, term_after=-1, hinted=True,
+            status=0, expected_len=None):
+        c = {"src": src, "lits": lits, "hist": hx(hist), "data": hx(data), "start": start,
+             "term_after": term_after, "expected": expected, "hinted": hinted,
+             "status": status}
+        if expected_len is not None:
+            c["expected_len"] = expected_len
+        cases.append(c)
+
+    l1 = [lit(b"a", 1, 1), lit(b"aardvark", 0, 10)]
+    add("fdr.cpp:339 SmallStreaming", l1, b"", b"aaar", [[0, 1], [1, 1], [2, 1]])
+    add("fdr.cpp:367 SmallStreaming", l1, b"aaar", b"dvark", [[2, 1], [4, 10]])
+    l2 = [lit(b"a", 1, 1), lit(b"kk", 1, 2), lit(b"aardvark", 0, 10)]
+    add("fdr.cpp:377 SmallStreaming2", l2, b"foobar", b"aardvarkkk",
+        [[0, 1], [1, 1], [5, 1], [7, 10], [8, 2], [9, 2]])
+    add("fdr.cpp:454 Stream1", [lit(b"f", 0, 0), lit(b"literal", 0, 1)],
+        b"fffffffffffffffff", b"ffffuuuuuuuuuuuuu", [[0, 0], [1, 0], [2, 0], [3, 0]])
+    # FDRTermS :697-717: default engine, callback terminates at the first match
+    add("fdr.cpp:697 FDRTermS", [lit(b"f", 0, 0), lit(b"ff", 0, 1)], b"fffffffffffffffff",
+        b"ffffuuuuuuuuuuuuu", None, term_after=1, hinted=False, status=1, expected_len=1)
+    return cases
+
+
 def main():
     with open(os.path.join(HERE, "noodle.json"), "w") as f:
         json.dump(noodle_cases(), f)
@@ -448,6 +480,8 @@ def main():
         json.dump(accel_cases(), f)
     with open(os.path.join(HERE, "dshufti.json"), "w") as f:
         json.dump(dshufti_cases(), f)
+    with open(os.path.join(HERE, "fdr_stream.json"), "w") as f:
+        json.dump(fdr_stream_cases(), f)
 
 
 if __name__ == "__main__":

@@ -349,3 +349,95 @@ def test_golden_dshufti_oracle(vsize):
             mis = (base_mis + c["start"]) % vsize
             r = oracle.shufti_double(*m, data, vector_size=vsize, mis=mis)
             assert dshufti_expect_ok(c, r, base_mis), (c["src"], vsize, base_mis, r)
+
+
+# ---------------------------------------------------------- streaming ----
+
+def stream_lits(c):
+    return [vsa.HwlmLiteral(bytes.fromhex(l["s"]), l["nocase"], l["id"], noruns=l["noruns"])
+            for l in c["lits"]]
+
+
+@pytest.mark.parametrize("hint", FDR_HINTS)
+def test_golden_fdr_stream_oracle(hint):
+    """fdr.cpp SmallStreaming / SmallStreaming2 / Stream1 / FDRTermS."""
+    for c in load("fdr_stream.json"):
+        lits = stream_lits(c)
+        blob = build_or_none(lits, hint) if c["hinted"] else vsa.hwlm_build(lits)
+        if blob is None or blob.is_noodle:
+            continue
+        st, m = oracle.fdr_exec_stream(vsa.engine_blob(blob), bytes.fromhex(c["hist"]),
+                                       bytes.fromhex(c["data"]), start=c["start"],
+                                       term_after=c["term_after"])
+        assert st == c["status"], c["src"]
+        if c["expected"] is not None:
+            assert m == [tuple(x) for x in c["expected"]], (c["src"], hint)
+        if "expected_len" in c:
+            assert len(m) == c["expected_len"], c["src"]
+
+
+def stream_expected(lits, hist, data, start):
+    """Streaming semantics (fdr.c:827 with len_history > 0): every
+    occurrence in hist + data ending at or after `start` (relative to data)
+    whose overhang into the history is at most len(hist)."""
+    h = len(hist)
+    occ = oracle.brute_force(lits, bytes(hist) + bytes(data))
+    return {(e - h, i) for e, i in occ if e - h >= start}
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_oracle_stream_semantics(seed):
+    rng = random.Random(4242 + seed)
+    for nl in (1, 3, 30, 200, 800):
+        lits = rand_lits(rng, nl, minlen=1, maxlen=8, msk_frac=0.0)
+        for l in lits:
+            l.noruns = False
+        blob = vsa.hwlm_build(lits)
+        for trial in range(6):
+            hist = rand_data(rng, rng.choice([1, 2, 5, 8, 15, 16, 17, 40]))
+            data = rand_data(rng, rng.choice([1, 3, 9, 16, 17, 31, 100, 700]))
+            start = rng.choice([0, 0, 1, 3, len(data) // 2])
+            if start >= len(data):
+                start = 0
+            st, m = oracle.hwlm_exec_stream(blob.ptr, hist, data, start=start, cap=1 << 16)
+            got = set(m)
+            if blob.is_noodle and start:
+                # hwlmExecStreaming falls back to a block scan from start
+                w = max(len(lits[0].s), len(lits[0].msk))
+                exp = {(e, i) for e, i in oracle.brute_force(lits, data) if e - w + 1 >= start}
+            else:
+                exp = stream_expected(lits, hist, data, start)
+            assert got == exp, (seed, nl, trial, len(hist), len(data), start)
+            ends = [e for e, _ in m]
+            assert ends == sorted(ends)
+
+
+def test_oracle_accel_correct_schemes_keep_matches():
+    """An accel scheme whose stop condition every match satisfies (the
+    literal's byte at `offset` from its start) never changes the match set
+    (hwlm.c:85-105 block, 114-175 streaming)."""
+    rng = random.Random(77)
+    for trial in range(20):
+        s = rand_data(rng, rng.randint(2, 5), b"abcdefgh")
+        lits = [vsa.HwlmLiteral(s + t, False, i)
+                for i, t in enumerate([b"", b"a", b"bb", b"cde"][:rng.randint(2, 4)])]
+        blob = vsa.hwlm_build(lits)
+        if blob.is_noodle:
+            continue
+        k = rng.randrange(len(s))
+        kind = rng.choice(["verm", "shufti", "truffle"] + (["dverm"] if k + 1 < len(s) else []))
+        if kind == "verm":
+            aux = vsa.accel_aux("verm", k, s[k])
+        elif kind == "dverm":
+            aux = vsa.accel_aux("dverm", k, s[k], s[k + 1])
+        elif kind == "shufti":
+            aux = vsa.accel_aux("shufti", k, masks=vsa.shufti_build_masks(bytes([s[k]])))
+        else:
+            aux = vsa.accel_aux("truffle", k, masks=vsa.truffle_build_masks(bytes([s[k]])))
+        blob.set_accel(aux)
+        data = rand_data(rng, rng.choice([20, 100, 3000]), b"abcdefgh")
+        st, m = oracle.hwlm_exec(blob.ptr, data, cap=1 << 16)
+        assert set(m) == oracle.brute_force(lits, data), (trial, kind)
+        hist = rand_data(rng, rng.choice([0, 3, 30]), b"abcdefgh")
+        st, m = oracle.hwlm_exec_stream(blob.ptr, hist, data, cap=1 << 16)
+        assert set(m) == stream_expected(lits, hist, data, 0), (trial, kind, len(hist))

@@ -91,6 +91,15 @@ _sig("fdrExec", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
      ctypes.c_size_t, HWLMCallback, ctypes.c_void_p, ctypes.c_uint64)
 _sig("noodExec", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
      ctypes.c_size_t, HWLMCallback, ctypes.c_void_p)
+_sig("hwlmExecStreaming", ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+     HWLMCallback, ctypes.c_void_p, ctypes.c_uint64)
+_sig("fdrExecStreaming", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+     ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, HWLMCallback, ctypes.c_void_p,
+     ctypes.c_uint64)
+_sig("noodExecStreaming", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+     ctypes.c_void_p, ctypes.c_size_t, HWLMCallback, ctypes.c_void_p)
+_sig("vsa_get_scratch_core_info", None, ctypes.POINTER(ctypes.c_long),
+     ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_long))
 _sig("vsa_shufti_find", ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
 _sig("vsa_shufti_double_find", ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
@@ -124,6 +133,9 @@ _sig("vsa_memcpy_d2h", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
 _sig("vsa_sync", ctypes.c_int, ctypes.c_void_p)
 _sig("vsa_scan_blocks", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_void_p, _u64p, _u64p, ctypes.c_void_p, ctypes.c_uint32,
+     ctypes.c_uint32, _u64p)
+_sig("vsa_scan_blocks_stream", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+     ctypes.c_void_p, _u64p, _u64p, ctypes.c_void_p, _u64p, ctypes.c_uint32,
      ctypes.c_uint32, _u64p)
 _sig("vsa_scan_wait", ctypes.c_int, ctypes.c_void_p, _u64p)
 _sig("vsa_scan_results", ctypes.c_int, ctypes.c_void_p,
@@ -300,6 +312,80 @@ def nood_exec(blob, data, start=0, cb=None, scratch=None):
     return rc if cb is not None else (rc, matches)
 
 
+ACCEL_TYPES = {"none": 0, "verm": 1, "verm_nocase": 2, "dverm": 3, "dverm_nocase": 4,
+               "shufti": 13, "truffle": 15}
+
+
+def accel_aux(kind, offset=0, c=0, c2=0, masks=None):
+    """An 80-byte union AccelAux image (accel.h:72-124) of the kinds an HWLM
+    header carries (hwlm.c:48-80): verm / dverm take chars c (, c2); shufti
+    and truffle take their two 16-byte masks."""
+    b = bytearray(80)
+    b[0] = ACCEL_TYPES[kind]
+    b[1] = offset
+    if kind.startswith("verm"):
+        b[2] = c
+    elif kind.startswith("dverm"):
+        b[2], b[3] = c, c2
+    elif kind in ("shufti", "truffle"):
+        m1, m2 = masks
+        b[16:32] = bytes(m1)
+        b[32:48] = bytes(m2)
+    return bytes(b)
+
+
+def _history(hist, filler):
+    """(keepalive, start address, hlen) of a history buffer with at least 16
+    readable bytes before its end (fdr.c:835-841): short histories are
+    preceded by `filler`."""
+    hist = bytes(hist)
+    pad = bytes(filler)[:16].rjust(16, b"\0") if len(hist) < 16 else b""
+    raw = pad + hist
+    b = ctypes.create_string_buffer(raw, max(1, len(raw)))
+    return b, ctypes.addressof(b) + len(pad), len(hist)
+
+
+def fdr_exec_stream(blob, hist, data, start=0, cb=None, groups=HWLM_ALL_GROUPS,
+                    scratch=None, filler=b""):
+    """fdrExecStreaming (fdr.h:75): matches of `data` whose literal may begin
+    inside `hist`; ends are relative to `data`."""
+    hk, hptr, hlen = _history(hist, filler)
+    keep, ptr, n = _as_buf(data)
+    ccb, matches = _runner(None, cb)
+    rc = lib.fdrExecStreaming(engine_blob(blob), hptr if hlen else None, hlen, ptr, n, start,
+                              ccb, scratch, groups)
+    return rc if cb is not None else (rc, matches)
+
+
+def nood_exec_stream(blob, hist, data, cb=None, scratch=None, filler=b""):
+    """noodExecStreaming (noodle_engine.h:52)."""
+    hk, hptr, hlen = _history(hist, filler)
+    keep, ptr, n = _as_buf(data)
+    ccb, matches = _runner(None, cb)
+    rc = lib.noodExecStreaming(engine_blob(blob), hptr if hlen else None, hlen, ptr, n, ccb,
+                               scratch)
+    return rc if cb is not None else (rc, matches)
+
+
+def hwlm_exec_stream(blob, hist, data, start=0, cb=None, groups=HWLM_ALL_GROUPS,
+                     filler=b""):
+    """hwlmExecStreaming (hwlm.h:137).  The reference reads buf / hbuf / hlen
+    from scratch->core_info; this builds a scratch image carrying them at the
+    offsets the library uses (vsa_get_scratch_core_info)."""
+    hk, hptr, hlen = _history(hist, filler)
+    keep, ptr, n = _as_buf(data)
+    offs = [ctypes.c_long() for _ in range(3)]
+    lib.vsa_get_scratch_core_info(*[ctypes.byref(o) for o in offs])
+    scratch = ctypes.create_string_buffer(max(o.value for o in offs) + 4096)
+    base = ctypes.addressof(scratch)
+    ctypes.c_void_p.from_address(base + offs[0].value).value = ptr
+    ctypes.c_void_p.from_address(base + offs[1].value).value = hptr if hlen else None
+    ctypes.c_size_t.from_address(base + offs[2].value).value = hlen
+    ccb, matches = _runner(None, cb)
+    rc = lib.hwlmExecStreaming(blob.ptr, n, start, ccb, base, groups)
+    return rc if cb is not None else (rc, matches)
+
+
 def _m16(x):
     x = bytes(x)
     assert len(x) == 16
@@ -467,6 +553,24 @@ class Context:
             len(off), flags, ctypes.byref(n))
         if rc != 0:
             raise RuntimeError("vsa_scan_blocks failed (%d)" % rc)
+        return n.value
+
+    def scan_blocks_stream(self, db, d_data, offsets, lens, hlens, starts=None, sort=True,
+                           asynchronous=False):
+        """vsa_scan_blocks_stream: block i is a streaming call whose hlens[i]
+        history bytes sit just before offsets[i] in the same device buffer."""
+        off = np.ascontiguousarray(offsets, np.uint64)
+        ln = np.ascontiguousarray(lens, np.uint64)
+        hl = np.ascontiguousarray(hlens, np.uint64)
+        st = None if starts is None else np.ascontiguousarray(starts, np.uint64)
+        n = ctypes.c_uint64()
+        flags = (0 if sort else 1) | (2 if asynchronous else 0)
+        rc = lib.vsa_scan_blocks_stream(
+            self.ptr, db.ptr, d_data, off.ctypes.data_as(_u64p), ln.ctypes.data_as(_u64p),
+            None if st is None else st.ctypes.data, hl.ctypes.data_as(_u64p), len(off), flags,
+            ctypes.byref(n))
+        if rc != 0:
+            raise RuntimeError("vsa_scan_blocks_stream failed (%d)" % rc)
         return n.value
 
     def scan_wait(self):

@@ -19,7 +19,17 @@ struct VsaBlock {
                            always applies from `start`. */
     int64_t org;        /* aligned (1 KiB, relative to data & ~15) origin of
                            the block's first segment */
+    uint64_t hlen;      /* streaming: len_history (confirm overhang bound,
+                           fdr_confirm_runtime.h:79-88); 0 = block mode */
+    uint32_t hist;      /* bytes readable before base (16 when streaming) */
+    uint32_t flags;     /* VSA_BLK_* */
 };
+
+/* The block is a streaming call with history (fdrExecStreaming fdr.c:827,
+ * len_history > 0): no FDR start state, the look-back starts one byte
+ * before `start` (getInitState fdr.c:129-142), Teddy / noodle read up to
+ * nMasks - 1 / msk_len - 1 history bytes. */
+#define VSA_BLK_STREAM 1u
 
 /* A confirmed literal match.  `key` sorts into the reference callback order:
  * end (bits 63..24), bucket (23..20), LitInfo index within its bucket's

@@ -205,6 +205,7 @@ __device__ __forceinline__ void confirm_one(const VsaLitParams &P, const ConfLds
     const u32 st = *((const u32 *)(fc + 32) + c);
     if (!st) return;
     const u64 base = P.blocks[blk].base;
+    const int64_t hlen = (int64_t)P.blocks[blk].hlen;
     const int64_t e = (int64_t)(aoff - mis - base); /* block-relative end */
     if (P.dbg & 1) {
         const u8 *A = P.data - mis;
@@ -225,7 +226,7 @@ __device__ __forceinline__ void confirm_one(const VsaLitParams &P, const ConfLds
         const u64 msk = ((u64)w0.w << 32) | w0.z;
         const u32 size = w1.w & 0xff;
         next = (w1.w >> 16) & 0xff;
-        if ((key & msk) == v && e + 1 >= (int64_t)size) {
+        if ((key & msk) == v && e + 1 + hlen >= (int64_t)size) {
             unsigned long long slot = atomicAdd(&P.counters[0], 1ULL);
             if (slot < P.out_cap) {
                 const u64 lidx = ((u64)(li - fc) >> 5) & VSA_KEY_LI_MASK;
@@ -275,7 +276,10 @@ struct IterState {
 struct SegCtx {
     u32 blk;
     int64_t blo, bhi; /* aoff of the block */
+    int64_t vlo;      /* lowest readable aoff (blo - history) */
     int64_t start, len, zbase;
+    int64_t qlo;      /* Teddy: lowest looked-up position (block-relative) */
+    bool stream;      /* streaming with history: no FDR start state */
 };
 
 /* Append one entry per lane with push set to the wave's ring (wave-uniform
@@ -331,11 +335,11 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 int64_t p = p0 + 4 * w + k;
-                if (p >= S.blo && p < S.bhi) m |= 0xffu << (8 * k);
+                if (p >= S.vlo && p < S.bhi) m |= 0xffu << (8 * k);
             }
             d[w] &= m;
         }
-        if (p0 + 16 < S.blo || p0 + 16 >= S.bhi) d[4] = 0;
+        if (p0 + 16 < S.vlo || p0 + 16 >= S.bhi) d[4] = 0;
     }
 
     /* own contributions: running state over the lane's 16 positions */
@@ -353,7 +357,7 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
             if constexpr (MODE == VSA_MODE_FDR) {
                 valid = q >= S.zbase && q < S.len;
             } else {
-                valid = q >= 0 && q < S.len;
+                valid = q >= S.qlo && q < S.len;
             }
             if (!valid) x = 0;
         }
@@ -380,7 +384,7 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     c[0] |= (u32)s_in;
     if constexpr (sizeof(S_t) == 8) c[1] |= (u32)(s_in >> 32);
     if (EDGE) {
-        if constexpr (MODE == VSA_MODE_FDR) {
+        if constexpr (MODE == VSA_MODE_FDR) if (!S.stream) {
             /* start state: byte i applies to end start + i (the short zone
              * shifts fdr->start by 16 - (len - start) against a scan from
              * len - 16, fdr.c:372-440 and :712-720, landing on start too) */
@@ -503,7 +507,7 @@ __device__ __forceinline__ IterState nood_iter(const VsaLitParams &P, const LitS
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 int64_t p = p0 + 4 * w + k;
-                if (p >= S.blo && p < S.bhi) m |= 0xffu << (8 * k);
+                if (p >= S.vlo && p < S.bhi) m |= 0xffu << (8 * k);
             }
             d[w] &= m;
         }
@@ -533,7 +537,10 @@ __device__ __forceinline__ IterState nood_iter(const VsaLitParams &P, const LitS
         if (((lo & mlo) == clo) & ((hi & mhi) == chi)) hits |= 1u << j;
     }
     if (EDGE) {
-        const int64_t elo = S.start + (int64_t)P.nood_len - 1;
+        /* noodExecStreaming (start 0): literals may begin up to
+         * min(hlen, msk_len - 1) bytes into the history (noodle_engine.cpp:
+         * 149-180) -- S.qlo carries that (0 in block mode) */
+        const int64_t elo = S.start + (int64_t)P.nood_len - 1 + S.qlo;
 #pragma unroll
         for (int j = 0; j < 16; j++) {
             const int64_t q = q0 + j;
@@ -794,13 +801,22 @@ vsa_lit_scan(VsaLitParams P) {
         S.blk = blk;
         S.blo = (int64_t)B.base + mis;
         S.bhi = S.blo + (int64_t)B.len;
+        S.vlo = S.blo - (int64_t)B.hist;
+        S.stream = (B.flags & VSA_BLK_STREAM) != 0;
+        S.qlo = 0;
+        if (S.stream) {
+            const int64_t back = (MODE == VSA_MODE_NOOD) ? (int64_t)P.nood_len - 1
+                                                         : (int64_t)(T::NL - 1);
+            if (MODE != VSA_MODE_NOOD || B.start == 0)
+                S.qlo = -min((int64_t)B.hlen, back);
+        }
         S.start = (int64_t)B.start;
         S.len = (int64_t)B.len;
         S.zbase = B.zbase;
         const int64_t s_lo = B.org + (int64_t)(seg - B.seg_first) * SEG;
         const int64_t s_hi = (s_lo + SEG < S.bhi) ? s_lo + SEG : S.bhi;
         const u32 niters = (u32)((s_hi - s_lo + 1023) >> 10);
-        const int64_t zlo = (MODE == VSA_MODE_FDR) ? B.zbase : 0;
+        const int64_t zlo = (MODE == VSA_MODE_FDR) ? B.zbase : S.qlo;
 
         /* iterations [f0, f1) are interior ("fast"): no byte of the 1 KiB
          * chunk or its successor byte lies outside the block, and the FDR
@@ -832,7 +848,7 @@ vsa_lit_scan(VsaLitParams P) {
                 const int64_t pk = ((u32)k < nf ? fb + 1024 * k : fb) + 16 * (int64_t)lane;
                 ring[k] = load_chunk_nc(A, pk);
             }
-            after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.blo, S.bhi);
+            after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.vlo, S.bhi);
         }
         /* prologue 1: table spill from positions s_lo-NL+1 .. s_lo-1 */
         IterState is;
@@ -845,10 +861,10 @@ vsa_lit_scan(VsaLitParams P) {
                 const int64_t p = s_lo - (T::NL - 1) + (int64_t)lane;
                 const int64_t q = p - S.blo;
                 if (q >= zlo && q < (int64_t)B.len) {
-                    const u8 b0 = load_byte_masked(A, p, S.blo, S.bhi);
+                    const u8 b0 = load_byte_masked(A, p, S.vlo, S.bhi);
                     u32 key;
                     if constexpr (T::KEY16) {
-                        const u8 b1 = load_byte_masked(A, p + 1, S.blo, S.bhi);
+                        const u8 b1 = load_byte_masked(A, p + 1, S.vlo, S.bhi);
                         key = ((u32)b0 | ((u32)b1 << 8)) & P.dmask;
                     } else {
                         key = b0;
@@ -867,7 +883,7 @@ vsa_lit_scan(VsaLitParams P) {
             is.carry = ((u64)shfl_u32((u32)(xv >> 32), 0) << 32) | shfl_u32((u32)xv, 0);
             /* prologue 2: the 8 bytes before s_lo (keys of the first ends) */
             u32 bb = 0;
-            if (lane < 8) bb = load_byte_masked(A, s_lo - 8 + (int64_t)lane, S.blo, S.bhi);
+            if (lane < 8) bb = load_byte_masked(A, s_lo - 8 + (int64_t)lane, S.vlo, S.bhi);
             u64 pb = (u64)bb << (8 * (lane & 7));
 #pragma unroll
             for (int dd = 1; dd < 8; dd <<= 1) {
@@ -880,7 +896,7 @@ vsa_lit_scan(VsaLitParams P) {
         for (u32 it = 0; it < f0; it++) {
             const int64_t ib = s_lo + 1024 * (int64_t)it;
             const uint4 cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
-            const u32 nxt0 = load_byte_masked(A, ib + 1024, S.blo, S.bhi);
+            const u32 nxt0 = load_byte_masked(A, ib + 1024, S.vlo, S.bhi);
             is = scan_iter<MODE, LDS_TABLE, true>(P, cl, L, S, mis, ib, cur, nxt0, is,
                                                  bucket_mask);
         }
@@ -897,7 +913,7 @@ vsa_lit_scan(VsaLitParams P) {
                     const int64_t pk = ((u32)k < nf ? fb + 1024 * k : fb) + 16 * (int64_t)lane;
                     ring[k] = load_chunk_nc(A, pk);
                 }
-                after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.blo, S.bhi);
+                after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.vlo, S.bhi);
             }
             const u32 ng = nf / LIT_DEPTH;
             for (u32 g = 0; g < ng; g++) {
@@ -929,7 +945,7 @@ vsa_lit_scan(VsaLitParams P) {
         for (u32 it = f1; it < niters; it++) {
             const int64_t ib = s_lo + 1024 * (int64_t)it;
             const uint4 cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
-            const u32 nxt0 = load_byte_masked(A, ib + 1024, S.blo, S.bhi);
+            const u32 nxt0 = load_byte_masked(A, ib + 1024, S.vlo, S.bhi);
             is = scan_iter<MODE, LDS_TABLE, true>(P, cl, L, S, mis, ib, cur, nxt0, is,
                                                  bucket_mask);
         }

@@ -361,7 +361,8 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
 
 int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
                      const uint64_t *offs, const uint64_t *lens, const uint64_t *starts,
-                     uint32_t nb, uint32_t flags, uint64_t *n_out) {
+                     uint32_t nb, uint32_t flags, uint64_t *n_out,
+                     const uint64_t *hlens = nullptr) {
     if (!c || !db || !d_data || !offs || !lens || (!nb)) return VSA_E_INVALID;
     int r = ensure_blocks(c, nb);
     if (r) return r;
@@ -388,8 +389,13 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         b.start = starts ? starts[i] : 0;
         b.seg_first = segs;
         int64_t len = (int64_t)b.len, st = (int64_t)b.start;
-        /* prepareZones fdr.c:625-659: short zone anchors at len - 16 */
+        b.hlen = hlens ? hlens[i] : 0;
+        b.hist = b.hlen ? 16 : 0;
+        b.flags = b.hlen ? VSA_BLK_STREAM : 0;
+        /* prepareZones fdr.c:625-659: short zone anchors at len - 16; with
+         * history the look-back also covers start - 1 (getInitState) */
         b.zbase = (len - st > 16) ? st : len - 16;
+        if (b.hlen) b.zbase = (len - st > 16) ? st - 1 : std::min(len - 16, st - 1);
         /* segments are 1 KiB-aligned (in data-aligned coordinates) and start
          * just before `start`: earlier positions cannot reach ends >= start */
         int64_t blo = (int64_t)b.base + mis;
@@ -562,6 +568,12 @@ struct ScratchLayoutProbe {
     uint8_t fdr_conf_offset;
 };
 
+std::atomic<long> g_core_buf_off{(long)(offsetof(ScratchLayoutProbe, core_info) +
+                                        offsetof(ScratchLayoutProbe::core_info_, buf))};
+std::atomic<long> g_core_hbuf_off{(long)(offsetof(ScratchLayoutProbe, core_info) +
+                                         offsetof(ScratchLayoutProbe::core_info_, hbuf))};
+std::atomic<long> g_core_hlen_off{(long)(offsetof(ScratchLayoutProbe, core_info) +
+                                         offsetof(ScratchLayoutProbe::core_info_, hlen))};
 std::atomic<long> g_fdr_conf_off{(long)offsetof(ScratchLayoutProbe, fdr_conf)};
 std::atomic<long> g_fdr_conf_offset_off{(long)offsetof(ScratchLayoutProbe, fdr_conf_offset)};
 
@@ -623,16 +635,26 @@ hwlm_error_t replay_lit(const vsa_db *db, const uint64_t *keys, uint64_t n,
 }
 
 /* scan one host buffer with the default context */
+/* One hwlmExec-equivalent scan of a host buffer.  hend != NULL: streaming
+ * with history (the 16 bytes before hend are copied in front of buf, as
+ * the reference reads them, fdr.c:380-560). */
 int scan_host(vsa_db *db, const uint8_t *buf, size_t len, size_t start,
-              std::vector<uint64_t> &keys, std::vector<uint32_t> &ids) {
+              std::vector<uint64_t> &keys, std::vector<uint32_t> &ids,
+              const uint8_t *hend = nullptr, size_t hlen = 0) {
     vsa_ctx *c = db->ctx;
     int r;
-    if ((r = ensure_in(c, len + 16)) != VSA_OK) return r;
-    if (len) {
-        VSA_CHECK(hipMemcpyAsync(c->ws.d_in, buf, len, hipMemcpyHostToDevice, c->stream));
+    const size_t pre = hend ? 16 : 0;
+    if ((r = ensure_in(c, pre + len + 16)) != VSA_OK) return r;
+    if (pre) {
+        VSA_CHECK(hipMemcpyAsync(c->ws.d_in, hend - 16, 16, hipMemcpyHostToDevice, c->stream));
     }
-    uint64_t off = 0, l = len, st = start, n = 0;
-    if ((r = scan_blocks_impl(c, db, c->ws.d_in, &off, &l, &st, 1, 0, &n)) != VSA_OK) return r;
+    if (len) {
+        VSA_CHECK(hipMemcpyAsync(c->ws.d_in + pre, buf, len, hipMemcpyHostToDevice, c->stream));
+    }
+    uint64_t off = 0, l = len, st = start, n = 0, hl = hlen;
+    if ((r = scan_blocks_impl(c, db, c->ws.d_in + pre, &off, &l, &st, 1, 0, &n,
+                              pre ? &hl : nullptr)) != VSA_OK)
+        return r;
     keys.resize(n);
     ids.resize(n);
     if (n) {
@@ -1163,6 +1185,67 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
     return VSA_OK;
 }
 
+/* run_hwlm_accel hwlm.c:48-80 (no minimum length, no offset) */
+static const uint8_t *hwlm_accel(const union AccelAux *a, const uint8_t *p,
+                                 const uint8_t *end) {
+    const size_t len = (size_t)(end - p);
+    switch (a->accel_type) {
+    case ACCEL_VERM:
+    case ACCEL_VERM_NOCASE:
+        return p + vsa_verm_find(0, a->verm.c, 0, 0, 0, a->accel_type == ACCEL_VERM_NOCASE, p,
+                                 len);
+    case ACCEL_DVERM:
+    case ACCEL_DVERM_NOCASE:
+        return p + vsa_verm_find(4, a->dverm.c1, a->dverm.c2, 0, 0,
+                                 a->accel_type == ACCEL_DVERM_NOCASE, p, len);
+    case ACCEL_SHUFTI:
+        return p + vsa_shufti_find(a->shufti.lo.b, a->shufti.hi.b, p, len, 0);
+    case ACCEL_TRUFFLE:
+        return p + vsa_truffle_find(a->truffle.mask1.b, a->truffle.mask2.b, p, len, 0);
+    default:
+        return p;
+    }
+}
+
+/* do_accel_block hwlm.c:85-105 */
+static size_t hwlm_accel_block(const union AccelAux *aa, const uint8_t *buf, size_t len,
+                               size_t start) {
+    if (len - start < 16) return start;
+    const uint8_t *ptr = hwlm_accel(aa, buf + start, buf + len);
+    if (aa->generic.offset) {
+        ptr -= aa->generic.offset;
+        if (ptr < buf) ptr = buf;
+    }
+    return (size_t)(ptr - buf);
+}
+
+/* do_accel_streaming hwlm.c:114-175 */
+static size_t hwlm_accel_stream(const union AccelAux *aux, const uint8_t *hbuf, size_t hlen,
+                                const uint8_t *buf, size_t len, size_t start) {
+    if (aux->accel_type == ACCEL_NONE || len - start < 16) return start;
+    const uint8_t offset = aux->generic.offset;
+    if (!start && hlen) {
+        const uint8_t *ptr1 = hbuf, *end1 = hbuf + hlen;
+        if (hlen >= 16) ptr1 = hwlm_accel(aux, ptr1, end1);
+        const bool inaccurate =
+            aux->accel_type == ACCEL_DVERM_NOCASE || aux->accel_type == ACCEL_DVERM;
+        if ((hlen <= 16 || inaccurate) && end1 != ptr1 && end1 - ptr1 <= 16) {
+            uint8_t temp[17];
+            const ptrdiff_t tlen = end1 - ptr1;
+            memcpy(temp, ptr1, (size_t)tlen);
+            memset(temp + tlen, 0, 17 - (size_t)tlen);
+            if (len) temp[tlen] = *buf;
+            const uint8_t *tp = hwlm_accel(aux, temp, temp + 17);
+            if (tp - temp >= tlen) ptr1 = end1;
+        }
+        if (ptr1 != end1) return start;
+    }
+    const uint8_t *ptr2 = buf + start;
+    const uint8_t *found = hwlm_accel(aux, ptr2, buf + len);
+    if (found >= ptr2 + offset) start += (size_t)(found - offset - ptr2);
+    return start;
+}
+
 /* --------------------------------------------------- drop-in literal -- */
 
 hwlm_error_t hwlmExec(const struct HWLM *tab, const uint8_t *buf, size_t len, size_t start,
@@ -1182,15 +1265,8 @@ hwlm_error_t hwlmExec(const struct HWLM *tab, const uint8_t *buf, size_t len, si
     const HWLM *h = (const HWLM *)db->hblob;
     const union AccelAux *aa = &h->accel0;
     if ((groups & ~h->accel1_groups) == 0) aa = &h->accel1;
-    if (aa->accel_type != ACCEL_NONE && len - start >= 16) {
-        int64_t r = run_accel(aa, buf + start, buf + len) - buf;
-        if (aa->generic.offset) {
-            r -= aa->generic.offset;
-            if (r < 0) r = 0;
-        }
-        start = (size_t)r;
-        if (start >= len) return HWLM_SUCCESS;
-    }
+    start = hwlm_accel_block(aa, buf, len, start);
+    if (start >= len) return HWLM_SUCCESS;
     if (scan_host(db, buf, len, start, keys, ids) != VSA_OK) return HWLM_ERROR_UNKNOWN;
     return replay_lit(db, keys.data(), keys.size(), cb, scratch, groups);
 }
@@ -1217,6 +1293,84 @@ hwlm_error_t noodExec(const struct noodTable *n, const uint8_t *buf, size_t len,
     std::vector<uint32_t> ids;
     if (scan_host(db, buf, len, start, keys, ids) != VSA_OK) return HWLM_ERROR_UNKNOWN;
     return replay_nood(keys.data(), ids.data(), keys.size(), cb, scratch);
+}
+
+/* ------------------------------------------------ drop-in streaming -- */
+
+/* fdrExecStreaming fdr.c:827-855.  len_history 0 scans as block mode (the
+ * reference then applies fdr->start and never confirms into history). */
+hwlm_error_t fdrExecStreaming(const struct FDR *fdr, const uint8_t *hbuf, size_t hlen,
+                              const uint8_t *buf, size_t len, size_t start, HWLMCallback cb,
+                              struct hs_scratch *scratch, hwlm_group_t groups) {
+    if (!fdr) return HWLM_ERROR_UNKNOWN;
+    if (start >= len) return HWLM_SUCCESS;
+    vsa_db *db = registry_get(fdr, HWLM_ENGINE_FDR);
+    if (!db) return HWLM_ERROR_UNKNOWN;
+    std::vector<uint64_t> keys;
+    std::vector<uint32_t> ids;
+    if (scan_host(db, buf, len, start, keys, ids, hlen ? hbuf + hlen : nullptr, hlen) != VSA_OK)
+        return HWLM_ERROR_UNKNOWN;
+    return replay_lit(db, keys.data(), keys.size(), cb, scratch, groups);
+}
+
+/* noodExecStreaming noodle_engine.cpp:136-185 */
+hwlm_error_t noodExecStreaming(const struct noodTable *n, const uint8_t *hbuf, size_t hlen,
+                               const uint8_t *buf, size_t len, HWLMCallback cb,
+                               struct hs_scratch *scratch) {
+    if (!n) return HWLM_ERROR_UNKNOWN;
+    if (len + hlen < n->msk_len || !len) return HWLM_SUCCESS;
+    vsa_db *db = registry_get(n, HWLM_ENGINE_NOOD);
+    if (!db) return HWLM_ERROR_UNKNOWN;
+    std::vector<uint64_t> keys;
+    std::vector<uint32_t> ids;
+    if (scan_host(db, buf, len, 0, keys, ids, hlen ? hbuf + hlen : nullptr, hlen) != VSA_OK)
+        return HWLM_ERROR_UNKNOWN;
+    return replay_nood(keys.data(), ids.data(), keys.size(), cb, scratch);
+}
+
+/* hwlmExecStreaming hwlm.c:207-247: buffers from scratch->core_info */
+hwlm_error_t hwlmExecStreaming(const struct HWLM *tab, size_t len, size_t start,
+                               HWLMCallback cb, struct hs_scratch *scratch,
+                               hwlm_group_t groups) {
+    if (!tab || !scratch) return HWLM_ERROR_UNKNOWN;
+    if (!groups) return HWLM_SUCCESS;
+    const char *sc = (const char *)scratch;
+    const uint8_t *buf, *hbuf;
+    size_t hlen;
+    memcpy(&buf, sc + g_core_buf_off.load(), sizeof(buf));
+    memcpy(&hbuf, sc + g_core_hbuf_off.load(), sizeof(hbuf));
+    memcpy(&hlen, sc + g_core_hlen_off.load(), sizeof(hlen));
+    const HWLM *h = (const HWLM *)tab;
+    const uint8_t *eng = (const uint8_t *)tab + VSA_ROUNDUP_CL(sizeof(HWLM));
+    if (h->type == HWLM_ENGINE_NOOD) {
+        if (start) return noodExec((const noodTable *)eng, buf, len, start, cb, scratch);
+        return noodExecStreaming((const noodTable *)eng, hbuf, hlen, buf, len, cb, scratch);
+    }
+    const union AccelAux *aa = &h->accel0;
+    if ((groups & ~h->accel1_groups) == 0) aa = &h->accel1;
+    start = hwlm_accel_stream(aa, hbuf, hlen, buf, len, start);
+    return fdrExecStreaming((const FDR *)eng, hbuf, hlen, buf, len, start, cb, scratch, groups);
+}
+
+int vsa_scan_blocks_stream(vsa_ctx_t *c, const vsa_db_t *db, const uint8_t *d_data,
+                           const uint64_t *offsets, const uint64_t *lens,
+                           const uint64_t *starts, const uint64_t *hlens, uint32_t nblocks,
+                           uint32_t flags, uint64_t *n_matches) {
+    uint64_t dummy;
+    return scan_blocks_impl(c, db, d_data, offsets, lens, starts, nblocks, flags,
+                            n_matches ? n_matches : &dummy, hlens);
+}
+
+void vsa_get_scratch_core_info(long *buf_off, long *hbuf_off, long *hlen_off) {
+    *buf_off = g_core_buf_off.load();
+    *hbuf_off = g_core_hbuf_off.load();
+    *hlen_off = g_core_hlen_off.load();
+}
+
+void vsa_set_scratch_core_info(long buf_off, long hbuf_off, long hlen_off) {
+    g_core_buf_off.store(buf_off);
+    g_core_hbuf_off.store(hbuf_off);
+    g_core_hlen_off.store(hlen_off);
 }
 
 /* ----------------------------------------------------- drop-in accel -- */
@@ -1383,27 +1537,52 @@ const uint8_t *vermicelliDoubleMaskedExec(char c1, char c2, char m1, char m2,
 }
 
 /* accel.c:35-180 dispatch for the forward schemes HWLM and NFAs use */
+/* accel.c:36-183: minimum lengths (16, 17 for the double forms, which stop
+ * one byte early), then rv = MAX(c + offset, rv) - offset. */
 const uint8_t *run_accel(const union AccelAux *accel, const uint8_t *c, const uint8_t *c_end) {
-    size_t len = (size_t)(c_end - c);
+    const size_t len = (size_t)(c_end - c);
+    const uint8_t *rv;
     switch (accel->accel_type) {
+    case ACCEL_NONE:
+        return c;
     case ACCEL_VERM:
-        return c + vsa_verm_find(0, accel->verm.c, 0, 0, 0, 0, c, len);
     case ACCEL_VERM_NOCASE:
-        return c + vsa_verm_find(0, accel->verm.c, 0, 0, 0, 1, c, len);
+        if (c + 15 >= c_end) return c;
+        rv = c + vsa_verm_find(0, accel->verm.c, 0, 0, 0, accel->accel_type == ACCEL_VERM_NOCASE,
+                               c, len);
+        break;
     case ACCEL_DVERM:
-        return c + vsa_verm_find(4, accel->dverm.c1, accel->dverm.c2, 0, 0, 0, c, len);
     case ACCEL_DVERM_NOCASE:
-        return c + vsa_verm_find(4, accel->dverm.c1, accel->dverm.c2, 0, 0, 1, c, len);
+        if (c + 16 + 1 >= c_end) return c;
+        rv = c + vsa_verm_find(4, accel->dverm.c1, accel->dverm.c2, 0, 0,
+                               accel->accel_type == ACCEL_DVERM_NOCASE, c, len - 1);
+        break;
     case ACCEL_DVERM_MASKED:
-        return c + vsa_verm_find(5, accel->dverm.c1, accel->dverm.c2, accel->dverm.m1,
-                                 accel->dverm.m2, 0, c, len);
+        if (c + 16 + 1 >= c_end) return c;
+        rv = c + vsa_verm_find(5, accel->dverm.c1, accel->dverm.c2, accel->dverm.m1,
+                               accel->dverm.m2, 0, c, len - 1);
+        break;
     case ACCEL_SHUFTI:
-        return c + vsa_shufti_find(accel->shufti.lo.b, accel->shufti.hi.b, c, len, 0);
+        if (c + 15 >= c_end) return c;
+        rv = c + vsa_shufti_find(accel->shufti.lo.b, accel->shufti.hi.b, c, len, 0);
+        break;
     case ACCEL_TRUFFLE:
-        return c + vsa_truffle_find(accel->truffle.mask1.b, accel->truffle.mask2.b, c, len, 0);
+        if (c + 15 >= c_end) return c;
+        rv = c + vsa_truffle_find(accel->truffle.mask1.b, accel->truffle.mask2.b, c, len, 0);
+        break;
+    case ACCEL_DSHUFTI:
+        if (c + 15 + 1 >= c_end) return c;
+        rv = c + vsa_shufti_double_find(accel->dshufti.lo1.b, accel->dshufti.hi1.b,
+                                        accel->dshufti.lo2.b, accel->dshufti.hi2.b, c, len - 1);
+        break;
+    case ACCEL_RED_TAPE:
+        rv = c_end;
+        break;
     default:
         return c;
     }
+    rv = std::max(c + accel->generic.offset, rv);
+    return rv - accel->generic.offset;
 }
 
 void vsa_set_scratch_layout(long fdr_conf_off, long fdr_conf_offset_off) {
