@@ -71,10 +71,25 @@ __device__ __forceinline__ u32 shfl_up_u32(u32 v, unsigned d) {
  * l the value of lane l-1 (lane 0 gets 0), down1 that of lane l+1 (lane 63
  * gets 0) */
 __device__ __forceinline__ u32 lane_up1(u32 v) {
-    return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+    return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, true);
 }
 __device__ __forceinline__ u32 lane_down1(u32 v) {
-    return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+    return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, true);
+}
+/* v with lane `l` replaced by the wave-uniform s (v_writelane) */
+template <int L>
+__device__ __forceinline__ u32 writelane_u32(u32 v, u32 s) {
+    /* s is wave-uniform; readfirstlane pins it to an SGPR (free when it is
+     * one already) */
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(readfirstlane_u32(s)), "n"(L));
+    return v;
+}
+/* three-input OR in one VALU op (the backend re-associates wide OR trees
+ * into two-input ORs) */
+__device__ __forceinline__ u32 or3(u32 a, u32 b, u32 c) {
+    u32 r;
+    asm("v_or3_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
 }
 __device__ __forceinline__ u32 shfl_xor_u32(u32 v, int m) {
     return (u32)__shfl_xor((int)v, m, WAVE);
@@ -111,6 +126,7 @@ struct LitTraits<VSA_MODE_FDR> {
     static constexpr int LB = 8;   /* bits per lane field (= buckets) */
     static constexpr int NL = 8;   /* lanes (positions looked back) */
     static constexpr int CW = 4;   /* conf dwords for 16 ends */
+    static constexpr int EW = 3;   /* uint4 words per candidate chunk entry */
     static constexpr bool KEY16 = true;
     typedef u64 S_t;
 };
@@ -119,6 +135,7 @@ struct LitTraits<VSA_MODE_TEDDY> {
     static constexpr int LB = 8;
     static constexpr int NL = 4;
     static constexpr int CW = 4;
+    static constexpr int EW = 3;
     static constexpr bool KEY16 = false;
     typedef u32 S_t;
 };
@@ -127,6 +144,7 @@ struct LitTraits<VSA_MODE_NOOD> {
     static constexpr int LB = 8;
     static constexpr int NL = 1; /* no look-back state */
     static constexpr int CW = 1;
+    static constexpr int EW = 1;
     static constexpr bool KEY16 = false;
     typedef u32 S_t;
 };
@@ -135,6 +153,7 @@ struct LitTraits<VSA_MODE_FAT> {
     static constexpr int LB = 16;
     static constexpr int NL = 4;
     static constexpr int CW = 8;
+    static constexpr int EW = 4;
     static constexpr bool KEY16 = false;
     typedef u64 S_t;
 };
@@ -154,24 +173,32 @@ struct ConfLds {
     PfRec pf[16]; /* one 32-B record per bucket for the scanners' prefilter */
 };
 
-/* queue entry: meta = aoff << 24 | blk << 4 | bucket; key = 8 bytes ending
- * at the candidate end (bytes before the block are 0, fdr.c:798-806) */
+/* confirm-queue entry (the confirm wave's private queue): meta = aoff << 24 |
+ * blk << 4 | bucket; key = 8 bytes ending at the candidate end (bytes
+ * before the block are 0, fdr.c:798-806) */
 struct QEnt {
     u64 meta;
     u64 key;
 };
 
 /* Candidates go from each scanning wave to the workgroup's confirm wave
- * through the scanning wave's own LDS ring of rsize (power of two) entries.
- * The scanner owns *head (entries written, published after the entries),
- * the confirm wave owns *tail (entries consumed).  LDS executes one wave's
- * instructions in order, so a published head implies visible entries. */
+ * through the scanning wave's own LDS ring of rsize (power of two) chunk
+ * entries: one entry per lane whose 16 ends hold any first-stage candidate,
+ * carrying the lane's candidate masks and the 24 bytes its confirm keys are
+ * cut from, so the scanning wave never loops over candidate bits (a wave
+ * looping for one lane's rare candidate wasted the other 63 lanes; the
+ * confirm wave expands the entries 64 at a time).  Entry layout, EW uint4
+ * words: {p0 | blk << 44 (u64), c[0..CW), pv2, pv3, d0..d3} (noodle: {meta,
+ * hits, 0}).  The scanner owns *head (entries written, published after the
+ * entries), the confirm wave owns *tail (entries consumed).  LDS executes
+ * one wave's instructions in order, so a published head implies visible
+ * entries. */
+#define ENT_BLK_SHIFT 44
 struct LitShared {
     const void *tab;
-    QEnt *ring;      /* this wave's ring */
+    uint4 *ring;     /* this wave's ring */
     u32 *head_pub;   /* this wave's published head */
     const u32 *tail; /* this wave's tail (written by the confirm wave) */
-    const u32 *slots;
     u32 rmask;
 };
 
@@ -282,32 +309,115 @@ struct SegCtx {
     bool stream;      /* streaming with history: no FDR start state */
 };
 
-/* Append one entry per lane with push set to the wave's ring (wave-uniform
- * call).  The ring cursor in `st` is updated identically by every lane. */
-template <typename ST>
-__device__ __forceinline__ void ring_push(const LitShared &L, ST &st, bool push, u64 meta,
-                                          u64 key) {
+/* Append one EW-word entry per lane with push set to the wave's ring
+ * (wave-uniform call), in batches of at most the ring size.  The ring cursor
+ * in `st` is updated identically by every lane. */
+template <int EW, typename ST>
+__device__ __forceinline__ void ring_push(const LitShared &L, ST &st, bool push,
+                                          const u32 (&w)[4 * EW]) {
     const u64 pm = __ballot(push);
     if (pm == 0) return;
     const u32 n = (u32)__popcll(pm);
-    /* room for n entries (the confirm wave frees them in order) */
-    if (st.head + n - st.tail_cache > L.rmask + 1) {
-        for (;;) {
-            st.tail_cache = readfirstlane_u32(lds_ld32(L.tail));
-            if (st.head + n - st.tail_cache <= L.rmask + 1) break;
-            __builtin_amdgcn_s_sleep(2);
+    const u32 r = __builtin_amdgcn_mbcnt_hi((u32)(pm >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((u32)pm, 0));
+    const u32 cap = L.rmask + 1;
+    for (u32 base = 0; base < n; base += cap) {
+        const u32 m = min(n - base, cap);
+        /* room for m entries (the confirm wave frees them in order) */
+        if (st.head + m - st.tail_cache > cap) {
+            for (;;) {
+                st.tail_cache = readfirstlane_u32(lds_ld32(L.tail));
+                if (st.head + m - st.tail_cache <= cap) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
         }
+        if (push && r - base < m) {
+            uint4 *q = L.ring + (size_t)((st.head + r - base) & L.rmask) * EW;
+#pragma unroll
+            for (int k = 0; k < EW; k++)
+                q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+        }
+        st.head += m;
+        asm volatile("" ::: "memory"); /* entries before the head (LDS order) */
+        if (lane_id() == 0) lds_st32(L.head_pub, st.head);
     }
-    if (push) {
-        const u32 r = __builtin_amdgcn_mbcnt_hi((u32)(pm >> 32),
-                                                 __builtin_amdgcn_mbcnt_lo((u32)pm, 0));
-        QEnt *q = &L.ring[(st.head + r) & L.rmask];
-        q->meta = meta;
-        q->key = key;
+}
+
+/* Shift-or of one lane's 16 table entries (the reference's running state,
+ * fdr.c:145-296 / teddy.c:921-971, restated without a serial chain): field
+ * k (LB bits) of x[j] is OR-ed into the conf field of end j + k.  Entries
+ * are grouped by j mod (32 / LB) so each group ORs dword-aligned, and each
+ * group is then shifted into place once (alignbyte) — 39 VALU for FDR's 16
+ * u64 entries against 64 for a per-position shift.  c = the conf fields of
+ * the lane's own 16 ends, s_out = the fields spilling into ends 16.. */
+template <int MODE>
+__device__ __forceinline__ void conf_accumulate(const typename LitTraits<MODE>::S_t (&x)[16],
+                                                u32 (&c)[LitTraits<MODE>::CW], u64 &s_out) {
+    auto lo = [&](int j) { return (u32)(u64)x[j]; };
+    auto hi = [&](int j) { return (u32)((u64)x[j] >> 32); };
+    if constexpr (LitTraits<MODE>::LB == 8 && sizeof(typename LitTraits<MODE>::S_t) == 4) {
+        /* Teddy: 4 one-byte fields per entry, no high dword */
+        u32 F[5];
+        F[0] = lo(0) | (lo(1) << 8) | (lo(2) << 16) | (lo(3) << 24);
+#pragma unroll
+        for (int i = 1; i < 4; i++) {
+            const u32 s1 = __builtin_amdgcn_alignbyte(lo(4 * i + 1), lo(4 * i - 3), 3);
+            const u32 s2 = __builtin_amdgcn_alignbyte(lo(4 * i + 2), lo(4 * i - 2), 2);
+            const u32 s3 = __builtin_amdgcn_alignbyte(lo(4 * i + 3), lo(4 * i - 1), 1);
+            F[i] = or3(lo(4 * i), s1, s2) | s3;
+        }
+        F[4] = or3(lo(13) >> 24, lo(14) >> 16, lo(15) >> 8);
+#pragma unroll
+        for (int i = 0; i < 4; i++) c[i] = F[i];
+        s_out = F[4];
+    } else if constexpr (LitTraits<MODE>::LB == 8) {
+        /* A[r][w] = dword w of the group j = 4 w' + r (before its r-byte
+         * shift); group 0 is folded straight into F */
+        u32 A[4][5];
+#pragma unroll
+        for (int r = 1; r < 4; r++) {
+            A[r][0] = lo(r);
+            A[r][1] = hi(r) | lo(4 + r);
+            A[r][2] = hi(4 + r) | lo(8 + r);
+            A[r][3] = hi(8 + r) | lo(12 + r);
+            A[r][4] = hi(12 + r);
+        }
+        u32 F[6];
+        F[0] = lo(0) | (A[1][0] << 8) | (A[2][0] << 16) | (A[3][0] << 24);
+#pragma unroll
+        for (int i = 1; i < 5; i++) {
+            const u32 g0a = hi(4 * (i - 1));
+            const u32 g0b = i < 4 ? lo(4 * i) : 0u;
+            const u32 s1 = __builtin_amdgcn_alignbyte(A[1][i], A[1][i - 1], 3);
+            const u32 s2 = __builtin_amdgcn_alignbyte(A[2][i], A[2][i - 1], 2);
+            const u32 s3 = __builtin_amdgcn_alignbyte(A[3][i], A[3][i - 1], 1);
+            F[i] = or3(or3(g0a, g0b, s1), s2, s3);
+        }
+        F[5] = or3(A[1][4] >> 24, A[2][4] >> 16, A[3][4] >> 8);
+#pragma unroll
+        for (int i = 0; i < 4; i++) c[i] = F[i];
+        s_out = ((u64)F[5] << 32) | F[4];
+    } else {
+        /* 16-bit fields: even j land dword-aligned, odd j half a dword up */
+        u32 A0[9], A1[9];
+        A0[0] = lo(0);
+        A1[0] = lo(1);
+#pragma unroll
+        for (int w = 1; w < 8; w++) {
+            A0[w] = hi(2 * w - 2) | lo(2 * w);
+            A1[w] = hi(2 * w - 1) | lo(2 * w + 1);
+        }
+        A0[8] = hi(14);
+        A1[8] = hi(15);
+        u32 F[10];
+        F[0] = A0[0] | (A1[0] << 16);
+#pragma unroll
+        for (int i = 1; i < 9; i++) F[i] = A0[i] | __builtin_amdgcn_alignbyte(A1[i], A1[i - 1], 2);
+        F[9] = A1[8] >> 16;
+#pragma unroll
+        for (int i = 0; i < 8; i++) c[i] = F[i];
+        s_out = ((u64)F[9] << 32) | F[8];
     }
-    st.head += n;
-    asm volatile("" ::: "memory"); /* entries before the head (LDS order) */
-    if (lane_id() == 0) lds_st32(L.head_pub, st.head);
 }
 
 /* One 1 KiB iteration at aoff `ib`: lane l owns bytes [ib + 16 l, +16).
@@ -325,9 +435,9 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     const int64_t q0 = p0 - S.blo;
 
     u32 d[5] = {chunk.x, chunk.y, chunk.z, chunk.w, 0};
-    u32 nx = lane_down1(d[0]);
-    if (lane == WAVE - 1) nx = nxt0;
-    d[4] = nx & 0xff;
+    /* next byte (only byte 0 of d[4] reaches a key: the 16-bit key of
+     * position 15 is bytes 15..16, masked to <= 16 bits) */
+    d[4] = writelane_u32<WAVE - 1>(lane_down1(d[0]), nxt0);
     if (EDGE) {
 #pragma unroll
         for (int w = 0; w < 4; w++) {
@@ -342,15 +452,12 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
         if (p0 + 16 < S.vlo || p0 + 16 >= S.bhi) d[4] = 0;
     }
 
-    /* own contributions: running state over the lane's 16 positions */
-    u32 c[T::CW];
-#pragma unroll
-    for (int i = 0; i < T::CW; i++) c[i] = 0;
-    S_t st = 0;
+    /* own contributions: the lane's 16 lookups ... */
+    S_t x[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) {
         u32 key = lit_key<MODE>(d, j, P.dmask);
-        S_t x = (S_t)lit_lookup<MODE, LDS_TABLE>(L.tab, key, lane);
+        x[j] = (S_t)lit_lookup<MODE, LDS_TABLE>(L.tab, key, lane);
         if (EDGE) {
             int64_t q = q0 + j;
             bool valid;
@@ -359,21 +466,19 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
             } else {
                 valid = q >= S.qlo && q < S.len;
             }
-            if (!valid) x = 0;
+            if (!valid) x[j] = 0;
         }
-        st |= x;
-        if constexpr (T::LB == 8) {
-            const u32 sel = (0x03020100u & ~(0xffu << (8 * (j & 3)))) | (0x04u << (8 * (j & 3)));
-            c[j >> 2] = __builtin_amdgcn_perm((u32)st, c[j >> 2], sel);
-        } else {
-            c[j >> 1] |= ((u32)st & 0xffffu) << (16 * (j & 1));
-        }
-        st >>= T::LB;
     }
+    /* ... OR-ed into place: field k of x[j] lands on end j + k */
+    u32 c[T::CW];
+    u64 s_out;
+    conf_accumulate<MODE>(x, c, s_out);
     /* spill from the previous lane (lane 0: from the previous chunk) */
-    const u64 s_out = (u64)st;
-    u64 s_in = ((u64)lane_up1((u32)(s_out >> 32)) << 32) | lane_up1((u32)s_out);
-    if (lane == 0) s_in = in.carry;
+    const u32 s_in_lo = writelane_u32<0>(lane_up1((u32)s_out), (u32)in.carry);
+    const u32 s_in_hi = sizeof(S_t) == 8
+                            ? writelane_u32<0>(lane_up1((u32)(s_out >> 32)), (u32)(in.carry >> 32))
+                            : 0u;
+    const u64 s_in = ((u64)s_in_hi << 32) | s_in_lo;
     IterState out;
     out.ncand = in.ncand;
     out.head = in.head;
@@ -408,14 +513,19 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
         }
     }
 
-    /* candidate bits (do_confirm_fdr skips empty buckets, cf == 0) */
+    /* candidate bits (do_confirm_fdr skips empty buckets, cf == 0): some
+     * ~c[i] & bucket_mask != 0  <=>  (AND_i c[i]) | ~bucket_mask != ~0, so
+     * the common no-candidate case costs an AND tree, not CW masks */
+    u32 all = c[0];
+#pragma unroll
+    for (int i = 1; i < T::CW; i++) all &= c[i];
+    if (!__any((all | ~bucket_mask) != 0xffffffffu)) return out;
     u32 any = 0;
 #pragma unroll
     for (int i = 0; i < T::CW; i++) {
         c[i] = ~c[i] & bucket_mask;
         any |= c[i];
     }
-    if (!__any(any != 0)) return out;
     if (P.dbg & 32) {
         /* diagnostic first-stage candidate count */
         u32 pc = 0;
@@ -433,56 +543,18 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
         pv2 = (u32)in.pbytes;
         pv3 = (u32)(in.pbytes >> 32);
     }
-    const u64 W0 = ((u64)pv3 << 32) | pv2;
-    const u64 W1 = ((u64)d[1] << 32) | d[0];
-    const u64 W2 = ((u64)d[3] << 32) | d[2];
-    /* Wave-uniform loop: each round every lane takes its lowest remaining
-     * candidate bit (over all conf words), so the rounds are the largest
-     * per-lane count, not words x bits.  The ring cursor is updated by every
-     * lane each round and stays wave-uniform. */
-    for (;;) {
-        u32 word = 0, bits = c[0];
+    /* one chunk entry per lane with candidates; the confirm wave expands it */
+    const u64 meta = (u64)p0 | ((u64)S.blk << ENT_BLK_SHIFT);
+    u32 w[4 * T::EW];
+    w[0] = (u32)meta;
+    w[1] = (u32)(meta >> 32);
 #pragma unroll
-        for (int k = 1; k < T::CW; k++) {
-            const bool take = bits == 0;
-            bits = take ? c[k] : bits;
-            word = take ? (u32)k : word;
-        }
-        const bool have = bits != 0;
-        if (!__any(have)) break;
-        bool push = false;
-        u64 key = 0, meta = 0;
-        if (have) {
-            const u32 bit = __ffs(bits) - 1;
+    for (int i = 0; i < T::CW; i++) w[2 + i] = c[i];
+    w[2 + T::CW] = pv2;
+    w[3 + T::CW] = pv3;
 #pragma unroll
-            for (int k = 0; k < T::CW; k++)
-                if (word == (u32)k) c[k] &= c[k] - 1;
-            u32 j, b;
-            if constexpr (T::LB == 8) {
-                j = 4 * word + (bit >> 3);
-                b = bit & 7;
-            } else {
-                j = 2 * word + (bit >> 4);
-                b = bit & 15;
-            }
-            /* key = bytes [j-7, j] = byte offset j+1 .. j+8 of W0:W1:W2 */
-            const u32 o = j + 1;
-            if (o < 8) key = (W0 >> (8 * o)) | (W1 << (64 - 8 * o));
-            else if (o == 8) key = W1;
-            else if (o < 16) key = (W1 >> (8 * (o - 8))) | (W2 << (64 - 8 * (o - 8)));
-            else key = W2;
-            /* LDS slot-bitmap prefilter: litIndex[hash] == 0 rejects */
-            const PfRec pf = cl.pf[b];
-            push = true;
-            if (pf.slot_off != 0xffffffffu) {
-                const u32 h = (u32)(((key & pf.andmsk) * P.pf_mult) >> pf.shift);
-                push = (L.slots[pf.slot_off + (h >> 5)] >> (h & 31)) & 1u;
-            }
-            if (P.dbg & 16) push = false;
-            meta = ((u64)(p0 + j) << 24) | ((u64)S.blk << 4) | b;
-        }
-        ring_push(L, out, push, meta, key);
-    }
+    for (int i = 0; i < 4; i++) w[4 + T::CW + i] = d[i];
+    ring_push<T::EW>(L, out, any != 0, w);
     return out;
 }
 
@@ -548,17 +620,9 @@ __device__ __forceinline__ IterState nood_iter(const VsaLitParams &P, const LitS
         }
     }
     if (!__any(hits != 0)) return out;
-    for (;;) {
-        const bool have = hits != 0;
-        if (!__any(have)) break;
-        u64 meta = 0;
-        if (have) {
-            const u32 j = __ffs(hits) - 1;
-            hits &= hits - 1;
-            meta = ((u64)(p0 + j) << 24) | ((u64)S.blk << 4);
-        }
-        ring_push(L, out, have, meta, 0);
-    }
+    const u64 meta = (u64)p0 | ((u64)S.blk << ENT_BLK_SHIFT);
+    const u32 ent[4] = {(u32)meta, (u32)(meta >> 32), hits, 0};
+    ring_push<1>(L, out, hits != 0, ent);
     return out;
 }
 
@@ -592,27 +656,67 @@ __device__ __forceinline__ uint4 load_chunk_nc(const u8 *A, int64_t p0) {
     return make_uint4(t.x, t.y, t.z, t.w);
 }
 
+/* unconditional wave load of the 1 KiB at A + ib (wave-uniform ib): lane l
+ * reads bytes [16 l, 16 l + 16).  The base goes through SGPRs so the load
+ * is an saddr global_load_dwordx4 with a 32-bit lane offset (no per-lane
+ * 64-bit address arithmetic in the sweep). */
+__device__ __forceinline__ const u8 *uniform_ptr(const u8 *p) {
+    const u64 a = (u64)p;
+    return (const u8 *)(((u64)readfirstlane_u32((u32)(a >> 32)) << 32) |
+                        readfirstlane_u32((u32)a));
+}
+__device__ __forceinline__ uint4 load_wave_kib(const u8 *base, u32 off) {
+    typedef u32 v4u __attribute__((ext_vector_type(4)));
+    /* global address space: a flat load would also count in lgkmcnt and
+     * serialize against the table's LDS reads */
+    typedef const __attribute__((address_space(1))) v4u gv4u;
+    gv4u *p = (gv4u *)(base + (off + 16 * lane_id()));
+    v4u t = __builtin_nontemporal_load(p);
+    return make_uint4(t.x, t.y, t.z, t.w);
+}
+
 #define LIT_DEPTH 4
 
-/* The workgroup's confirm wave: gathers up to 64 entries per round from the
- * scanning waves' rings (each consumed in order) and runs the exact
- * confirm.  Its global-memory latency never stalls a scanning wave.  Exits
- * once every scanning wave has finished (q_done, read before the heads) and
- * every ring is empty. */
+/* The workgroup's confirm wave: gathers up to 64 chunk entries per round
+ * from the scanning waves' rings (each consumed in order), expands their
+ * candidate bits one per lane per round, drops the candidates whose litIndex
+ * slot is empty (LDS slot bitmap: litIndex[hash] == 0 means no LitInfo
+ * chain, fdr_confirm_runtime.h:55-58), queues the rest in its private LDS
+ * queue and runs the exact confirm 64 at a time.  Its global-memory latency
+ * never stalls a scanning wave.  Exits once every scanning wave has finished
+ * (q_done, read before the heads), every ring is empty and the queue is
+ * drained. */
 #define LIT_SCANNERS (LIT_WAVES - 1)
+#define PQ_CAP 128
 template <int MODE>
 __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLds &cl,
-                                             const QEnt *rings, u32 rsize, const u32 *heads,
-                                             u32 *tails, const u32 *q_done, u32 mis) {
+                                             const uint4 *rings, u32 rsize, const u32 *heads,
+                                             u32 *tails, const u32 *q_done, u32 mis,
+                                             const u32 *slots, QEnt *pq) {
+    typedef LitTraits<MODE> T;
+    constexpr int EW = T::EW;
+    constexpr int CW = T::CW;
     const u32 lane = lane_id();
     u32 rr = 0; /* round-robin start */
     u32 consumed = 0;
+    u32 pq_head = 0, pq_tail = 0; /* private queue cursors (wave-uniform) */
+    auto confirm_batch = [&](u32 k) {
+        asm volatile("" ::: "memory");
+        if (lane < k) {
+            const QEnt q = pq[(pq_tail + lane) & (PQ_CAP - 1)];
+            confirm_one(P, cl, q.meta, q.key, mis);
+        }
+        asm volatile("" ::: "memory");
+        pq_tail += k;
+        consumed += k;
+    };
     for (;;) {
         const bool all_done = lds_ld32(q_done) == LIT_SCANNERS;
         asm volatile("" ::: "memory");
         u32 filled = 0;
-        u64 meta = 0, key = 0;
-        bool mine = false;
+        u32 e[4 * EW];
+#pragma unroll
+        for (int i = 0; i < 4 * EW; i++) e[i] = 0;
         for (u32 i = 0; i < LIT_SCANNERS && filled < (u32)WAVE; i++) {
             u32 w = rr + i;
             if (w >= LIT_SCANNERS) w -= LIT_SCANNERS;
@@ -622,33 +726,111 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
             const u32 avail = h - t;
             if (!avail) continue;
             const u32 take = min(avail, (u32)WAVE - filled);
-            if (lane >= filled && lane < filled + take) {
-                const QEnt e = rings[(size_t)w * rsize + ((t + lane - filled) & (rsize - 1))];
-                meta = e.meta;
-                key = e.key;
-                mine = true;
+            if (lane - filled < take) {
+                const uint4 *q =
+                    rings + ((size_t)w * rsize + ((t + lane - filled) & (rsize - 1))) * EW;
+#pragma unroll
+                for (int k = 0; k < EW; k++) {
+                    const uint4 v = q[k];
+                    e[4 * k] = v.x;
+                    e[4 * k + 1] = v.y;
+                    e[4 * k + 2] = v.z;
+                    e[4 * k + 3] = v.w;
+                }
             }
             filled += take;
             asm volatile("" ::: "memory");
             if (lane == 0) lds_st32(&tails[w], t + take);
         }
         rr = rr + 1 == LIT_SCANNERS ? 0 : rr + 1;
-        consumed += filled;
         if (filled == 0) {
+            if (pq_head != pq_tail) {
+                confirm_batch(pq_head - pq_tail); /* < 64 queued */
+                continue;
+            }
             if (all_done) break;
             __builtin_amdgcn_s_sleep(4);
             continue;
         }
-        if (mine) {
-            if constexpr (MODE == VSA_MODE_NOOD) {
-                /* noodle hits are final: emit (end, id) */
-                const unsigned long long slot = atomicAdd(&P.counters[0], 1ULL);
-                if (slot < P.out_cap) {
-                    P.out_keys[slot] = ((meta >> 24) - mis) << VSA_KEY_END_SHIFT;
-                    P.out_ids[slot] = P.nood_id;
+        const u64 meta0 = ((u64)e[1] << 32) | e[0];
+        const u64 p0 = meta0 & ((1ULL << ENT_BLK_SHIFT) - 1);
+        const u32 blk = (u32)(meta0 >> ENT_BLK_SHIFT);
+        if constexpr (MODE == VSA_MODE_NOOD) {
+            /* noodle hits are final: emit (end, id) */
+            u32 hits = e[2];
+            if (hits) {
+                const u32 n = (u32)__popc(hits);
+                unsigned long long slot = atomicAdd(&P.counters[0], (unsigned long long)n);
+                consumed += n;
+                for (; hits; hits &= hits - 1, slot++) {
+                    const u32 j = __ffs(hits) - 1;
+                    if (slot < P.out_cap) {
+                        P.out_keys[slot] = (p0 + j - mis) << VSA_KEY_END_SHIFT;
+                        P.out_ids[slot] = P.nood_id;
+                    }
                 }
-            } else {
-                confirm_one(P, cl, meta, key, mis);
+            }
+            continue;
+        } else {
+            u32 c[CW];
+#pragma unroll
+            for (int i = 0; i < CW; i++) c[i] = e[2 + i];
+            const u64 W0 = ((u64)e[3 + CW] << 32) | e[2 + CW];
+            const u64 W1 = ((u64)e[5 + CW] << 32) | e[4 + CW];
+            const u64 W2 = ((u64)e[7 + CW] << 32) | e[6 + CW];
+            /* Wave-uniform loop: each round every lane takes its lowest
+             * remaining candidate bit (over all conf words). */
+            for (;;) {
+                u32 word = 0, bits = c[0];
+#pragma unroll
+                for (int k = 1; k < CW; k++) {
+                    const bool take = bits == 0;
+                    bits = take ? c[k] : bits;
+                    word = take ? (u32)k : word;
+                }
+                const bool have = bits != 0;
+                if (!__any(have)) break;
+                bool push = false;
+                u64 key = 0, meta = 0;
+                if (have) {
+                    const u32 bit = __ffs(bits) - 1;
+#pragma unroll
+                    for (int k = 0; k < CW; k++)
+                        if (word == (u32)k) c[k] &= c[k] - 1;
+                    u32 j, b;
+                    if constexpr (T::LB == 8) {
+                        j = 4 * word + (bit >> 3);
+                        b = bit & 7;
+                    } else {
+                        j = 2 * word + (bit >> 4);
+                        b = bit & 15;
+                    }
+                    /* key = bytes [j-7, j] = byte offset j+1 .. j+8 of W0:W1:W2 */
+                    const u32 o = j + 1;
+                    if (o < 8) key = (W0 >> (8 * o)) | (W1 << (64 - 8 * o));
+                    else if (o == 8) key = W1;
+                    else if (o < 16) key = (W1 >> (8 * (o - 8))) | (W2 << (64 - 8 * (o - 8)));
+                    else key = W2;
+                    /* LDS slot-bitmap prefilter: litIndex[hash] == 0 rejects */
+                    const PfRec pf = cl.pf[b];
+                    push = true;
+                    if (pf.slot_off != 0xffffffffu) {
+                        const u32 h = (u32)(((key & pf.andmsk) * P.pf_mult) >> pf.shift);
+                        push = (slots[pf.slot_off + (h >> 5)] >> (h & 31)) & 1u;
+                    }
+                    if (P.dbg & 16) push = false;
+                    meta = ((p0 + j) << 24) | ((u64)blk << 4) | b;
+                }
+                const u64 pm = __ballot(push);
+                if (push) {
+                    const u32 r = __builtin_amdgcn_mbcnt_hi(
+                        (u32)(pm >> 32), __builtin_amdgcn_mbcnt_lo((u32)pm, 0));
+                    QEnt *q = &pq[(pq_head + r) & (PQ_CAP - 1)];
+                    q->meta = meta;
+                    q->key = key;
+                }
+                pq_head += (u32)__popcll(pm);
+                if (pq_head - pq_tail >= (u32)WAVE) confirm_batch(WAVE);
             }
         }
     }
@@ -665,6 +847,7 @@ vsa_lit_scan(VsaLitParams P) {
     extern __shared__ __align__(16) u8 smem[];
     __shared__ ConfLds cl;
     __shared__ u32 q_heads[LIT_WAVES], q_tails[LIT_WAVES], q_done;
+    __shared__ QEnt pq[PQ_CAP]; /* the confirm wave's private queue */
     const u32 tid = threadIdx.x;
     const u32 lane = lane_id();
     const u32 wave = tid / WAVE;
@@ -696,8 +879,8 @@ vsa_lit_scan(VsaLitParams P) {
         for (u32 i = tid; i < 256 * 32; i += LIT_THREADS) dst[i] = P.table[i >> 5];
         tab = smem;
     }
-    QEnt *rings = (QEnt *)(smem + ((tab_bytes + 15) & ~15u));
-    u32 *slots = (u32 *)(rings + (size_t)LIT_SCANNERS * P.qcap);
+    uint4 *rings = (uint4 *)(smem + ((tab_bytes + 15) & ~15u));
+    u32 *slots = (u32 *)(rings + (size_t)LIT_SCANNERS * P.qcap * T::EW);
     for (u32 i = tid; i < P.slot_words; i += LIT_THREADS) slots[i] = P.slotmap[i];
     if (tid < 16) {
         const u32 off = P.conf_off[tid];
@@ -730,7 +913,7 @@ vsa_lit_scan(VsaLitParams P) {
 
     const u32 mis = (u32)((uintptr_t)P.data & 15);
     if (wave == LIT_WAVES - 1) {
-        confirm_wave<MODE>(P, cl, rings, P.qcap, q_heads, q_tails, &q_done, mis);
+        confirm_wave<MODE>(P, cl, rings, P.qcap, q_heads, q_tails, &q_done, mis, slots, pq);
         return;
     }
 
@@ -749,10 +932,9 @@ vsa_lit_scan(VsaLitParams P) {
     }
     LitShared L;
     L.tab = tab;
-    L.ring = rings + (size_t)wave * P.qcap;
+    L.ring = rings + (size_t)wave * P.qcap * T::EW;
     L.head_pub = &q_heads[wave];
     L.tail = &q_tails[wave];
-    L.slots = slots;
     L.rmask = P.qcap - 1;
 
     const u8 *A = P.data - mis;
@@ -836,20 +1018,6 @@ vsa_lit_scan(VsaLitParams P) {
         const int64_t fb = s_lo + 1024 * (int64_t)f0;
         uint4 ring[LIT_DEPTH];
         u32 after = 0;
-        /* issue the sweep's first loads before the prologue's dependent
-         * byte loads, so one memory latency covers both */
-#ifndef LIT_EARLY
-#define LIT_EARLY 0
-#endif
-        const bool early = LIT_EARLY && (f0 == 0) && (nf > 0);
-        if (early) {
-#pragma unroll
-            for (int k = 0; k < LIT_DEPTH; k++) {
-                const int64_t pk = ((u32)k < nf ? fb + 1024 * k : fb) + 16 * (int64_t)lane;
-                ring[k] = load_chunk_nc(A, pk);
-            }
-            after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.vlo, S.bhi);
-        }
         /* prologue 1: table spill from positions s_lo-NL+1 .. s_lo-1 */
         IterState is;
         is.ncand = ncand_total;
@@ -907,14 +1075,12 @@ vsa_lit_scan(VsaLitParams P) {
              * (the next chunk's first byte).  Every load is unconditional (an
              * out-of-range prefetch re-reads the current chunk) so the wait
              * counters stay exact. */
-            if (!early) {
+            /* segment base in SGPRs, 32-bit offsets (segments <= 64 KiB) */
+            const u8 *sb = uniform_ptr(A + fb);
 #pragma unroll
-                for (int k = 0; k < LIT_DEPTH; k++) {
-                    const int64_t pk = ((u32)k < nf ? fb + 1024 * k : fb) + 16 * (int64_t)lane;
-                    ring[k] = load_chunk_nc(A, pk);
-                }
-                after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.vlo, S.bhi);
-            }
+            for (int k = 0; k < LIT_DEPTH; k++)
+                ring[k] = load_wave_kib(sb, (u32)k < nf ? 1024u * k : 0u);
+            after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.vlo, S.bhi);
             const u32 ng = nf / LIT_DEPTH;
             for (u32 g = 0; g < ng; g++) {
 #pragma unroll
@@ -925,8 +1091,8 @@ vsa_lit_scan(VsaLitParams P) {
                     const u32 nxt0 = (it + 1 < nf) ? nb : after;
                     is = scan_iter<MODE, LDS_TABLE, false>(P, cl, L, S, mis, ib, ring[k], nxt0,
                                                           is, bucket_mask);
-                    const int64_t pn = (it + LIT_DEPTH < nf) ? ib + 1024 * LIT_DEPTH : ib;
-                    ring[k] = load_chunk_nc(A, pn + 16 * (int64_t)lane);
+                    const u32 itn = (it + LIT_DEPTH < nf) ? it + LIT_DEPTH : it;
+                    ring[k] = load_wave_kib(sb, 1024u * itn);
                 }
             }
             const u32 rem = nf - ng * LIT_DEPTH;

@@ -55,7 +55,8 @@ namespace {
 
 const int LIT_WAVES = 16;
 const int LIT_THREADS = 1024;
-const size_t LDS_BUDGET = 160 * 1024 - 2048; /* minus static LDS */
+const size_t LDS_BUDGET = 160 * 1024 - 4096; /* minus static LDS (confirm params,
+                                                ring cursors, 2 KiB confirm queue) */
 const uint32_t SLOT_WORDS_MAX = 4096;        /* 16 KiB of slot bitmaps */
 
 /* d_counters layout (u64): [0..7] scan counters, [16 + 16 r] region
@@ -223,17 +224,17 @@ int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds) {
     return VSA_OK;
 }
 
-/* LDS plan: table + per-wave queues (QEnt 16 B) + slot bitmaps */
-/* dynamic LDS = table + one confirm ring per scanning wave (power of two,
- * 64..1024 entries of 16 B) + slot bitmaps */
-size_t plan_lds(size_t tab, uint32_t slot_words, uint32_t *qcap) {
+/* dynamic LDS = table + one candidate ring per scanning wave (power of two,
+ * 16..1024 chunk entries of ent bytes: 48 FDR / Teddy, 64 Fat Teddy, 16
+ * noodle; pushes larger than the ring go in batches) + slot bitmaps */
+size_t plan_lds(size_t tab, uint32_t slot_words, size_t ent, uint32_t *qcap) {
     const size_t scanners = LIT_WAVES - 1;
     tab = (tab + 15) & ~(size_t)15;
     size_t rest = LDS_BUDGET > tab + slot_words * 4 ? LDS_BUDGET - tab - slot_words * 4 : 0;
-    uint32_t q = 64;
-    while (q < 1024 && (size_t)(2 * q) * 16 * scanners <= rest) q *= 2;
+    uint32_t q = 16;
+    while (q < 1024 && (size_t)(2 * q) * ent * scanners <= rest) q *= 2;
     *qcap = q;
-    return tab + (size_t)q * 16 * scanners + (size_t)slot_words * 4;
+    return tab + (size_t)q * ent * scanners + (size_t)slot_words * 4;
 }
 
 int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
@@ -277,7 +278,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
             P.dbg = e ? (uint32_t)atoi(e) : 0u;
         }
         for (int b = 0; b < 16; b++) P.slot_off[b] = 0xffffffffu;
-        size_t lds = plan_lds(0, 0, &P.qcap);
+        size_t lds = plan_lds(0, 0, 16, &P.qcap);
         return launch_lit<VSA_MODE_NOOD, false>(c, P, lds);
     }
     VsaLitParams P;
@@ -314,17 +315,17 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     if (db->mode == VSA_MODE_FDR) {
         size_t tb = (size_t)db->table_entries * 8;
         if (tb <= 128 * 1024) {
-            size_t lds = plan_lds(tb, db->slot_words, &P.qcap);
+            size_t lds = plan_lds(tb, db->slot_words, 48, &P.qcap);
             if (lds <= LDS_BUDGET) return launch_lit<VSA_MODE_FDR, true>(c, P, lds);
         }
-        size_t lds = plan_lds(0, db->slot_words, &P.qcap);
+        size_t lds = plan_lds(0, db->slot_words, 48, &P.qcap);
         return launch_lit<VSA_MODE_FDR, false>(c, P, lds);
     }
     if (db->mode == VSA_MODE_TEDDY) {
-        size_t lds = plan_lds(256 * 32 * 4, db->slot_words, &P.qcap);
+        size_t lds = plan_lds(256 * 32 * 4, db->slot_words, 48, &P.qcap);
         return launch_lit<VSA_MODE_TEDDY, true>(c, P, lds);
     }
-    size_t lds = plan_lds(256 * 32 * 8, db->slot_words, &P.qcap);
+    size_t lds = plan_lds(256 * 32 * 8, db->slot_words, 64, &P.qcap);
     return launch_lit<VSA_MODE_FAT, true>(c, P, lds);
 }
 
@@ -955,7 +956,7 @@ int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
         uint32_t qc = 0;
         uint32_t bits = 14;
         if (getenv("VSA_FDR_DOMAIN")) bits = (uint32_t)std::min(15, std::max(9, atoi(getenv("VSA_FDR_DOMAIN"))));
-        else if (plan_lds((size_t)8 << 14, db->slot_words, &qc) > LDS_BUDGET) bits = 13;
+        else if (plan_lds((size_t)8 << 14, db->slot_words, 48, &qc) > LDS_BUDGET) bits = 13;
         std::vector<uint64_t> T;
         derive_fdr_table(eng, db->conf_off, bits, T);
         db->table_entries = 1u << bits;
