@@ -24,7 +24,7 @@ $(LIB): $(CSRC)/compile.o $(CSRC)/kernels.o $(CSRC)/runtime.o
 
 $(ORACLE): oracle/oracle.c
 	mkdir -p oracle/_build
-	gcc -O2 -std=gnu11 -fPIC -shared -Wall $< -o $@
+	gcc -O2 -std=gnu11 -fPIC -shared -Wall -pthread $< -o $@
 
 clean:
 	rm -f $(CSRC)/*.o $(LIB) $(ORACLE)

@@ -193,6 +193,12 @@ int vsa_scan_copy_device(vsa_ctx_t *ctx, uint64_t *d_keys, uint32_t *d_ids, uint
 /* Candidates handed to the confirm stage (after the LDS slot prefilter) in
  * the last scan. */
 uint64_t vsa_scan_candidates(vsa_ctx_t *ctx);
+/* Diagnostics of the last literal scan (device counters 0..15): [0]
+ * matches, [2] confirm candidates; with VSA_DEBUG_FLAGS bit 6 the confirm
+ * waves' cycles: [4] gathering, [5] expanding, [6] confirming, [7] idle,
+ * and counts: [8] gather rounds, [9] chunk entries, [10] expansion rounds,
+ * [11] confirm batches. */
+int vsa_scan_debug_counters(vsa_ctx_t *ctx, uint64_t out[16]);
 /* Device time (ms, hipEvents on the scan stream) of the last scan kernel. */
 double vsa_scan_kernel_ms(vsa_ctx_t *ctx);
 

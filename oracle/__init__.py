@@ -18,7 +18,7 @@ LIB = os.path.join(HERE, "_build", "liboracle.so")
 
 def build():
     os.makedirs(os.path.join(HERE, "_build"), exist_ok=True)
-    subprocess.check_call(["gcc", "-O2", "-std=gnu11", "-fPIC", "-shared", "-Wall",
+    subprocess.check_call(["gcc", "-O2", "-std=gnu11", "-fPIC", "-shared", "-Wall", "-pthread",
                            os.path.join(HERE, "oracle.c"), "-o", LIB])
 
 
@@ -234,3 +234,17 @@ def brute_force(lits, data, start=0):
             if end >= start:
                 out.add((end, lit.id))
     return out
+
+
+_sig("orc_fdr_count_mt", ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+     ctypes.c_int)
+
+
+def fdr_count_mt(engine_ptr, data, nthreads):
+    """match count of the scalar fdrExec restatement over `nthreads` stripes
+    (timing harness for bench.py's cpu_baseline; see oracle.c)"""
+    buf = np.ascontiguousarray(data, dtype=np.uint8)
+    n = _lib.orc_fdr_count_mt(engine_ptr, buf.ctypes.data, len(buf), int(nthreads))
+    if n < 0:
+        raise RuntimeError("orc_fdr_count_mt failed")
+    return n

@@ -724,3 +724,47 @@ u64a orc_fdr_candidates(const void *eng, const u8 *buf, size_t len) {
     }
     return count;
 }
+
+/* ---- multi-threaded timing harness (bench.py cpu_baseline only) ------- *
+ * The scalar fdrExec restatement over nthreads contiguous stripes of one
+ * buffer, each stripe an independent block scan of [lo - 7, hi) with start
+ * = lo - (lo - 7): literals are at most 8 bytes (hwlm.h:75), so every end in
+ * [lo, hi) sees the same bytes and the stripes' match counts sum to the
+ * single-call count.  Counts only (cap 0). */
+#include <pthread.h>
+
+typedef struct {
+    const void *eng;
+    const u8 *buf;
+    size_t len, start;
+    long n;
+    int status;
+} orc_mt_job;
+
+static void *orc_mt_run(void *p) {
+    orc_mt_job *j = (orc_mt_job *)p;
+    j->n = orc_fdr_exec(j->eng, j->buf, j->len, j->start, ~0ULL, NULL, 0, -1, ~0ULL,
+                        &j->status);
+    return NULL;
+}
+
+long orc_fdr_count_mt(const void *eng, const u8 *buf, size_t len, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    orc_mt_job jobs[256];
+    pthread_t th[256];
+    const size_t s = len / (size_t)nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        const size_t lo = (size_t)t * s, hi = t == nthreads - 1 ? len : lo + s;
+        const size_t blo = lo >= 7 ? lo - 7 : 0;
+        jobs[t] = (orc_mt_job){eng, buf + blo, hi - blo, lo - blo, 0, 0};
+        if (pthread_create(&th[t], NULL, orc_mt_run, &jobs[t]) != 0) return -1;
+    }
+    long n = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        if (jobs[t].status != 0) n = -1;
+        if (n >= 0) n += jobs[t].n;
+    }
+    return n;
+}

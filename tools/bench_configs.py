@@ -76,6 +76,7 @@ def cfg_literal(ctx, torch, name, lits, n, plant_every, seed, steps, warmup, sam
         nm[0] = ctx.scan_blocks(db, dptr, [0], [n])
 
     kms, wall = timed(step, steps, warmup, ctx)
+    ncand = int(ctx.candidates())
     host = data[:sample].cpu().numpy()
     k = ctx.scan_blocks(db, dptr, [0], [sample])
     res = ctx.results(k)
@@ -85,7 +86,8 @@ def cfg_literal(ctx, torch, name, lits, n, plant_every, seed, steps, warmup, sam
     else:
         _, want = oracle.fdr_exec(vsa.engine_blob(blob), host, cap=1 << 22)
     line(name, n, kms, wall, 16 * nm[0], got == want,
-         {"engine_id": blob.engine_id, "matches": nm[0], "sample_bytes": sample})
+         {"engine_id": blob.engine_id, "matches": nm[0], "confirm_candidates": ncand,
+          "sample_bytes": sample})
     db.close()
     del data
 

@@ -145,6 +145,7 @@ _sig("vsa_scan_copy", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
 _sig("vsa_scan_copy_device", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_uint64, _u64p)
 _sig("vsa_scan_candidates", ctypes.c_uint64, ctypes.c_void_p)
+_sig("vsa_scan_debug_counters", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)
 _sig("vsa_scan_kernel_ms", ctypes.c_double, ctypes.c_void_p)
 _sig("vsa_class_scan", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, _u64p,
@@ -594,6 +595,12 @@ class Context:
 
     def candidates(self):
         return lib.vsa_scan_candidates(self.ptr)
+
+    def debug_counters(self):
+        """device counters 0..15 of the last scan (see vsa_scan_debug_counters)"""
+        out = (ctypes.c_uint64 * 16)()
+        _check(lib.vsa_scan_debug_counters(self.ptr, out))
+        return list(out)
 
     def kernel_ms(self):
         """Device time of the last scan kernel (hipEvents on the scan stream)."""

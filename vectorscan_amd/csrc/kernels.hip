@@ -84,6 +84,27 @@ __device__ __forceinline__ u32 writelane_u32(u32 v, u32 s) {
     asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(readfirstlane_u32(s)), "n"(L));
     return v;
 }
+/* LDS byte address of an 8-byte table entry: base + 8 * (16-bit half H of
+ * w) in one op (v_mad_u32_u16 with op_sel picks the half, no bfe/shift) */
+template <int H>
+__device__ __forceinline__ u32 tab_addr16(u32 w, u32 base) {
+    u32 r;
+    if constexpr (H == 0)
+        asm("v_mad_u32_u16 %0, %1, 8, %2" : "=v"(r) : "v"(w), "s"(base));
+    else
+        asm("v_mad_u32_u16 %0, %1, 8, %2 op_sel:[1,0,0,0]" : "=v"(r) : "v"(w), "s"(base));
+    return r;
+}
+typedef const __attribute__((address_space(3))) u64 lds_u64_t;
+typedef const __attribute__((address_space(3))) u8 lds_u8_t;
+__device__ __forceinline__ u64 lds_ld64(u32 addr) { return *(lds_u64_t *)(uintptr_t)addr; }
+
+/* Teddy tables live at this LDS byte address (64 KiB; rings and slot
+ * bitmaps below it) */
+#define TEDDY_TAB_LDS 0x10000u
+typedef const __attribute__((address_space(3))) u32 lds_u32_t;
+__device__ __forceinline__ u32 lds_ld32c(u32 addr) { return *(lds_u32_t *)(uintptr_t)addr; }
+
 /* three-input OR in one VALU op (the backend re-associates wide OR trees
  * into two-input ORs) */
 __device__ __forceinline__ u32 or3(u32 a, u32 b, u32 c) {
@@ -130,21 +151,25 @@ struct LitTraits<VSA_MODE_FDR> {
     static constexpr bool KEY16 = true;
     typedef u64 S_t;
 };
+/* Teddy: the first stage is an exact per-byte table derived from the
+ * confirm records (runtime.hip derive_teddy_table), 8 positions x 8
+ * buckets; the reference's nibble masks (teddy_compile.cpp:439) admit up to
+ * 36 byte pairs per bucket and position where the literals have 6 */
 template <>
 struct LitTraits<VSA_MODE_TEDDY> {
     static constexpr int LB = 8;
-    static constexpr int NL = 4;
+    static constexpr int NL = 8;
     static constexpr int CW = 4;
     static constexpr int EW = 3;
     static constexpr bool KEY16 = false;
-    typedef u32 S_t;
+    typedef u64 S_t;
 };
 template <>
 struct LitTraits<VSA_MODE_NOOD> {
     static constexpr int LB = 8;
     static constexpr int NL = 1; /* no look-back state */
     static constexpr int CW = 1;
-    static constexpr int EW = 1;
+    static constexpr int EW = 2; /* {meta}, {hits} */
     static constexpr bool KEY16 = false;
     typedef u32 S_t;
 };
@@ -181,25 +206,32 @@ struct QEnt {
     u64 key;
 };
 
-/* Candidates go from each scanning wave to the workgroup's confirm wave
- * through the scanning wave's own LDS ring of rsize (power of two) chunk
- * entries: one entry per lane whose 16 ends hold any first-stage candidate,
- * carrying the lane's candidate masks and the 24 bytes its confirm keys are
- * cut from, so the scanning wave never loops over candidate bits (a wave
- * looping for one lane's rare candidate wasted the other 63 lanes; the
- * confirm wave expands the entries 64 at a time).  Entry layout, EW uint4
- * words: {p0 | blk << 44 (u64), c[0..CW), pv2, pv3, d0..d3} (noodle: {meta,
- * hits, 0}).  The scanner owns *head (entries written, published after the
- * entries), the confirm wave owns *tail (entries consumed).  LDS executes
- * one wave's instructions in order, so a published head implies visible
- * entries. */
-#define ENT_BLK_SHIFT 44
+/* Candidates go from the scanning waves to the workgroup's confirm wave
+ * through one shared LDS ring of 2^lg chunk entries: one entry per lane
+ * whose 16 ends hold any first-stage candidate, carrying the lane's
+ * candidate masks and the 24 bytes its confirm keys are cut from, so the
+ * scanning wave never loops over candidate bits (a wave looping for one
+ * lane's rare candidate wasted the other 63 lanes; the confirm wave expands
+ * the entries 64 at a time).  Entry layout, EW uint4 words: {meta, c[0..CW),
+ * pv2, pv3, d0..d3} (noodle: {meta}, {hits}), meta = p0 | blk << 40 | lap
+ * << 60.  A scanner reserves slots with one LDS atomic on *head, waits for
+ * room against *tail, writes words 1.. and then word 0; lap = (position >>
+ * lg) & 15 marks word 0 as written for this pass of the ring (LDS executes a
+ * wave's instructions in order, so a visible word 0 implies visible words
+ * 1..).  The confirm wave reads the 64 slots at its tail and takes the
+ * leading run whose lap matches: one LDS round trip per gather. */
+#define ENT_BLK_SHIFT 40
+#define ENT_LAP_SHIFT 60
+#define ENT_P0_MASK ((1ULL << ENT_BLK_SHIFT) - 1)
 struct LitShared {
     const void *tab;
-    uint4 *ring;     /* this wave's ring */
-    u32 *head_pub;   /* this wave's published head */
-    const u32 *tail; /* this wave's tail (written by the confirm wave) */
-    u32 rmask;
+    u32 tab_lds;     /* LDS byte address of tab (LDS tables) */
+    u32 kmask2;      /* FDR key mask in both 16-bit halves */
+    u32 tsel;        /* Teddy: TEDDY_TAB_LDS | this lane's copy offset */
+    uint4 *ring;     /* the shared ring */
+    u32 *head;       /* positions reserved (LDS atomic) */
+    const u32 *tail; /* positions consumed (written by the confirm wave) */
+    u32 lg;          /* log2 ring entries (>= 6) */
 };
 
 __device__ __forceinline__ u32 lds_ld32(const u32 *p) {
@@ -271,8 +303,6 @@ __device__ __forceinline__ u64 lit_lookup(const void *tab, u32 key, u32 lane) {
     if constexpr (MODE == VSA_MODE_FDR) {
         (void)lane;
         return ((const u64 *)tab)[key];
-    } else if constexpr (MODE == VSA_MODE_TEDDY) {
-        return ((const u32 *)tab)[(key << 5) | (lane & 31)];
     } else {
         return ((const u64 *)tab)[(key << 5) | (lane & 31)];
     }
@@ -320,26 +350,29 @@ __device__ __forceinline__ void ring_push(const LitShared &L, ST &st, bool push,
     const u32 n = (u32)__popcll(pm);
     const u32 r = __builtin_amdgcn_mbcnt_hi((u32)(pm >> 32),
                                              __builtin_amdgcn_mbcnt_lo((u32)pm, 0));
-    const u32 cap = L.rmask + 1;
-    for (u32 base = 0; base < n; base += cap) {
-        const u32 m = min(n - base, cap);
-        /* room for m entries (the confirm wave frees them in order) */
-        if (st.head + m - st.tail_cache > cap) {
-            for (;;) {
-                st.tail_cache = readfirstlane_u32(lds_ld32(L.tail));
-                if (st.head + m - st.tail_cache <= cap) break;
-                __builtin_amdgcn_s_sleep(2);
-            }
+    /* one reservation (n <= 64 <= ring size): the earliest unwritten
+     * reservation always fits, so waiting for room cannot deadlock */
+    u32 pos = 0;
+    if (lane_id() == 0)
+        pos = __hip_atomic_fetch_add(L.head, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    pos = readfirstlane_u32(pos);
+    const u32 cap = 1u << L.lg;
+    if (pos + n - st.tail_cache > cap) {
+        for (;;) {
+            st.tail_cache = readfirstlane_u32(lds_ld32(L.tail));
+            if (pos + n - st.tail_cache <= cap) break;
+            __builtin_amdgcn_s_sleep(2);
         }
-        if (push && r - base < m) {
-            uint4 *q = L.ring + (size_t)((st.head + r - base) & L.rmask) * EW;
+    }
+    if (push) {
+        const u32 slot = pos + r;
+        uint4 *q = L.ring + (size_t)(slot & (cap - 1)) * EW;
 #pragma unroll
-            for (int k = 0; k < EW; k++)
-                q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
-        }
-        st.head += m;
-        asm volatile("" ::: "memory"); /* entries before the head (LDS order) */
-        if (lane_id() == 0) lds_st32(L.head_pub, st.head);
+        for (int k = 1; k < EW; k++)
+            q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+        asm volatile("" ::: "memory"); /* word 0 (with the lap) last */
+        const u32 lap = (slot >> L.lg) & 15u;
+        q[0] = make_uint4(w[0], w[1] | (lap << (ENT_LAP_SHIFT - 32)), w[2], w[3]);
     }
 }
 
@@ -454,10 +487,31 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
 
     /* own contributions: the lane's 16 lookups ... */
     S_t x[16];
+    u32 km[4], ko[4]; /* FDR/LDS: keys of even / odd positions, two per dword */
+    if constexpr (MODE == VSA_MODE_FDR && LDS_TABLE) {
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            km[w] = d[w] & L.kmask2;
+            ko[w] = __builtin_amdgcn_alignbyte(d[w + 1], d[w], 1) & L.kmask2;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < 16; j++) {
-        u32 key = lit_key<MODE>(d, j, P.dmask);
-        x[j] = (S_t)lit_lookup<MODE, LDS_TABLE>(L.tab, key, lane);
+        if constexpr (MODE == VSA_MODE_FDR && LDS_TABLE) {
+            /* position 4w + r: key = 16-bit half r >> 1 of km[w] (r even)
+             * or ko[w] (r odd) */
+            const u32 kw = (j & 1) ? ko[j >> 2] : km[j >> 2];
+            const u32 a = (j & 2) ? tab_addr16<1>(kw, L.tab_lds) : tab_addr16<0>(kw, L.tab_lds);
+            x[j] = lds_ld64(a);
+        } else if constexpr (MODE == VSA_MODE_TEDDY || MODE == VSA_MODE_FAT) {
+            /* byte r of d[w] -> address byte 1, L.tsel = 0x10000 | lane slot */
+            const u32 sel = 0x0c020000u | ((4u + (j & 3)) << 8);
+            const u32 a = __builtin_amdgcn_perm(d[j >> 2], L.tsel, sel);
+            x[j] = lds_ld64(a);
+        } else {
+            u32 key = lit_key<MODE>(d, j, P.dmask);
+            x[j] = (S_t)lit_lookup<MODE, LDS_TABLE>(L.tab, key, lane);
+        }
         if (EDGE) {
             int64_t q = q0 + j;
             bool valid;
@@ -469,6 +523,11 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
             if (!valid) x[j] = 0;
         }
     }
+#ifdef VSA_EXTRA_VALU
+    /* experiment build: VSA_EXTRA_VALU dependent VALU ops per iteration */
+#pragma unroll
+    for (int i = 0; i < VSA_EXTRA_VALU; i++) asm volatile("v_or_b32 %0, %0, %0" : "+v"(d[i & 3]));
+#endif
     /* ... OR-ed into place: field k of x[j] lands on end j + k */
     u32 c[T::CW];
     u64 s_out;
@@ -546,6 +605,8 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     /* one chunk entry per lane with candidates; the confirm wave expands it */
     const u64 meta = (u64)p0 | ((u64)S.blk << ENT_BLK_SHIFT);
     u32 w[4 * T::EW];
+#pragma unroll
+    for (int i = 0; i < 4 * T::EW; i++) w[i] = 0;
     w[0] = (u32)meta;
     w[1] = (u32)(meta >> 32);
 #pragma unroll
@@ -621,8 +682,8 @@ __device__ __forceinline__ IterState nood_iter(const VsaLitParams &P, const LitS
     }
     if (!__any(hits != 0)) return out;
     const u64 meta = (u64)p0 | ((u64)S.blk << ENT_BLK_SHIFT);
-    const u32 ent[4] = {(u32)meta, (u32)(meta >> 32), hits, 0};
-    ring_push<1>(L, out, hits != 0, ent);
+    const u32 ent[8] = {(u32)meta, (u32)(meta >> 32), 0, 0, hits, 0, 0, 0};
+    ring_push<2>(L, out, hits != 0, ent);
     return out;
 }
 
@@ -690,17 +751,31 @@ __device__ __forceinline__ uint4 load_wave_kib(const u8 *base, u32 off) {
 #define PQ_CAP 128
 template <int MODE>
 __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLds &cl,
-                                             const uint4 *rings, u32 rsize, const u32 *heads,
-                                             u32 *tails, const u32 *q_done, u32 mis,
-                                             const u32 *slots, QEnt *pq) {
+                                             const uint4 *ring, u32 lg, u32 *tail_p,
+                                             const u32 *q_done, u32 mis, const u32 *slots,
+                                             QEnt *pq) {
     typedef LitTraits<MODE> T;
     constexpr int EW = T::EW;
     constexpr int CW = T::CW;
     const u32 lane = lane_id();
-    u32 rr = 0; /* round-robin start */
+    const u32 cap = 1u << lg;
+    u32 tail = 0; /* ring positions consumed (wave-uniform) */
+    u32 filled = 0;
     u32 consumed = 0;
     u32 pq_head = 0, pq_tail = 0; /* private queue cursors (wave-uniform) */
+    /* VSA_DEBUG_FLAGS bit 6: cycles per phase + counts -> counters[4..11] */
+    const bool prof = (P.dbg & 64) != 0;
+    u64 pc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    u64 tmark = prof ? __builtin_amdgcn_s_memtime() : 0;
+    auto phase = [&](int i) {
+        if (prof) {
+            const u64 now = __builtin_amdgcn_s_memtime();
+            pc[i] += now - tmark;
+            tmark = now;
+        }
+    };
     auto confirm_batch = [&](u32 k) {
+        phase(1);
         asm volatile("" ::: "memory");
         if (lane < k) {
             const QEnt q = pq[(pq_tail + lane) & (PQ_CAP - 1)];
@@ -709,40 +784,48 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
         asm volatile("" ::: "memory");
         pq_tail += k;
         consumed += k;
+        pc[7]++;
+        phase(2);
     };
     for (;;) {
         const bool all_done = lds_ld32(q_done) == LIT_SCANNERS;
         asm volatile("" ::: "memory");
-        u32 filled = 0;
+        /* gather: the 64 slots at the tail, the leading run of written ones */
         u32 e[4 * EW];
+        {
+            const u32 pos = tail + lane;
+            const uint4 *q = ring + (size_t)(pos & (cap - 1)) * EW;
+            const uint4 v0 = q[0];
+            asm volatile("" ::: "memory"); /* word 0 (lap) before words 1.. */
+            e[0] = v0.x;
+            e[1] = v0.y;
+            e[2] = v0.z;
+            e[3] = v0.w;
 #pragma unroll
-        for (int i = 0; i < 4 * EW; i++) e[i] = 0;
-        for (u32 i = 0; i < LIT_SCANNERS && filled < (u32)WAVE; i++) {
-            u32 w = rr + i;
-            if (w >= LIT_SCANNERS) w -= LIT_SCANNERS;
-            const u32 h = readfirstlane_u32(lds_ld32(&heads[w]));
-            const u32 t = readfirstlane_u32(lds_ld32(&tails[w]));
-            asm volatile("" ::: "memory");
-            const u32 avail = h - t;
-            if (!avail) continue;
-            const u32 take = min(avail, (u32)WAVE - filled);
-            if (lane - filled < take) {
-                const uint4 *q =
-                    rings + ((size_t)w * rsize + ((t + lane - filled) & (rsize - 1))) * EW;
-#pragma unroll
-                for (int k = 0; k < EW; k++) {
-                    const uint4 v = q[k];
-                    e[4 * k] = v.x;
-                    e[4 * k + 1] = v.y;
-                    e[4 * k + 2] = v.z;
-                    e[4 * k + 3] = v.w;
-                }
+            for (int k = 1; k < EW; k++) {
+                const uint4 v = q[k];
+                e[4 * k] = v.x;
+                e[4 * k + 1] = v.y;
+                e[4 * k + 2] = v.z;
+                e[4 * k + 3] = v.w;
             }
-            filled += take;
-            asm volatile("" ::: "memory");
-            if (lane == 0) lds_st32(&tails[w], t + take);
+            const bool ready = (e[1] >> (ENT_LAP_SHIFT - 32)) == ((pos >> lg) & 15u);
+            const u64 rb = __ballot(ready);
+            filled = ~rb ? (u32)__builtin_ctzll(~rb) : (u32)WAVE;
+            asm volatile("" ::: "memory"); /* entries read before they are freed */
+            if (filled) {
+                tail += filled;
+                if (lane == 0) lds_st32(tail_p, tail);
+            }
+            if (lane >= filled) {
+#pragma unroll
+                for (int i = 0; i < 4 * EW; i++) e[i] = 0;
+            }
+            e[1] &= (1u << (ENT_LAP_SHIFT - 32)) - 1; /* strip the lap */
         }
-        rr = rr + 1 == LIT_SCANNERS ? 0 : rr + 1;
+        pc[4]++;
+        pc[5] += filled;
+        phase(0);
         if (filled == 0) {
             if (pq_head != pq_tail) {
                 confirm_batch(pq_head - pq_tail); /* < 64 queued */
@@ -750,14 +833,15 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
             }
             if (all_done) break;
             __builtin_amdgcn_s_sleep(4);
+            phase(3);
             continue;
         }
         const u64 meta0 = ((u64)e[1] << 32) | e[0];
-        const u64 p0 = meta0 & ((1ULL << ENT_BLK_SHIFT) - 1);
+        const u64 p0 = meta0 & ENT_P0_MASK;
         const u32 blk = (u32)(meta0 >> ENT_BLK_SHIFT);
         if constexpr (MODE == VSA_MODE_NOOD) {
             /* noodle hits are final: emit (end, id) */
-            u32 hits = e[2];
+            u32 hits = e[4];
             if (hits) {
                 const u32 n = (u32)__popc(hits);
                 unsigned long long slot = atomicAdd(&P.counters[0], (unsigned long long)n);
@@ -790,6 +874,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                 }
                 const bool have = bits != 0;
                 if (!__any(have)) break;
+                pc[6]++;
                 bool push = false;
                 u64 key = 0, meta = 0;
                 if (have) {
@@ -832,11 +917,16 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                 pq_head += (u32)__popcll(pm);
                 if (pq_head - pq_tail >= (u32)WAVE) confirm_batch(WAVE);
             }
+            phase(1);
         }
     }
     /* confirm-stage candidates (first-stage count instead under dbg & 32) */
     if (P.counters && lane == 0 && consumed && !(P.dbg & 32))
         atomicAdd(&P.counters[2], (unsigned long long)consumed);
+    if (prof && lane == 0) {
+        phase(1);
+        for (int i = 0; i < 8; i++) atomicAdd(&P.counters[4 + i], (unsigned long long)pc[i]);
+    }
 }
 
 template <int MODE, bool LDS_TABLE>
@@ -846,11 +936,13 @@ vsa_lit_scan(VsaLitParams P) {
     typedef typename T::S_t S_t;
     extern __shared__ __align__(16) u8 smem[];
     __shared__ ConfLds cl;
-    __shared__ u32 q_heads[LIT_WAVES], q_tails[LIT_WAVES], q_done;
+    __shared__ u32 q_head, q_tail, q_done;
     __shared__ QEnt pq[PQ_CAP]; /* the confirm wave's private queue */
     const u32 tid = threadIdx.x;
     const u32 lane = lane_id();
-    const u32 wave = tid / WAVE;
+    /* provably wave-uniform: the confirm wave's s_setprio is a scalar
+     * instruction that an EXEC-masked branch would run in every wave */
+    const u32 wave = readfirstlane_u32(tid / WAVE);
 
     /* ---- stage tables into LDS ---- */
     u32 tab_bytes = 0;
@@ -865,22 +957,20 @@ vsa_lit_scan(VsaLitParams P) {
         } else {
             tab = P.table;
         }
-    } else if constexpr (MODE == VSA_MODE_TEDDY) {
-        /* byte-combined masks, replicated 32x: lane group of 32 hits 32 banks */
-        tab_bytes = 256 * 32 * 4;
-        u32 *dst = (u32 *)smem;
-        for (u32 i = tid; i < 256 * 32; i += LIT_THREADS) dst[i] = (u32)P.table[i >> 5];
-        tab = smem;
     } else if constexpr (MODE == VSA_MODE_NOOD) {
         tab = nullptr;
     } else {
-        tab_bytes = 256 * 32 * 8;
-        u64 *dst = (u64 *)smem;
+        /* Teddy / Fat Teddy: the byte table (u64 entries) at LDS 0x10000,
+         * one copy per lane & 31, so a lane group's lookups hit distinct
+         * bank pairs and the address of byte c is 0x10000 | c << 8 |
+         * (lane & 31) << 3: one v_perm (TEDDY_TAB_LDS) */
+        u8 *tb = smem + (TEDDY_TAB_LDS - (u32)(uintptr_t)(lds_u8_t *)smem);
+        u64 *dst = (u64 *)tb;
         for (u32 i = tid; i < 256 * 32; i += LIT_THREADS) dst[i] = P.table[i >> 5];
-        tab = smem;
+        tab = tb;
     }
     uint4 *rings = (uint4 *)(smem + ((tab_bytes + 15) & ~15u));
-    u32 *slots = (u32 *)(rings + (size_t)LIT_SCANNERS * P.qcap * T::EW);
+    u32 *slots = (u32 *)(rings + (size_t)P.qcap * T::EW);
     for (u32 i = tid; i < P.slot_words; i += LIT_THREADS) slots[i] = P.slotmap[i];
     if (tid < 16) {
         const u32 off = P.conf_off[tid];
@@ -904,16 +994,20 @@ vsa_lit_scan(VsaLitParams P) {
         }
         cl.pf[tid] = pf;
     }
-    if (tid < LIT_WAVES) {
-        q_heads[tid] = 0;
-        q_tails[tid] = 0;
+    if (tid == 0) {
+        q_head = 0;
+        q_tail = 0;
+        q_done = 0;
     }
-    if (tid == 0) q_done = 0;
+    /* every slot starts with lap 15, never the first pass's lap 0 */
+    for (u32 i = tid; i < P.qcap; i += LIT_THREADS)
+        rings[(size_t)i * T::EW] = make_uint4(0, 15u << (ENT_LAP_SHIFT - 32), 0, 0);
     __syncthreads();
 
     const u32 mis = (u32)((uintptr_t)P.data & 15);
     if (wave == LIT_WAVES - 1) {
-        confirm_wave<MODE>(P, cl, rings, P.qcap, q_heads, q_tails, &q_done, mis, slots, pq);
+        __builtin_amdgcn_s_setprio(2); /* issue ahead of the scanners on its SIMD */
+        confirm_wave<MODE>(P, cl, rings, 31 - __clz(P.qcap), &q_tail, &q_done, mis, slots, pq);
         return;
     }
 
@@ -932,10 +1026,13 @@ vsa_lit_scan(VsaLitParams P) {
     }
     LitShared L;
     L.tab = tab;
-    L.ring = rings + (size_t)wave * P.qcap * T::EW;
-    L.head_pub = &q_heads[wave];
-    L.tail = &q_tails[wave];
-    L.rmask = P.qcap - 1;
+    L.tab_lds = (u32)(uintptr_t)(lds_u8_t *)smem;
+    L.kmask2 = (P.dmask & 0xffffu) * 0x10001u;
+    L.tsel = TEDDY_TAB_LDS | ((lane & 31) << 3);
+    L.ring = rings;
+    L.head = &q_head;
+    L.tail = &q_tail;
+    L.lg = 31 - __clz(P.qcap);
 
     const u8 *A = P.data - mis;
     const int64_t SEG = (int64_t)P.seg_bytes;

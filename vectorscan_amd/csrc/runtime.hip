@@ -224,17 +224,17 @@ int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds) {
     return VSA_OK;
 }
 
-/* dynamic LDS = table + one candidate ring per scanning wave (power of two,
- * 16..1024 chunk entries of ent bytes: 48 FDR / Teddy, 64 Fat Teddy, 16
- * noodle; pushes larger than the ring go in batches) + slot bitmaps */
-size_t plan_lds(size_t tab, uint32_t slot_words, size_t ent, uint32_t *qcap) {
-    const size_t scanners = LIT_WAVES - 1;
+/* dynamic LDS = table + the shared candidate ring (power of two, 64..4096
+ * chunk entries of ent bytes: 48 FDR / Teddy, 64 Fat Teddy, 32 noodle; 64
+ * is the most one wave pushes at once) + slot bitmaps */
+size_t plan_lds(size_t tab, uint32_t slot_words, size_t ent, uint32_t *qcap,
+                size_t budget = LDS_BUDGET) {
     tab = (tab + 15) & ~(size_t)15;
-    size_t rest = LDS_BUDGET > tab + slot_words * 4 ? LDS_BUDGET - tab - slot_words * 4 : 0;
-    uint32_t q = 16;
-    while (q < 1024 && (size_t)(2 * q) * ent * scanners <= rest) q *= 2;
+    size_t rest = budget > tab + slot_words * 4 ? budget - tab - slot_words * 4 : 0;
+    uint32_t q = 64;
+    while (q < 4096 && (size_t)(2 * q) * ent <= rest) q *= 2;
     *qcap = q;
-    return tab + (size_t)q * ent * scanners + (size_t)slot_words * 4;
+    return tab + (size_t)q * ent + (size_t)slot_words * 4;
 }
 
 int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
@@ -278,7 +278,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
             P.dbg = e ? (uint32_t)atoi(e) : 0u;
         }
         for (int b = 0; b < 16; b++) P.slot_off[b] = 0xffffffffu;
-        size_t lds = plan_lds(0, 0, 16, &P.qcap);
+        size_t lds = plan_lds(0, 0, 32, &P.qcap);
         return launch_lit<VSA_MODE_NOOD, false>(c, P, lds);
     }
     VsaLitParams P;
@@ -295,6 +295,9 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.table = db->d_table; /* derived FDR table / combined Teddy table */
     P.table_entries = db->table_entries;
     P.dmask = db->dmask;
+    /* experiment only (wrong results): every FDR lookup hits entry 0, a
+     * broadcast, so the run shows the filter without LDS bank conflicts */
+    if (getenv("VSA_EXP_DMASK_ZERO")) P.dmask = 0;
     P.state_lo = db->state_lo;
     P.state_hi = db->state_hi;
     const uint32_t conf_offset_in_eng = ((const uint32_t *)(db->hblob + VSA_ROUNDUP_CL(sizeof(HWLM))))[4];
@@ -321,11 +324,16 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         size_t lds = plan_lds(0, db->slot_words, 48, &P.qcap);
         return launch_lit<VSA_MODE_FDR, false>(c, P, lds);
     }
+    /* Teddy / Fat Teddy: the 64 KiB table sits at LDS 0x10000 (kernels.hip
+     * TEDDY_TAB_LDS), ring + slot bitmaps below it after the static LDS */
+    const size_t below = 0x10000 - (160 * 1024 - LDS_BUDGET);
+    const size_t teddy_dyn = 128 * 1024;
     if (db->mode == VSA_MODE_TEDDY) {
-        size_t lds = plan_lds(256 * 32 * 4, db->slot_words, 48, &P.qcap);
-        return launch_lit<VSA_MODE_TEDDY, true>(c, P, lds);
+        if (plan_lds(0, db->slot_words, 48, &P.qcap, below) > below) return VSA_E_INVALID;
+        return launch_lit<VSA_MODE_TEDDY, true>(c, P, teddy_dyn);
     }
-    size_t lds = plan_lds(256 * 32 * 8, db->slot_words, 64, &P.qcap);
+    if (plan_lds(0, db->slot_words, 64, &P.qcap, below) > below) return VSA_E_INVALID;
+    size_t lds = teddy_dyn;
     return launch_lit<VSA_MODE_FAT, true>(c, P, lds);
 }
 
@@ -878,6 +886,53 @@ static void derive_fdr_table(const uint8_t *eng, const uint32_t conf_off[8], uin
     }
 }
 
+/* Teddy / Fat Teddy first stage, rebuilt at load like FDR's: bit (k * lb +
+ * b) of W[c] is 0 when some literal of bucket b has byte c (under its
+ * mask) k bytes before its end (LitInfo v / msk, fdr_confirm.h:57-65), for
+ * k < nl.  Every literal the confirm accepts passes, so the confirmed set is
+ * the reference's; the reference's nibble masks (teddy_compile.cpp:439-509,
+ * teddy.c:921-971) pass every byte of a bucket's nibble product. */
+static void derive_teddy_table(const uint8_t *eng, const uint32_t *conf_off, uint32_t nb,
+                               uint32_t nl, uint32_t lb, std::vector<uint64_t> &W) {
+    W.assign(256, ~0ULL);
+    uint64_t always = 0;
+    const uint8_t *confBase = eng + ((const uint32_t *)eng)[4];
+    for (uint32_t b = 0; b < nb; b++) {
+        if (!conf_off[b]) continue;
+        const uint8_t *fc = confBase + conf_off[b];
+        const FDRConfirm *cf = (const FDRConfirm *)fc;
+        const uint32_t *li = (const uint32_t *)(fc + sizeof(FDRConfirm));
+        std::vector<uint32_t> offs;
+        for (uint32_t h = 0; h < (1u << cf->nBits); h++) {
+            uint32_t o = li[h];
+            if (!o) continue;
+            for (;;) {
+                offs.push_back(o);
+                const LitInfo *L = (const LitInfo *)(fc + o);
+                if (!L->next) break;
+                o += sizeof(LitInfo);
+            }
+        }
+        std::sort(offs.begin(), offs.end());
+        offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
+        for (uint32_t o : offs) {
+            const LitInfo *L = (const LitInfo *)(fc + o);
+            for (uint32_t k = 0; k < nl; k++) {
+                const uint64_t bit = 1ULL << (k * lb + b);
+                const uint8_t m = (uint8_t)(L->msk >> (8 * (7 - k)));
+                const uint8_t v = (uint8_t)(L->v >> (8 * (7 - k))) & m;
+                if (!m) {
+                    always |= bit;
+                    continue;
+                }
+                for (uint32_t ch = 0; ch < 256; ch++)
+                    if ((ch & m) == v) W[ch] &= ~bit;
+            }
+        }
+    }
+    for (auto &w : W) w &= ~always;
+}
+
 int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
     if (!c || !hwlm || !out || size < VSA_ROUNDUP_CL(sizeof(HWLM))) return VSA_E_INVALID;
     VSA_CHECK(hipSetDevice(c->device));
@@ -965,26 +1020,10 @@ int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
         VSA_CHECK(hipMemcpy(db->d_table, T.data(), T.size() * 8, hipMemcpyHostToDevice));
     }
     if (db->mode == VSA_MODE_TEDDY || db->mode == VSA_MODE_FAT) {
-        /* combine nibble masks per byte value (teddy.c:921-971): field j of
-         * W[c] = lo_j[c & 15] | hi_j[c >> 4] for the 8 (or 16) buckets */
-        const uint32_t nm = vsa_teddy_num_masks(db->engine_id);
-        const uint8_t *mb = eng + 64;
-        std::vector<uint64_t> W(256, 0);
-        for (int ch = 0; ch < 256; ch++) {
-            uint64_t w = 0;
-            for (uint32_t j = 0; j < nm; j++) {
-                if (db->mode == VSA_MODE_TEDDY) {
-                    const uint8_t *lo = mb + j * 32, *hi = lo + 16;
-                    w |= (uint64_t)(lo[ch & 15] | hi[ch >> 4]) << (8 * j);
-                } else {
-                    const uint8_t *lo = mb + j * 64, *hi = lo + 32;
-                    uint64_t v = (uint64_t)(lo[ch & 15] | hi[ch >> 4]) |
-                                 ((uint64_t)(lo[16 + (ch & 15)] | hi[16 + (ch >> 4)]) << 8);
-                    w |= v << (16 * j);
-                }
-            }
-            W[ch] = w;
-        }
+        /* exact byte table from the confirm records (derive_teddy_table) */
+        std::vector<uint64_t> W;
+        if (db->mode == VSA_MODE_TEDDY) derive_teddy_table(eng, db->conf_off, 8, 8, 8, W);
+        else derive_teddy_table(eng, db->conf_off, 16, 4, 16, W);
         VSA_CHECK(hipMalloc(&db->d_table, 256 * 8));
         VSA_CHECK(hipMemcpy(db->d_table, W.data(), 256 * 8, hipMemcpyHostToDevice));
     }
@@ -1120,6 +1159,13 @@ int vsa_scan_copy_device(vsa_ctx_t *c, uint64_t *d_keys, uint32_t *d_ids, uint64
 }
 
 uint64_t vsa_scan_candidates(vsa_ctx_t *c) { return c ? c->last_cand : 0; }
+
+int vsa_scan_debug_counters(vsa_ctx_t *c, uint64_t out[16]) {
+    if (!c || !out) return VSA_E_INVALID;
+    VSA_CHECK(hipStreamSynchronize(c->stream));
+    VSA_CHECK(hipMemcpy(out, c->ws.d_counters, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return VSA_OK;
+}
 
 double vsa_scan_kernel_ms(vsa_ctx_t *c) { return c ? c->last_kernel_ms : 0.0; }
 
