@@ -256,6 +256,59 @@ def test_gpu_class_scan_256mib(ctx):
     assert cnt == len(idx) and f == idx[0] and l == idx[-1] + 1
 
 
+@pytest.mark.parametrize("n,nchars,seed", [((8 << 20) + 13, 5, 31), ((9 << 20) + 1023, 100, 32),
+                                           ((16 << 20) + 1, 0, 33), ((12 << 20) + 4097, 256, 34)])
+def test_gpu_class_scan_lut_ragged(ctx, n, nchars, seed):
+    """The pair-LUT class kernel (buffers >= 8 MiB): ragged lengths (last
+    wave span and last lane partial), empty and full classes, random
+    classes; bitmap, first, last and count against numpy."""
+    rng = np.random.default_rng(seed)
+    data = rng.integers(0, 256, n, dtype=np.uint8)
+    chars = sorted(rng.choice(256, nchars, replace=False).tolist()) if nchars < 256 \
+        else list(range(256))
+    cls = vsa.class_bitmap(chars)
+    nbm = ((n + 63) // 64) * 8
+    dbuf = ctx.malloc(n + 64)
+    dbm = ctx.malloc(nbm)
+    try:
+        ctx.h2d(dbuf, data)
+        ctx.h2d(dbm, np.zeros(nbm, np.uint8))
+        f, l, cnt = ctx.class_scan(cls, dbuf, n, d_bitmap=dbm)
+        bm = np.zeros(nbm, np.uint8)
+        ctx.d2h(bm, dbm)
+    finally:
+        ctx.free(dbuf)
+        ctx.free(dbm)
+    member = np.isin(data, np.array(chars, np.uint8))
+    exp = np.packbits(member, bitorder="little")
+    assert np.array_equal(bm[:len(exp)], exp)
+    idx = np.nonzero(member)[0]
+    assert cnt == len(idx)
+    assert f == (idx[0] if len(idx) else n)
+    assert l == (idx[-1] + 1 if len(idx) else 0)
+
+
+@pytest.mark.parametrize("lit,nocase", [(b"abcde", False), (b"aBcDe", True), (b"q", False),
+                                        (b"xy", True), (b"\x00\x00", False)])
+def test_gpu_noodle_16mib_planted(ctx, lit, nocase):
+    """Noodle over 16 MiB with planted occurrences (the key prefilter path
+    and its full compare), exact sequence vs the oracle."""
+    rng = np.random.default_rng(len(lit) * 7 + nocase)
+    n = 16 << 20
+    data = rng.integers(0x20, 0x7F, n, dtype=np.uint8)
+    pos = rng.integers(0, n - 8, 3000)
+    for p in pos.tolist():
+        s = lit.swapcase() if nocase and p & 1 else lit
+        data[p:p + len(s)] = np.frombuffer(s, np.uint8)
+    blob = vsa.hwlm_build([vsa.HwlmLiteral(lit, nocase, 77)])
+    assert blob.is_noodle
+    got = batch_run(ctx, blob, [data.tobytes()])[0]
+    st, m = oracle.nood_exec(vsa.engine_blob(blob), data, cap=1 << 22)
+    assert st == 0
+    assert got == m
+    assert len(m) >= 1000
+
+
 @pytest.mark.gpu
 def test_gpu_dropin_reused_address():
     """A database freed and rebuilt at the same address (same size, other

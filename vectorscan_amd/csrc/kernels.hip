@@ -652,6 +652,25 @@ __device__ __forceinline__ IterState nood_iter(const VsaLitParams &P, const LitS
     }
     IterState out = in;
     out.pbytes = ((u64)readlane_u32(d[3], WAVE - 1) << 32) | readlane_u32(d[2], WAVE - 1);
+    if (!EDGE) {
+        /* key prefilter (the reference scans for the literal's key bytes
+         * before confirming, noodle_engine_simd.hpp:173-226): the last two
+         * literal bytes under their masks, four positions per dword, with a
+         * SWAR zero-byte test; the full compare runs only when some lane
+         * has a key hit (msk_len 1: the second byte's mask and cmp are 0) */
+        const u32 M1 = (u32)(P.nood_msk >> 56) * 0x01010101u;
+        const u32 C1 = (u32)(P.nood_cmp >> 56) * 0x01010101u;
+        const u32 M0 = ((u32)(P.nood_msk >> 48) & 0xffu) * 0x01010101u;
+        const u32 C0 = ((u32)(P.nood_cmp >> 48) & 0xffu) * 0x01010101u;
+        u32 z = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const u32 prev = __builtin_amdgcn_alignbyte(d[k], k ? d[k - 1] : pv3, 3);
+            const u32 t = ((d[k] & M1) ^ C1) | ((prev & M0) ^ C0);
+            z |= (t - 0x01010101u) & ~t;
+        }
+        if (!__any((z & 0x80808080u) != 0)) return out;
+    }
     const u32 w[6] = {pv2, pv3, d[0], d[1], d[2], d[3]};
     const u32 mlo = (u32)P.nood_msk, mhi = (u32)(P.nood_msk >> 32);
     const u32 clo = (u32)P.nood_cmp, chi = (u32)(P.nood_cmp >> 32);
@@ -832,10 +851,16 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                 continue;
             }
             if (all_done) break;
+            /* idle: yield issue priority while polling */
+            __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_s_sleep(4);
             phase(3);
             continue;
         }
+        /* entries in hand: issue ahead of the scanners on this SIMD (the
+         * youngest wave otherwise loses VALU arbitration to all of them);
+         * noodle entries are final matches, where priority measured slower */
+        if constexpr (MODE != VSA_MODE_NOOD) __builtin_amdgcn_s_setprio(2);
         const u64 meta0 = ((u64)e[1] << 32) | e[0];
         const u64 p0 = meta0 & ENT_P0_MASK;
         const u32 blk = (u32)(meta0 >> ENT_BLK_SHIFT);
@@ -1006,7 +1031,7 @@ vsa_lit_scan(VsaLitParams P) {
 
     const u32 mis = (u32)((uintptr_t)P.data & 15);
     if (wave == LIT_WAVES - 1) {
-        __builtin_amdgcn_s_setprio(2); /* issue ahead of the scanners on its SIMD */
+
         confirm_wave<MODE>(P, cl, rings, 31 - __clz(P.qcap), &q_tail, &q_done, mis, slots, pq);
         return;
     }
@@ -1374,5 +1399,124 @@ __global__ void __launch_bounds__(256) vsa_pair_scan(VsaPairParams P) {
         if (fh != ~0ULL) atomicMin(P.first, fh);
         if (fa != ~0ULL) atomicMin(P.first + 16, fa);
         if (ft != ~0ULL) atomicMin(P.first + 32, ft);
+    }
+}
+
+/* ================================================== class scan (LUT) === */
+
+/* Large-buffer byte-class scan (shufti / truffle / vermicelli reduced to a
+ * 256-bit class, as vsa_class_scan).  Each workgroup first expands the class
+ * into a 64 KiB LDS table over byte PAIRS, T[w] = member(w & 0xff) |
+ * member(w >> 8) << 1, so one LDS byte read classifies two input bytes and
+ * its address is one v_mad_u32_u16 of the raw input dword (no per-byte
+ * extract / shift / test).  One persistent 1024-thread workgroup per CU;
+ * wave g owns the contiguous 1 KiB-aligned span [g * span, (g + 1) * span)
+ * and sweeps it with a 4-deep ring of unconditional 1 KiB wave loads (the
+ * structure tools/probe_stream.hip measured at 6.6-6.8 TB/s).  Output as
+ * vsa_class_scan: 1 bit per byte (u16 per lane), first / last / count. */
+template <int H>
+__device__ __forceinline__ u32 lut_addr16(u32 w, u32 base) {
+    u32 r;
+    if constexpr (H == 0)
+        asm("v_mad_u32_u16 %0, %1, 1, %2" : "=v"(r) : "v"(w), "s"(base));
+    else
+        asm("v_mad_u32_u16 %0, %1, 1, %2 op_sel:[1,0,0,0]" : "=v"(r) : "v"(w), "s"(base));
+    return r;
+}
+typedef const __attribute__((address_space(3))) u8 lds_cu8_t;
+__device__ __forceinline__ u32 lds_ld8(u32 addr) { return *(lds_cu8_t *)(uintptr_t)addr; }
+
+#define CLS_DEPTH 4
+__global__ void __launch_bounds__(1024) vsa_class_scan_lut(VsaClassParams P, u64 span) {
+    __shared__ __align__(16) u8 T[65536];
+    __shared__ u8 mem[256];
+    const u32 tid = threadIdx.x;
+    const u32 lane = lane_id();
+    if (tid < 256) mem[tid] = (u8)((P.cls[tid >> 5] >> (tid & 31)) & 1u);
+    __syncthreads();
+    {
+        /* dword i holds T[4i .. 4i+3]: low bytes 4i & 0xff .., high byte i >> 6 */
+        const u32 *m4 = (const u32 *)mem;
+        u32 *T4 = (u32 *)T;
+        for (u32 i = tid; i < 16384; i += 1024)
+            T4[i] = m4[i & 63] | ((u32)mem[i >> 6] * 0x02020202u);
+    }
+    __syncthreads();
+    const u32 base = readfirstlane_u32((u32)(uintptr_t)(lds_cu8_t *)T);
+    const u32 wave = readfirstlane_u32(tid / WAVE);
+    const u64 g = (u64)blockIdx.x * 16 + wave;
+    const u64 lo = g * span;
+    const u64 hi = min(lo + span, (u64)P.len);
+    unsigned long long first = ~0ULL, last = 0, cnt = 0;
+    if (lo < hi) {
+        const u32 nit = (u32)((hi - lo + 1023) >> 10);
+        /* full iterations: the whole 1 KiB lies inside [0, len) */
+        const u32 nfull = (u32)min((u64)nit, ((u64)P.len - lo) >> 10);
+        const u8 *sb = uniform_ptr(P.data + lo);
+        uint4 ring[CLS_DEPTH];
+#pragma unroll
+        for (int k = 0; k < CLS_DEPTH; k++) ring[k] = load_wave_kib(sb, (u32)k < nfull ? 1024u * k : 0u);
+        auto classify = [&](u32 it, const uint4 v, u32 valid_bytes) {
+            const u32 dw[4] = {v.x, v.y, v.z, v.w};
+            u32 bits = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const u32 r0 = lds_ld8(lut_addr16<0>(dw[k], base));
+                const u32 r1 = lds_ld8(lut_addr16<1>(dw[k], base));
+                bits |= (r0 | (r1 << 2)) << (4 * k);
+            }
+            if (valid_bytes < 16) bits &= (1u << valid_bytes) - 1u;
+            const u64 p0 = lo + 1024 * (u64)it + 16 * lane;
+            if (P.bitmap) ((uint16_t *)P.bitmap)[p0 >> 4] = (uint16_t)bits;
+            if (bits) {
+                const u64 f = p0 + (u64)(__ffs(bits) - 1);
+                const u64 l = p0 + (u64)(31 - __clz(bits)) + 1;
+                first = f < first ? f : first;
+                last = l > last ? l : last;
+                cnt += __popc(bits);
+            }
+        };
+        u32 it = 0;
+        for (; it + CLS_DEPTH <= nfull; it += CLS_DEPTH) {
+#pragma unroll
+            for (int k = 0; k < CLS_DEPTH; k++) {
+                const uint4 v = ring[k];
+                const u32 itn = it + k + CLS_DEPTH;
+                ring[k] = load_wave_kib(sb, 1024u * (itn < nfull ? itn : it + k));
+                classify(it + k, v, 16);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < CLS_DEPTH - 1; k++)
+            if (it + k < nfull) classify(it + k, ring[k], 16);
+        it = nfull;
+        /* the ragged last iteration (buffer end): bytes past len read as 0 */
+        for (; it < nit; it++) {
+            const u64 p0 = lo + 1024 * (u64)it + 16 * lane;
+            u32 d[4] = {0, 0, 0, 0};
+            u32 nv = 0;
+            if (p0 < hi) {
+                nv = (u32)min((u64)16, hi - p0);
+                for (u32 b = 0; b < nv; b++) d[b >> 2] |= (u32)P.data[p0 + b] << (8 * (b & 3));
+            }
+            if (p0 < hi) classify(it, make_uint4(d[0], d[1], d[2], d[3]), nv);
+        }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        u32 flo = shfl_down_u32((u32)first, d), fhi = shfl_down_u32((u32)(first >> 32), d);
+        u64 of = ((u64)fhi << 32) | flo;
+        if (of < first) first = of;
+        u32 llo = shfl_down_u32((u32)last, d), lhi = shfl_down_u32((u32)(last >> 32), d);
+        u64 ol = ((u64)lhi << 32) | llo;
+        if (ol > last) last = ol;
+        u32 clo = shfl_down_u32((u32)cnt, d), chi = shfl_down_u32((u32)(cnt >> 32), d);
+        cnt += ((u64)chi << 32) | clo;
+    }
+    if (lane == 0) {
+        const u32 sl = 16 * ((blockIdx.x * 16 + wave) % P.slots);
+        if (first != ~0ULL) atomicMin(P.first + sl, first);
+        if (last) atomicMax(P.last + sl, last);
+        if (cnt) atomicAdd(P.count + sl, cnt);
     }
 }

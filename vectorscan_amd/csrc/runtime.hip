@@ -38,6 +38,7 @@
 template <int MODE, bool LDS_TABLE>
 __global__ void vsa_lit_scan(VsaLitParams P);
 __global__ void vsa_class_scan(VsaClassParams P);
+__global__ void vsa_class_scan_lut(VsaClassParams P, uint64_t span);
 __global__ void vsa_pair_scan(VsaPairParams P);
 
 #define VSA_CHECK(x)                                                          \
@@ -1204,12 +1205,21 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
     P.last = part + 1;
     P.count = part + 2;
     P.slots = CLASS_SLOTS;
-    uint64_t chunks = (len + 15) / 16;
-    uint64_t want = (chunks + 255) / 256;
-    uint64_t cap = (uint64_t)c->num_cus * 8;
-    uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
     VSA_CHECK(hipEventRecord(c->ev0, c->stream));
-    hipLaunchKernelGGL(vsa_class_scan, dim3(grid), dim3(256), 0, c->stream, P);
+    if (!cls2 && len >= ((uint64_t)8 << 20) && !getenv("VSA_CLASS_SIMPLE")) {
+        /* large buffers: pair-LUT kernel, one 1024-thread workgroup per CU,
+         * a contiguous 1 KiB-aligned span per wave */
+        const uint64_t waves = (uint64_t)c->num_cus * 16;
+        const uint64_t span = ((len + waves - 1) / waves + 1023) & ~(uint64_t)1023;
+        hipLaunchKernelGGL(vsa_class_scan_lut, dim3(c->num_cus), dim3(1024), 0, c->stream, P,
+                           span);
+    } else {
+        uint64_t chunks = (len + 15) / 16;
+        uint64_t want = (chunks + 255) / 256;
+        uint64_t cap = (uint64_t)c->num_cus * 8;
+        uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
+        hipLaunchKernelGGL(vsa_class_scan, dim3(grid), dim3(256), 0, c->stream, P);
+    }
     VSA_CHECK(hipGetLastError());
     VSA_CHECK(hipEventRecord(c->ev1, c->stream));
     VSA_CHECK(hipMemcpyAsync(w.h_counters + CLASS_BASE, part, 16 * CLASS_SLOTS * 8,
