@@ -13,3 +13,5 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/fetch -o run -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu > $OUT/bench_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/write -o run -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu > $OUT/bench_write.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/cfg -o run -- \
+    python3 tools/bench_configs.py --steps 5 --warmup 1 > $OUT/configs_trace.log 2>&1
