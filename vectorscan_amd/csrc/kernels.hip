@@ -102,8 +102,6 @@ __device__ __forceinline__ u64 lds_ld64(u32 addr) { return *(lds_u64_t *)(uintpt
 /* Teddy tables live at this LDS byte address (64 KiB; rings and slot
  * bitmaps below it) */
 #define TEDDY_TAB_LDS 0x10000u
-typedef const __attribute__((address_space(3))) u32 lds_u32_t;
-__device__ __forceinline__ u32 lds_ld32c(u32 addr) { return *(lds_u32_t *)(uintptr_t)addr; }
 
 /* three-input OR in one VALU op (the backend re-associates wide OR trees
  * into two-input ORs) */
@@ -241,11 +239,6 @@ __device__ __forceinline__ void lds_st32(u32 *p, u32 v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-/* wave-uniform ring cursor of a scanning wave */
-struct RingCur {
-    u32 head, tail_cache;
-};
-
 __device__ __forceinline__ u32 conf_hash(u64 key, u64 andmsk, u64 mult, u32 nbits) {
     return (u32)(((key & andmsk) * mult) >> (64 - nbits));
 }
@@ -326,7 +319,6 @@ struct IterState {
     u64 carry;  /* pending table contributions into the next chunk's first ends */
     u64 pbytes; /* the 8 bytes before the next chunk (lane 63's d[2..3]) */
     u32 ncand;  /* first-stage candidates so far (diagnostic, wave-uniform) */
-    u32 head;   /* ring entries written by this wave (wave-uniform) */
     u32 tail_cache; /* last tail read from the confirm wave */
 };
 
@@ -388,22 +380,7 @@ __device__ __forceinline__ void conf_accumulate(const typename LitTraits<MODE>::
                                                 u32 (&c)[LitTraits<MODE>::CW], u64 &s_out) {
     auto lo = [&](int j) { return (u32)(u64)x[j]; };
     auto hi = [&](int j) { return (u32)((u64)x[j] >> 32); };
-    if constexpr (LitTraits<MODE>::LB == 8 && sizeof(typename LitTraits<MODE>::S_t) == 4) {
-        /* Teddy: 4 one-byte fields per entry, no high dword */
-        u32 F[5];
-        F[0] = lo(0) | (lo(1) << 8) | (lo(2) << 16) | (lo(3) << 24);
-#pragma unroll
-        for (int i = 1; i < 4; i++) {
-            const u32 s1 = __builtin_amdgcn_alignbyte(lo(4 * i + 1), lo(4 * i - 3), 3);
-            const u32 s2 = __builtin_amdgcn_alignbyte(lo(4 * i + 2), lo(4 * i - 2), 2);
-            const u32 s3 = __builtin_amdgcn_alignbyte(lo(4 * i + 3), lo(4 * i - 1), 1);
-            F[i] = or3(lo(4 * i), s1, s2) | s3;
-        }
-        F[4] = or3(lo(13) >> 24, lo(14) >> 16, lo(15) >> 8);
-#pragma unroll
-        for (int i = 0; i < 4; i++) c[i] = F[i];
-        s_out = F[4];
-    } else if constexpr (LitTraits<MODE>::LB == 8) {
+    if constexpr (LitTraits<MODE>::LB == 8) {
         /* A[r][w] = dword w of the group j = 4 w' + r (before its r-byte
          * shift); group 0 is folded straight into F */
         u32 A[4][5];
@@ -540,7 +517,6 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     const u64 s_in = ((u64)s_in_hi << 32) | s_in_lo;
     IterState out;
     out.ncand = in.ncand;
-    out.head = in.head;
     out.tail_cache = in.tail_cache;
     out.carry = ((u64)readlane_u32((u32)(s_out >> 32), WAVE - 1) << 32) |
                 readlane_u32((u32)s_out, WAVE - 1);
@@ -770,7 +746,8 @@ __device__ __forceinline__ uint4 load_wave_kib(const u8 *base, u32 off) {
 #define PQ_CAP 128
 template <int MODE>
 __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLds &cl,
-                                             const uint4 *ring, u32 lg, u32 *tail_p,
+                                             const uint4 *ring, u32 lg, const u32 *head_p,
+                                             u32 *tail_p,
                                              const u32 *q_done, u32 mis, const u32 *slots,
                                              QEnt *pq) {
     typedef LitTraits<MODE> T;
@@ -809,26 +786,35 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
     for (;;) {
         const bool all_done = lds_ld32(q_done) == LIT_SCANNERS;
         asm volatile("" ::: "memory");
-        /* gather: the 64 slots at the tail, the leading run of written ones */
+        /* gather: the slots at the tail that scanners have reserved (one
+         * broadcast read of the reservation counter, so an idle poll costs
+         * one LDS cycle, not 64 entries), the leading run of written ones */
         u32 e[4 * EW];
-        {
-            const u32 pos = tail + lane;
-            const uint4 *q = ring + (size_t)(pos & (cap - 1)) * EW;
-            const uint4 v0 = q[0];
-            asm volatile("" ::: "memory"); /* word 0 (lap) before words 1.. */
-            e[0] = v0.x;
-            e[1] = v0.y;
-            e[2] = v0.z;
-            e[3] = v0.w;
 #pragma unroll
-            for (int k = 1; k < EW; k++) {
-                const uint4 v = q[k];
-                e[4 * k] = v.x;
-                e[4 * k + 1] = v.y;
-                e[4 * k + 2] = v.z;
-                e[4 * k + 3] = v.w;
+        for (int i = 0; i < 4 * EW; i++) e[i] = 0;
+        filled = 0;
+        const u32 reserved = readfirstlane_u32(lds_ld32(head_p)) - tail;
+        if (reserved) {
+            const u32 pos = tail + lane;
+            bool ready = false;
+            if (lane < reserved) {
+                const uint4 *q = ring + (size_t)(pos & (cap - 1)) * EW;
+                const uint4 v0 = q[0];
+                asm volatile("" ::: "memory"); /* word 0 (lap) before words 1.. */
+                e[0] = v0.x;
+                e[1] = v0.y;
+                e[2] = v0.z;
+                e[3] = v0.w;
+#pragma unroll
+                for (int k = 1; k < EW; k++) {
+                    const uint4 v = q[k];
+                    e[4 * k] = v.x;
+                    e[4 * k + 1] = v.y;
+                    e[4 * k + 2] = v.z;
+                    e[4 * k + 3] = v.w;
+                }
+                ready = (e[1] >> (ENT_LAP_SHIFT - 32)) == ((pos >> lg) & 15u);
             }
-            const bool ready = (e[1] >> (ENT_LAP_SHIFT - 32)) == ((pos >> lg) & 15u);
             const u64 rb = __ballot(ready);
             filled = ~rb ? (u32)__builtin_ctzll(~rb) : (u32)WAVE;
             asm volatile("" ::: "memory"); /* entries read before they are freed */
@@ -853,7 +839,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
             if (all_done) break;
             /* idle: yield issue priority while polling */
             __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_s_sleep(4);
+            __builtin_amdgcn_s_sleep(8);
             phase(3);
             continue;
         }
@@ -1032,7 +1018,10 @@ vsa_lit_scan(VsaLitParams P) {
     const u32 mis = (u32)((uintptr_t)P.data & 15);
     if (wave == LIT_WAVES - 1) {
 
-        confirm_wave<MODE>(P, cl, rings, 31 - __clz(P.qcap), &q_tail, &q_done, mis, slots, pq);
+#ifndef VSA_EXP_NO_CONFIRM /* experiment: VGPR use of the scanning path alone */
+        confirm_wave<MODE>(P, cl, rings, 31 - __clz(P.qcap), &q_head, &q_tail, &q_done, mis,
+                           slots, pq);
+#endif
         return;
     }
 
@@ -1062,7 +1051,7 @@ vsa_lit_scan(VsaLitParams P) {
     const u8 *A = P.data - mis;
     const int64_t SEG = (int64_t)P.seg_bytes;
     u32 ncand_total = 0;
-    u32 ring_head = 0, ring_tail_cache = 0;
+    u32 ring_tail_cache = 0;
 
     /* Segment scheduling.  The segments are split into NREG contiguous
      * regions; workgroup b works in region b % NREG first (workgroups are
@@ -1143,7 +1132,6 @@ vsa_lit_scan(VsaLitParams P) {
         /* prologue 1: table spill from positions s_lo-NL+1 .. s_lo-1 */
         IterState is;
         is.ncand = ncand_total;
-        is.head = ring_head;
         is.tail_cache = ring_tail_cache;
         {
             S_t x = 0;
@@ -1238,7 +1226,6 @@ vsa_lit_scan(VsaLitParams P) {
                                                  bucket_mask);
         }
         ncand_total = is.ncand;
-        ring_head = is.head;
         ring_tail_cache = is.tail_cache;
     }
     /* every push of this wave precedes this (LDS order) */
@@ -1432,6 +1419,20 @@ __global__ void __launch_bounds__(1024) vsa_class_scan_lut(VsaClassParams P, u64
     __shared__ u8 mem[256];
     const u32 tid = threadIdx.x;
     const u32 lane = lane_id();
+    const u32 wave = readfirstlane_u32(tid / WAVE);
+    const u64 g = (u64)blockIdx.x * 16 + wave;
+    const u64 lo = g * span;
+    const u64 hi = min(lo + span, (u64)P.len);
+    const u32 nit = lo < hi ? (u32)((hi - lo + 1023) >> 10) : 0u;
+    /* full iterations: the whole 1 KiB lies inside [0, len) */
+    const u32 nfull = lo < hi ? (u32)min((u64)nit, ((u64)P.len - lo) >> 10) : 0u;
+    const u8 *sb = uniform_ptr(P.data + (lo < hi ? lo : 0));
+    /* the first ring loads go out before the table is built (plain loads
+     * stay in flight across the barriers) */
+    uint4 ring[CLS_DEPTH];
+#pragma unroll
+    for (int k = 0; k < CLS_DEPTH; k++)
+        ring[k] = nfull ? load_wave_kib(sb, (u32)k < nfull ? 1024u * k : 0u) : make_uint4(0, 0, 0, 0);
     if (tid < 256) mem[tid] = (u8)((P.cls[tid >> 5] >> (tid & 31)) & 1u);
     __syncthreads();
     {
@@ -1443,19 +1444,8 @@ __global__ void __launch_bounds__(1024) vsa_class_scan_lut(VsaClassParams P, u64
     }
     __syncthreads();
     const u32 base = readfirstlane_u32((u32)(uintptr_t)(lds_cu8_t *)T);
-    const u32 wave = readfirstlane_u32(tid / WAVE);
-    const u64 g = (u64)blockIdx.x * 16 + wave;
-    const u64 lo = g * span;
-    const u64 hi = min(lo + span, (u64)P.len);
     unsigned long long first = ~0ULL, last = 0, cnt = 0;
     if (lo < hi) {
-        const u32 nit = (u32)((hi - lo + 1023) >> 10);
-        /* full iterations: the whole 1 KiB lies inside [0, len) */
-        const u32 nfull = (u32)min((u64)nit, ((u64)P.len - lo) >> 10);
-        const u8 *sb = uniform_ptr(P.data + lo);
-        uint4 ring[CLS_DEPTH];
-#pragma unroll
-        for (int k = 0; k < CLS_DEPTH; k++) ring[k] = load_wave_kib(sb, (u32)k < nfull ? 1024u * k : 0u);
         auto classify = [&](u32 it, const uint4 v, u32 valid_bytes) {
             const u32 dw[4] = {v.x, v.y, v.z, v.w};
             u32 bits = 0;

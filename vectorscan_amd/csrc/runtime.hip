@@ -179,7 +179,7 @@ int ensure_blocks(vsa_ctx *c, uint32_t n) {
 }
 
 /* Segment size (bytes, multiple of 1 KiB) for the literal-scan kernel's
- * static assignment: at most 64 KiB, at least 4 KiB, and sized so the
+ * assignment: at most 128 KiB (VSA_SEG_MAX_KIB), at least 4 KiB, and sized so the
  * segment count is just under a multiple of the scanning-wave count
  * (every wave gets k or k-1 segments, no long tail).  spans[] are the
  * per-block byte spans from their 1 KiB-aligned origins. */
@@ -191,7 +191,10 @@ uint64_t pick_seg_bytes(const std::vector<int64_t> &spans, uint64_t waves) {
     };
     uint64_t total = 0;
     for (int64_t sp : spans) total += (uint64_t)sp;
-    uint64_t seg = 64 << 10;
+    uint64_t seg = 128 << 10; /* 64-256 KiB measured equal for FDR, 128 KiB
+                                 5-8 % faster for Teddy / noodle at 1 GiB */
+    if (const char *e = getenv("VSA_SEG_MAX_KIB"))
+        seg = (uint64_t)std::max(4, std::min(4096, atoi(e))) << 10;
     while (seg > (4u << 10) && count(seg) < 2 * waves) seg >>= 1;
     const uint64_t k = (count(seg) + waves - 1) / waves; /* rounds per wave */
     if (k >= 2) {
