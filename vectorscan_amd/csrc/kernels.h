@@ -65,6 +65,8 @@ struct VsaLitParams {
     const uint32_t *slotmap;     /* per-bucket bitmap of litIndex[h] != 0 */
     uint32_t slot_words;
     uint32_t slot_off[16];       /* word offset per bucket, ~0 = no prefilter */
+    uint8_t slot_bits[16];       /* bits of the prefilter hash per bucket (the
+                                    bucket's nBits, fewer when coarsened) */
     uint64_t nood_msk, nood_cmp; /* noodle msk / cmp << 8 * (8 - msk_len) */
     uint32_t nood_len, nood_id;  /* noodTable msk_len, id */
     uint64_t pf_mult;            /* FDRConfirm.mult shared by the prefiltered

@@ -243,52 +243,96 @@ __device__ __forceinline__ u32 conf_hash(u64 key, u64 andmsk, u64 mult, u32 nbit
     return (u32)(((key & andmsk) * mult) >> (64 - nbits));
 }
 
-/* Exact confirm of one candidate (fdr_confirm_runtime.h:43-102 minus the
- * sequential state, which the host replays): walk the LitInfo chain of
- * litIndex[hash] and emit every literal with (key & msk) == v whose start
- * lies inside the block. */
-__device__ __forceinline__ void confirm_one(const VsaLitParams &P, const ConfLds &cl,
-                                            u64 meta, u64 key, u32 mis) {
-    const u32 b = (u32)(meta & 15);
-    const u32 blk = (u32)((meta >> 4) & 0xfffff);
-    const u64 aoff = meta >> 24;
-    const u8 *fc = P.conf_base + cl.off[b];
-    const u32 c = conf_hash(key, cl.andmsk[b], cl.mult[b], cl.nbits[b]);
-    const u32 st = *((const u32 *)(fc + 32) + c);
-    if (!st) return;
-    const u64 base = P.blocks[blk].base;
-    const int64_t hlen = (int64_t)P.blocks[blk].hlen;
-    const int64_t e = (int64_t)(aoff - mis - base); /* block-relative end */
-    if (P.dbg & 1) {
-        const u8 *A = P.data - mis;
-        const int64_t blo = (int64_t)base + mis;
-        u64 k2 = 0;
-        for (int k = 0; k < 8; k++) {
-            int64_t p = (int64_t)aoff - 7 + k;
-            k2 |= (u64)(p >= blo ? A[p] : 0) << (8 * k);
+/* Exact confirm of up to CU candidates per lane (fdr_confirm_runtime.h:43-102
+ * minus the sequential state, which the host replays): for each, walk the
+ * LitInfo chain of litIndex[hash] and emit every literal with (key & msk) ==
+ * v whose start lies inside the block.  The candidates' global loads
+ * (litIndex slot, block record, each chain step) are independent, so they
+ * are issued together: one memory latency per chain step for all of them. */
+#define CONF_U 4
+__device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfLds &cl,
+                                              const QEnt (&q)[CONF_U], const bool (&valid)[CONF_U],
+                                              u32 mis) {
+    const u8 *fc[CONF_U], *li[CONF_U];
+    u32 st[CONF_U], b[CONF_U];
+    u64 base[CONF_U];
+    int64_t hlen[CONF_U], e[CONF_U];
+#pragma unroll
+    for (int i = 0; i < CONF_U; i++) {
+        b[i] = (u32)(q[i].meta & 15);
+        const u32 blk = (u32)((q[i].meta >> 4) & 0xfffff);
+        fc[i] = P.conf_base + cl.off[b[i]];
+        st[i] = 0;
+        base[i] = 0;
+        hlen[i] = 0;
+        if (valid[i]) {
+            const u32 c = conf_hash(q[i].key, cl.andmsk[b[i]], cl.mult[b[i]], cl.nbits[b[i]]);
+            st[i] = *((const u32 *)(fc[i] + 32) + c);
+            base[i] = P.blocks[blk].base;
+            hlen[i] = (int64_t)P.blocks[blk].hlen;
         }
-        if (k2 != key) atomicAdd(&P.counters[3], 1ULL);
     }
-    const u8 *li = fc + st;
-    u32 next;
-    do {
-        const uint4 w0 = *(const uint4 *)li;        /* v, msk */
-        const uint4 w1 = *(const uint4 *)(li + 16); /* groups | id,size,flags,next */
-        const u64 v = ((u64)w0.y << 32) | w0.x;
-        const u64 msk = ((u64)w0.w << 32) | w0.z;
-        const u32 size = w1.w & 0xff;
-        next = (w1.w >> 16) & 0xff;
-        if ((key & msk) == v && e + 1 + hlen >= (int64_t)size) {
-            unsigned long long slot = atomicAdd(&P.counters[0], 1ULL);
-            if (slot < P.out_cap) {
-                const u64 lidx = ((u64)(li - fc) >> 5) & VSA_KEY_LI_MASK;
-                P.out_keys[slot] = ((base + (u64)e) << VSA_KEY_END_SHIFT) |
-                                   ((u64)b << VSA_KEY_BUCKET_SHIFT) | lidx;
-                P.out_ids[slot] = w1.z;
+    bool live[CONF_U];
+#pragma unroll
+    for (int i = 0; i < CONF_U; i++) {
+        live[i] = st[i] != 0;
+        li[i] = fc[i] + st[i];
+        e[i] = (int64_t)((q[i].meta >> 24) - mis - base[i]); /* block-relative end */
+    }
+    /* wave-uniform loop (every lane stays in, so the output slot reservation
+     * below is one atomic per wave and step, not one per match: a single
+     * returning atomic word saturates near 90 per microsecond chip-wide) */
+    for (;;) {
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < CONF_U; i++) any |= live[i];
+        if (!__any(any)) break;
+        uint4 w0[CONF_U], w1[CONF_U];
+#pragma unroll
+        for (int i = 0; i < CONF_U; i++) {
+            if (live[i]) {
+                w0[i] = *(const uint4 *)li[i];        /* v, msk */
+                w1[i] = *(const uint4 *)(li[i] + 16); /* groups | id,size,flags,next */
             }
         }
-        li += 32;
-    } while (next);
+        bool mt[CONF_U];
+        u32 rank[CONF_U], tot = 0;
+#pragma unroll
+        for (int i = 0; i < CONF_U; i++) {
+            mt[i] = false;
+            if (live[i]) {
+                const u64 v = ((u64)w0[i].y << 32) | w0[i].x;
+                const u64 msk = ((u64)w0[i].w << 32) | w0[i].z;
+                const u32 size = w1[i].w & 0xff;
+                mt[i] = (q[i].key & msk) == v && e[i] + 1 + hlen[i] >= (int64_t)size;
+            }
+            const u64 pm = __ballot(mt[i]);
+            rank[i] = tot + __builtin_amdgcn_mbcnt_hi((u32)(pm >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((u32)pm, 0));
+            tot += (u32)__popcll(pm);
+        }
+        if (tot) {
+            unsigned long long s0 = 0;
+            if (lane_id() == 0) s0 = atomicAdd(&P.counters[0], (unsigned long long)tot);
+            const u64 sb = ((u64)readlane_u32((u32)(s0 >> 32), 0) << 32) | readlane_u32((u32)s0, 0);
+#pragma unroll
+            for (int i = 0; i < CONF_U; i++) {
+                const u64 slot = sb + rank[i];
+                if (mt[i] && slot < P.out_cap) {
+                    const u64 lidx = ((u64)(li[i] - fc[i]) >> 5) & VSA_KEY_LI_MASK;
+                    P.out_keys[slot] = ((base[i] + (u64)e[i]) << VSA_KEY_END_SHIFT) |
+                                       ((u64)b[i] << VSA_KEY_BUCKET_SHIFT) | lidx;
+                    P.out_ids[slot] = w1[i].z;
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < CONF_U; i++) {
+            if (!live[i]) continue;
+            li[i] += 32;
+            live[i] = ((w1[i].w >> 16) & 0xff) != 0;
+        }
+    }
 }
 
 template <int MODE, bool LDS_TABLE>
@@ -743,7 +787,7 @@ __device__ __forceinline__ uint4 load_wave_kib(const u8 *base, u32 off) {
  * (q_done, read before the heads), every ring is empty and the queue is
  * drained. */
 #define LIT_SCANNERS (LIT_WAVES - 1)
-#define PQ_CAP 128
+#define PQ_CAP 512 /* >= CONF_U * 64 + 63 */
 template <int MODE>
 __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLds &cl,
                                              const uint4 *ring, u32 lg, const u32 *head_p,
@@ -770,13 +814,19 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
             tmark = now;
         }
     };
+    /* confirm k <= CONF_U * 64 queued candidates, CONF_U per lane */
     auto confirm_batch = [&](u32 k) {
         phase(1);
         asm volatile("" ::: "memory");
-        if (lane < k) {
-            const QEnt q = pq[(pq_tail + lane) & (PQ_CAP - 1)];
-            confirm_one(P, cl, q.meta, q.key, mis);
+        QEnt q[CONF_U];
+        bool valid[CONF_U];
+#pragma unroll
+        for (int i = 0; i < CONF_U; i++) {
+            const u32 j = lane + (u32)WAVE * i;
+            valid[i] = j < k;
+            q[i] = valid[i] ? pq[(pq_tail + j) & (PQ_CAP - 1)] : QEnt{0, 0};
         }
+        confirm_multi(P, cl, q, valid, mis); /* every lane: wave-uniform inside */
         asm volatile("" ::: "memory");
         pq_tail += k;
         consumed += k;
@@ -833,7 +883,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
         phase(0);
         if (filled == 0) {
             if (pq_head != pq_tail) {
-                confirm_batch(pq_head - pq_tail); /* < 64 queued */
+                confirm_batch(pq_head - pq_tail); /* < CONF_U * 64 queued */
                 continue;
             }
             if (all_done) break;
@@ -853,9 +903,16 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
         if constexpr (MODE == VSA_MODE_NOOD) {
             /* noodle hits are final: emit (end, id) */
             u32 hits = e[4];
-            if (hits) {
-                const u32 n = (u32)__popc(hits);
-                unsigned long long slot = atomicAdd(&P.counters[0], (unsigned long long)n);
+            /* one output reservation per gather (wave prefix of hit counts) */
+            u32 total;
+            const u32 n = (u32)__popc(hits);
+            const u32 pre = wave_excl_scan(n, &total);
+            total = readfirstlane_u32(total);
+            if (total) {
+                unsigned long long s0 = 0;
+                if (lane == 0) s0 = atomicAdd(&P.counters[0], (unsigned long long)total);
+                u64 slot = (((u64)readlane_u32((u32)(s0 >> 32), 0) << 32) |
+                            readlane_u32((u32)s0, 0)) + pre;
                 consumed += n;
                 for (; hits; hits &= hits - 1, slot++) {
                     const u32 j = __ffs(hits) - 1;
@@ -926,7 +983,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                     q->key = key;
                 }
                 pq_head += (u32)__popcll(pm);
-                if (pq_head - pq_tail >= (u32)WAVE) confirm_batch(WAVE);
+                if (pq_head - pq_tail >= (u32)WAVE * CONF_U) confirm_batch(WAVE * CONF_U);
             }
             phase(1);
         }
@@ -993,7 +1050,7 @@ vsa_lit_scan(VsaLitParams P) {
             cl.andmsk[tid] = pf.andmsk = *(const u64 *)fc;
             cl.mult[tid] = *(const u64 *)(fc + 8);
             cl.nbits[tid] = *(const u32 *)(fc + 16);
-            pf.shift = 64 - cl.nbits[tid];
+            pf.shift = 64 - (P.slot_bits[tid] ? P.slot_bits[tid] : cl.nbits[tid]);
             /* the prefilter hashes with the kernel-wide multiplier */
             if (cl.mult[tid] != P.pf_mult) pf.slot_off = 0xffffffffu;
         } else {

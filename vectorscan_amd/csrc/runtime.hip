@@ -56,9 +56,10 @@ namespace {
 
 const int LIT_WAVES = 16;
 const int LIT_THREADS = 1024;
-const size_t LDS_BUDGET = 160 * 1024 - 4096; /* minus static LDS (confirm params,
-                                                ring cursors, 2 KiB confirm queue) */
-const uint32_t SLOT_WORDS_MAX = 4096;        /* 16 KiB of slot bitmaps */
+const size_t LDS_BUDGET = 160 * 1024 - 12288; /* minus static LDS (confirm params,
+                                                 ring cursors, 8 KiB confirm queue) */
+const uint32_t SLOT_WORDS_MAX = 3072;        /* 12 KiB of slot bitmaps (coarsened
+                                                beyond, see vsa_db_load) */
 
 /* d_counters layout (u64): [0..7] scan counters, [16 + 16 r] region
  * tickets (one 128-B line each), [PAIR_BASE + 16 k] double-shufti stage
@@ -124,6 +125,7 @@ struct vsa_db {
     uint32_t *d_slots = nullptr; /* litIndex-occupancy bitmaps (prefilter) */
     uint32_t slot_words = 0;
     uint32_t slot_off[16];
+    uint8_t slot_bits[16] = {0}; /* prefilter hash bits per bucket (<= nBits) */
     uint64_t pf_mult = 0;
 };
 
@@ -318,6 +320,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.slotmap = db->d_slots;
     P.slot_words = db->slot_words;
     memcpy(P.slot_off, db->slot_off, sizeof(P.slot_off));
+    memcpy(P.slot_bits, db->slot_bits, sizeof(P.slot_bits));
     P.pf_mult = db->pf_mult;
     if (db->mode == VSA_MODE_FDR) {
         size_t tb = (size_t)db->table_entries * 8;
@@ -979,22 +982,43 @@ int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
         for (uint32_t b = 0; b < 16; b++) db->slot_off[b] = 0xffffffffu;
         const bool no_pf = getenv("VSA_NO_PREFILTER") != nullptr;
         db->pf_mult = 0;
+        /* eligible buckets (one kernel-wide multiplier); when the exact
+         * bitmaps exceed SLOT_WORDS_MAX the largest are coarsened: bit h >> k
+         * of a 2^(nbits - k)-bit map = OR of the exact bits it covers (the
+         * hash's top nbits - k bits), still a no-false-negative prefilter */
+        uint32_t nb_full[16] = {0}, nb_use[16] = {0};
         for (uint32_t b = 0; b < db->nbuckets && !no_pf; b++) {
             if (!db->conf_off[b]) continue;
             const uint8_t *fc = (const uint8_t *)confBase + db->conf_off[b];
             const uint32_t nbits = *(const uint32_t *)(fc + 16);
             const uint64_t mult = *(const uint64_t *)(fc + 8);
             if (!db->pf_mult) db->pf_mult = mult;
-            if (mult != db->pf_mult) continue; /* kernel hashes with one multiplier */
-            if (nbits > 24) continue;
-            const uint32_t n = 1u << nbits;
-            const uint32_t words = (n + 31) / 32;
+            if (mult != db->pf_mult || nbits > 24 || nbits < 1) continue;
+            nb_full[b] = nb_use[b] = nbits;
+        }
+        auto words_of = [](uint32_t bits) { return bits ? ((1u << bits) + 31) / 32 : 0u; };
+        for (;;) {
+            uint32_t tot = 0, big = 16;
+            for (uint32_t b = 0; b < 16; b++) {
+                tot += words_of(nb_use[b]);
+                if (nb_use[b] > 5 && (big == 16 || nb_use[b] > nb_use[big])) big = b;
+            }
+            if (tot <= SLOT_WORDS_MAX || big == 16) break;
+            nb_use[big]--;
+        }
+        for (uint32_t b = 0; b < db->nbuckets; b++) {
+            if (!nb_use[b]) continue;
+            const uint8_t *fc = (const uint8_t *)confBase + db->conf_off[b];
+            const uint32_t n = 1u << nb_full[b], k = nb_full[b] - nb_use[b];
+            const uint32_t words = words_of(nb_use[b]);
             if (slots.size() + words > SLOT_WORDS_MAX) continue;
             const uint32_t *li = (const uint32_t *)(fc + 32);
             db->slot_off[b] = (uint32_t)slots.size();
+            db->slot_bits[b] = (uint8_t)nb_use[b];
             slots.resize(slots.size() + words, 0);
             for (uint32_t h = 0; h < n; h++) {
-                if (li[h]) slots[db->slot_off[b] + h / 32] |= 1u << (h % 32);
+                const uint32_t c = h >> k;
+                if (li[h]) slots[db->slot_off[b] + c / 32] |= 1u << (c % 32);
             }
         }
         db->slot_words = (uint32_t)slots.size();
