@@ -276,6 +276,13 @@ int vsa_shufti_build_double_masks(const uint8_t onechar[32], const uint8_t *pair
 int64_t vsa_verm_find(int mode, uint8_t c1, uint8_t c2, uint8_t m1, uint8_t m2,
                       int nocase, const uint8_t *buf, size_t len);
 
+/* Host-only: the first-stage table the engine derives from an FDR / Teddy
+ * blob's confirm records (FDR: 2^14 u64 entries, 8 positions x 8 buckets,
+ * key = b[p] | (b[p+1] & 0x3f) << 8; Teddy: 256 entries, 8 x 8; Fat Teddy:
+ * 256 entries, 4 x 16).  Returns entries written or a VSA_E_* code. */
+int vsa_derive_first_stage(const void *hwlm, size_t size, uint64_t *table, uint32_t cap,
+                           uint32_t *key_bits, uint32_t *field_bits);
+
 /* Optional: hs_scratch field offsets for INCLUDED_JUMP squash replay
  * (offsetof(struct hs_scratch, fdr_conf / fdr_conf_offset)); the defaults
  * are the x86-64 layout of src/scratch.h:172-219. */

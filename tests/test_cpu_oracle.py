@@ -441,3 +441,51 @@ def test_oracle_accel_correct_schemes_keep_matches():
         hist = rand_data(rng, rng.choice([0, 3, 30]), b"abcdefgh")
         st, m = oracle.hwlm_exec_stream(blob.ptr, hist, data, cap=1 << 16)
         assert set(m) == stream_expected(lits, hist, data, 0), (trial, kind, len(hist))
+
+
+# ------------------------------------------------- derived first stages ---
+
+def _first_stage_candidates(table, key_bits, field_bits, data):
+    """numpy restatement of the kernels' first stage: candidate ends (any
+    bucket) from the derived table; positions before the buffer pass."""
+    b = np.frombuffer(bytes(data), np.uint8).astype(np.uint64)
+    n = len(b)
+    if key_bits == 14:
+        nxt = np.concatenate([b[1:], np.zeros(1, np.uint64)])
+        key = b | ((nxt & np.uint64(0x3F)) << np.uint64(8))
+    else:
+        key = b
+    x = table[key.astype(np.int64)]
+    nfields = 64 // field_bits
+    fmask = np.uint64((1 << field_bits) - 1)
+    conf = np.zeros(n, np.uint64)
+    for k in range(nfields):
+        f = (x >> np.uint64(field_bits * k)) & fmask
+        conf[k:] |= f[:n - k]
+    return np.nonzero((~conf) & fmask)[0]
+
+
+@pytest.mark.parametrize("nlits,hint,minlen", [(2000, 0, 1), (2000, 0, 4), (40, 11, 1),
+                                                (40, 17, 4), (60, 3, 1), (60, 8, 4)])
+def test_derived_first_stage_no_false_negatives(nlits, hint, minlen):
+    """The first stage the engine derives from the confirm records (FDR
+    domain-14 table, Teddy / Fat Teddy exact byte tables)
+    passes every end the reference's confirm accepts, and (literals of 4+
+    bytes) stays selective."""
+    import bench
+    rng = random.Random(900 + nlits + hint + minlen)
+    lits = [vsa.HwlmLiteral(bytes(rng.randint(0x20, 0x7E)
+                                  for _ in range(rng.randint(minlen, 8))),
+                            rng.random() < 0.1, i) for i in range(nlits)]
+    blob = build_or_none(lits, hint)
+    if blob is None:
+        pytest.skip("engine not buildable for this set")
+    table, kb, fb = vsa.derive_first_stage(blob)
+    data = bench.make_corpus(1 << 20, lits, seed=nlits + hint, plant_every=512)
+    st, m = oracle.fdr_exec(vsa.engine_blob(blob), data, cap=1 << 20)
+    assert st == 0 and len(m) > 1000
+    cand = set(_first_stage_candidates(table, kb, fb, data).tolist())
+    missing = [e for e, _ in m if e not in cand]
+    assert not missing, missing[:10]
+    if minlen >= 4:
+        assert len(cand) < 0.05 * len(data), len(cand)

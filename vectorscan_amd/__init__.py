@@ -146,6 +146,8 @@ _sig("vsa_scan_copy_device", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, cty
      ctypes.c_uint64, _u64p)
 _sig("vsa_scan_candidates", ctypes.c_uint64, ctypes.c_void_p)
 _sig("vsa_scan_debug_counters", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)
+_sig("vsa_derive_first_stage", ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+     ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32))
 _sig("vsa_scan_kernel_ms", ctypes.c_double, ctypes.c_void_p)
 _sig("vsa_class_scan", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, _u64p,
@@ -258,6 +260,19 @@ def hwlm_build(lits, engine_hint=-1, allow_noodle=True, allow_teddy=True,
     if rc != 0:
         raise BuildError("hwlm_build failed (%d)" % rc)
     return Blob(out.value, size.value)
+
+
+def derive_first_stage(blob):
+    """(table u64 array, key_bits, field_bits) the engine derives from an FDR
+    or Teddy blob's confirm records (host only; see vsa_derive_first_stage)"""
+    cap = 1 << 14
+    out = np.zeros(cap, np.uint64)
+    kb, fb = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    n = lib.vsa_derive_first_stage(blob.ptr, blob.size, out.ctypes.data, cap, ctypes.byref(kb),
+                                   ctypes.byref(fb))
+    if n < 0:
+        raise BuildError("vsa_derive_first_stage failed with %d" % n)
+    return out[:n], kb.value, fb.value
 
 
 def engine_blob(blob):

@@ -1074,6 +1074,41 @@ int vsa_db_free(vsa_db_t *db) {
     return VSA_OK;
 }
 
+/* Host-only: the first stage vsa_db_load derives for an HWLM blob (FDR:
+ * 2^bits stride-1 entries keyed by b[p] | (b[p+1] & mask) << 8; Teddy / Fat
+ * Teddy: 256 byte entries), for tests and tools.  *key_bits = 14 for FDR,
+ * 8 for Teddy; *field_bits = buckets per field (8 or 16).  Returns the
+ * number of entries written (<= cap), or a VSA_E_* code. */
+int vsa_derive_first_stage(const void *hwlm, size_t size, uint64_t *table, uint32_t cap,
+                           uint32_t *key_bits, uint32_t *field_bits) {
+    if (!hwlm || !table || size < VSA_ROUNDUP_CL(sizeof(HWLM))) return VSA_E_INVALID;
+    const HWLM *h = (const HWLM *)hwlm;
+    if (h->type != HWLM_ENGINE_FDR) return VSA_E_INVALID;
+    const uint8_t *eng = (const uint8_t *)hwlm + VSA_ROUNDUP_CL(sizeof(HWLM));
+    const uint32_t id = ((const uint32_t *)eng)[0];
+    const uint32_t *confBase = (const uint32_t *)(eng + ((const uint32_t *)eng)[4]);
+    uint32_t conf_off[16] = {0};
+    std::vector<uint64_t> T;
+    if (id == VSA_ENGINE_FDR) {
+        for (int b = 0; b < 8; b++) conf_off[b] = confBase[b];
+        derive_fdr_table(eng, conf_off, 14, T);
+        *key_bits = 14;
+        *field_bits = 8;
+    } else if (vsa_engine_is_teddy(id)) {
+        const bool fat = vsa_engine_is_fat(id);
+        for (int b = 0; b < (fat ? 16 : 8); b++) conf_off[b] = confBase[b];
+        if (fat) derive_teddy_table(eng, conf_off, 16, 4, 16, T);
+        else derive_teddy_table(eng, conf_off, 8, 8, 8, T);
+        *key_bits = 8;
+        *field_bits = fat ? 16 : 8;
+    } else {
+        return VSA_E_INVALID;
+    }
+    const uint32_t n = (uint32_t)std::min<size_t>(cap, T.size());
+    memcpy(table, T.data(), n * sizeof(uint64_t));
+    return (int)n;
+}
+
 int vsa_db_engine(const vsa_db_t *db) {
     if (!db) return VSA_E_INVALID;
     return db->type == HWLM_ENGINE_NOOD ? HWLM_ENGINE_NOOD : (int)db->engine_id;
