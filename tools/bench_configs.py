@@ -8,6 +8,8 @@ config 4, the headline).  One JSON line per workload:
         output = 1 bit per byte bitmap + first / last / count
   cfg3  Teddy 48 literals (8 buckets) and 64 literals (Fat Teddy), len 4-8
         printable, seed 7+n — 1 GiB printable, seed 3, planted every 4 KiB
+  cfg4s the cfg 4 database over a 1 GiB stream cut into 16 KiB / 1 MiB
+        writes, each a streaming call with history, one batched launch
 
 value = input bytes / kernel time (hipEvents on the scan stream); each line
 also carries wall time per call (launch + count read-back + sort) and a
@@ -92,6 +94,40 @@ def cfg_literal(ctx, torch, name, lits, n, plant_every, seed, steps, warmup, sam
     del data
 
 
+def cfg_stream(ctx, torch, steps, warmup, chunk):
+    """cfg 4 database over 1 GiB as ONE stream cut into `chunk`-byte writes,
+    every write a streaming call (fdrExecStreaming semantics, 16 history
+    bytes) in one batched launch; parity = the same match records as the
+    whole buffer scanned as one block (itself oracle-pinned)."""
+    import bench
+    import vectorscan_amd as vsa
+    n = 1 << 30
+    lits = bench.make_literals(5000, seed=12)
+    blob = vsa.hwlm_build(lits)
+    db = vsa.Database(ctx, blob)
+    data = bench.make_corpus_device(torch, n, lits, seed=5, plant_every=64 << 10,
+                                    device=torch.device("cuda", 0))
+    torch.cuda.synchronize()
+    dptr = data.data_ptr()
+    offs = np.arange(0, n, chunk, dtype=np.uint64)
+    lens = np.full(len(offs), chunk, np.uint64)
+    hl = np.minimum(offs, 16).astype(np.uint64)
+    nm = [0]
+
+    def step():
+        nm[0] = ctx.scan_blocks_stream(db, dptr, offs, lens, hl)
+
+    kms, wall = timed(step, steps, warmup, ctx)
+    got = ctx.results(nm[0])
+    k1 = ctx.scan_blocks(db, dptr, [0], [n])
+    want = ctx.results(k1)
+    ok = bool(np.array_equal(got["key"], want["key"]) and np.array_equal(got["id"], want["id"]))
+    line("cfg4s FDR 5k stream of %d KiB writes, 1 GiB" % (chunk >> 10), n, kms, wall,
+         16 * nm[0], ok, {"matches": nm[0], "blocks": len(offs)})
+    db.close()
+    del data
+
+
 def cfg_class(ctx, torch, steps, warmup):
     import vectorscan_amd as vsa
     n = 256 << 20
@@ -137,7 +173,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--only", default="1,2,3")
+    ap.add_argument("--only", default="1,2,3,4s")
     args = ap.parse_args()
     import torch
     import vectorscan_amd as vsa
@@ -150,6 +186,9 @@ def main():
                         lits, 1 << 30, 4096, 1, args.steps, args.warmup, 16 << 20)
     if "2" in only:
         cfg_class(ctx, torch, args.steps, args.warmup)
+    if "4s" in only:
+        for chunk in (16 << 10, 1 << 20):
+            cfg_stream(ctx, torch, args.steps, args.warmup, chunk)
     if "3" in only:
         for nl in (48, 64):
             cfg_literal(ctx, torch, "cfg3 teddy %d literals 1 GiB" % nl,
