@@ -56,6 +56,7 @@ struct VsaLitParams {
     uint32_t nregions;      /* ticket regions (counters[16 + 16 r], one
                                128-B line each), <= 8 */
     uint64_t nsegs;
+    const uint32_t *seg_blk;  /* block of each segment */
     const uint64_t *table;  /* FDR domain table / Teddy combined byte table */
     uint32_t table_entries;
     uint32_t dmask;

@@ -903,16 +903,11 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
         if constexpr (MODE == VSA_MODE_NOOD) {
             /* noodle hits are final: emit (end, id) */
             u32 hits = e[4];
-            /* one output reservation per gather (wave prefix of hit counts) */
-            u32 total;
-            const u32 n = (u32)__popc(hits);
-            const u32 pre = wave_excl_scan(n, &total);
-            total = readfirstlane_u32(total);
-            if (total) {
-                unsigned long long s0 = 0;
-                if (lane == 0) s0 = atomicAdd(&P.counters[0], (unsigned long long)total);
-                u64 slot = (((u64)readlane_u32((u32)(s0 >> 32), 0) << 32) |
-                            readlane_u32((u32)s0, 0)) + pre;
+            /* one atomic per lane with hits (measured faster here than a
+             * wave prefix sum + one atomic per gather) */
+            if (hits) {
+                const u32 n = (u32)__popc(hits);
+                unsigned long long slot = atomicAdd(&P.counters[0], (unsigned long long)n);
                 consumed += n;
                 for (; hits; hits &= hits - 1, slot++) {
                     const u32 j = __ffs(hits) - 1;
@@ -1125,27 +1120,37 @@ vsa_lit_scan(VsaLitParams P) {
     u32 reg_i = 0; /* regions tried so far */
     u32 reg = blockIdx.x % nreg;
     auto region_lo = [&](u32 r) { return P.nsegs * r / nreg; };
-    auto next_seg = [&](u64 cur, bool first) -> u64 {
-        if (!P.dynamic) return first ? (u64)blockIdx.x * LIT_SCANNERS + wave : cur + G;
+    /* the next ticket is taken (lane 0, returning atomic) during the last
+     * group of the current segment's sweep, so its latency hides behind
+     * that group without one wave holding a whole segment ahead */
+    auto take = [&]() -> unsigned long long {
+        unsigned long long t = 0;
+        if (lane == 0) t = atomicAdd(&P.counters[16 + 16 * reg], 1ULL);
+        return t;
+    };
+    auto resolve = [&](unsigned long long t0) -> u64 {
+        u64 t = ((u64)readlane_u32((u32)(t0 >> 32), 0) << 32) | readlane_u32((u32)t0, 0);
         for (;;) {
-            unsigned long long t = 0;
-            if (lane == 0) t = atomicAdd(&P.counters[16 + 16 * reg], 1ULL);
-            t = ((u64)readlane_u32((u32)(t >> 32), 0) << 32) | readlane_u32((u32)t, 0);
             const u64 sg = region_lo(reg) + t;
             if (sg < region_lo(reg + 1)) return sg;
             if (++reg_i == nreg) return P.nsegs; /* every region drained */
             reg = (reg + 1) % nreg;
+            const unsigned long long t1 = take();
+            t = ((u64)readlane_u32((u32)(t1 >> 32), 0) << 32) | readlane_u32((u32)t1, 0);
         }
     };
-    for (u64 seg = next_seg(0, true); seg < P.nsegs; seg = next_seg(seg, false)) {
-        /* block of the segment: last block with seg_first <= seg */
-        u32 lo = 0, hi = P.nblocks - 1;
-        while (lo < hi) {
-            const u32 mid = (lo + hi + 1) >> 1;
-            if (P.blocks[mid].seg_first <= seg) lo = mid;
-            else hi = mid - 1;
-        }
-        const u32 blk = readfirstlane_u32(lo);
+    u64 seg = P.dynamic ? resolve(take()) : (u64)blockIdx.x * LIT_SCANNERS + wave;
+    while (seg < P.nsegs) {
+        unsigned long long t_next = 0;
+        bool have_next = false;
+        auto prefetch_ticket = [&]() {
+            if (P.dynamic && !have_next) {
+                t_next = take();
+                have_next = true;
+            }
+        };
+        /* block of the segment: host-built segment -> block table */
+        const u32 blk = readfirstlane_u32(P.seg_blk[seg]);
         const VsaBlock B = P.blocks[blk];
         SegCtx S;
         S.blk = blk;
@@ -1250,6 +1255,7 @@ vsa_lit_scan(VsaLitParams P) {
             after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.vlo, S.bhi);
             const u32 ng = nf / LIT_DEPTH;
             for (u32 g = 0; g < ng; g++) {
+                if (g + 1 == ng) prefetch_ticket();
 #pragma unroll
                 for (int k = 0; k < LIT_DEPTH; k++) {
                     const u32 it = g * LIT_DEPTH + k;
@@ -1275,6 +1281,7 @@ vsa_lit_scan(VsaLitParams P) {
                 }
             }
         }
+        prefetch_ticket();
         for (u32 it = f1; it < niters; it++) {
             const int64_t ib = s_lo + 1024 * (int64_t)it;
             const uint4 cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
@@ -1284,6 +1291,7 @@ vsa_lit_scan(VsaLitParams P) {
         }
         ncand_total = is.ncand;
         ring_tail_cache = is.tail_cache;
+        seg = P.dynamic ? resolve(t_next) : seg + G;
     }
     /* every push of this wave precedes this (LDS order) */
     if (lane == 0) __hip_atomic_fetch_add(&q_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

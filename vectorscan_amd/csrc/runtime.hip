@@ -83,6 +83,9 @@ struct Workspace {
     VsaBlock *d_blocks = nullptr;
     VsaBlock *h_blocks = nullptr;
     uint32_t blocks_cap = 0;
+    uint32_t *d_segblk = nullptr; /* block of each segment */
+    uint32_t *h_segblk = nullptr;
+    uint64_t segblk_cap = 0;
 };
 
 } // namespace
@@ -165,6 +168,20 @@ int ensure_in(vsa_ctx *c, size_t need) {
     size_t cap = std::max<size_t>(need + 64, 1u << 20);
     VSA_CHECK(hipMalloc(&w.d_in, cap));
     w.in_cap = cap;
+    return VSA_OK;
+}
+
+int ensure_segblk(vsa_ctx *c, uint64_t n) {
+    Workspace &w = c->ws;
+    if (n <= w.segblk_cap) return VSA_OK;
+    if (w.d_segblk) (void)hipFree(w.d_segblk);
+    if (w.h_segblk) (void)hipHostFree(w.h_segblk);
+    w.d_segblk = nullptr;
+    w.h_segblk = nullptr;
+    const uint64_t cap = std::max<uint64_t>(n, 1024);
+    VSA_CHECK(hipMalloc(&w.d_segblk, cap * sizeof(uint32_t)));
+    VSA_CHECK(hipHostMalloc((void **)&w.h_segblk, cap * sizeof(uint32_t), hipHostMallocDefault));
+    w.segblk_cap = cap;
     return VSA_OK;
 }
 
@@ -264,6 +281,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         memset(&P, 0, sizeof(P));
         P.data = d_data;
         P.blocks = w.d_blocks;
+        P.seg_blk = w.d_segblk;
         P.nblocks = nb;
         P.seg_bytes = seg_bytes;
     P.dynamic = getenv("VSA_STATIC_SEGS") ? 0u : 1u;
@@ -291,6 +309,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     memset(&P, 0, sizeof(P));
     P.data = d_data;
     P.blocks = w.d_blocks;
+    P.seg_blk = w.d_segblk;
     P.nblocks = nb;
     P.seg_bytes = seg_bytes;
     P.dynamic = getenv("VSA_STATIC_SEGS") ? 0u : 1u;
@@ -380,6 +399,9 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
                      uint32_t nb, uint32_t flags, uint64_t *n_out,
                      const uint64_t *hlens = nullptr) {
     if (!c || !db || !d_data || !offs || !lens || (!nb)) return VSA_E_INVALID;
+    /* an asynchronous scan still in flight may be reading the pinned block
+     * and segment tables rewritten below: let it finish first */
+    if (c->pending) VSA_CHECK(hipStreamSynchronize(c->stream));
     int r = ensure_blocks(c, nb);
     if (r) return r;
     if ((r = ensure_out(c, 1)) != VSA_OK) return r;
@@ -423,6 +445,16 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
     }
     VSA_CHECK(hipMemcpyAsync(c->ws.d_blocks, c->ws.h_blocks, nb * sizeof(VsaBlock),
                              hipMemcpyHostToDevice, c->stream));
+    if (segs) {
+        /* the kernel maps a segment ticket to its block with one load */
+        if ((r = ensure_segblk(c, segs)) != VSA_OK) return r;
+        for (uint32_t i = 0; i < nb; i++) {
+            const uint64_t e = (i + 1 < nb) ? c->ws.h_blocks[i + 1].seg_first : segs;
+            for (uint64_t sg = c->ws.h_blocks[i].seg_first; sg < e; sg++) c->ws.h_segblk[sg] = i;
+        }
+        VSA_CHECK(hipMemcpyAsync(c->ws.d_segblk, c->ws.h_segblk, segs * sizeof(uint32_t),
+                                 hipMemcpyHostToDevice, c->stream));
+    }
     int end_bits = bits_for(span);
     if (segs == 0) {
         c->last_n = 0;
@@ -808,6 +840,8 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (w.h_counters) (void)hipHostFree(w.h_counters);
     if (w.d_blocks) (void)hipFree(w.d_blocks);
     if (w.h_blocks) (void)hipHostFree(w.h_blocks);
+    if (w.d_segblk) (void)hipFree(w.d_segblk);
+    if (w.h_segblk) (void)hipHostFree(w.h_segblk);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     (void)hipStreamDestroy(c->stream);
