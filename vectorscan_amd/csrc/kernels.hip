@@ -674,19 +674,22 @@ __device__ __forceinline__ IterState nood_iter(const VsaLitParams &P, const LitS
     out.pbytes = ((u64)readlane_u32(d[3], WAVE - 1) << 32) | readlane_u32(d[2], WAVE - 1);
     if (!EDGE) {
         /* key prefilter (the reference scans for the literal's key bytes
-         * before confirming, noodle_engine_simd.hpp:173-226): the last two
-         * literal bytes under their masks, four positions per dword, with a
-         * SWAR zero-byte test; the full compare runs only when some lane
-         * has a key hit (msk_len 1: the second byte's mask and cmp are 0) */
-        const u32 M1 = (u32)(P.nood_msk >> 56) * 0x01010101u;
-        const u32 C1 = (u32)(P.nood_cmp >> 56) * 0x01010101u;
-        const u32 M0 = ((u32)(P.nood_msk >> 48) & 0xffu) * 0x01010101u;
-        const u32 C0 = ((u32)(P.nood_cmp >> 48) & 0xffu) * 0x01010101u;
+         * before confirming, noodle_engine_simd.hpp:173-226): the last
+         * three literal bytes under their masks, four positions per dword,
+         * with a SWAR zero-byte test; the full compare runs only when some
+         * lane has a key hit (shorter literals: the missing bytes' mask and
+         * cmp are 0, always equal) */
+        auto rep8 = [](u64 v, int byte) { return ((u32)(v >> (8 * byte)) & 0xffu) * 0x01010101u; };
+        const u32 M2 = rep8(P.nood_msk, 7), C2 = rep8(P.nood_cmp, 7);
+        const u32 M1 = rep8(P.nood_msk, 6), C1 = rep8(P.nood_cmp, 6);
+        const u32 M0 = rep8(P.nood_msk, 5), C0 = rep8(P.nood_cmp, 5);
         u32 z = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const u32 prev = __builtin_amdgcn_alignbyte(d[k], k ? d[k - 1] : pv3, 3);
-            const u32 t = ((d[k] & M1) ^ C1) | ((prev & M0) ^ C0);
+            const u32 lo = k ? d[k - 1] : pv3;
+            const u32 p1 = __builtin_amdgcn_alignbyte(d[k], lo, 3);
+            const u32 p2 = __builtin_amdgcn_alignbyte(d[k], lo, 2);
+            const u32 t = or3((d[k] & M2) ^ C2, (p1 & M1) ^ C1, (p2 & M0) ^ C0);
             z |= (t - 0x01010101u) & ~t;
         }
         if (!__any((z & 0x80808080u) != 0)) return out;
