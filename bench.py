@@ -109,8 +109,8 @@ def cpu_baseline(blob, sample_fn, threads, budget_s=10.0, chunk=256 << 20, max_b
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--gib", type=float, default=4.0, help="corpus GiB per rank")
     ap.add_argument("--blocks", type=int, default=4)
     ap.add_argument("--lits", type=int, default=5000)
