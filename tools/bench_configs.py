@@ -171,8 +171,8 @@ def cfg_class(ctx, torch, steps, warmup):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--only", default="1,2,3,4s")
     args = ap.parse_args()
     import torch
