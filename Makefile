@@ -4,10 +4,11 @@ ARCH ?= gfx950
 CSRC := vectorscan_amd/csrc
 LIB := vectorscan_amd/libvectorscan_amd.so
 ORACLE := oracle/_build/liboracle.so
+HARNESS := tests/c/abi_harness
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
             -Wno-unused-parameter -Iinclude
 
-all: $(LIB) $(ORACLE)
+all: $(LIB) $(ORACLE) $(HARNESS)
 
 $(CSRC)/compile.o: $(CSRC)/compile.cpp $(CSRC)/hs_layout.h $(CSRC)/vsa_internal.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -26,7 +27,14 @@ $(ORACLE): oracle/oracle.c
 	mkdir -p oracle/_build
 	gcc -O2 -std=gnu11 -fPIC -shared -Wall -pthread $< -o $@
 
+# test-only C caller of the drop-ins (real __m128i signatures), checked
+# against the oracle
+$(HARNESS): tests/c/abi_harness.c include/vectorscan_amd.h $(LIB) $(ORACLE)
+	gcc -O2 -std=gnu11 -Wall -Iinclude $< -o $@ -Lvectorscan_amd -lvectorscan_amd \
+	    -Loracle/_build -loracle -Wl,-rpath,'$$ORIGIN/../../vectorscan_amd' \
+	    -Wl,-rpath,'$$ORIGIN/../../oracle/_build'
+
 clean:
-	rm -f $(CSRC)/*.o $(LIB) $(ORACLE)
+	rm -f $(CSRC)/*.o $(LIB) $(ORACLE) $(HARNESS)
 
 .PHONY: all clean

@@ -2,28 +2,40 @@
 """bench.py — GB/s scanned, hsbench block mode, FDR 5k-literal database
 (BASELINE.json configs[3], the north star's headline workload).
 
-One step = one device launch that scans the rank's 4 GiB corpus as 4 x 1 GiB
-blocks (each block one hwlmExec: hs_scan takes a 32-bit length,
-src/hs_runtime.h:479) and leaves the confirmed matches sorted in reference
-callback order in HBM; the match count is read back every step.  Inputs are
-resident in HBM before the timed region.
+The corpus is ONE 4 GiB synthetic corpus made of 4 x 1 GiB blocks (each
+block one hs_scan / hwlmExec call: hs_scan takes a 32-bit length,
+src/hs_runtime.h:479).  One step = one pass of the hot path over the whole
+corpus: every rank scans its stripe of it (one device launch), its confirmed
+matches are sorted on the device into the reference callback order and their
+count is read back; with N > 1 ranks the step ends with the RCCL gather of
+every rank's match records to rank 0, merged in end order (where the
+sequential host replay would run).  Inputs are resident in HBM before the
+timed region.
 
-Multi-GPU: one process per GPU (torch.distributed, RCCL); every rank scans
-its own 4 GiB stripe of an N x 4 GiB corpus (weak scaling, no data-path
-collective in the scan); each step ends with the RCCL gather of the ranks'
-sorted match records to rank 0 (where the sequential host replay runs,
-vectorscan_amd/stripe.py).  The timed region is bracketed by barrier +
-synchronize and the max over ranks is reported.
+Multi-GPU: one process per GPU.  `--gpus N` without a torchrun
+environment spawns the N rank processes itself (before any GPU call); under
+torchrun (WORLD_SIZE set) it checks N against WORLD_SIZE.  The corpus's end
+positions are cut into N contiguous ranges (vectorscan_amd/stripe.py
+plan_corpus_stripes): rank r holds its range plus the 7 bytes before it and
+scans one window per block it overlaps, reporting only its own ends, so the
+union over ranks is exactly the single-GPU match set (strong scaling: total
+work fixed).  The timed region is bracketed by barrier + synchronize and the
+max over ranks is reported.
 
-Extra JSON fields: roofline (kernel-only HBM GB/s from hipEvents vs the 8 TB/s
-MI355X peak), cpu_baseline (the scalar oracle on a bounded sample of the
-same corpus, striped over the box's 16-thread CPU share), parity (GPU ==
-oracle on a 64 MiB sample).
+Parity (every run): rank 0 checks the TIMED step's gathered match set, per
+block, against the oracle (oracle/oracle.c, the scalar restatement) over all
+4 GiB: match count and an order-free (sum, xor) digest of the (end, id) pairs
+(`parity_bytes` = bytes checked), plus sortedness of the merged keys.
+
+Extra JSON fields: roofline (rank 0's scan kernel from hipEvents vs the 8 TB/s
+MI355X peak; PMC traffic from profiles/), cpu_baseline (timed on the same
+host cores, see --cpu-kind).
 """
 import argparse
 import json
 import os
 import random
+import socket
 import sys
 import time
 
@@ -34,6 +46,7 @@ sys.path.insert(0, ROOT)
 
 PRINTABLE = np.arange(0x20, 0x7F, dtype=np.uint8)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+CHUNK = 64 << 20       # corpus generation unit (position-addressable)
 
 
 def make_literals(n, seed=12, minlen=4, maxlen=8, nocase_frac=0.02):
@@ -71,39 +84,50 @@ def make_corpus(n, lits, seed=5, plant_every=64 << 10):
     return data
 
 
-def make_corpus_device(torch, n, lits, seed, plant_every, device):
-    """same construction on the GPU (torch is plumbing here)."""
+def make_corpus_device(torch, lo, hi, total, lits, seed, plant_every, device, plan=None):
+    """Bytes [lo, hi) of the synthetic corpus of `total` bytes, generated on
+    the GPU (torch is plumbing here).  Position-addressable: 64 MiB chunk k
+    comes from its own generator, so every rank builds exactly its stripe of
+    the same global corpus."""
+    out = torch.empty(hi - lo, dtype=torch.uint8, device=device)
     g = torch.Generator(device=device)
-    g.manual_seed(seed)
-    data = torch.empty(n, dtype=torch.uint8, device=device)
-    chunk = 256 << 20
-    for o in range(0, n, chunk):
-        m = min(chunk, n - o)
-        data[o:o + m] = torch.randint(0x20, 0x7F, (m,), dtype=torch.uint8, device=device,
-                                      generator=g)
-    idx, val = plant_plan(n, lits, seed, plant_every)
-    data[torch.from_numpy(idx).to(device)] = torch.from_numpy(val).to(device)
-    return data
+    for k in range(lo // CHUNK, (hi - 1) // CHUNK + 1 if hi > lo else 0):
+        g.manual_seed(seed * 1000003 + k)
+        c = torch.randint(0x20, 0x7F, (CHUNK,), dtype=torch.uint8, device=device, generator=g)
+        a, b = max(lo, k * CHUNK), min(hi, (k + 1) * CHUNK)
+        out[a - lo:b - lo] = c[a - k * CHUNK:b - k * CHUNK]
+    idx, val = plan if plan is not None else plant_plan(total, lits, seed, plant_every)
+    sel = (idx >= lo) & (idx < hi)
+    if sel.any():
+        out[torch.from_numpy(idx[sel] - lo).to(device)] = torch.from_numpy(val[sel]).to(device)
+    return out
 
 
-def cpu_baseline(blob, sample_fn, threads, budget_s=10.0, chunk=256 << 20, max_bytes=2 << 30):
-    """scalar oracle (oracle/oracle.c restatement of fdrExec) on a bounded
-    sample: chunks of the rank-0 corpus, each striped over `threads` host
-    threads (7-byte halo, counts only), until `budget_s` of wall time."""
+def block_digests(ends, ids, block_len, nblocks):
+    """per-block (count, sum, xor) digests of global (end, id) records"""
     import oracle
-    import vectorscan_amd as vsa
-    eng = vsa.engine_blob(blob)
-    done, t, i = 0, 0.0, 0
-    while t < budget_s and done < max_bytes:
-        buf = sample_fn(i * chunk, chunk)
-        if len(buf) == 0:
-            break
-        t0 = time.perf_counter()
-        oracle.fdr_count_mt(eng, buf, threads)
-        t += time.perf_counter() - t0
-        done += len(buf)
-        i += 1
-    return done, t
+    ends = np.asarray(ends, np.uint64)
+    ids = np.asarray(ids, np.uint64)
+    blk = (ends // np.uint64(block_len)).astype(np.int64)
+    out = []
+    for b in range(nblocks):
+        sel = blk == b
+        out.append(oracle.digest_of(ends[sel] - np.uint64(b * block_len), ids[sel]))
+    return out
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawned(rank, world, port, args):
+    os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    run(args)
 
 
 def main():
@@ -111,15 +135,29 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--gib", type=float, default=4.0, help="corpus GiB per rank")
+    ap.add_argument("--gib", type=float, default=4.0, help="corpus GiB (whole job)")
     ap.add_argument("--blocks", type=int, default=4)
     ap.add_argument("--lits", type=int, default=5000)
-    ap.add_argument("--cpu-budget", type=float, default=10.0)
-    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline timing")
+    ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="host threads for cpu_baseline (default min(16, cpus))")
+                    help="host threads for the oracle / cpu_baseline (default min(16, cpus))")
     args = ap.parse_args()
+    env_world = int(os.environ.get("WORLD_SIZE", "0"))
+    if env_world:
+        if args.gpus not in (1, env_world):
+            raise SystemExit("bench: --gpus %d but WORLD_SIZE=%d" % (args.gpus, env_world))
+        args.gpus = env_world
+        run(args)
+    elif args.gpus > 1:
+        # one process per GPU, started before this process touches the GPU
+        import torch.multiprocessing as mp
+        mp.spawn(_spawned, args=(args.gpus, _free_port(), args), nprocs=args.gpus, join=True)
+    else:
+        run(args)
 
+
+def run(args):
     import torch
     import vectorscan_amd as vsa
     from vectorscan_amd import stripe
@@ -128,47 +166,72 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
 
     ctx = vsa.Context(local)
     lits = make_literals(args.lits, seed=12)
     blob = vsa.hwlm_build(lits)
     db = vsa.Database(ctx, blob)
 
-    n = int(args.gib * (1 << 30))
-    data = make_corpus_device(torch, n, lits, seed=5 + 1000 * rank, plant_every=64 << 10,
-                              device=dev)
+    total = int(args.gib * (1 << 30))
+    bl = (total + args.blocks - 1) // args.blocks
+    nblocks = (total + bl - 1) // bl
+    plant_every = 64 << 10
+    pplan = plant_plan(total, lits, 5, plant_every)
+    cuts, plan = stripe.plan_corpus_stripes(total, bl, world)
+    wins = plan[rank]
+    # this rank's bytes: its windows (own range + 7-byte halo), from g0
+    g0 = min((w.wlo for w in wins), default=cuts[rank]) & ~255
+    g1 = cuts[rank + 1]
+    data = make_corpus_device(torch, g0, g1, total, lits, 5, plant_every, dev, pplan)
     torch.cuda.synchronize()
-    bl = n // args.blocks
-    offs = [i * bl for i in range(args.blocks)]
-    lens = [bl] * (args.blocks - 1) + [n - bl * (args.blocks - 1)]
     dptr = data.data_ptr()
+    offs = [w.wlo - g0 for w in wins]
+    lens = [w.wlen for w in wins]
+    rlos = [w.rlo for w in wins]
+    local_bytes = g1 - cuts[rank]
 
-    # N > 1: the step ends with the RCCL gather of every rank's sorted match
-    # records to rank 0 (device to device, over xGMI), where the host replay
-    # would run; the scan itself has no data-path collective.
-    gcap = 1 << 21
-    gkeys = torch.zeros(gcap, dtype=torch.int64, device=dev) if dist is not None else None
-    gids = torch.zeros(gcap, dtype=torch.int32, device=dev) if dist is not None else None
-    gathered = [0]
+    # N > 1: RCCL gather of the ranks' sorted records to rank 0 (device to
+    # device over xGMI), padded to the largest count
+    st = {"cap": 0, "gk": None, "gi": None, "keys": None, "ids": None}
+    g0s = None
+    if dist is not None:
+        t = torch.tensor([g0], dtype=torch.int64, device=dev)
+        g0s_t = torch.zeros(world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(g0s_t, t)
+        g0s = g0s_t.cpu().tolist()
 
     def step():
-        n_local = ctx.scan_blocks(db, dptr, offs, lens)
+        n_local = ctx.scan_blocks_ex(db, dptr, offs, lens, None, rlos)
         if dist is None:
             return n_local
-        if n_local > gcap:
-            raise RuntimeError("bench: %d matches exceed the gather buffer" % n_local)
-        ctx.results_to_device(gkeys.data_ptr(), gids.data_ptr(), gcap)
+        cnt = torch.tensor([n_local], dtype=torch.int64, device=dev)
+        counts = torch.zeros(world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(counts, cnt)
+        cl = counts.cpu().tolist()
+        m = max(max(cl), 1)
+        if m > st["cap"]:
+            st["cap"] = m + m // 4
+            st["gk"] = torch.zeros(st["cap"], dtype=torch.int64, device=dev)
+            st["gi"] = torch.zeros(st["cap"], dtype=torch.int32, device=dev)
+            st["ak"] = torch.zeros(world * st["cap"], dtype=torch.int64, device=dev)
+            st["ai"] = torch.zeros(world * st["cap"], dtype=torch.int32, device=dev)
+        ctx.results_to_device(st["gk"].data_ptr(), st["gi"].data_ptr(), st["cap"])
         ctx.sync()
-        got = stripe.gather_to_root(dist, gkeys, gids, n_local)
-        if got is not None:
-            gathered[0] = int(got[0].shape[0])
-        return n_local
+        ak, ai = st["ak"][:world * m], st["ai"][:world * m]
+        dist.all_gather_into_tensor(ak, st["gk"][:m])
+        dist.all_gather_into_tensor(ai, st["gi"][:m])
+        if rank == 0:
+            # merge in end order: ranks own increasing end ranges; keys
+            # become global corpus offsets
+            st["keys"] = torch.cat([ak[r * m:r * m + cl[r]] + (g0s[r] << 24)
+                                    for r in range(world)])
+            st["ids"] = torch.cat([ai[r * m:r * m + cl[r]] for r in range(world)])
+        return int(sum(cl))
 
     for _ in range(args.warmup):
         step()
@@ -189,55 +252,65 @@ def main():
     barrier()
     t1 = time.perf_counter()
     el = t1 - t0
-    ncand = int(ctx.candidates())  # of the last timed step
+    ncand = int(ctx.candidates())  # rank 0, last timed step
     if dist is not None:
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
-        cnt = torch.tensor([nm], dtype=torch.int64, device=dev)
-        dist.all_reduce(cnt)
-        total_matches = int(cnt.item())
-    else:
-        total_matches = nm
     ms_step = el / args.steps * 1e3
-    gbs = world * n / (el / args.steps) / 1e9
+    gbs = total / (el / args.steps) / 1e9
+
+    # records of the last timed step, global offsets (rank 0)
+    if rank == 0:
+        if dist is None:
+            res = ctx.results(nm)
+            keys, ids = res["key"], res["id"].astype(np.uint64)
+        else:
+            keys = st["keys"].cpu().numpy().view(np.uint64)
+            ids = st["ids"].cpu().numpy().astype(np.uint64)
+    kavg = float(np.mean(kms))
+    del data
+    torch.cuda.empty_cache()
 
     out = None
     if rank == 0:
-        kavg = float(np.mean(kms))
-        alg_bytes = n + 16 * nm  # input once + one 16-B record per match
+        import oracle
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        eng = vsa.engine_blob(blob)
+        parity, parity_bytes, cpu = None, 0, None
+        if not args.no_parity:
+            ends = keys >> np.uint64(24)
+            sorted_ok = bool(np.all(keys[1:] >= keys[:-1])) if len(keys) > 1 else True
+            got = block_digests(ends, ids, bl, nblocks)
+            want, t_cpu = [], 0.0
+            for b in range(nblocks):
+                lo, hi = b * bl, min(total, (b + 1) * bl)
+                host = make_corpus_device(torch, lo, hi, total, lits, 5, plant_every, dev,
+                                          pplan).cpu().numpy()
+                tc = time.perf_counter()
+                want.append(oracle.digest_mt(eng, host, threads))
+                t_cpu += time.perf_counter() - tc
+                parity_bytes += hi - lo
+                del host
+            parity = sorted_ok and got == want and sum(w[0] for w in want) == nm
+            if not parity:
+                print("bench: PARITY FAILURE got %s want %s sorted %s" % (got, want, sorted_ok),
+                      file=sys.stderr, flush=True)
+            if not args.no_cpu:
+                cpu = {"value": round(parity_bytes / t_cpu / 1e9, 4), "unit": "GB/s",
+                       "cores": threads, "kind": "port",
+                       "sample": "the whole %d-byte corpus: oracle/oracle.c scalar fdrExec "
+                                 "restatement, %d threads over contiguous stripes (7-byte "
+                                 "halo); host: %s" % (parity_bytes, threads, _cpu_model())}
+        alg_bytes = local_bytes + 16 * nm // world  # rank 0's input + its share of records
         achieved = alg_bytes / (kavg * 1e-3) / 1e9
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_fdr5k_4gib.json")
-        if os.path.exists(pmc):
+        if world == 1 and os.path.exists(pmc):
             try:
                 traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        # parity + CPU baseline on a bounded sample of block 0
-        sample = 64 << 20
-
-        def sample_fn(off, ln):
-            ln = min(ln, bl - off)
-            return data[off:off + ln].cpu().numpy()
-
-        import oracle
-        host = sample_fn(0, sample)
-        st, m_o = oracle.fdr_exec(vsa.engine_blob(blob), host, cap=1 << 20)
-        ns = ctx.scan_blocks(db, dptr, [0], [len(host)])
-        res = ctx.results(ns)
-        m_g = list(zip((res["key"] >> np.uint64(24)).tolist(), res["id"].tolist()))
-        parity = (m_g == m_o)
-        cpu = None
-        if not args.no_cpu and world == 1:
-            # the GPU box's CPU share is 16 threads (os.cpu_count() shows the
-            # whole host there)
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            done, t = cpu_baseline(blob, sample_fn, threads, budget_s=args.cpu_budget)
-            cpu = {"value": round(done / t / 1e9, 4), "unit": "GB/s", "cores": threads,
-                   "kind": "port",
-                   "sample": "%d MiB of rank-0 block 0, oracle/oracle.c fdrExec restatement "
-                             "(scalar), %d threads over contiguous stripes" % (done >> 20, threads)}
         out = {
             "metric": "GB/s scanned (hsbench block mode), FDR 5k literals",
             "value": round(gbs, 3),
@@ -247,21 +320,22 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (uniform printable 0x20-0x7E, 1 planted literal / 64 KiB)",
-            "config": {"workload": "cfg4: FDR %d literals len 4-8 (2%% nocase), %.0f GiB per "
-                                   "GPU as %d blocks, engine id %s" %
-                                   (args.lits, args.gib, args.blocks, blob.engine_id),
-                       "global_bytes": world * n, "parallelism": "stripe%d" % world},
-            "matches": total_matches,
-            "gathered_to_rank0": gathered[0] if dist is not None else None,
+            "config": {"workload": "cfg4: FDR %d literals len 4-8 (2%% nocase), one %.0f GiB "
+                                   "corpus as %d blocks striped over %d GPU(s), engine id %s" %
+                                   (args.lits, args.gib, nblocks, world, blob.engine_id),
+                       "global_bytes": total, "parallelism": "stripe%d" % world},
+            "matches": nm,
             "confirm_candidates": ncand,
             "parity": parity,
+            "parity_bytes": parity_bytes,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "kernel_ms": round(kavg, 4)},
+                         "traffic": traffic, "kernel_ms": round(kavg, 4),
+                         "scope": "rank 0 scan kernel (%d input bytes)" % local_bytes},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
@@ -270,6 +344,16 @@ def main():
         dist.destroy_process_group()
     db.close()
     ctx.close()
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return "%s, %d cpus visible" % (line.split(":", 1)[1].strip(), os.cpu_count())
+    except OSError:
+        pass
+    return "unknown"
 
 
 if __name__ == "__main__":

@@ -83,7 +83,9 @@ hwlm_error_t noodExecStreaming(const struct noodTable *n, const uint8_t *hbuf, s
 /* Accel find-first / find-last (src/nfa/shufti.h:46-55, truffle.h:45-49,
  * vermicelli.hpp:47-95, accel.h:148).  Return values as the reference:
  * forward scans return buf_end when nothing is found, reverse scans
- * buf - 1. */
+ * buf - 1.  These signatures have no error channel: on a device failure
+ * they return the no-skip answer (buf forward, buf_end - 1 reverse, c for
+ * run_accel) and vsa_last_error() reports VSA_E_DEVICE. */
 const uint8_t *shuftiExec(vsa_m128_t mask_lo, vsa_m128_t mask_hi,
                           const uint8_t *buf, const uint8_t *buf_end);
 const uint8_t *rshuftiExec(vsa_m128_t mask_lo, vsa_m128_t mask_hi,
@@ -132,7 +134,8 @@ typedef struct vsa_ctx vsa_ctx_t; /* stream + workspace, one per thread */
 typedef struct vsa_db vsa_db_t;   /* device copy of one HWLM blob */
 
 /* Sorted confirmed match: end = key >> 24, bucket = (key >> 20) & 15,
- * confirm-chain index = key & 0xfffff; id = literal id. */
+ * LitInfo offset from its FDRConfirm in 8-byte units = key & 0xfffff (the
+ * confirm-chain order); id = literal id. */
 typedef struct {
     uint64_t key;
     uint32_t id;
@@ -169,6 +172,15 @@ int vsa_scan_blocks(vsa_ctx_t *ctx, const vsa_db_t *db, const uint8_t *d_data,
                     const uint64_t *offsets, const uint64_t *lens,
                     const uint64_t *starts, uint32_t nblocks, uint32_t flags,
                     uint64_t *n_matches);
+/* As vsa_scan_blocks, plus report_lo[i] (may be NULL): ends below it are not
+ * reported, while the FDR start state still applies from starts[i].  A
+ * stripe of one block cut at lo is scanned as the window [lo - 7, hi) with
+ * start 0 and report_lo 7 (literals are <= 8 bytes, hwlm.h:75): exactly the
+ * block's matches ending in [lo, hi), see vectorscan_amd/stripe.py. */
+int vsa_scan_blocks_ex(vsa_ctx_t *ctx, const vsa_db_t *db, const uint8_t *d_data,
+                       const uint64_t *offsets, const uint64_t *lens,
+                       const uint64_t *starts, const uint64_t *report_lo,
+                       uint32_t nblocks, uint32_t flags, uint64_t *n_matches);
 /* As vsa_scan_blocks, each block a streaming call: hlens[i] bytes of
  * history sit immediately before offsets[i] in d_data (at least 16 bytes
  * before each block with hlens[i] > 0 must be readable); hlens[i] = 0 is a
@@ -287,11 +299,16 @@ int vsa_derive_first_stage(const void *hwlm, size_t size, uint64_t *table, uint3
  * (offsetof(struct hs_scratch, fdr_conf / fdr_conf_offset)); the defaults
  * are the x86-64 layout of src/scratch.h:172-219. */
 void vsa_set_scratch_layout(long fdr_conf_off, long fdr_conf_offset_off);
+void vsa_get_scratch_layout(long *fdr_conf_off, long *fdr_conf_offset_off);
 
 /* Optional: offsets of core_info.buf / hbuf / hlen inside hs_scratch for
  * hwlmExecStreaming (defaults: x86-64 layout of scratch.h:91-191). */
 void vsa_set_scratch_core_info(long buf_off, long hbuf_off, long hlen_off);
 void vsa_get_scratch_core_info(long *buf_off, long *hbuf_off, long *hlen_off);
+
+/* VSA_E_DEVICE if a pointer-returning drop-in of this thread hit a device
+ * failure since the last call (then cleared), else VSA_OK. */
+int vsa_last_error(void);
 
 const char *vsa_version(void);
 

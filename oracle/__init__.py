@@ -148,6 +148,30 @@ def nood_exec_stream(engine_ptr, hist, data, term_after=-1, cap=4096, filler=HIS
                        cap, 0, filler)
 
 
+_sig("orc_fdr_exec_squash", _i64, _vp, _vp, _sz, _sz, _u64, _vp, _sz, _vp, _sz,
+     ctypes.POINTER(_int))
+
+
+def fdr_exec_squash(engine_ptr, data, squash, start=0, groups=ALL, cap=1 << 16):
+    """fdrExec whose callback, on reporting literal id, runs a Rose
+    INCLUDED_JUMP with squash mask squash[id] (program_runtime.c:2985-2997:
+    *scratch->fdr_conf &= ~squash << (fdr_conf_offset & ~7)).  `squash` is a
+    dict id -> u8 mask."""
+    n = max(squash) + 1 if squash else 0
+    tab = np.zeros(max(n, 1), np.uint8)
+    for k, v in squash.items():
+        tab[k] = v
+    keep, p, ln = _buf(data)
+    while True:
+        out = (_Match * max(1, cap))()
+        st = _int()
+        cnt = _lib.orc_fdr_exec_squash(engine_ptr, p, ln, start, groups, out, cap,
+                                       tab.ctypes.data, n, ctypes.byref(st))
+        if cnt <= cap:
+            return st.value, [(out[i].end, out[i].id) for i in range(cnt)]
+        cap = cnt
+
+
 def nood_exec(engine_ptr, data, start=0, term_after=-1, cap=4096):
     return _run(_lib.orc_nood_exec, engine_ptr, data, start, [], term_after, cap)
 
@@ -238,6 +262,45 @@ def brute_force(lits, data, start=0):
 
 _sig("orc_fdr_count_mt", ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
      ctypes.c_int)
+
+
+_sig("orc_digest_mt", ctypes.c_long, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+     ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p)
+
+M64 = (1 << 64) - 1
+
+
+def digest_mt(engine_ptr, data, nthreads, nood=False):
+    """(count, sum, xor) of the block scan's (end, id) match set (oracle.c
+    orc_digest_mt: the scalar restatement over `nthreads` stripes with a
+    7-byte halo).  Compare with :func:`digest_of`."""
+    buf = np.ascontiguousarray(data, dtype=np.uint8)
+    out = np.zeros(2, np.uint64)
+    n = _lib.orc_digest_mt(engine_ptr, int(nood), buf.ctypes.data, len(buf), int(nthreads),
+                           out.ctypes.data)
+    if n < 0:
+        raise RuntimeError("orc_digest_mt failed")
+    return int(n), int(out[0]), int(out[1])
+
+
+def mix64(x):
+    """splitmix64 finalizer over a uint64 numpy array (oracle.c orc_mix64)."""
+    with np.errstate(over="ignore"):
+        z = np.asarray(x, np.uint64) + np.uint64(0x9e3779b97f4a7c15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+        return z ^ (z >> np.uint64(31))
+
+
+def digest_of(ends, ids):
+    """(count, sum, xor) digest of an (end, id) match set, as orc_digest_mt."""
+    e = np.asarray(ends, np.uint64)
+    i = np.asarray(ids, np.uint64)
+    m = mix64((e << np.uint64(32)) ^ i)
+    with np.errstate(over="ignore"):
+        s = int(np.sum(m, dtype=np.uint64)) & M64
+    x = int(np.bitwise_xor.reduce(m)) if len(m) else 0
+    return int(len(m)), s, x
 
 
 def fdr_count_mt(engine_ptr, data, nthreads):

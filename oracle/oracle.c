@@ -19,7 +19,7 @@
  *                         src/nfa/x86/truffle.hpp:36-62
  *   vermicelli            src/nfa/vermicelli_simd.cpp:493-622
  *
- * Parity pin: tests/test_oracle_golden.py checks every entry point here
+ * Parity pin: tests/test_cpu_oracle.py checks every entry point here
  * against the known answers of the reference's own unit tests
  * (unit/internal/{noodle,fdr,shufti,truffle,vermicelli,rvermicelli}.cpp),
  * restated as data in tests/golden/.
@@ -86,9 +86,38 @@ typedef struct {
     size_t n;
     long term_after;
     u64a ret_groups; /* value the emulated callback returns */
+    /* digest mode (orc_digest_mt): ends < drop_below are not counted; the
+     * rest fold into dsum / dxor as mix64((base + end) << 32 ^ id) */
+    int digest;
+    u64a drop_below, base, dsum, dxor;
+    /* INCLUDED_JUMP emulation (program_runtime.c:2985-2997): after reporting
+     * literal id, a Rose program holding squash[id] != 0 clears those
+     * buckets from the live FDR confirm word (scratch->fdr_conf, set only
+     * during FDR confirms, fdr_confirm_runtime.h:62-64; Teddy passes none,
+     * teddy_runtime_common.h:436-439) */
+    const u8 *squash;
+    size_t squash_n;
 } cbctx;
 
+/* splitmix64 finalizer: the per-match term of the order-free match-set
+ * digest (count, sum, xor) shared with the GPU-side check in bench.py */
+static inline u64a orc_mix64(u64a x) {
+    u64a z = x + 0x9e3779b97f4a7c15ULL;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+
 static u64a emit(cbctx *c, u64a end, u32 id) {
+    if (c->digest) {
+        if (end >= c->drop_below) {
+            const u64a m = orc_mix64(((c->base + end) << 32) ^ id);
+            c->dsum += m;
+            c->dxor ^= m;
+            c->n++;
+        }
+        return c->ret_groups;
+    }
     if (c->n < c->cap) {
         c->out[c->n].end = end;
         c->out[c->n].id = id;
@@ -251,6 +280,54 @@ long orc_rdverm(u8 c1, u8 c2, int nocase, const u8 *buf, size_t len) {
     return -1;
 }
 
+/* run_accel accel.c:36-183 on an AccelAux image (accel.h:72-146: type at
+ * 0, offset at 1, verm c / dverm c1 c2 m1 m2 at 2.., m128 masks from 16):
+ * minimum lengths (16, 17 for the double forms, which stop one byte early),
+ * then rv = MAX(c + offset, rv) - offset.  Returns rv - c.  Double shufti
+ * is the VECTORSIZE-64 build at the buffer's own alignment. */
+long orc_run_accel(const u8 *aux, const u8 *c, size_t len) {
+    const u8 type = aux[0], off = aux[1];
+    long r;
+    switch (type) {
+    case 0: /* ACCEL_NONE */
+        return 0;
+    case 1: /* ACCEL_VERM */
+    case 2: /* ACCEL_VERM_NOCASE */
+        if (len <= 15) return 0;
+        r = orc_verm(aux[2], type == 2, 0, 0, c, len);
+        break;
+    case 3: /* ACCEL_DVERM */
+    case 4: /* ACCEL_DVERM_NOCASE */
+        if (len <= 17) return 0;
+        r = orc_dverm(aux[2], aux[3], type == 4, c, len - 1);
+        break;
+    case 17: /* ACCEL_DVERM_MASKED */
+        if (len <= 17) return 0;
+        r = orc_dverm_masked(aux[2], aux[3], aux[4], aux[5], c, len - 1);
+        break;
+    case 13: /* ACCEL_SHUFTI */
+        if (len <= 15) return 0;
+        r = orc_shufti(aux + 16, aux + 32, c, len);
+        break;
+    case 15: /* ACCEL_TRUFFLE */
+        if (len <= 15) return 0;
+        r = orc_truffle(aux + 16, aux + 32, c, len);
+        break;
+    case 14: /* ACCEL_DSHUFTI */
+        if (len <= 16) return 0;
+        r = orc_shufti_double(aux + 16, aux + 32, aux + 48, aux + 64, c, len - 1, 64,
+                              (long)((uintptr_t)c % 64));
+        break;
+    case 16: /* ACCEL_RED_TAPE */
+        r = (long)len;
+        break;
+    default:
+        return 0;
+    }
+    if (r < (long)off) r = off;
+    return r - off;
+}
+
 /* ============================================================ noodle == */
 
 /* noodle_engine.cpp:75-134 + scan bounds noodle_engine_simd.hpp:173-273:
@@ -294,7 +371,7 @@ static inline u8 rbyte(const rtargs *a, long p) {
 /* fdr_confirm_runtime.h:43-102 (block mode: len_history == 0) */
 static void conf_with_bit(const struct o_FDRConfirm *fc, const rtargs *a,
                           size_t i, u64a *control, u32 *last_match,
-                          u64a conf_key) {
+                          u64a conf_key, u64a *conf, u32 bit) {
     u32 c = (u32)(((conf_key & fc->andmsk) * fc->mult) >> (64 - fc->nBits));
     const u32 *litIndex = (const u32 *)((const u8 *)fc + 32);
     u32 st = litIndex[c];
@@ -309,6 +386,10 @@ static void conf_with_bit(const struct o_FDRConfirm *fc, const rtargs *a,
         if (!(li->groups & *control)) goto out;
         *last_match = li->id;
         *control = emit(a->cb, i, li->id);
+        if (conf && li->id < a->cb->squash_n && a->cb->squash[li->id]) {
+            /* INCLUDED_JUMP: *fdr_conf &= ~squash << (fdr_conf_offset & ~7) */
+            *conf &= (~(u64a)a->cb->squash[li->id]) << (bit & ~7u);
+        }
     out:
         next = li->next;
         li++;
@@ -422,7 +503,7 @@ static int fdr_run(const struct o_FDR *fdr, const rtargs *a, u64a control) {
                     if (!(fc->groups & control)) continue;
                     long e = it + byte;
                     conf_with_bit(fc, a, (size_t)e, &control, &last_match,
-                                  conf_key_at(a, e));
+                                  conf_key_at(a, e), &conf, bit);
                 }
                 if (!control) return 1;
             }
@@ -508,7 +589,7 @@ static int teddy_run(const struct o_Teddy *t, const rtargs *a, u64a control,
                 if (!(fc->groups & control)) continue;
                 long e = base + i;
                 conf_with_bit(fc, a, (size_t)e, &control, &last_match,
-                              conf_key_at(a, e));
+                              conf_key_at(a, e), NULL, 0);
             }
             if ((i % (fat ? 4 : 8)) == (fat ? 3 : 7) && !control) return 1;
         }
@@ -588,6 +669,15 @@ long orc_fdr_exec(const void *eng, const u8 *buf, size_t len, size_t start,
                   u64a groups, orc_match *out, size_t cap, long term_after,
                   u64a cb_ret, int *status) {
     cbctx cb = {out, cap, 0, term_after, cb_ret};
+    *status = fdr_dispatch(eng, buf, len, start, groups, &cb);
+    return (long)cb.n;
+}
+
+/* fdrExec with the INCLUDED_JUMP squash table squash[id] (n entries) */
+long orc_fdr_exec_squash(const void *eng, const u8 *buf, size_t len, size_t start,
+                         u64a groups, orc_match *out, size_t cap, const u8 *squash,
+                         size_t squash_n, int *status) {
+    cbctx cb = {out, cap, 0, -1, ~0ULL, 0, 0, 0, 0, 0, squash, squash_n};
     *status = fdr_dispatch(eng, buf, len, start, groups, &cb);
     return (long)cb.n;
 }
@@ -725,46 +815,62 @@ u64a orc_fdr_candidates(const void *eng, const u8 *buf, size_t len) {
     return count;
 }
 
-/* ---- multi-threaded timing harness (bench.py cpu_baseline only) ------- *
- * The scalar fdrExec restatement over nthreads contiguous stripes of one
- * buffer, each stripe an independent block scan of [lo - 7, hi) with start
- * = lo - (lo - 7): literals are at most 8 bytes (hwlm.h:75), so every end in
- * [lo, hi) sees the same bytes and the stripes' match counts sum to the
- * single-call count.  Counts only (cap 0). */
+/* ---- multi-threaded harness (bench.py parity check + cpu_baseline) ---- *
+ * The scalar block scan (fdrExec, or noodExec for a noodle table) of one
+ * buffer over nthreads contiguous stripes: thread t owns the ends [lo, hi)
+ * and scans the window [lo - 7, hi) as its own block from 0, dropping the
+ * ends below lo.  Literals are at most 8 bytes (hwlm.h:75) and the FDR start
+ * state only touches the first 7 ends of a block (fdr_compile.cpp:129-151),
+ * so every owned end sees exactly the single-call result (NOREPEAT aside,
+ * which is sequential host state: the digests cover the confirmed set).
+ * Output: the match count and the (sum, xor) digest of the (end, id) set. */
 #include <pthread.h>
 
 typedef struct {
     const void *eng;
+    int nood;
     const u8 *buf;
-    size_t len, start;
-    long n;
+    size_t len;
+    cbctx cb;
     int status;
 } orc_mt_job;
 
 static void *orc_mt_run(void *p) {
     orc_mt_job *j = (orc_mt_job *)p;
-    j->n = orc_fdr_exec(j->eng, j->buf, j->len, j->start, ~0ULL, NULL, 0, -1, ~0ULL,
-                        &j->status);
+    if (j->nood) j->status = nood_run((const struct o_nood *)j->eng, j->buf, j->len, 0, &j->cb);
+    else j->status = fdr_dispatch(j->eng, j->buf, j->len, 0, ~0ULL, &j->cb);
     return NULL;
 }
 
-long orc_fdr_count_mt(const void *eng, const u8 *buf, size_t len, int nthreads) {
+/* eng: the engine inside an HWLM blob; nood != 0 for a noodle table */
+long orc_digest_mt(const void *eng, int nood, const u8 *buf, size_t len, int nthreads,
+                   u64a out[2]) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
+    if ((size_t)nthreads > len / 64 + 1) nthreads = (int)(len / 64 + 1);
     orc_mt_job jobs[256];
     pthread_t th[256];
     const size_t s = len / (size_t)nthreads;
     for (int t = 0; t < nthreads; t++) {
         const size_t lo = (size_t)t * s, hi = t == nthreads - 1 ? len : lo + s;
         const size_t blo = lo >= 7 ? lo - 7 : 0;
-        jobs[t] = (orc_mt_job){eng, buf + blo, hi - blo, lo - blo, 0, 0};
+        cbctx cb = {NULL, 0, 0, -1, ~0ULL, 1, lo - blo, blo, 0, 0};
+        jobs[t] = (orc_mt_job){eng, nood, buf + blo, hi - blo, cb, 0};
         if (pthread_create(&th[t], NULL, orc_mt_run, &jobs[t]) != 0) return -1;
     }
     long n = 0;
+    out[0] = out[1] = 0;
     for (int t = 0; t < nthreads; t++) {
         pthread_join(th[t], NULL);
         if (jobs[t].status != 0) n = -1;
-        if (n >= 0) n += jobs[t].n;
+        if (n >= 0) n += (long)jobs[t].cb.n;
+        out[0] += jobs[t].cb.dsum;
+        out[1] ^= jobs[t].cb.dxor;
     }
     return n;
+}
+
+long orc_fdr_count_mt(const void *eng, const u8 *buf, size_t len, int nthreads) {
+    u64a d[2];
+    return orc_digest_mt(eng, 0, buf, len, nthreads, d);
 }

@@ -1,0 +1,135 @@
+"""BASELINE configs at parity-test scale through the HIP path (C ABI), bit
+exact against the oracle:
+
+* cfg 3 — Teddy / Fat Teddy on the 48-literal (seed 55) and 64-literal
+  (seed 71) printable sets, >= 64 MiB printable corpus (seed 3) with a
+  literal planted every 4 KiB, for the default engine choice (Fat Teddy 8 on
+  an AVX2+ target, teddy_engine_description.cpp:111-115) and forced 8-bucket
+  Teddy engines (the SSE build picks 18);
+* cfg 4 striping — one corpus of several blocks cut into N rank stripes
+  (bench.py's N-GPU split, stripe.plan_corpus_stripes), every stripe scanned
+  through vsa_scan_blocks_ex on this one GPU: the union in rank order equals
+  the per-block single scans (sequence, not just the set).
+"""
+import numpy as np
+import pytest
+
+import bench
+import oracle
+import vectorscan_amd as vsa
+from vectorscan_amd import stripe
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = vsa.Context(0)
+    yield c
+    c.close()
+
+
+def cfg3_lits(n):
+    """cfg 3 literal sets (tools/bench_configs.py lits_printable): length
+    4-8, printable, seed 7 + n (48 -> 55, 64 -> 71)"""
+    import random
+    r = random.Random(7 + n)
+    out = []
+    for i in range(n):
+        ln = r.randint(4, 8)
+        out.append(vsa.HwlmLiteral(bytes(r.randint(0x20, 0x7E) for _ in range(ln)), False, i))
+    return out
+
+
+def scan_one(ctx, blob, data):
+    """one device block scan of a host array; sorted (end, id) list"""
+    n = len(data)
+    d = ctx.malloc(n + 64)
+    try:
+        ctx.h2d(d, data)
+        db = vsa.Database(ctx, blob)
+        k = ctx.scan_blocks(db, d, [0], [n])
+        res = ctx.results(k)
+        db.close()
+    finally:
+        ctx.free(d)
+    return list(zip((res["key"] >> np.uint64(24)).tolist(), res["id"].tolist()))
+
+
+@pytest.mark.parametrize("nl,hint,engine", [
+    (48, -1, 8),    # default choice: Fat Teddy, 4 masks
+    (48, 18, 18),   # 8-bucket Teddy, 4 masks, packed (the SSE build's choice)
+    (48, 17, 17),   # 8-bucket Teddy, 4 masks
+    (48, 11, 11),   # 8-bucket Teddy, 1 mask (many more first-stage candidates)
+    (64, -1, 8),    # default choice: Fat Teddy
+    (64, 3, 3),     # Fat Teddy, 1 mask
+])
+def test_gpu_cfg3_teddy_64mib(ctx, nl, hint, engine):
+    lits = cfg3_lits(nl)
+    blob = vsa.hwlm_build(lits, engine_hint=hint)
+    assert blob.engine_id == engine
+    data = bench.make_corpus(64 << 20, lits, seed=3, plant_every=4096)
+    got = scan_one(ctx, blob, data)
+    st, want = oracle.fdr_exec(vsa.engine_blob(blob), data, cap=1 << 22)
+    assert st == 0
+    assert got == want
+    assert len(want) >= (64 << 20) // 4096
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_gpu_corpus_stripes(ctx, world):
+    """bench.py's split of one corpus (4 blocks) over `world` ranks, each
+    rank's windows scanned as one launch on this GPU from a buffer holding
+    only that rank's bytes: merged records == per-block oracle sequences."""
+    lits = bench.make_literals(5000, seed=12)
+    blob = vsa.hwlm_build(lits)
+    total, bl = (48 << 20) + 4099, 12 << 20
+    data = bench.make_corpus(total, lits, seed=5, plant_every=16 << 10)
+    cuts, plan = stripe.plan_corpus_stripes(total, bl, world, align=1 << 12)
+    db = vsa.Database(ctx, blob)
+    got = []
+    for r in range(world):
+        wins = plan[r]
+        g0 = min(w.wlo for w in wins) & ~255
+        g1 = cuts[r + 1]
+        d = ctx.malloc(g1 - g0 + 64)
+        try:
+            ctx.h2d(d, data[g0:g1])
+            k = ctx.scan_blocks_ex(db, d, [w.wlo - g0 for w in wins], [w.wlen for w in wins],
+                                   None, [w.rlo for w in wins])
+            res = ctx.results(k)
+        finally:
+            ctx.free(d)
+        got += list(zip(((res["key"] >> np.uint64(24)) + np.uint64(g0)).tolist(),
+                        res["id"].tolist()))
+    db.close()
+    want = []
+    for b in range(0, total, bl):
+        _, m = oracle.fdr_exec(vsa.engine_blob(blob), data[b:b + bl], cap=1 << 20)
+        want += [(e + b, i) for e, i in m]
+    assert got == want
+    assert len(want) >= total // (16 << 10)
+
+
+def test_gpu_report_lo_keeps_start_state(ctx):
+    """report_lo cuts reported ends without moving the FDR start state:
+    a block scanned with report_lo = k reports exactly the block scan's ends
+    >= k; scanned with start = k instead, short-literal buckets drop the
+    literals that begin before k (fdr->start, fdr_compile.cpp:129-151)."""
+    lits = [vsa.HwlmLiteral(s, False, i) for i, s in enumerate(
+        [b"abcdefgh", b"cdefgh", b"efgh", b"gh", b"xyzw", b"zw"])]
+    blob = vsa.hwlm_build(lits, engine_hint=0)
+    data = np.frombuffer(b"..abcdefgh..xyzw.." * 4000, np.uint8)
+    _, full = oracle.fdr_exec(vsa.engine_blob(blob), data, cap=1 << 20)
+    db = vsa.Database(ctx, blob)
+    d = ctx.malloc(len(data) + 64)
+    try:
+        ctx.h2d(d, data)
+        for k in (0, 1, 5, 9, 10, 11, 17, 1000, 40001):
+            n = ctx.scan_blocks_ex(db, d, [0], [len(data)], None, [k])
+            res = ctx.results(n)
+            got = list(zip((res["key"] >> np.uint64(24)).tolist(), res["id"].tolist()))
+            assert got == [(e, i) for e, i in full if e >= k], k
+    finally:
+        ctx.free(d)
+        db.close()

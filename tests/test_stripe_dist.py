@@ -132,3 +132,92 @@ def test_gather_to_root_world3():
         assert p.exitcode == 0
     assert keys == [0, 1, 2, 3, 4, 200, 201, 202]
     assert ids == [0, 1, 2, 3, 4, 20, 21, 22]
+
+
+# ------------------------------------------- whole-corpus striping (bench)
+
+def _corpus_case(seed, total, block_len):
+    rng = random.Random(seed)
+    lits = rand_lits(rng, 300, minlen=1, maxlen=8, msk_frac=0.1)
+    for l in lits:
+        l.noruns = False
+    blob = vsa.hwlm_build(lits)
+    r = np.random.default_rng(seed)
+    data = r.choice(np.frombuffer(b"abcdefghABCD", np.uint8), total)
+    return blob, data
+
+
+def _windows_matches(blob, data, wins):
+    """oracle scan of each window as its own block from 0, ends >= rlo kept,
+    as global (end, id) in window order"""
+    out = []
+    for w in wins:
+        win = data[w.wlo:w.wlo + w.wlen]
+        _, m = oracle.fdr_exec(vsa.engine_blob(blob), win, cap=1 << 20)
+        out += [(e + w.wlo, i) for e, i in m if e >= w.rlo]
+    return out
+
+
+@pytest.mark.parametrize("total,block_len,world", [
+    (50000, 20000, 2), (50000, 20000, 3), (65536, 65536, 8), (70001, 9999, 5)])
+def test_corpus_stripes_union_equals_per_block_scan(total, block_len, world):
+    """plan_corpus_stripes (bench.py's N-GPU split): the union over ranks of
+    every window's reported ends equals the per-block single scans."""
+    blob, data = _corpus_case(total + world, total, block_len)
+    cuts, plan = st.plan_corpus_stripes(total, block_len, world, align=64)
+    assert cuts[0] == 0 and cuts[-1] == total
+    got = []
+    for r in range(world):
+        for w in plan[r]:
+            assert cuts[r] <= w.wlo + w.rlo and w.wlo + w.wlen <= cuts[r + 1]
+        got += _windows_matches(blob, data, plan[r])
+    want = []
+    for b in range(0, total, block_len):
+        _, m = oracle.fdr_exec(vsa.engine_blob(blob), data[b:b + block_len], cap=1 << 20)
+        want += [(e + b, i) for e, i in m]
+    assert got == want and len(want) > 100
+
+
+def _corpus_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        blob, data = _corpus_case(9, 40000, 15000)
+        cuts, plan = st.plan_corpus_stripes(40000, 15000, world, align=64)
+        m = _windows_matches(blob, data, plan[rank])
+        ge, gi = st.gather_matches(dist, [e for e, _ in m], [i for _, i in m])
+        if rank == 0:
+            q.put(list(zip(ge.tolist(), gi.tolist())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_corpus_stripes_gloo_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_corpus_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    blob, data = _corpus_case(9, 40000, 15000)
+    want = []
+    for b in range(0, 40000, 15000):
+        _, m = oracle.fdr_exec(vsa.engine_blob(blob), data[b:b + 15000], cap=1 << 20)
+        want += [(e + b, i) for e, i in m]
+    assert got == want
+
+
+def test_digest_matches_oracle_list():
+    """oracle.digest_mt (bench.py's full-corpus check) == digest of the
+    single-call oracle match list, for any thread count"""
+    blob, data = _corpus_case(3, 300000, 300000)
+    _, m = oracle.fdr_exec(vsa.engine_blob(blob), data, cap=1 << 20)
+    want = oracle.digest_of([e for e, _ in m], [i for _, i in m])
+    for t in (1, 2, 7, 16):
+        assert oracle.digest_mt(vsa.engine_blob(blob), data, t) == want

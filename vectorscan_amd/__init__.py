@@ -134,6 +134,9 @@ _sig("vsa_sync", ctypes.c_int, ctypes.c_void_p)
 _sig("vsa_scan_blocks", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_void_p, _u64p, _u64p, ctypes.c_void_p, ctypes.c_uint32,
      ctypes.c_uint32, _u64p)
+_sig("vsa_scan_blocks_ex", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+     ctypes.c_void_p, _u64p, _u64p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+     ctypes.c_uint32, _u64p)
 _sig("vsa_scan_blocks_stream", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_void_p, _u64p, _u64p, ctypes.c_void_p, _u64p, ctypes.c_uint32,
      ctypes.c_uint32, _u64p)
@@ -153,6 +156,9 @@ _sig("vsa_class_scan", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, _u64p,
      _u64p, _u64p, ctypes.c_uint32)
 _sig("vsa_version", ctypes.c_char_p)
+_sig("vsa_set_scratch_layout", None, ctypes.c_long, ctypes.c_long)
+_sig("vsa_get_scratch_layout", None, ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_long))
+_sig("vsa_last_error", ctypes.c_int)
 
 
 class HwlmLiteral:
@@ -569,6 +575,24 @@ class Context:
             len(off), flags, ctypes.byref(n))
         if rc != 0:
             raise RuntimeError("vsa_scan_blocks failed (%d)" % rc)
+        return n.value
+
+    def scan_blocks_ex(self, db, d_data, offsets, lens, starts=None, report_lo=None,
+                       sort=True, asynchronous=False):
+        """vsa_scan_blocks_ex: as scan_blocks, ends below report_lo[i] of
+        block i are not reported (the FDR start state stays at starts[i])."""
+        off = np.ascontiguousarray(offsets, np.uint64)
+        ln = np.ascontiguousarray(lens, np.uint64)
+        st = None if starts is None else np.ascontiguousarray(starts, np.uint64)
+        rl = None if report_lo is None else np.ascontiguousarray(report_lo, np.uint64)
+        n = ctypes.c_uint64()
+        flags = (0 if sort else 1) | (2 if asynchronous else 0)
+        rc = lib.vsa_scan_blocks_ex(
+            self.ptr, db.ptr, d_data, off.ctypes.data_as(_u64p), ln.ctypes.data_as(_u64p),
+            None if st is None else st.ctypes.data, None if rl is None else rl.ctypes.data,
+            len(off), flags, ctypes.byref(n))
+        if rc != 0:
+            raise RuntimeError("vsa_scan_blocks_ex failed (%d)" % rc)
         return n.value
 
     def scan_blocks_stream(self, db, d_data, offsets, lens, hlens, starts=None, sort=True,

@@ -19,6 +19,10 @@ struct VsaBlock {
                            always applies from `start`. */
     int64_t org;        /* aligned (1 KiB, relative to data & ~15) origin of
                            the block's first segment */
+    int64_t rlo;        /* ends < rlo are not reported either; unlike `start`
+                           it does not move the FDR start state (a stripe
+                           window [lo - 7, hi) keeps ends >= 7 of a block
+                           scanned from its own first byte, stripe.py) */
     uint64_t hlen;      /* streaming: len_history (confirm overhang bound,
                            fdr_confirm_runtime.h:79-88); 0 = block mode */
     uint32_t hist;      /* bytes readable before base (16 when streaming) */
@@ -32,8 +36,9 @@ struct VsaBlock {
 #define VSA_BLK_STREAM 1u
 
 /* A confirmed literal match.  `key` sorts into the reference callback order:
- * end (bits 63..24), bucket (23..20), LitInfo index within its bucket's
- * confirm structure (19..0) — fdr.c:299-333 / teddy_runtime_common.h:419-440
+ * end (bits 63..24), bucket (23..20), LitInfo offset within its bucket's
+ * confirm structure in 8-byte units (19..0; LitInfo is 8-aligned,
+ * fdr_confirm_compile.cpp:256) — fdr.c:299-333 / teddy_runtime_common.h:419-440
  * walk candidates LSB-first (end, then bucket) and each chain in memory
  * order. */
 #define VSA_KEY_END_SHIFT 24

@@ -319,7 +319,7 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
             for (int i = 0; i < CONF_U; i++) {
                 const u64 slot = sb + rank[i];
                 if (mt[i] && slot < P.out_cap) {
-                    const u64 lidx = ((u64)(li[i] - fc[i]) >> 5) & VSA_KEY_LI_MASK;
+                    const u64 lidx = ((u64)(li[i] - fc[i]) >> 3) & VSA_KEY_LI_MASK;
                     P.out_keys[slot] = ((base[i] + (u64)e[i]) << VSA_KEY_END_SHIFT) |
                                        ((u64)b[i] << VSA_KEY_BUCKET_SHIFT) | lidx;
                     P.out_ids[slot] = w1[i].z;
@@ -371,6 +371,7 @@ struct SegCtx {
     int64_t blo, bhi; /* aoff of the block */
     int64_t vlo;      /* lowest readable aoff (blo - history) */
     int64_t start, len, zbase;
+    int64_t rlo;      /* lowest reported end: max(start, block rlo) */
     int64_t qlo;      /* Teddy: lowest looked-up position (block-relative) */
     bool stream;      /* streaming with history: no FDR start state */
 };
@@ -581,11 +582,11 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
                 }
             }
         }
-        /* only ends in [start, len) are reported */
+        /* only ends in [max(start, rlo), len) are reported */
 #pragma unroll
         for (int j = 0; j < 16; j++) {
             int64_t q = q0 + j;
-            if (q < S.start || q >= S.len) {
+            if (q < S.rlo || q >= S.len) {
                 if constexpr (T::LB == 8) c[j >> 2] |= 0xffu << (8 * (j & 3));
                 else c[j >> 1] |= 0xffffu << (16 * (j & 1));
             }
@@ -719,7 +720,7 @@ __device__ __forceinline__ IterState nood_iter(const VsaLitParams &P, const LitS
 #pragma unroll
         for (int j = 0; j < 16; j++) {
             const int64_t q = q0 + j;
-            if (q < elo || q >= S.len) hits &= ~(1u << j);
+            if (q < elo || q < S.rlo || q >= S.len) hits &= ~(1u << j);
         }
     }
     if (!__any(hits != 0)) return out;
@@ -1171,6 +1172,7 @@ vsa_lit_scan(VsaLitParams P) {
         S.start = (int64_t)B.start;
         S.len = (int64_t)B.len;
         S.zbase = B.zbase;
+        S.rlo = B.rlo > S.start ? B.rlo : S.start;
         const int64_t s_lo = B.org + (int64_t)(seg - B.seg_first) * SEG;
         const int64_t s_hi = (s_lo + SEG < S.bhi) ? s_lo + SEG : S.bhi;
         const u32 niters = (u32)((s_hi - s_lo + 1023) >> 10);
@@ -1180,7 +1182,7 @@ vsa_lit_scan(VsaLitParams P) {
          * chunk or its successor byte lies outside the block, and the FDR
          * start state / `start` cut-off are behind it.  The rest (at most a
          * couple per block) run the checked path one at a time. */
-        const int64_t fast_lo = S.blo + S.start + 16;
+        const int64_t fast_lo = S.blo + S.rlo + 16;
         u32 f0 = 0, f1 = niters;
         if (s_lo < fast_lo) f0 = (u32)min((int64_t)niters, (fast_lo - s_lo + 1023) >> 10);
         {

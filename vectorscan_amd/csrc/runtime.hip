@@ -99,11 +99,18 @@ struct vsa_ctx {
     uint64_t last_n = 0;
     uint64_t last_cand = 0;
     bool pending = false; /* async scan in flight */
-    uint32_t pending_flags = 0;
-    uint64_t pending_end_bits = 0;
-    const vsa_db *pending_db = nullptr;
-    /* relaunch information for overflow */
-    std::vector<VsaBlock> blocks;
+    /* the last launch (relaunched after an output overflow; the block and
+     * segment tables it reads stay in the pinned/device workspace until the
+     * next scan) */
+    struct {
+        const vsa_db *db = nullptr;
+        const uint8_t *d_data = nullptr;
+        uint32_t nb = 0;
+        uint64_t segs = 0;
+        uint32_t seg_bytes = 0;
+        int end_bits = 0;
+        uint32_t flags = 0;
+    } launch;
     /* kernel-only timing of the last scan (hipEvents on the scan stream) */
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_kernel_ms = 0.0;
@@ -394,14 +401,20 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     return VSA_OK;
 }
 
+int complete_scan(vsa_ctx *c, uint64_t *n_out);
+
 int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
                      const uint64_t *offs, const uint64_t *lens, const uint64_t *starts,
                      uint32_t nb, uint32_t flags, uint64_t *n_out,
-                     const uint64_t *hlens = nullptr) {
+                     const uint64_t *hlens = nullptr, const uint64_t *rlos = nullptr) {
     if (!c || !db || !d_data || !offs || !lens || (!nb)) return VSA_E_INVALID;
     /* an asynchronous scan still in flight may be reading the pinned block
-     * and segment tables rewritten below: let it finish first */
-    if (c->pending) VSA_CHECK(hipStreamSynchronize(c->stream));
+     * and segment tables rewritten below: let it finish first.  Its results
+     * are superseded by this scan (vsa_scan_wait then reports this one). */
+    if (c->pending) {
+        c->pending = false;
+        VSA_CHECK(hipStreamSynchronize(c->stream));
+    }
     int r = ensure_blocks(c, nb);
     if (r) return r;
     if ((r = ensure_out(c, 1)) != VSA_OK) return r;
@@ -425,6 +438,7 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         b.base = offs[i];
         b.len = lens[i];
         b.start = starts ? starts[i] : 0;
+        b.rlo = rlos ? (int64_t)rlos[i] : 0;
         b.seg_first = segs;
         int64_t len = (int64_t)b.len, st = (int64_t)b.start;
         b.hlen = hlens ? hlens[i] : 0;
@@ -462,20 +476,33 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         *n_out = 0;
         return VSA_OK;
     }
+    c->launch.db = db;
+    c->launch.d_data = d_data;
+    c->launch.nb = nb;
+    c->launch.segs = segs;
+    c->launch.seg_bytes = (uint32_t)seg_bytes;
+    c->launch.end_bits = end_bits;
+    c->launch.flags = flags;
+    if ((r = launch_scan(c, db, d_data, nb, segs, (uint32_t)seg_bytes)) != VSA_OK) return r;
+    if (flags & VSA_SCAN_ASYNC) {
+        c->pending = true;
+        *n_out = 0;
+        return VSA_OK;
+    }
+    return complete_scan(c, n_out);
+}
+
+/* Count + sort of the last launch; on an output overflow the buffers grow
+ * to the reported count and the same launch runs again (twice at most: the
+ * count of an identical launch does not change). */
+int complete_scan(vsa_ctx *c, uint64_t *n_out) {
     for (int attempt = 0; attempt < 3; attempt++) {
-        if ((r = launch_scan(c, db, d_data, nb, segs, (uint32_t)seg_bytes)) != VSA_OK) return r;
-        if (flags & VSA_SCAN_ASYNC) {
-            c->pending = true;
-            c->pending_flags = flags;
-            c->pending_end_bits = (uint64_t)end_bits;
-            c->pending_db = db;
-            c->blocks.assign(c->ws.h_blocks, c->ws.h_blocks + nb);
-            *n_out = 0;
-            return VSA_OK;
-        }
-        r = finish_scan(c, flags, end_bits, n_out);
+        int r = finish_scan(c, c->launch.flags, c->launch.end_bits, n_out);
         if (r != VSA_E_OVERFLOW) return r;
         if ((r = ensure_out(c, c->ws.h_counters[0])) != VSA_OK) return r;
+        if ((r = launch_scan(c, c->launch.db, c->launch.d_data, c->launch.nb, c->launch.segs,
+                             c->launch.seg_bytes)) != VSA_OK)
+            return r;
     }
     return VSA_E_OVERFLOW;
 }
@@ -654,7 +681,7 @@ hwlm_error_t replay_lit(const vsa_db *db, const uint64_t *keys, uint64_t n,
             const uint32_t lidx = (uint32_t)(keys[k] & VSA_KEY_LI_MASK);
             if (squashed & (1u << b)) continue;
             const LitInfo *li =
-                (const LitInfo *)(confBase + db->conf_off[b] + (size_t)lidx * 32);
+                (const LitInfo *)(confBase + db->conf_off[b] + (size_t)lidx * 8);
             if (last_match == li->id && (li->flags & FDR_LIT_FLAG_NOREPEAT)) continue;
             if (!(li->groups & control)) continue;
             last_match = li->id;
@@ -1011,6 +1038,9 @@ int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
         }
         const uint32_t *confBase = (const uint32_t *)(eng + ((const uint32_t *)eng)[4]);
         for (uint32_t b = 0; b < db->nbuckets; b++) db->conf_off[b] = confBase[b];
+        /* match keys carry a LitInfo's offset from its FDRConfirm in 8-byte
+         * units in 20 bits (kernels.h): engines up to 8 MiB */
+        if (engine_size(eng, HWLM_ENGINE_FDR) > ((size_t)8 << 20)) return VSA_E_INVALID;
         /* prefilter bitmaps: bit h of bucket b = (litIndex_b[h] != 0) */
         std::vector<uint32_t> slots;
         for (uint32_t b = 0; b < 16; b++) db->slot_off[b] = 0xffffffffu;
@@ -1194,19 +1224,7 @@ int vsa_scan_wait(vsa_ctx_t *c, uint64_t *n_matches) {
     }
     c->pending = false;
     uint64_t n = 0;
-    int r = finish_scan(c, c->pending_flags, (int)c->pending_end_bits, &n);
-    if (r == VSA_E_OVERFLOW) {
-        /* grow and rescan synchronously */
-        if ((r = ensure_out(c, c->ws.h_counters[0])) != VSA_OK) return r;
-        uint32_t nb = (uint32_t)c->blocks.size();
-        memcpy(c->ws.h_blocks, c->blocks.data(), nb * sizeof(VsaBlock));
-        uint64_t segs = 0;
-        for (auto &b : c->blocks) {
-            if (b.start < b.len) segs = std::max<uint64_t>(segs, b.seg_first + 1);
-        }
-        (void)segs;
-        return VSA_E_OVERFLOW;
-    }
+    int r = complete_scan(c, &n); /* overflow: grow and rescan synchronously */
     if (n_matches) *n_matches = n;
     return r;
 }
@@ -1342,22 +1360,27 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
 static const uint8_t *hwlm_accel(const union AccelAux *a, const uint8_t *p,
                                  const uint8_t *end) {
     const size_t len = (size_t)(end - p);
+    int64_t r;
     switch (a->accel_type) {
     case ACCEL_VERM:
     case ACCEL_VERM_NOCASE:
-        return p + vsa_verm_find(0, a->verm.c, 0, 0, 0, a->accel_type == ACCEL_VERM_NOCASE, p,
-                                 len);
+        r = vsa_verm_find(0, a->verm.c, 0, 0, 0, a->accel_type == ACCEL_VERM_NOCASE, p, len);
+        break;
     case ACCEL_DVERM:
     case ACCEL_DVERM_NOCASE:
-        return p + vsa_verm_find(4, a->dverm.c1, a->dverm.c2, 0, 0,
-                                 a->accel_type == ACCEL_DVERM_NOCASE, p, len);
+        r = vsa_verm_find(4, a->dverm.c1, a->dverm.c2, 0, 0,
+                          a->accel_type == ACCEL_DVERM_NOCASE, p, len);
+        break;
     case ACCEL_SHUFTI:
-        return p + vsa_shufti_find(a->shufti.lo.b, a->shufti.hi.b, p, len, 0);
+        r = vsa_shufti_find(a->shufti.lo.b, a->shufti.hi.b, p, len, 0);
+        break;
     case ACCEL_TRUFFLE:
-        return p + vsa_truffle_find(a->truffle.mask1.b, a->truffle.mask2.b, p, len, 0);
+        r = vsa_truffle_find(a->truffle.mask1.b, a->truffle.mask2.b, p, len, 0);
+        break;
     default:
         return p;
     }
+    return r < 0 ? p : p + r; /* device failure: no skip (the scan reports it) */
 }
 
 /* do_accel_block hwlm.c:85-105 */
@@ -1505,6 +1528,15 @@ hwlm_error_t hwlmExecStreaming(const struct HWLM *tab, size_t len, size_t start,
     return fdrExecStreaming((const FDR *)eng, hbuf, hlen, buf, len, start, cb, scratch, groups);
 }
 
+int vsa_scan_blocks_ex(vsa_ctx_t *c, const vsa_db_t *db, const uint8_t *d_data,
+                       const uint64_t *offsets, const uint64_t *lens, const uint64_t *starts,
+                       const uint64_t *report_lo, uint32_t nblocks, uint32_t flags,
+                       uint64_t *n_matches) {
+    uint64_t dummy;
+    return scan_blocks_impl(c, db, d_data, offsets, lens, starts, nblocks, flags,
+                            n_matches ? n_matches : &dummy, nullptr, report_lo);
+}
+
 int vsa_scan_blocks_stream(vsa_ctx_t *c, const vsa_db_t *db, const uint8_t *d_data,
                            const uint64_t *offsets, const uint64_t *lens,
                            const uint64_t *starts, const uint64_t *hlens, uint32_t nblocks,
@@ -1595,13 +1627,49 @@ int64_t vsa_verm_find(int mode, uint8_t c1, uint8_t c2, uint8_t m1, uint8_t m2, 
 
 static void m128_bytes(vsa_m128_t m, uint8_t out[16]) { memcpy(out, &m, 16); }
 
+/* The pointer-returning drop-ins have no error channel in the reference
+ * ABI.  A device failure (the vsa_*_find helpers return -2) is recorded for
+ * vsa_last_error() and answered with the no-skip pointer: buf for forward
+ * scans, buf_end - 1 for reverse ones (every accel caller, hwlm.c:48-105 and
+ * accel.c:35-180, then scans from there), never buf + (-2). */
+static thread_local int t_last_error = VSA_OK;
+
+static void note_error(const char *who) {
+    t_last_error = VSA_E_DEVICE;
+    if (getenv("VSA_DEBUG")) fprintf(stderr, "vsa: %s: device failure\n", who);
+}
+
+static const uint8_t *fwd_result(int64_t r, const uint8_t *buf, const uint8_t *buf_end,
+                                 const char *who) {
+    if (r == -2) {
+        note_error(who);
+        return buf;
+    }
+    return r < 0 ? buf_end : buf + r;
+}
+
+static const uint8_t *rev_result(int64_t r, const uint8_t *buf, const uint8_t *buf_end,
+                                 const char *who) {
+    if (r == -2) {
+        note_error(who);
+        return buf_end - 1;
+    }
+    return buf + r; /* -1: buf - 1, "not found" */
+}
+
+int vsa_last_error(void) {
+    const int e = t_last_error;
+    t_last_error = VSA_OK;
+    return e;
+}
+
 const uint8_t *shuftiExec(vsa_m128_t mask_lo, vsa_m128_t mask_hi, const uint8_t *buf,
                           const uint8_t *buf_end) {
     uint8_t lo[16], hi[16];
     m128_bytes(mask_lo, lo);
     m128_bytes(mask_hi, hi);
-    int64_t r = vsa_shufti_find(lo, hi, buf, (size_t)(buf_end - buf), 0);
-    return r < 0 ? buf_end : buf + r;
+    return fwd_result(vsa_shufti_find(lo, hi, buf, (size_t)(buf_end - buf), 0), buf, buf_end,
+                      "shuftiExec");
 }
 
 static uint32_t g_vector_size = 64; /* reference VECTORSIZE emulated by shuftiDoubleExec */
@@ -1624,8 +1692,8 @@ const uint8_t *shuftiDoubleExec(vsa_m128_t mask1_lo, vsa_m128_t mask1_hi, vsa_m1
     m128_bytes(mask1_hi, hi1);
     m128_bytes(mask2_lo, lo2);
     m128_bytes(mask2_hi, hi2);
-    int64_t r = vsa_shufti_double_find(lo1, hi1, lo2, hi2, buf, (size_t)(buf_end - buf));
-    return r < 0 ? buf_end : buf + r;
+    return fwd_result(vsa_shufti_double_find(lo1, hi1, lo2, hi2, buf, (size_t)(buf_end - buf)),
+                      buf, buf_end, "shuftiDoubleExec");
 }
 
 int vsa_shufti_build_double_masks(const uint8_t onechar[32], const uint8_t *pairs,
@@ -1639,7 +1707,8 @@ const uint8_t *rshuftiExec(vsa_m128_t mask_lo, vsa_m128_t mask_hi, const uint8_t
     uint8_t lo[16], hi[16];
     m128_bytes(mask_lo, lo);
     m128_bytes(mask_hi, hi);
-    return buf + vsa_shufti_find(lo, hi, buf, (size_t)(buf_end - buf), 1);
+    return rev_result(vsa_shufti_find(lo, hi, buf, (size_t)(buf_end - buf), 1), buf, buf_end,
+                      "rshuftiExec");
 }
 
 const uint8_t *truffleExec(vsa_m128_t mask1, vsa_m128_t mask2, const uint8_t *buf,
@@ -1647,8 +1716,8 @@ const uint8_t *truffleExec(vsa_m128_t mask1, vsa_m128_t mask2, const uint8_t *bu
     uint8_t a[16], b[16];
     m128_bytes(mask1, a);
     m128_bytes(mask2, b);
-    int64_t r = vsa_truffle_find(a, b, buf, (size_t)(buf_end - buf), 0);
-    return r < 0 ? buf_end : buf + r;
+    return fwd_result(vsa_truffle_find(a, b, buf, (size_t)(buf_end - buf), 0), buf, buf_end,
+                      "truffleExec");
 }
 
 const uint8_t *rtruffleExec(vsa_m128_t mask1, vsa_m128_t mask2, const uint8_t *buf,
@@ -1656,37 +1725,49 @@ const uint8_t *rtruffleExec(vsa_m128_t mask1, vsa_m128_t mask2, const uint8_t *b
     uint8_t a[16], b[16];
     m128_bytes(mask1, a);
     m128_bytes(mask2, b);
-    return buf + vsa_truffle_find(a, b, buf, (size_t)(buf_end - buf), 1);
+    return rev_result(vsa_truffle_find(a, b, buf, (size_t)(buf_end - buf), 1), buf, buf_end,
+                      "rtruffleExec");
+}
+
+static const uint8_t *verm_fwd(int mode, char c1, char c2, char m1, char m2, char nocase,
+                               const uint8_t *buf, const uint8_t *buf_end, const char *who) {
+    return fwd_result(vsa_verm_find(mode, (uint8_t)c1, (uint8_t)c2, (uint8_t)m1, (uint8_t)m2,
+                                    nocase, buf, (size_t)(buf_end - buf)),
+                      buf, buf_end, who);
+}
+
+static const uint8_t *verm_rev(int mode, char c1, char c2, char nocase, const uint8_t *buf,
+                               const uint8_t *buf_end, const char *who) {
+    return rev_result(vsa_verm_find(mode, (uint8_t)c1, (uint8_t)c2, 0, 0, nocase, buf,
+                                    (size_t)(buf_end - buf)),
+                      buf, buf_end, who);
 }
 
 const uint8_t *vermicelliExec(char c, char nocase, const uint8_t *buf, const uint8_t *buf_end) {
-    return buf + vsa_verm_find(0, (uint8_t)c, 0, 0, 0, nocase, buf, (size_t)(buf_end - buf));
+    return verm_fwd(0, c, 0, 0, 0, nocase, buf, buf_end, "vermicelliExec");
 }
 const uint8_t *nvermicelliExec(char c, char nocase, const uint8_t *buf, const uint8_t *buf_end) {
-    return buf + vsa_verm_find(1, (uint8_t)c, 0, 0, 0, nocase, buf, (size_t)(buf_end - buf));
+    return verm_fwd(1, c, 0, 0, 0, nocase, buf, buf_end, "nvermicelliExec");
 }
 const uint8_t *rvermicelliExec(char c, char nocase, const uint8_t *buf, const uint8_t *buf_end) {
-    return buf + vsa_verm_find(2, (uint8_t)c, 0, 0, 0, nocase, buf, (size_t)(buf_end - buf));
+    return verm_rev(2, c, 0, nocase, buf, buf_end, "rvermicelliExec");
 }
 const uint8_t *rnvermicelliExec(char c, char nocase, const uint8_t *buf,
                                 const uint8_t *buf_end) {
-    return buf + vsa_verm_find(3, (uint8_t)c, 0, 0, 0, nocase, buf, (size_t)(buf_end - buf));
+    return verm_rev(3, c, 0, nocase, buf, buf_end, "rnvermicelliExec");
 }
 const uint8_t *vermicelliDoubleExec(char c1, char c2, char nocase, const uint8_t *buf,
                                     const uint8_t *buf_end) {
-    return buf + vsa_verm_find(4, (uint8_t)c1, (uint8_t)c2, 0, 0, nocase, buf,
-                               (size_t)(buf_end - buf));
+    return verm_fwd(4, c1, c2, 0, 0, nocase, buf, buf_end, "vermicelliDoubleExec");
 }
 const uint8_t *rvermicelliDoubleExec(char c1, char c2, char nocase, const uint8_t *buf,
                                      const uint8_t *buf_end) {
-    return buf + vsa_verm_find(6, (uint8_t)c1, (uint8_t)c2, 0, 0, nocase, buf,
-                               (size_t)(buf_end - buf));
+    return verm_rev(6, c1, c2, nocase, buf, buf_end, "rvermicelliDoubleExec");
 }
 
 const uint8_t *vermicelliDoubleMaskedExec(char c1, char c2, char m1, char m2,
                                           const uint8_t *buf, const uint8_t *buf_end) {
-    return buf + vsa_verm_find(5, (uint8_t)c1, (uint8_t)c2, (uint8_t)m1, (uint8_t)m2, 0, buf,
-                               (size_t)(buf_end - buf));
+    return verm_fwd(5, c1, c2, m1, m2, 0, buf, buf_end, "vermicelliDoubleMaskedExec");
 }
 
 /* accel.c:35-180 dispatch for the forward schemes HWLM and NFAs use */
@@ -1694,46 +1775,51 @@ const uint8_t *vermicelliDoubleMaskedExec(char c1, char c2, char m1, char m2,
  * one byte early), then rv = MAX(c + offset, rv) - offset. */
 const uint8_t *run_accel(const union AccelAux *accel, const uint8_t *c, const uint8_t *c_end) {
     const size_t len = (size_t)(c_end - c);
-    const uint8_t *rv;
+    int64_t r;
     switch (accel->accel_type) {
     case ACCEL_NONE:
         return c;
     case ACCEL_VERM:
     case ACCEL_VERM_NOCASE:
         if (c + 15 >= c_end) return c;
-        rv = c + vsa_verm_find(0, accel->verm.c, 0, 0, 0, accel->accel_type == ACCEL_VERM_NOCASE,
-                               c, len);
+        r = vsa_verm_find(0, accel->verm.c, 0, 0, 0, accel->accel_type == ACCEL_VERM_NOCASE, c,
+                          len);
         break;
     case ACCEL_DVERM:
     case ACCEL_DVERM_NOCASE:
         if (c + 16 + 1 >= c_end) return c;
-        rv = c + vsa_verm_find(4, accel->dverm.c1, accel->dverm.c2, 0, 0,
-                               accel->accel_type == ACCEL_DVERM_NOCASE, c, len - 1);
+        r = vsa_verm_find(4, accel->dverm.c1, accel->dverm.c2, 0, 0,
+                          accel->accel_type == ACCEL_DVERM_NOCASE, c, len - 1);
         break;
     case ACCEL_DVERM_MASKED:
         if (c + 16 + 1 >= c_end) return c;
-        rv = c + vsa_verm_find(5, accel->dverm.c1, accel->dverm.c2, accel->dverm.m1,
-                               accel->dverm.m2, 0, c, len - 1);
+        r = vsa_verm_find(5, accel->dverm.c1, accel->dverm.c2, accel->dverm.m1, accel->dverm.m2,
+                          0, c, len - 1);
         break;
     case ACCEL_SHUFTI:
         if (c + 15 >= c_end) return c;
-        rv = c + vsa_shufti_find(accel->shufti.lo.b, accel->shufti.hi.b, c, len, 0);
+        r = vsa_shufti_find(accel->shufti.lo.b, accel->shufti.hi.b, c, len, 0);
         break;
     case ACCEL_TRUFFLE:
         if (c + 15 >= c_end) return c;
-        rv = c + vsa_truffle_find(accel->truffle.mask1.b, accel->truffle.mask2.b, c, len, 0);
+        r = vsa_truffle_find(accel->truffle.mask1.b, accel->truffle.mask2.b, c, len, 0);
         break;
     case ACCEL_DSHUFTI:
         if (c + 15 + 1 >= c_end) return c;
-        rv = c + vsa_shufti_double_find(accel->dshufti.lo1.b, accel->dshufti.hi1.b,
-                                        accel->dshufti.lo2.b, accel->dshufti.hi2.b, c, len - 1);
+        r = vsa_shufti_double_find(accel->dshufti.lo1.b, accel->dshufti.hi1.b,
+                                   accel->dshufti.lo2.b, accel->dshufti.hi2.b, c, len - 1);
         break;
     case ACCEL_RED_TAPE:
-        rv = c_end;
+        r = (int64_t)len;
         break;
     default:
         return c;
     }
+    if (r < 0) { /* device failure: no acceleration (see fwd_result) */
+        note_error("run_accel");
+        return c;
+    }
+    const uint8_t *rv = c + r;
     rv = std::max(c + accel->generic.offset, rv);
     return rv - accel->generic.offset;
 }
@@ -1741,6 +1827,11 @@ const uint8_t *run_accel(const union AccelAux *accel, const uint8_t *c, const ui
 void vsa_set_scratch_layout(long fdr_conf_off, long fdr_conf_offset_off) {
     g_fdr_conf_off.store(fdr_conf_off);
     g_fdr_conf_offset_off.store(fdr_conf_offset_off);
+}
+
+void vsa_get_scratch_layout(long *fdr_conf_off, long *fdr_conf_offset_off) {
+    *fdr_conf_off = g_fdr_conf_off.load();
+    *fdr_conf_offset_off = g_fdr_conf_offset_off.load();
 }
 
 /* ---------------------------------------------------------- builder --- */

@@ -60,6 +60,43 @@ def plan_block_stripes(length, start, world, min_stripe=1 << 16):
     return out
 
 
+@dataclass
+class Window:
+    block: int   # block index (one hs_scan / hwlmExec call each)
+    wlo: int     # window start, global corpus offset
+    wlen: int    # window length
+    rlo: int     # first reported end inside the window (report_lo)
+
+
+def plan_corpus_stripes(total, block_len, world, align=1 << 16):
+    """North-star striping: one corpus of `total` bytes made of
+    blocks of `block_len` bytes (the last may be shorter), its end positions
+    split into `world` contiguous ranges (cut at multiples of `align`).  Rank r
+    owns ends [cut_r, cut_{r+1}); for every block it overlaps it scans the
+    window [max(block_lo, lo - 7), hi) as that block's own scan from 0 and
+    reports ends >= lo only (vsa_scan_blocks_ex report_lo): exact, because
+    literals are <= 8 bytes (hwlm.h:75) and the FDR start state only touches
+    a block's first 7 ends.  Returns (cuts, [[Window, ...] per rank])."""
+    if world < 1 or block_len < 1:
+        raise ValueError("world and block_len must be >= 1")
+    cuts = [min(total, ((total * r) // world) // align * align) for r in range(world)]
+    cuts.append(total)
+    plan = []
+    for r in range(world):
+        lo, hi = cuts[r], cuts[r + 1]
+        wins = []
+        b = lo // block_len
+        while lo < hi and b * block_len < hi:
+            blo, bhi = b * block_len, min(total, (b + 1) * block_len)
+            olo, ohi = max(lo, blo), min(hi, bhi)
+            if olo < ohi:
+                wlo = blo if olo == blo else max(blo, olo - HALO)
+                wins.append(Window(b, wlo, ohi - wlo, olo - wlo))
+            b += 1
+        plan.append(wins)
+    return cuts, plan
+
+
 def localize(stripe, ends, ids):
     """Window-relative results -> block-relative, halo ends dropped."""
     ends = np.asarray(ends, np.int64) + stripe.wlo
