@@ -13,6 +13,9 @@ all: $(LIB) $(ORACLE) $(HARNESS)
 $(CSRC)/compile.o: $(CSRC)/compile.cpp $(CSRC)/hs_layout.h $(CSRC)/vsa_internal.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(CSRC)/flood.o: $(CSRC)/flood.cpp $(CSRC)/hs_layout.h $(CSRC)/vsa_internal.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(CSRC)/kernels.o: $(CSRC)/kernels.hip $(CSRC)/kernels.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -20,7 +23,7 @@ $(CSRC)/runtime.o: $(CSRC)/runtime.hip $(CSRC)/kernels.h $(CSRC)/hs_layout.h \
                    $(CSRC)/vsa_internal.h include/vectorscan_amd.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(CSRC)/compile.o $(CSRC)/kernels.o $(CSRC)/runtime.o
+$(LIB): $(CSRC)/compile.o $(CSRC)/flood.o $(CSRC)/kernels.o $(CSRC)/runtime.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
 
 $(ORACLE): oracle/oracle.c

@@ -65,6 +65,15 @@ _sig("orc_nood_exec_stream", _i64, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _i64,
 
 ALL = (1 << 64) - 1
 
+_sig("orc_set_vector_size", None, ctypes.c_long)
+
+
+def set_vector_size(v):
+    """Teddy build whose loop shape the flood restatement follows (16 SSE,
+    32 AVX2, 64 AVX-512 VBMI; default 64) — vsa.set_accel_vector_size on the
+    engine side."""
+    _lib.orc_set_vector_size(int(v))
+
 
 def _buf(data):
     if isinstance(data, np.ndarray):

@@ -30,6 +30,7 @@
  */
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 typedef uint8_t u8;
@@ -404,6 +405,105 @@ static u64a conf_key_at(const rtargs *a, long e) {
     return v;
 }
 
+/* ============================================================== flood == */
+
+/* fdr_internal.h:50-61 */
+struct o_FDRFlood {
+    u64a allGroups;
+    u32 suffix;
+    u16 idCount;
+    u32 ids[16];
+    u64a groups[16];
+};
+
+static inline u64a o_ld8(const u8 *p) {
+    u64a v;
+    memcpy(&v, p, 8);
+    return v;
+}
+/* *(const u64a *)ROUNDUP_PTR(p, 8) */
+static inline u64a o_ldr8(const u8 *p) {
+    return o_ld8((const u8 *)(((uintptr_t)p + 7) & ~(uintptr_t)7));
+}
+
+/* nextFloodDetect flood_runtime.h:41-83 (FLOOD_64): threshold offset */
+static size_t o_next_flood_detect(const u8 *buf, size_t len) {
+    if (len < 256) return len;
+    if (o_ldr8(buf) == o_ldr8(buf + 8)) return 32;
+    if (o_ldr8(buf + len / 2) == o_ldr8(buf + len / 2 + 8)) return 32;
+    if (o_ldr8(buf + len - 24) == o_ldr8(buf + len - 16)) return 32;
+    return len;
+}
+
+/* floodDetect flood_runtime.h:85-335 without the reports: at loop pointer
+ * i, *fsize = bytes the main loop skips (0: none) and *flp the flood record;
+ * returns the next threshold. */
+static size_t o_flood_probe(const u8 *buf, size_t len, u32 i, const u8 *fBase, u32 iterBytes,
+                            u32 *backoff, u32 *fsize, const struct o_FDRFlood **flp) {
+    size_t mainLoopLen = len > 2 * (size_t)iterBytes ? len - 2 * (size_t)iterBytes : 0;
+    u32 j = i;
+    u8 c = buf[i];
+    u32 fIdx = ((const u32 *)fBase)[c];
+    const struct o_FDRFlood *fl = (const struct o_FDRFlood *)(fBase + 4 * 256) + fIdx;
+    u64a cmpVal = c;
+    cmpVal |= cmpVal << 8;
+    cmpVal |= cmpVal << 16;
+    cmpVal |= cmpVal << 32;
+    *fsize = 0;
+    *flp = fl;
+    if (o_ldr8(buf + i) != cmpVal || fl->idCount >= 16) {
+        *backoff *= 2;
+        goto floodout;
+    }
+    if (i < fl->suffix + 7) {
+        *backoff *= 2;
+        goto floodout;
+    }
+    j = i - fl->suffix;
+    j -= (u32)((uintptr_t)buf + j) & 0x7;
+    for (; j + 32 < mainLoopLen; j += 32) {
+        if (o_ld8(buf + j + 24) != cmpVal || o_ld8(buf + j + 16) != cmpVal ||
+            o_ld8(buf + j + 8) != cmpVal || o_ld8(buf + j) != cmpVal)
+            break;
+    }
+    for (; j + 8 < mainLoopLen; j += 8) {
+        if (o_ld8(buf + j) != cmpVal) break;
+    }
+    for (; j < mainLoopLen; j++) {
+        if (buf[j] != c) break;
+    }
+    if (j > i) {
+        j--;
+        *fsize = ((j - i) / iterBytes) * iterBytes;
+    } else {
+        *backoff *= 2;
+    }
+floodout:
+    if ((u32)(j + *backoff) < mainLoopLen - 128) return (size_t)(i > j ? i : j) + *backoff;
+    return mainLoopLen;
+}
+
+/* the reports of one flood (flood_runtime.h:191-319: the unrolled cases
+ * visit ends in groups of 4 (idCount <= 2) or 2, all ids per end) */
+static void o_flood_report(const struct o_FDRFlood *fl, u32 i, u32 floodSize, u64a *control,
+                           cbctx *cb) {
+    if (!fl->idCount || !(*control & fl->allGroups)) return;
+    u32 step = fl->idCount <= 2 ? 4 : 2;
+    for (u32 t = 0; t < floodSize && (*control & fl->allGroups); t += step) {
+        for (u32 k = 0; k < step; k++) {
+            for (u32 d = 0; d < fl->idCount; d++) {
+                if (*control & fl->groups[d]) *control = emit(cb, i + t + k, fl->ids[d]);
+            }
+        }
+    }
+}
+
+/* Teddy build whose loop shape the flood emulation follows (16: SSE
+ * teddy.c:1004-1066 with AVX2 Fat Teddy; 32: AVX2 teddy.c:823-888 /
+ * teddy_avx2.c:593-660; 64: VBMI teddy.c:335-388 / teddy_avx2.c:395-447) */
+static long o_teddy_vsize = 64;
+void orc_set_vector_size(long v) { o_teddy_vsize = v; }
+
 /* ================================================================ FDR == */
 
 /* a "zone" buffer as in fdr.c:50-80; we keep a logical byte accessor */
@@ -479,14 +579,31 @@ static int fdr_run(const struct o_FDR *fdr, const rtargs *a, u64a control) {
     } else {
         memcpy(&state, fdr->start, 16);
     }
+    /* floods: only the main zone's pointer can pass tryFloodDetect (the
+     * other zones point floodPtr past their own buffers, fdr.c:392, :509,
+     * :569); the skipped iterations leave `state` as it was (FDR_MAIN_LOOP) */
+    const u8 *fBase = (const u8 *)fdr + fdr->floodOffset;
+    size_t tfd = o_next_flood_detect(a->buf, len);
+    u32 backoff = 32;
     for (int zi = 0; zi < nz; zi++) {
         zone *z = &zones[zi];
+        const int main_zone = remaining > 16 && zi == 1 && nz == 3;
         /* variable_byte_shift_m128(state, shift) | zone_or_mask[shift] */
         state <<= 8 * z->shift;
         u128 orm = 0;
         for (int k = 0; k < z->shift; k++) orm |= (u128)0xff << (8 * k);
         state |= orm;
         for (long it = z->zstart; it + 16 <= z->zend; it += 16) {
+            if (main_zone && (size_t)it > tfd) {
+                u32 fsz;
+                const struct o_FDRFlood *fl;
+                tfd = o_flood_probe(a->buf, len, (u32)it, fBase, 16, &backoff, &fsz, &fl);
+                if (fsz) {
+                    o_flood_report(fl, (u32)it, fsz, &control, a->cb);
+                    it += fsz;
+                }
+                if (!control) return 1;
+            }
             u64a c0, c8;
             get_conf(z, it, fdr->stride, fdr->domainMask, ft, &c0, &c8, &state);
             for (int half = 0; half < 2; half++) {
@@ -519,10 +636,76 @@ static int fdr_run(const struct o_FDR *fdr, const rtargs *a, u64a control) {
  * at byte i (8 or 16 bucket bits); the candidate word for byte i ORs
  * res[j][i - j], taking i - j < 0 from the previous block (palignr with the
  * carried res_old, zero at the start). */
+/* The flood checks of one Teddy call: CHECK_FLOOD sits at the top of the
+ * main loop (teddy_runtime_common.h:73-80) of the emulated build's shape;
+ * events[k] = {loop pointer, bytes skipped, record}.  Returns the count. */
+typedef struct {
+    u32 i, size;
+    const struct o_FDRFlood *fl;
+} o_flood_ev;
+
+static size_t o_teddy_floods(const struct o_Teddy *t, const rtargs *a, int fat, u32 nMasks,
+                             o_flood_ev *ev, size_t cap) {
+    const u8 *buf = a->buf;
+    size_t len = a->len, p = a->start, step, iter;
+    size_t tfd = o_next_flood_detect(buf, len);
+    if (tfd >= len) return 0;
+    if (o_teddy_vsize >= 64) {
+        /* VBMI: head block of loopBytes = W - (nMasks - 1), then loopBytes */
+        step = (fat ? 32 : 64) - (nMasks - 1);
+        iter = fat ? 32 : 64;
+        if (p + step <= len) p += step;
+    } else {
+        /* SSE (16-B blocks) / AVX2 (32-B halves; Fat Teddy always 16-B):
+         * aligned head block, one block, then two blocks per iteration */
+        size_t blk = (!fat && o_teddy_vsize == 32) ? 32 : 16;
+        uintptr_t A = (uintptr_t)buf + p;
+        uintptr_t ms = (A + blk - 1) & ~(uintptr_t)(blk - 1);
+        if (A < ms) p += ms - A;
+        if (p + blk <= len) p += blk;
+        step = iter = 2 * blk;
+    }
+    const u8 *fBase = (const u8 *)t + t->floodOffset;
+    u32 backoff = 32;
+    size_t n = 0;
+    for (; p + step <= len; p += step) {
+        if (p > tfd) {
+            u32 fsz;
+            const struct o_FDRFlood *fl;
+            tfd = o_flood_probe(buf, len, (u32)p, fBase, (u32)iter, &backoff, &fsz, &fl);
+            if (fsz && n < cap) {
+                ev[n].i = (u32)p;
+                ev[n].size = fsz;
+                ev[n].fl = fl;
+                n++;
+                p += fsz;
+            }
+        }
+    }
+    return n;
+}
+
+static int teddy_loop(const struct o_Teddy *t, const rtargs *a, u64a control, int fat,
+                      u32 nMasks, const o_flood_ev *fev, size_t nfev);
+
 static int teddy_run(const struct o_Teddy *t, const rtargs *a, u64a control,
                      int fat, u32 nMasks) {
+    size_t len = a->len;
+    /* floods are >= 32 bytes apart; none when the first threshold is len */
+    const size_t fcap = o_next_flood_detect(a->buf, len) < len ? len / 32 + 1 : 0;
+    o_flood_ev *fev = fcap ? (o_flood_ev *)malloc(fcap * sizeof(o_flood_ev)) : NULL;
+    const size_t nfev = fev ? o_teddy_floods(t, a, fat, nMasks, fev, fcap) : 0;
+    const int rv = teddy_loop(t, a, control, fat, nMasks, fev, nfev);
+    free(fev);
+    return rv;
+}
+
+static int teddy_loop(const struct o_Teddy *t, const rtargs *a, u64a control, int fat,
+                      u32 nMasks, const o_flood_ev *fev, size_t nfev) {
     const u8 *buf = a->buf;
     size_t len = a->len;
+    size_t fe = 0;
+    long skip_lo = 0, skip_hi = 0;
     const u8 *maskBase = (const u8 *)t + 64;
     const u32 *confBase = (const u32 *)((const u8 *)t + t->confOffset);
     u32 nb = fat ? 16 : 8;
@@ -578,6 +761,17 @@ static int teddy_run(const struct o_Teddy *t, const rtargs *a, u64a control,
         memcpy(old, res, sizeof(res));
         u16 full = fat ? 0xffff : 0xff;
         for (int i = 0; i < 16; i++) {
+            const long e = base + i;
+            while (fe < nfev && (long)fev[fe].i <= e) {
+                /* the loop pointer passed tryFloodDetect: the flood reports,
+                 * then the main loop skips its ends */
+                o_flood_report(fev[fe].fl, fev[fe].i, fev[fe].size, &control, a->cb);
+                if (!control) return 1;
+                skip_lo = fev[fe].i;
+                skip_hi = (long)fev[fe].i + fev[fe].size;
+                fe++;
+            }
+            if (e >= skip_lo && e < skip_hi) continue;
             u16 cand = (u16)(~r[i]) & full;
             while (cand) {
                 u32 b = (u32)__builtin_ctz(cand);
@@ -587,7 +781,6 @@ static int teddy_run(const struct o_Teddy *t, const rtargs *a, u64a control,
                 const struct o_FDRConfirm *fc =
                     (const struct o_FDRConfirm *)((const u8 *)confBase + cf);
                 if (!(fc->groups & control)) continue;
-                long e = base + i;
                 conf_with_bit(fc, a, (size_t)e, &control, &last_match,
                               conf_key_at(a, e), NULL, 0);
             }

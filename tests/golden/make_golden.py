@@ -469,6 +469,119 @@ def fdr_stream_cases():
     return cases
 
 
+def _isalpha(c):
+    return 0x41 <= c <= 0x5A or 0x61 <= c <= 0x7A
+
+
+def fdr_flood_cases():
+    """unit/internal/fdr_flood.cpp:148-560 (FDRFloodp, every char c, the
+    engine built with the default Grey, i.e. flood detection on): literal
+    sets generated from c and the per-id match counts the tests assert over
+    a 1024-byte buffer filled with c (and with cAlt = c ^ bit).  Ids a test
+    does not assert are absent from `expected`.  Literal = [s, nocase, id,
+    msk, cmp] (hex strings)."""
+    N = 1024
+    out = []
+    for c in range(256):
+        bit = 1 << (c & 7)
+        cAlt = c ^ bit
+        cb = bit == 0x20 and _isalpha(c)  # bit == CASE_BIT && isalpha(c)
+
+        # NoMask :148-233
+        lits = []
+        for i in range(4):
+            L = 1 << i
+            s = bytearray([c] * L)
+            lits.append([hx(s), 0, i * 8 + 0, "", ""])
+            s[0] = cAlt
+            lits.append([hx(s), 0, i * 8 + 1, "", ""])
+            lits.append([hx(s), 1, i * 8 + 2, "", ""])
+            s[0] = c
+            s[-1] = cAlt
+            lits.append([hx(s), 0, i * 8 + 3, "", ""])
+            lits.append([hx(s), 1, i * 8 + 4, "", ""])
+            sa = bytearray([cAlt] * L)
+            lits.append([hx(sa), 1, i * 8 + 5, "", ""])
+            sa[0] = c
+            lits.append([hx(sa), 1, i * 8 + 6, "", ""])
+            lits.append([hx(sa), 0, i * 8 + 7, "", ""])
+        exp_c, exp_alt = {}, {}
+        for i in range(4):
+            cnt = N - (1 << i) + 1
+            one = cnt if i == 0 else 0
+            exp_c.update({i * 8 + 0: cnt, i * 8 + 1: 0, i * 8 + 3: 0, i * 8 + 7: one})
+            if cb:
+                exp_c.update({i * 8 + k: cnt for k in (2, 4, 5, 6)})
+            else:
+                exp_c.update({i * 8 + 2: 0, i * 8 + 4: 0, i * 8 + 5: 0, i * 8 + 6: one})
+            exp_alt.update({i * 8 + 0: 0, i * 8 + 1: one, i * 8 + 3: one, i * 8 + 5: cnt,
+                            i * 8 + 7: 0})
+            if cb:
+                exp_alt.update({i * 8 + k: cnt for k in (2, 4, 6)})
+            else:
+                exp_alt.update({i * 8 + 2: one, i * 8 + 4: one, i * 8 + 6: 0})
+        out.append({"src": "fdr_flood.cpp:148 NoMask", "c": c, "lits": lits,
+                    "runs": [{"fill": c, "expected": exp_c}, {"fill": cAlt, "expected": exp_alt}]})
+
+        # WithMask :235-402 (StreamingMask :404-558 builds the same set)
+        lits = []
+        s4, s4a = bytes([c] * 4), bytes([cAlt] * 4)
+        for i in range(4):
+            ml = 1 << i
+            msk, cmp = bytearray(ml), bytearray(ml)
+            cmp[0], msk[0] = cAlt, 0xFF
+
+            def add(st, nc, k):
+                lits.append([hx(st), nc, i * 12 + k, hx(msk), hx(cmp)])
+            if ml > len(s4):
+                add(s4, 0, 0)
+                add(s4, 1, 1)
+            if cb:
+                add(s4, 1, 2)
+            if (cAlt & bit) == 0:
+                msk[0] = (~bit) & 0xFF
+                add(s4, 0, 3)
+                add(s4, 1, 4)
+            cmp[0], msk[0] = c, 0xFF
+            add(s4, 0, 5)
+            add(s4, 1, 6)
+            if ml > len(s4a):
+                add(s4a, 0, 7)
+                add(s4a, 1, 8)
+            if cb:
+                add(s4a, 1, 9)
+                cmp[ml - 1], msk[ml - 1] = cAlt, 0xFF
+                add(s4, 1, 10)
+                cmp[0] = cAlt
+                add(s4, 1, 11)
+        cnt4 = N - 4 + 1
+        exp_c, exp_alt = {}, {}
+        for i in range(4):
+            ml = 1 << i
+            cm = min(cnt4, N - ml + 1)
+            exp_c.update({i * 12 + 0: 0, i * 12 + 1: 0, i * 12 + 2: 0})
+            if (cAlt & bit) == 0:
+                exp_c.update({i * 12 + 3: cm, i * 12 + 4: cm})
+            if ml > 4:
+                exp_c.update({i * 12 + 5: cm, i * 12 + 6: cm, i * 12 + 7: 0,
+                              i * 12 + 8: cm if cb else 0})
+            else:
+                exp_c.update({i * 12 + 5: cnt4, i * 12 + 6: cnt4})
+            if cb:
+                exp_c.update({i * 12 + 9: cm, i * 12 + 10: 0, i * 12 + 11: 0})
+            exp_alt.update({i * 12 + k: 0 for k in (0, 3, 5, 6, 7, 8, 9)})
+            if cb:
+                exp_alt.update({i * 12 + 1: cm if ml > 4 else 0, i * 12 + 2: cm,
+                                i * 12 + 4: cm if 0x61 <= c <= 0x7A else 0,
+                                i * 12 + 10: cnt4 if ml == 1 else 0, i * 12 + 11: cm})
+            else:
+                exp_alt.update({i * 12 + k: 0 for k in (1, 2, 4, 10, 11)})
+        out.append({"src": "fdr_flood.cpp:235 WithMask / :404 StreamingMask", "c": c,
+                    "lits": lits, "stream": True,
+                    "runs": [{"fill": c, "expected": exp_c}, {"fill": cAlt, "expected": exp_alt}]})
+    return out
+
+
 def main():
     with open(os.path.join(HERE, "noodle.json"), "w") as f:
         json.dump(noodle_cases(), f)
@@ -482,6 +595,8 @@ def main():
         json.dump(dshufti_cases(), f)
     with open(os.path.join(HERE, "fdr_stream.json"), "w") as f:
         json.dump(fdr_stream_cases(), f)
+    with open(os.path.join(HERE, "fdr_flood.json"), "w") as f:
+        json.dump(fdr_flood_cases(), f, separators=(",", ":"))
 
 
 if __name__ == "__main__":

@@ -233,11 +233,14 @@ def _check(rc):
 
 
 def hwlm_build(lits, engine_hint=-1, allow_noodle=True, allow_teddy=True,
-               allow_fat_teddy=True, allow_flood=False):
+               allow_fat_teddy=True, allow_flood=True):
     """hwlmBuildProto + hwlmBuild (hwlm_build.cpp:120-214).
 
     ``engine_hint`` mirrors fdrBuildProtoHinted (fdr_compile.cpp:899-910):
     0 forces FDR (domain 9, stride 1), 3..18 a Teddy engine id.
+    ``allow_flood`` is Grey::fdrAllowFlood (default on, grey.cpp:68): off,
+    every flood record carries idCount = FDR_FLOOD_MAX_IDS and never fires
+    (flood_compile.cpp:191-195).
     Returns a :class:`Blob`; raises :class:`BuildError` when the literal set
     cannot be built with the requested engine.
     """

@@ -137,7 +137,13 @@ struct vsa_db {
     uint32_t slot_off[16];
     uint8_t slot_bits[16] = {0}; /* prefilter hash bits per bucket (<= nBits) */
     uint64_t pf_mult = 0;
+    bool flood_live = false;     /* some FDRFlood record can fire (idCount < max) */
 };
+
+/* VECTORSIZE of the reference build emulated where results depend on it:
+ * shuftiDoubleExec's per-block lanes and the Teddy loop shape of the flood
+ * shortcut (flood.cpp) */
+static uint32_t g_vector_size = 64;
 
 namespace {
 
@@ -662,19 +668,55 @@ hwlm_error_t replay_nood(const uint64_t *keys, const uint32_t *ids, uint64_t n,
     return HWLM_SUCCESS;
 }
 
+/* the flood shortcut's reports (flood_runtime.h:191-319): per group of
+ * S = 4 (idCount <= 2) or 2 ends, each end reports every flood id whose
+ * groups meet the live control, the run stopping once control leaves
+ * allGroups; no confirm, no NOREPEAT */
+bool emit_flood(const vsa::FloodEvent &ev, HWLMCallback cb, hs_scratch *scratch,
+                uint64_t &control) {
+    const FDRFlood *fl = ev.fl;
+    if (fl->idCount && (control & fl->allGroups)) {
+        const uint32_t S = fl->idCount <= 2 ? 4 : 2;
+        for (uint32_t t = 0; t < ev.size && (control & fl->allGroups); t += S)
+            for (uint32_t k = 0; k < S; k++)
+                for (uint32_t d = 0; d < fl->idCount; d++)
+                    if (control & fl->groups[d])
+                        control = cb((size_t)(ev.i + t + k), fl->ids[d], scratch);
+    }
+    return control != HWLM_TERMINATE_MATCHING;
+}
+
+/* The confirmed records of one call, in reference order, through the
+ * callback with confWithBit's sequential state; `floods` (ascending) replace
+ * the ends they skip. */
 hwlm_error_t replay_lit(const vsa_db *db, const uint64_t *keys, uint64_t n,
-                        HWLMCallback cb, hs_scratch *scratch, hwlm_group_t groups) {
+                        HWLMCallback cb, hs_scratch *scratch, hwlm_group_t groups,
+                        const std::vector<vsa::FloodEvent> *floods = nullptr) {
     const uint8_t *eng = db->hblob + VSA_ROUNDUP_CL(sizeof(HWLM));
     const uint8_t *confBase = eng + ((const uint32_t *)eng)[4];
     const bool squash_ok = scratch && db->mode == VSA_MODE_FDR;
     const long co = g_fdr_conf_off.load(), coo = g_fdr_conf_offset_off.load();
+    const size_t nf = floods ? floods->size() : 0;
+    size_t fe = 0;
+    uint64_t skip_lo = 0, skip_hi = 0; /* ends a flood replaced */
     uint64_t control = groups;
     uint32_t last_match = ~0u;
     uint64_t i = 0;
-    while (i < n) {
-        const uint64_t end = keys[i] >> VSA_KEY_END_SHIFT;
+    while (i < n || fe < nf) {
+        const uint64_t end = i < n ? keys[i] >> VSA_KEY_END_SHIFT : ~0ULL;
+        if (fe < nf && (*floods)[fe].i <= end) {
+            const vsa::FloodEvent &ev = (*floods)[fe++];
+            if (!emit_flood(ev, cb, scratch, control)) return HWLM_TERMINATED;
+            skip_lo = ev.i;
+            skip_hi = (uint64_t)ev.i + ev.size;
+            continue;
+        }
         uint64_t j = i;
         while (j < n && (keys[j] >> VSA_KEY_END_SHIFT) == end) j++;
+        if (end >= skip_lo && end < skip_hi) {
+            i = j;
+            continue;
+        }
         uint32_t squashed = 0;
         for (uint64_t k = i; k < j; k++) {
             const uint32_t b = (uint32_t)(keys[k] >> VSA_KEY_BUCKET_SHIFT) & 15;
@@ -707,6 +749,16 @@ hwlm_error_t replay_lit(const vsa_db *db, const uint64_t *keys, uint64_t n,
         i = j;
     }
     return HWLM_SUCCESS;
+}
+
+/* flood events of one call when the blob's flood table is live */
+const std::vector<vsa::FloodEvent> *floods_for(const vsa_db *db, const uint8_t *buf, size_t len,
+                                               size_t start,
+                                               std::vector<vsa::FloodEvent> &ev) {
+    if (!db->flood_live || db->type != HWLM_ENGINE_FDR) return nullptr;
+    vsa::flood_events(buf, len, start, db->hblob + VSA_ROUNDUP_CL(sizeof(HWLM)),
+                      g_vector_size, ev);
+    return ev.empty() ? nullptr : &ev;
 }
 
 /* scan one host buffer with the default context */
@@ -1038,6 +1090,14 @@ int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
         }
         const uint32_t *confBase = (const uint32_t *)(eng + ((const uint32_t *)eng)[4]);
         for (uint32_t b = 0; b < db->nbuckets; b++) db->conf_off[b] = confBase[b];
+        {
+            /* flood table (fdr_compile.cpp:204-211): 256 x u32 index, records */
+            const uint8_t *fb = eng + ((const uint32_t *)eng)[5];
+            const uint32_t *fidx = (const uint32_t *)fb;
+            const FDRFlood *fr = (const FDRFlood *)(fb + 1024);
+            for (int ch = 0; ch < 256 && !db->flood_live; ch++)
+                db->flood_live = fr[fidx[ch]].idCount < FDR_FLOOD_MAX_IDS;
+        }
         /* match keys carry a LitInfo's offset from its FDRConfirm in 8-byte
          * units in 20 bits (kernels.h): engines up to 8 MiB */
         if (engine_size(eng, HWLM_ENGINE_FDR) > ((size_t)8 << 20)) return VSA_E_INVALID;
@@ -1444,7 +1504,9 @@ hwlm_error_t hwlmExec(const struct HWLM *tab, const uint8_t *buf, size_t len, si
     start = hwlm_accel_block(aa, buf, len, start);
     if (start >= len) return HWLM_SUCCESS;
     if (scan_host(db, buf, len, start, keys, ids) != VSA_OK) return HWLM_ERROR_UNKNOWN;
-    return replay_lit(db, keys.data(), keys.size(), cb, scratch, groups);
+    std::vector<vsa::FloodEvent> ev;
+    return replay_lit(db, keys.data(), keys.size(), cb, scratch, groups,
+                      floods_for(db, buf, len, start, ev));
 }
 
 hwlm_error_t fdrExec(const struct FDR *fdr, const uint8_t *buf, size_t len, size_t start,
@@ -1456,7 +1518,9 @@ hwlm_error_t fdrExec(const struct FDR *fdr, const uint8_t *buf, size_t len, size
     std::vector<uint64_t> keys;
     std::vector<uint32_t> ids;
     if (scan_host(db, buf, len, start, keys, ids) != VSA_OK) return HWLM_ERROR_UNKNOWN;
-    return replay_lit(db, keys.data(), keys.size(), cb, scratch, groups);
+    std::vector<vsa::FloodEvent> ev;
+    return replay_lit(db, keys.data(), keys.size(), cb, scratch, groups,
+                      floods_for(db, buf, len, start, ev));
 }
 
 hwlm_error_t noodExec(const struct noodTable *n, const uint8_t *buf, size_t len, size_t start,
@@ -1486,7 +1550,9 @@ hwlm_error_t fdrExecStreaming(const struct FDR *fdr, const uint8_t *hbuf, size_t
     std::vector<uint32_t> ids;
     if (scan_host(db, buf, len, start, keys, ids, hlen ? hbuf + hlen : nullptr, hlen) != VSA_OK)
         return HWLM_ERROR_UNKNOWN;
-    return replay_lit(db, keys.data(), keys.size(), cb, scratch, groups);
+    std::vector<vsa::FloodEvent> ev;
+    return replay_lit(db, keys.data(), keys.size(), cb, scratch, groups,
+                      floods_for(db, buf, len, start, ev));
 }
 
 /* noodExecStreaming noodle_engine.cpp:136-185 */
@@ -1672,8 +1738,6 @@ const uint8_t *shuftiExec(vsa_m128_t mask_lo, vsa_m128_t mask_hi, const uint8_t 
                       "shuftiExec");
 }
 
-static uint32_t g_vector_size = 64; /* reference VECTORSIZE emulated by shuftiDoubleExec */
-
 void vsa_set_accel_vector_size(uint32_t vsize) {
     if (vsize == 16 || vsize == 32 || vsize == 64) g_vector_size = vsize;
 }
@@ -1841,7 +1905,7 @@ void vsa_build_opts_default(vsa_build_opts_t *o) {
     o->allow_noodle = 1;
     o->allow_teddy = 1;
     o->allow_fat_teddy = 1;
-    o->allow_flood = 0;
+    o->allow_flood = 1; /* the reference Grey default (grey.cpp:68) */
 }
 
 int vsa_hwlm_build(const vsa_literal_t *lits, size_t n, const vsa_build_opts_t *opts,

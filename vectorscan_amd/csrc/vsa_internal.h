@@ -37,9 +37,23 @@ struct BuildOptions {
     bool allow_noodle = true;
     bool allow_teddy = true;
     bool allow_fat_teddy = true; /* the GPU runs 16-bucket Teddy natively */
-    bool allow_flood = false;    /* see DESIGN.md "flood" */
+    bool allow_flood = true;     /* Grey::fdrAllowFlood (grey.cpp:68) */
     int engine_hint = -1;        /* -1: choose; 0: FDR d9 s1; 3..18 Teddy id */
 };
+
+/* One flood shortcut taken by the reference main loop (flood.cpp): the
+ * flood ids of `fl` are reported at ends [i, i + size) and the main loop
+ * skips those ends. */
+struct FloodEvent {
+    u32 i;
+    u32 size;
+    const FDRFlood *fl;
+};
+/* Flood events of one fdrExec / fdrExecStreaming call on the engine `eng`
+ * (FDR or Teddy) over the host buffer (its address matters), in order.
+ * vsize selects the Teddy build emulated (16 SSE, 32 AVX2, 64 VBMI). */
+void flood_events(const u8 *buf, size_t len, size_t start, const u8 *eng, u32 vsize,
+                  std::vector<FloodEvent> &out);
 
 Literal makeLiteral(const u8 *s, size_t len, bool nocase, bool noruns, u32 id,
                     u64a groups, const u8 *msk, const u8 *cmp, size_t mlen);
