@@ -290,7 +290,7 @@ int64_t vsa_verm_find(int mode, uint8_t c1, uint8_t c2, uint8_t m1, uint8_t m2,
 
 /* Host-only: the first-stage table the engine derives from an FDR / Teddy
  * blob's confirm records (FDR: 2^14 u64 entries, 8 positions x 8 buckets,
- * key = b[p] | (b[p+1] & 0x3f) << 8; Teddy: 256 entries, 8 x 8; Fat Teddy:
+ * key = (b[p] & 0x7f) | (b[p+1] & 0x7f) << 7; Teddy: 256 entries, 8 x 8; Fat Teddy:
  * 256 entries, 4 x 16).  Returns entries written or a VSA_E_* code. */
 int vsa_derive_first_stage(const void *hwlm, size_t size, uint64_t *table, uint32_t cap,
                            uint32_t *key_bits, uint32_t *field_bits);

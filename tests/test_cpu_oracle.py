@@ -452,7 +452,8 @@ def _first_stage_candidates(table, key_bits, field_bits, data):
     n = len(b)
     if key_bits == 14:
         nxt = np.concatenate([b[1:], np.zeros(1, np.uint64)])
-        key = b | ((nxt & np.uint64(0x3F)) << np.uint64(8))
+        # vsa_fdr_key (kernels.h): 7 bits of each byte
+        key = (b & np.uint64(0x7F)) | ((nxt & np.uint64(0x7F)) << np.uint64(7))
     else:
         key = b
     x = table[key.astype(np.int64)]

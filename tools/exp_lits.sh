@@ -1,8 +1,6 @@
 #!/bin/bash
-# literal-count sweep of the FDR path (4 GiB): time, confirm candidates, confirm-wave phases
-set -e
-OUT=gpurun_out/lits
-mkdir -p $OUT
+# kernel time + confirm-wave counters vs literal-set size (4 GiB, FDR)
+timeout -k 10 120 python3 bench.py --steps 20 --warmup 20 --no-cpu --no-parity | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('bench', d['ms_per_step'], d['roofline']['kernel_ms'])" || exit 1
 for n in 1000 5000 10000 20000 50000; do
-  timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-cpu --lits $n 2>/dev/null | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('lits $n', d['config']['workload'][-12:], d['roofline']['kernel_ms'], d['roofline']['frac'], d['parity'], d['confirm_candidates'], d['matches'])" >> $OUT/lits.txt
+  LITS=$n VSA_DEBUG_FLAGS=64 timeout -k 10 200 python3 tools/exp_counters.py || exit 1
 done

@@ -45,6 +45,17 @@ struct VsaBlock {
 #define VSA_KEY_BUCKET_SHIFT 20
 #define VSA_KEY_LI_MASK 0xfffffu
 
+/* Key of the derived FDR first stage (runtime.hip derive_fdr_table) for the
+ * byte pair (b0, b1) at positions (p, p + 1), dmask = 2^bits - 1 (bits 13 or
+ * 14): the low 7 bits of b0 and the low bits - 7 bits of b1.  The kernels
+ * compute it two keys per dword (kernels.hip fdr_key2). */
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+static inline uint32_t vsa_fdr_key(uint32_t b0, uint32_t b1, uint32_t dmask) {
+    return (b0 & 0x7fu) | ((b1 << 7) & dmask & ~0x7fu);
+}
+
 enum VsaLitMode {
     VSA_MODE_FDR = 0,   /* 8 lanes x 8 buckets, 2-byte key & domainMask */
     VSA_MODE_TEDDY = 1, /* 4 lanes x 8 buckets, 1-byte key */
@@ -82,7 +93,11 @@ struct VsaLitParams {
                                     (mismatches -> counters[3]); bit1 drop all
                                     candidates (filter-only timing); bit3 stop
                                     after the candidate test; bit4 skip the
-                                    push; bit5 count first-stage candidates */
+                                    push; bit5 count first-stage candidates;
+                                    bit6 confirm-wave phase counters; bit7
+                                    the confirm wave drops what it gathers;
+                                    bit8 32-B ring entries (drops the data);
+                                    bit10 confirm wave at base priority */
     uint64_t *out_keys;
     uint32_t *out_ids;
     uint64_t out_cap;

@@ -84,6 +84,13 @@ __device__ __forceinline__ u32 writelane_u32(u32 v, u32 s) {
     asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(readfirstlane_u32(s)), "n"(L));
     return v;
 }
+/* vsa_fdr_key of the byte pairs (0, 1) and (2, 3) of x, one per 16-bit half:
+ * the low 7 bits of the first byte, then the second byte's low bits under
+ * km = (dmask & ~0x7f) in both halves (the shift's bit 16 -> 15 spill is
+ * outside km) */
+__device__ __forceinline__ u32 fdr_key2(u32 x, u32 km) {
+    return (x & 0x007f007fu) | ((x >> 1) & km);
+}
 /* LDS byte address of an 8-byte table entry: base + 8 * (16-bit half H of
  * w) in one op (v_mad_u32_u16 with op_sel picks the half, no bfe/shift) */
 template <int H>
@@ -205,31 +212,36 @@ struct QEnt {
 };
 
 /* Candidates go from the scanning waves to the workgroup's confirm wave
- * through one shared LDS ring of 2^lg chunk entries: one entry per lane
- * whose 16 ends hold any first-stage candidate, carrying the lane's
- * candidate masks and the 24 bytes its confirm keys are cut from, so the
- * scanning wave never loops over candidate bits (a wave looping for one
- * lane's rare candidate wasted the other 63 lanes; the confirm wave expands
- * the entries 64 at a time).  Entry layout, EW uint4 words: {meta, c[0..CW),
- * pv2, pv3, d0..d3} (noodle: {meta}, {hits}), meta = p0 | blk << 40 | lap
- * << 60.  A scanner reserves slots with one LDS atomic on *head, waits for
- * room against *tail, writes words 1.. and then word 0; lap = (position >>
- * lg) & 15 marks word 0 as written for this pass of the ring (LDS executes a
- * wave's instructions in order, so a visible word 0 implies visible words
- * 1..).  The confirm wave reads the 64 slots at its tail and takes the
- * leading run whose lap matches: one LDS round trip per gather. */
+ * through per-wave single-producer LDS rings of 2^lg chunk entries: one
+ * entry per lane whose 16 ends hold any first-stage candidate, carrying the
+ * lane's candidate masks and the 24 bytes its confirm keys are cut from, so
+ * the scanning wave never loops over candidate bits (the confirm wave
+ * expands the entries 64 at a time).  Entry layout, EW uint4 words: {meta,
+ * c[0..CW), pv2, pv3, d0..d3} (noodle: {meta}, {hits}), meta = p0 | blk << 40.  A scanning wave owns its ring's head (a register: no atomic,
+ * no LDS round trip on a push), waits for room only against its cached
+ * copy of the tail the confirm wave publishes, writes the entries and then
+ * publishes its head with a plain LDS store (LDS executes a wave's
+ * instructions in order, so a visible head implies visible entries).  The
+ * confirm wave polls the 15 heads with one broadcast read (lane 4 r + k
+ * reads head r) and then reads only the available slots tail_r + k, k < 4:
+ * one instruction per idle poll, and masked lanes cost no LDS banks.  (A
+ * shared ring reserved with a returning LDS atomic cost the scanners that
+ * atomic's round trip on every push, ~1000 cycles under the bank-conflicted
+ * lookups.) */
 #define ENT_BLK_SHIFT 40
 #define ENT_LAP_SHIFT 60
 #define ENT_P0_MASK ((1ULL << ENT_BLK_SHIFT) - 1)
+#define RING_SLOTS 4 /* slots of each ring read per gather */
 struct LitShared {
     const void *tab;
     u32 tab_lds;     /* LDS byte address of tab (LDS tables) */
     u32 kmask2;      /* FDR key mask in both 16-bit halves */
     u32 tsel;        /* Teddy: TEDDY_TAB_LDS | this lane's copy offset */
-    uint4 *ring;     /* the shared ring */
-    u32 *head;       /* positions reserved (LDS atomic) */
-    const u32 *tail; /* positions consumed (written by the confirm wave) */
-    u32 lg;          /* log2 ring entries (>= 6) */
+    uint4 *ring;     /* this wave's ring */
+    const u32 *tail; /* this ring's consumed position (written by the confirm wave) */
+    u32 *head;       /* this ring's published head (written by this wave) */
+    u32 lg;          /* log2 ring entries (>= 2) */
+    u32 dbg;         /* VsaLitParams.dbg */
 };
 
 __device__ __forceinline__ u32 lds_ld32(const u32 *p) {
@@ -349,10 +361,10 @@ __device__ __forceinline__ u64 lit_lookup(const void *tab, u32 key, u32 lane) {
 template <int MODE>
 __device__ __forceinline__ u32 lit_key(const u32 d[5], int j, u32 dmask) {
     if constexpr (LitTraits<MODE>::KEY16) {
-        /* dmask = 2^bits - 1 (fdr_compile.cpp:185-187, and the derived
-         * table): one bit-field extract while the key sits in one dword */
-        if ((j & 3) != 3) return __builtin_amdgcn_ubfe(d[j >> 2], 8 * (j & 3), 32 - __clz(dmask));
-        return __builtin_amdgcn_alignbyte(d[(j >> 2) + 1], d[j >> 2], 3) & dmask;
+        /* vsa_fdr_key of bytes j, j + 1 (the derived table's key) */
+        const u32 w = (j & 3) != 3 ? d[j >> 2] >> (8 * (j & 3))
+                                   : __builtin_amdgcn_alignbyte(d[(j >> 2) + 1], d[j >> 2], 3);
+        return vsa_fdr_key(w & 0xff, (w >> 8) & 0xff, dmask);
     } else {
         (void)dmask;
         return (d[j >> 2] >> (8 * (j & 3))) & 0xff;
@@ -364,6 +376,7 @@ struct IterState {
     u64 pbytes; /* the 8 bytes before the next chunk (lane 63's d[2..3]) */
     u32 ncand;  /* first-stage candidates so far (diagnostic, wave-uniform) */
     u32 tail_cache; /* last tail read from the confirm wave */
+    u32 head;       /* entries this wave has pushed to its ring */
 };
 
 struct SegCtx {
@@ -377,8 +390,8 @@ struct SegCtx {
 };
 
 /* Append one EW-word entry per lane with push set to the wave's ring
- * (wave-uniform call), in batches of at most the ring size.  The ring cursor
- * in `st` is updated identically by every lane. */
+ * (wave-uniform call), in batches of at most the ring size.  The head and
+ * tail cache in `st` are updated identically by every lane. */
 template <int EW, typename ST>
 __device__ __forceinline__ void ring_push(const LitShared &L, ST &st, bool push,
                                           const u32 (&w)[4 * EW]) {
@@ -387,29 +400,30 @@ __device__ __forceinline__ void ring_push(const LitShared &L, ST &st, bool push,
     const u32 n = (u32)__popcll(pm);
     const u32 r = __builtin_amdgcn_mbcnt_hi((u32)(pm >> 32),
                                              __builtin_amdgcn_mbcnt_lo((u32)pm, 0));
-    /* one reservation (n <= 64 <= ring size): the earliest unwritten
-     * reservation always fits, so waiting for room cannot deadlock */
-    u32 pos = 0;
-    if (lane_id() == 0)
-        pos = __hip_atomic_fetch_add(L.head, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    pos = readfirstlane_u32(pos);
     const u32 cap = 1u << L.lg;
-    if (pos + n - st.tail_cache > cap) {
-        for (;;) {
-            st.tail_cache = readfirstlane_u32(lds_ld32(L.tail));
-            if (pos + n - st.tail_cache <= cap) break;
-            __builtin_amdgcn_s_sleep(2);
+    for (u32 b0 = 0; b0 < n; b0 += cap) {
+        const u32 m = n - b0 < cap ? n - b0 : cap;
+        const u32 pos = st.head;
+        if (pos + m - st.tail_cache > cap) {
+            for (;;) {
+                st.tail_cache = readfirstlane_u32(lds_ld32(L.tail));
+                if (pos + m - st.tail_cache <= cap) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
         }
-    }
-    if (push) {
-        const u32 slot = pos + r;
-        uint4 *q = L.ring + (size_t)(slot & (cap - 1)) * EW;
+        if (push && r >= b0 && r < b0 + m) {
+            const u32 slot = pos + r - b0;
+            uint4 *q = L.ring + (size_t)(slot & (cap - 1)) * EW;
 #pragma unroll
-        for (int k = 1; k < EW; k++)
-            q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
-        asm volatile("" ::: "memory"); /* word 0 (with the lap) last */
-        const u32 lap = (slot >> L.lg) & 15u;
-        q[0] = make_uint4(w[0], w[1] | (lap << (ENT_LAP_SHIFT - 32)), w[2], w[3]);
+            for (int k = 0; k < EW; k++)
+                if (k < 2 || !(L.dbg & 256)) /* experiment: short entries */
+                    q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+        }
+        st.head = pos + m;
+        /* the batch's entries before its head (a later batch may wait for
+         * the confirm wave to drain this one) */
+        asm volatile("" ::: "memory");
+        if (lane_id() == 0) lds_st32(L.head, st.head);
     }
 }
 
@@ -513,8 +527,8 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     if constexpr (MODE == VSA_MODE_FDR && LDS_TABLE) {
 #pragma unroll
         for (int w = 0; w < 4; w++) {
-            km[w] = d[w] & L.kmask2;
-            ko[w] = __builtin_amdgcn_alignbyte(d[w + 1], d[w], 1) & L.kmask2;
+            km[w] = fdr_key2(d[w], L.kmask2);
+            ko[w] = fdr_key2(__builtin_amdgcn_alignbyte(d[w + 1], d[w], 1), L.kmask2);
         }
     }
 #pragma unroll
@@ -563,6 +577,7 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     IterState out;
     out.ncand = in.ncand;
     out.tail_cache = in.tail_cache;
+    out.head = in.head;
     out.carry = ((u64)readlane_u32((u32)(s_out >> 32), WAVE - 1) << 32) |
                 readlane_u32((u32)s_out, WAVE - 1);
     out.pbytes = ((u64)readlane_u32(d[3], WAVE - 1) << 32) | readlane_u32(d[2], WAVE - 1);
@@ -791,19 +806,23 @@ __device__ __forceinline__ uint4 load_wave_kib(const u8 *base, u32 off) {
  * (q_done, read before the heads), every ring is empty and the queue is
  * drained. */
 #define LIT_SCANNERS (LIT_WAVES - 1)
-#define PQ_CAP 512 /* >= CONF_U * 64 + 63 */
+#define EXP_U 1     /* candidate bits per lane per expansion round (4 measured
+                       slower: the expansion is VALU-bound, not latency-bound) */
+#define PQ_CAP 512  /* >= CONF_U * 64 + EXP_U * 64 - 1 */
 template <int MODE>
 __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLds &cl,
-                                             const uint4 *ring, u32 lg, const u32 *head_p,
-                                             u32 *tail_p,
-                                             const u32 *q_done, u32 mis, const u32 *slots,
-                                             QEnt *pq) {
+                                             const uint4 *rings, u32 lg, u32 *tails,
+                                             const u32 *heads, const u32 *q_done, u32 mis,
+                                             const u32 *slots, QEnt *pq) {
     typedef LitTraits<MODE> T;
     constexpr int EW = T::EW;
     constexpr int CW = T::CW;
     const u32 lane = lane_id();
     const u32 cap = 1u << lg;
-    u32 tail = 0; /* ring positions consumed (wave-uniform) */
+    /* lane 4 r + k reads slot tail_r + k of ring r (r < LIT_SCANNERS) */
+    const u32 rr = lane >> 2, rk = lane & 3;
+    const bool ring_lane = rr < LIT_SCANNERS;
+    u32 tail = 0; /* ring rr's consumed position (same in its 4 lanes) */
     u32 filled = 0;
     u32 consumed = 0;
     u32 pq_head = 0, pq_tail = 0; /* private queue cursors (wave-uniform) */
@@ -840,47 +859,30 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
     for (;;) {
         const bool all_done = lds_ld32(q_done) == LIT_SCANNERS;
         asm volatile("" ::: "memory");
-        /* gather: the slots at the tail that scanners have reserved (one
-         * broadcast read of the reservation counter, so an idle poll costs
-         * one LDS cycle, not 64 entries), the leading run of written ones */
+        /* poll: the 15 heads in one broadcast read */
+        const u32 avail = ring_lane ? lds_ld32(&heads[rr]) - tail : 0u;
+        const bool valid = rk < avail;
         u32 e[4 * EW];
 #pragma unroll
         for (int i = 0; i < 4 * EW; i++) e[i] = 0;
-        filled = 0;
-        const u32 reserved = readfirstlane_u32(lds_ld32(head_p)) - tail;
-        if (reserved) {
-            const u32 pos = tail + lane;
-            bool ready = false;
-            if (lane < reserved) {
-                const uint4 *q = ring + (size_t)(pos & (cap - 1)) * EW;
-                const uint4 v0 = q[0];
-                asm volatile("" ::: "memory"); /* word 0 (lap) before words 1.. */
-                e[0] = v0.x;
-                e[1] = v0.y;
-                e[2] = v0.z;
-                e[3] = v0.w;
+        filled = (u32)__popcll(__ballot(valid));
+        if (filled) {
+            /* gather the available slots (up to RING_SLOTS per ring) */
+            if (valid) {
+                const uint4 *q = rings + ((size_t)rr * cap + ((tail + rk) & (cap - 1))) * EW;
 #pragma unroll
-                for (int k = 1; k < EW; k++) {
+                for (int k = 0; k < EW; k++) {
                     const uint4 v = q[k];
                     e[4 * k] = v.x;
                     e[4 * k + 1] = v.y;
                     e[4 * k + 2] = v.z;
                     e[4 * k + 3] = v.w;
                 }
-                ready = (e[1] >> (ENT_LAP_SHIFT - 32)) == ((pos >> lg) & 15u);
             }
-            const u64 rb = __ballot(ready);
-            filled = ~rb ? (u32)__builtin_ctzll(~rb) : (u32)WAVE;
             asm volatile("" ::: "memory"); /* entries read before they are freed */
-            if (filled) {
-                tail += filled;
-                if (lane == 0) lds_st32(tail_p, tail);
-            }
-            if (lane >= filled) {
-#pragma unroll
-                for (int i = 0; i < 4 * EW; i++) e[i] = 0;
-            }
-            e[1] &= (1u << (ENT_LAP_SHIFT - 32)) - 1; /* strip the lap */
+            const u32 run = avail < RING_SLOTS ? avail : RING_SLOTS;
+            tail += run;
+            if (rk == 0 && ring_lane && run) lds_st32(&tails[rr], tail);
         }
         pc[4]++;
         pc[5] += filled;
@@ -897,10 +899,17 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
             phase(3);
             continue;
         }
-        /* entries in hand: issue ahead of the scanners on this SIMD (the
-         * youngest wave otherwise loses VALU arbitration to all of them);
-         * noodle entries are final matches, where priority measured slower */
-        if constexpr (MODE != VSA_MODE_NOOD) __builtin_amdgcn_s_setprio(2);
+        if (P.dbg & 128) continue; /* experiment: drop gathered entries */
+        /* a backlog (many entries per gather): issue ahead of the scanners
+         * on this SIMD (the youngest wave otherwise loses VALU arbitration
+         * to all of them), as large literal sets need; a light load runs at
+         * base priority, which measured 1.5 % faster at cfg 4.  Noodle
+         * entries are final matches, where priority measured slower. */
+        if constexpr (MODE != VSA_MODE_NOOD)
+        {
+            if (filled >= 16 && !(P.dbg & 1024)) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         const u64 meta0 = ((u64)e[1] << 32) | e[0];
         const u64 p0 = meta0 & ENT_P0_MASK;
         const u32 blk = (u32)(meta0 >> ENT_BLK_SHIFT);
@@ -929,59 +938,83 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
             const u64 W0 = ((u64)e[3 + CW] << 32) | e[2 + CW];
             const u64 W1 = ((u64)e[5 + CW] << 32) | e[4 + CW];
             const u64 W2 = ((u64)e[7 + CW] << 32) | e[6 + CW];
-            /* Wave-uniform loop: each round every lane takes its lowest
-             * remaining candidate bit (over all conf words). */
+            /* Wave-uniform loop: each round every lane takes its EXP_U
+             * lowest remaining candidate bits (over all conf words), so the
+             * prefilter's dependent LDS reads (bucket record, slot word) of
+             * up to 4 x 64 candidates are in flight together. */
             for (;;) {
-                u32 word = 0, bits = c[0];
+                bool have[EXP_U];
+                u32 jj[EXP_U], bb[EXP_U];
 #pragma unroll
-                for (int k = 1; k < CW; k++) {
-                    const bool take = bits == 0;
-                    bits = take ? c[k] : bits;
-                    word = take ? (u32)k : word;
-                }
-                const bool have = bits != 0;
-                if (!__any(have)) break;
-                pc[6]++;
-                bool push = false;
-                u64 key = 0, meta = 0;
-                if (have) {
+                for (int u = 0; u < EXP_U; u++) {
+                    u32 word = 0, bits = c[0];
+#pragma unroll
+                    for (int k = 1; k < CW; k++) {
+                        const bool take = bits == 0;
+                        bits = take ? c[k] : bits;
+                        word = take ? (u32)k : word;
+                    }
+                    have[u] = bits != 0;
                     const u32 bit = __ffs(bits) - 1;
 #pragma unroll
                     for (int k = 0; k < CW; k++)
-                        if (word == (u32)k) c[k] &= c[k] - 1;
-                    u32 j, b;
+                        if (have[u] && word == (u32)k) c[k] &= c[k] - 1;
                     if constexpr (T::LB == 8) {
-                        j = 4 * word + (bit >> 3);
-                        b = bit & 7;
+                        jj[u] = 4 * word + (bit >> 3);
+                        bb[u] = bit & 7;
                     } else {
-                        j = 2 * word + (bit >> 4);
-                        b = bit & 15;
+                        jj[u] = 2 * word + (bit >> 4);
+                        bb[u] = bit & 15;
                     }
+                }
+                if (!__any(have[0])) break;
+                pc[6]++;
+                u64 key[EXP_U];
+                PfRec pf[EXP_U];
+#pragma unroll
+                for (int u = 0; u < EXP_U; u++) {
                     /* key = bytes [j-7, j] = byte offset j+1 .. j+8 of W0:W1:W2 */
-                    const u32 o = j + 1;
-                    if (o < 8) key = (W0 >> (8 * o)) | (W1 << (64 - 8 * o));
-                    else if (o == 8) key = W1;
-                    else if (o < 16) key = (W1 >> (8 * (o - 8))) | (W2 << (64 - 8 * (o - 8)));
-                    else key = W2;
+                    const u32 o = jj[u] + 1;
+                    u64 k8;
+                    if (o < 8) k8 = (W0 >> (8 * o)) | (W1 << (64 - 8 * o));
+                    else if (o == 8) k8 = W1;
+                    else if (o < 16) k8 = (W1 >> (8 * (o - 8))) | (W2 << (64 - 8 * (o - 8)));
+                    else k8 = W2;
+                    key[u] = k8;
+                    /* unconditional reads (bb in range either way), so the
+                     * EXP_U reads of each kind are in flight together */
+                    pf[u] = cl.pf[bb[u] & 15];
+                }
+                u32 sw[EXP_U], sh[EXP_U];
+                bool chk[EXP_U];
+#pragma unroll
+                for (int u = 0; u < EXP_U; u++) {
                     /* LDS slot-bitmap prefilter: litIndex[hash] == 0 rejects */
-                    const PfRec pf = cl.pf[b];
-                    push = true;
-                    if (pf.slot_off != 0xffffffffu) {
-                        const u32 h = (u32)(((key & pf.andmsk) * P.pf_mult) >> pf.shift);
-                        push = (slots[pf.slot_off + (h >> 5)] >> (h & 31)) & 1u;
+                    chk[u] = have[u] && pf[u].slot_off != 0xffffffffu;
+                    const u32 h = (u32)(((key[u] & pf[u].andmsk) * P.pf_mult) >> pf[u].shift);
+                    sh[u] = h & 31;
+                    sw[u] = chk[u] ? lds_ld32(&slots[pf[u].slot_off + (h >> 5)]) : ~0u;
+                }
+                bool push[EXP_U];
+#pragma unroll
+                for (int u = 0; u < EXP_U; u++) {
+                    push[u] = have[u] && ((sw[u] >> sh[u]) & 1u);
+                    if (P.dbg & 16) push[u] = false;
+                }
+#pragma unroll
+                for (int u = 0; u < EXP_U; u++) {
+                    const u64 pm = __ballot(push[u]);
+                    if (push[u]) {
+                        const u32 r = __builtin_amdgcn_mbcnt_hi(
+                            (u32)(pm >> 32), __builtin_amdgcn_mbcnt_lo((u32)pm, 0));
+                        QEnt *q = &pq[(pq_head + r) & (PQ_CAP - 1)];
+                        q->meta = ((p0 + jj[u]) << 24) | ((u64)blk << 4) | bb[u];
+                        q->key = key[u];
                     }
-                    if (P.dbg & 16) push = false;
-                    meta = ((p0 + j) << 24) | ((u64)blk << 4) | b;
+                    pq_head += (u32)__popcll(pm);
                 }
-                const u64 pm = __ballot(push);
-                if (push) {
-                    const u32 r = __builtin_amdgcn_mbcnt_hi(
-                        (u32)(pm >> 32), __builtin_amdgcn_mbcnt_lo((u32)pm, 0));
-                    QEnt *q = &pq[(pq_head + r) & (PQ_CAP - 1)];
-                    q->meta = meta;
-                    q->key = key;
-                }
-                pq_head += (u32)__popcll(pm);
+                /* < 256 queued before the round, <= 4 x 64 added: one batch
+                 * brings the queue back under 256 (PQ_CAP 512) */
                 if (pq_head - pq_tail >= (u32)WAVE * CONF_U) confirm_batch(WAVE * CONF_U);
             }
             phase(1);
@@ -1003,7 +1036,7 @@ vsa_lit_scan(VsaLitParams P) {
     typedef typename T::S_t S_t;
     extern __shared__ __align__(16) u8 smem[];
     __shared__ ConfLds cl;
-    __shared__ u32 q_head, q_tail, q_done;
+    __shared__ u32 q_tails[16], q_heads[16], q_done;
     __shared__ QEnt pq[PQ_CAP]; /* the confirm wave's private queue */
     const u32 tid = threadIdx.x;
     const u32 lane = lane_id();
@@ -1036,8 +1069,9 @@ vsa_lit_scan(VsaLitParams P) {
         for (u32 i = tid; i < 256 * 32; i += LIT_THREADS) dst[i] = P.table[i >> 5];
         tab = tb;
     }
+    /* LIT_SCANNERS rings of qcap entries each, then the slot bitmaps */
     uint4 *rings = (uint4 *)(smem + ((tab_bytes + 15) & ~15u));
-    u32 *slots = (u32 *)(rings + (size_t)P.qcap * T::EW);
+    u32 *slots = (u32 *)(rings + (size_t)LIT_SCANNERS * P.qcap * T::EW);
     for (u32 i = tid; i < P.slot_words; i += LIT_THREADS) slots[i] = P.slotmap[i];
     if (tid < 16) {
         const u32 off = P.conf_off[tid];
@@ -1061,21 +1095,18 @@ vsa_lit_scan(VsaLitParams P) {
         }
         cl.pf[tid] = pf;
     }
-    if (tid == 0) {
-        q_head = 0;
-        q_tail = 0;
-        q_done = 0;
+    if (tid < 16) {
+        q_tails[tid] = 0;
+        q_heads[tid] = 0;
     }
-    /* every slot starts with lap 15, never the first pass's lap 0 */
-    for (u32 i = tid; i < P.qcap; i += LIT_THREADS)
-        rings[(size_t)i * T::EW] = make_uint4(0, 15u << (ENT_LAP_SHIFT - 32), 0, 0);
+    if (tid == 0) q_done = 0;
     __syncthreads();
 
     const u32 mis = (u32)((uintptr_t)P.data & 15);
     if (wave == LIT_WAVES - 1) {
 
 #ifndef VSA_EXP_NO_CONFIRM /* experiment: VGPR use of the scanning path alone */
-        confirm_wave<MODE>(P, cl, rings, 31 - __clz(P.qcap), &q_head, &q_tail, &q_done, mis,
+        confirm_wave<MODE>(P, cl, rings, 31 - __clz(P.qcap), q_tails, q_heads, &q_done, mis,
                            slots, pq);
 #endif
         return;
@@ -1097,17 +1128,18 @@ vsa_lit_scan(VsaLitParams P) {
     LitShared L;
     L.tab = tab;
     L.tab_lds = (u32)(uintptr_t)(lds_u8_t *)smem;
-    L.kmask2 = (P.dmask & 0xffffu) * 0x10001u;
+    L.kmask2 = (P.dmask & 0xff80u) * 0x10001u;
     L.tsel = TEDDY_TAB_LDS | ((lane & 31) << 3);
-    L.ring = rings;
-    L.head = &q_head;
-    L.tail = &q_tail;
+    L.ring = rings + (size_t)wave * P.qcap * T::EW;
+    L.tail = &q_tails[wave];
+    L.head = &q_heads[wave];
     L.lg = 31 - __clz(P.qcap);
+    L.dbg = P.dbg;
 
     const u8 *A = P.data - mis;
     const int64_t SEG = (int64_t)P.seg_bytes;
     u32 ncand_total = 0;
-    u32 ring_tail_cache = 0;
+    u32 ring_tail_cache = 0, ring_head = 0;
 
     /* Segment scheduling.  The segments are split into NREG contiguous
      * regions; workgroup b works in region b % NREG first (workgroups are
@@ -1200,6 +1232,7 @@ vsa_lit_scan(VsaLitParams P) {
         IterState is;
         is.ncand = ncand_total;
         is.tail_cache = ring_tail_cache;
+        is.head = ring_head;
         {
             S_t x = 0;
             if (lane < (u32)(T::NL - 1)) {
@@ -1210,7 +1243,7 @@ vsa_lit_scan(VsaLitParams P) {
                     u32 key;
                     if constexpr (T::KEY16) {
                         const u8 b1 = load_byte_masked(A, p + 1, S.vlo, S.bhi);
-                        key = ((u32)b0 | ((u32)b1 << 8)) & P.dmask;
+                        key = vsa_fdr_key(b0, b1, P.dmask);
                     } else {
                         key = b0;
                     }
@@ -1296,6 +1329,7 @@ vsa_lit_scan(VsaLitParams P) {
         }
         ncand_total = is.ncand;
         ring_tail_cache = is.tail_cache;
+        ring_head = is.head;
         seg = P.dynamic ? resolve(t_next) : seg + G;
     }
     /* every push of this wave precedes this (LDS order) */

@@ -260,17 +260,19 @@ int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds) {
     return VSA_OK;
 }
 
-/* dynamic LDS = table + the shared candidate ring (power of two, 64..4096
- * chunk entries of ent bytes: 48 FDR / Teddy, 64 Fat Teddy, 32 noodle; 64
- * is the most one wave pushes at once) + slot bitmaps */
+/* dynamic LDS = table + one candidate ring per scanning wave (power of
+ * two, 4..64 chunk entries of ent bytes: 48 FDR / Teddy, 64 Fat Teddy, 32
+ * noodle; a push of up to 64 lanes is split into ring-sized batches) + slot
+ * bitmaps */
 size_t plan_lds(size_t tab, uint32_t slot_words, size_t ent, uint32_t *qcap,
                 size_t budget = LDS_BUDGET) {
+    const size_t waves = LIT_WAVES - 1;
     tab = (tab + 15) & ~(size_t)15;
     size_t rest = budget > tab + slot_words * 4 ? budget - tab - slot_words * 4 : 0;
-    uint32_t q = 64;
-    while (q < 4096 && (size_t)(2 * q) * ent <= rest) q *= 2;
+    uint32_t q = 4;
+    while (q < 64 && waves * (size_t)(2 * q) * ent <= rest) q *= 2;
     *qcap = q;
-    return tab + (size_t)q * ent + (size_t)slot_words * 4;
+    return tab + waves * (size_t)q * ent + (size_t)slot_words * 4;
 }
 
 int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
@@ -937,18 +939,18 @@ void *vsa_ctx_stream(vsa_ctx_t *c) { return c ? (void *)c->stream : nullptr; }
  * rebuilt from the engine's own confirm records (every LitInfo's v / msk,
  * fdr_confirm.h:57-65), in the reference's bucket layout: bit (k * 8 + b)
  * of T[key] is 0 when some literal of bucket b is consistent with the two
- * bytes (key & 0xff, key >> 8) sitting k bytes before its end
- * (getMultiEntriesAtPosition, fdr_compile.cpp:520-600, restated over the
- * 8-byte confirm window; the byte after the end is a don't-care).  Every
- * literal the confirm accepts is consistent at every window, so the set of
- * confirmed matches is exactly the reference's, for any stride / domain of
- * the bytecode, while a wider domain (14 bits: the whole first byte and 6
- * bits of the second) cuts false candidates. */
+ * bytes sitting k bytes before its end (getMultiEntriesAtPosition,
+ * fdr_compile.cpp:520-600, restated over the 8-byte confirm window; the
+ * byte after the end is a don't-care).  Every literal the confirm accepts is
+ * consistent at every window, so the set of confirmed matches is exactly the
+ * reference's, for any stride / domain of the bytecode and any key function.
+ * The key is fdr_key (kernels.h): 7 bits of each byte, the two halves of a
+ * printable pair exactly (the reference's domainMask keeps the first byte
+ * whole and cuts the second, fdr_compile.cpp:185-187); on the cfg-4 set
+ * this admits 2.8x fewer first-stage candidates than 8 + 6 bits. */
 static void derive_fdr_table(const uint8_t *eng, const uint32_t conf_off[8], uint32_t bits,
                              std::vector<uint64_t> &T) {
     const uint32_t n = 1u << bits;
-    const uint32_t hi_bits = bits - 8;            /* bits of the second byte */
-    const uint32_t hi_mask = (1u << hi_bits) - 1;
     T.assign(n, ~0ULL);
     uint64_t always = 0; /* (k, b) columns open for every key */
     const uint8_t *confBase = eng + ((const uint32_t *)eng)[4];
@@ -978,26 +980,23 @@ static void derive_fdr_table(const uint8_t *eng, const uint32_t conf_off[8], uin
                 const uint8_t m0 = (uint8_t)(L->msk >> (8 * (7 - k)));
                 const uint8_t v0 = (uint8_t)(L->v >> (8 * (7 - k))) & m0;
                 /* second key byte: k - 1 before the end (k = 0: past it) */
-                uint32_t m1 = 0, v1 = 0;
+                uint8_t m1 = 0, v1 = 0;
                 if (k >= 1) {
-                    m1 = (uint8_t)(L->msk >> (8 * (8 - k))) & hi_mask;
+                    m1 = (uint8_t)(L->msk >> (8 * (8 - k)));
                     v1 = (uint8_t)(L->v >> (8 * (8 - k))) & m1;
                 }
-                if (!m0 && !m1) {
-                    always |= bit;
+                /* every (x0, x1) consistent with the literal -> its key */
+                std::vector<uint32_t> c0, c1;
+                for (uint32_t x = 0; x < 256; x++) {
+                    if ((x & m0) == v0) c0.push_back(x);
+                    if ((x & m1) == v1) c1.push_back(x);
+                }
+                if (c0.size() * c1.size() >= 65536) {
+                    always |= bit; /* no constraint at this position */
                     continue;
                 }
-                /* enumerate the free bits of both bytes */
-                const uint32_t f0 = 0xffu & ~m0, f1 = hi_mask & ~m1;
-                uint32_t x0 = 0;
-                do {
-                    uint32_t x1 = 0;
-                    do {
-                        T[(v0 | x0) | ((v1 | x1) << 8)] &= ~bit;
-                        x1 = (x1 - f1) & f1;
-                    } while (x1);
-                    x0 = (x0 - f0) & f0;
-                } while (x0);
+                for (uint32_t x0 : c0)
+                    for (uint32_t x1 : c1) T[vsa_fdr_key(x0, x1, n - 1)] &= ~bit;
             }
         }
     }
