@@ -28,7 +28,7 @@ $(LIB): $(CSRC)/compile.o $(CSRC)/flood.o $(CSRC)/kernels.o $(CSRC)/runtime.o
 
 $(ORACLE): oracle/oracle.c
 	mkdir -p oracle/_build
-	gcc -O2 -std=gnu11 -fPIC -shared -Wall -pthread $< -o $@
+	gcc -O2 -march=x86-64-v3 -std=gnu11 -fPIC -shared -Wall -pthread $< -o $@
 
 # test-only C caller of the drop-ins (real __m128i signatures), checked
 # against the oracle

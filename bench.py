@@ -28,8 +28,9 @@ block, against the oracle (oracle/oracle.c, the scalar restatement) over all
 (`parity_bytes` = bytes checked), plus sortedness of the merged keys.
 
 Extra JSON fields: roofline (rank 0's scan kernel from hipEvents vs the 8 TB/s
-MI355X peak; PMC traffic from profiles/), cpu_baseline (timed on the same
-host cores, see --cpu-kind).
+MI355X peak; PMC traffic from profiles/), cpu_baseline (the SSE2 port of
+the reference FDR main loop over the same 4 GiB on the host's 16-thread
+share, its match set checked too).
 """
 import argparse
 import json
@@ -282,14 +283,20 @@ def run(args):
             ends = keys >> np.uint64(24)
             sorted_ok = bool(np.all(keys[1:] >= keys[:-1])) if len(keys) > 1 else True
             got = block_digests(ends, ids, bl, nblocks)
-            want, t_cpu = [], 0.0
+            want, t_cpu, cpu_ok = [], 0.0, True
             for b in range(nblocks):
                 lo, hi = b * bl, min(total, (b + 1) * bl)
                 host = make_corpus_device(torch, lo, hi, total, lits, 5, plant_every, dev,
                                           pplan).cpu().numpy()
-                tc = time.perf_counter()
                 want.append(oracle.digest_mt(eng, host, threads))
-                t_cpu += time.perf_counter() - tc
+                if not args.no_cpu:
+                    # CPU baseline: the SSE2 port of fdr.c's main loop
+                    # (get_conf_stride_1 :145-213 + confirm), same bytes,
+                    # same host threads; its result must match as well
+                    tc = time.perf_counter()
+                    d = oracle.digest_mt(eng, host, threads, simd=True)
+                    t_cpu += time.perf_counter() - tc
+                    cpu_ok = cpu_ok and d == want[-1]
                 parity_bytes += hi - lo
                 del host
             parity = sorted_ok and got == want and sum(w[0] for w in want) == nm
@@ -298,10 +305,13 @@ def run(args):
                       file=sys.stderr, flush=True)
             if not args.no_cpu:
                 cpu = {"value": round(parity_bytes / t_cpu / 1e9, 4), "unit": "GB/s",
-                       "cores": threads, "kind": "port",
-                       "sample": "the whole %d-byte corpus: oracle/oracle.c scalar fdrExec "
-                                 "restatement, %d threads over contiguous stripes (7-byte "
-                                 "halo); host: %s" % (parity_bytes, threads, _cpu_model())}
+                       "cores": threads, "kind": "port", "match_set_equal": cpu_ok,
+                       "sample": "the whole %d-byte corpus, 4 x 1 GiB blocks: oracle/oracle.c "
+                                 "SSE2 port of the reference FDR main loop (fdr.c:145-333, "
+                                 "m128 state, flood checks) on the reference bytecode's own "
+                                 "domain-%d table, %d threads over contiguous stripes (7-byte "
+                                 "halo); host: %s" % (parity_bytes, blob_domain(blob), threads,
+                                                     _cpu_model())}
         alg_bytes = local_bytes + 16 * nm // world  # rank 0's input + its share of records
         achieved = alg_bytes / (kavg * 1e-3) / 1e9
         traffic = None
@@ -344,6 +354,12 @@ def run(args):
         dist.destroy_process_group()
     db.close()
     ctx.close()
+
+
+def blob_domain(blob):
+    """FDR.domain of the blob's engine (fdr_internal.h:69-85, byte 25)"""
+    import ctypes
+    return ctypes.string_at(blob.ptr + 192 + 25, 1)[0]
 
 
 def _cpu_model():

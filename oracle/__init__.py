@@ -18,7 +18,8 @@ LIB = os.path.join(HERE, "_build", "liboracle.so")
 
 def build():
     os.makedirs(os.path.join(HERE, "_build"), exist_ok=True)
-    subprocess.check_call(["gcc", "-O2", "-std=gnu11", "-fPIC", "-shared", "-Wall", "-pthread",
+    subprocess.check_call(["gcc", "-O2", "-march=x86-64-v3", "-std=gnu11", "-fPIC", "-shared",
+                           "-Wall", "-pthread",
                            os.path.join(HERE, "oracle.c"), "-o", LIB])
 
 
@@ -105,6 +106,18 @@ def hwlm_exec(blob_ptr, data, start=0, groups=ALL, term_after=-1, cap=4096, cb_r
 
 def fdr_exec(engine_ptr, data, start=0, groups=ALL, term_after=-1, cap=4096, cb_ret=ALL):
     return _run(_lib.orc_fdr_exec, engine_ptr, data, start, [groups], term_after, cap, cb_ret)
+
+
+def fdr_exec_simd(engine_ptr, data, start=0, groups=ALL, cap=1 << 16):
+    """fdrExec through the SSE2 main loop (the CPU baseline engine)"""
+    keep, p, n = _buf(data)
+    while True:
+        out = (_Match * max(1, cap))()
+        st = _int()
+        cnt = _lib.orc_fdr_exec_simd(engine_ptr, p, n, start, groups, out, cap, ctypes.byref(st))
+        if cnt <= cap:
+            return st.value, [(out[i].end, out[i].id) for i in range(cnt)]
+        cap = cnt
 
 
 # the 16 bytes before the end of a short history, as the reference's
@@ -279,14 +292,20 @@ _sig("orc_digest_mt", ctypes.c_long, ctypes.c_void_p, ctypes.c_int, ctypes.c_voi
 M64 = (1 << 64) - 1
 
 
-def digest_mt(engine_ptr, data, nthreads, nood=False):
+_sig("orc_digest_mt2", ctypes.c_long, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+     ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p)
+_sig("orc_fdr_exec_simd", _i64, _vp, _vp, _sz, _sz, _u64, _vp, _sz, ctypes.POINTER(_int))
+
+
+def digest_mt(engine_ptr, data, nthreads, nood=False, simd=False):
     """(count, sum, xor) of the block scan's (end, id) match set (oracle.c
-    orc_digest_mt: the scalar restatement over `nthreads` stripes with a
-    7-byte halo).  Compare with :func:`digest_of`."""
+    orc_digest_mt: the restatement over `nthreads` stripes with a 7-byte
+    halo; simd: the FDR main zone through the SSE2 get_conf_stride_1 port,
+    the CPU baseline).  Compare with :func:`digest_of`."""
     buf = np.ascontiguousarray(data, dtype=np.uint8)
     out = np.zeros(2, np.uint64)
-    n = _lib.orc_digest_mt(engine_ptr, int(nood), buf.ctypes.data, len(buf), int(nthreads),
-                           out.ctypes.data)
+    n = _lib.orc_digest_mt2(engine_ptr, int(nood), int(simd), buf.ctypes.data, len(buf),
+                            int(nthreads), out.ctypes.data)
     if n < 0:
         raise RuntimeError("orc_digest_mt failed")
     return int(n), int(out[0]), int(out[1])

@@ -359,6 +359,7 @@ typedef struct {
     const u8 *hend;
     size_t hlen;
     int stream;
+    int simd; /* FDR main zone through get_conf_m128 (the SIMD baseline) */
 } rtargs;
 
 /* byte at logical position p (0 = buf[0]): history bytes when streaming,
@@ -540,6 +541,52 @@ static void get_conf(const zone *z, long it, u32 stride, u16 dmask,
     *s = st >> 64;
 }
 
+/* get_conf_stride_1 fdr.c:145-213 with SSE2 m128 state, as the reference
+ * runs it (unaligned 64-bit loads from the buffer, one table load per
+ * position, lshiftbyte_m128 = _mm_slli_si128, or-tree, two 8-byte conf
+ * words) — the CPU baseline's main-zone loop, where every byte it touches
+ * is inside the buffer (the main zone ends 3 bytes before len, fdr.c:649). */
+#include <emmintrin.h>
+
+static inline __m128i ld_entry(const u64a *ft, u64a idx) {
+    return _mm_loadl_epi64((const __m128i *)(ft + idx));
+}
+
+static inline void get_conf_m128(const u8 *itPtr, u64a domain_mask, const u64a *ft,
+                                 u64a *conf0, u64a *conf8, __m128i *s) {
+    u64a it_hi, it_lo;
+    u32 r15;
+    memcpy(&it_hi, itPtr, 8);
+    memcpy(&it_lo, itPtr + 8, 8);
+    memcpy(&r15, itPtr + 15, 4);
+    __m128i st0 = ld_entry(ft, domain_mask & it_hi);
+    __m128i st1 = _mm_slli_si128(ld_entry(ft, domain_mask & (it_hi >> 8)), 1);
+    __m128i st2 = _mm_slli_si128(ld_entry(ft, domain_mask & (it_hi >> 16)), 2);
+    __m128i st3 = _mm_slli_si128(ld_entry(ft, domain_mask & (it_hi >> 24)), 3);
+    __m128i st4 = _mm_slli_si128(ld_entry(ft, domain_mask & (it_hi >> 32)), 4);
+    __m128i st5 = _mm_slli_si128(ld_entry(ft, domain_mask & (it_hi >> 40)), 5);
+    __m128i st6 = _mm_slli_si128(ld_entry(ft, domain_mask & (it_hi >> 48)), 6);
+    __m128i st7 = _mm_slli_si128(
+        ld_entry(ft, domain_mask & ((it_hi >> 56) | (it_lo << 8))), 7);
+    __m128i st8 = ld_entry(ft, domain_mask & it_lo);
+    __m128i st9 = _mm_slli_si128(ld_entry(ft, domain_mask & (it_lo >> 8)), 1);
+    __m128i st10 = _mm_slli_si128(ld_entry(ft, domain_mask & (it_lo >> 16)), 2);
+    __m128i st11 = _mm_slli_si128(ld_entry(ft, domain_mask & (it_lo >> 24)), 3);
+    __m128i st12 = _mm_slli_si128(ld_entry(ft, domain_mask & (it_lo >> 32)), 4);
+    __m128i st13 = _mm_slli_si128(ld_entry(ft, domain_mask & (it_lo >> 40)), 5);
+    __m128i st14 = _mm_slli_si128(ld_entry(ft, domain_mask & (it_lo >> 48)), 6);
+    __m128i st15 = _mm_slli_si128(ld_entry(ft, domain_mask & r15), 7);
+    st0 = _mm_or_si128(_mm_or_si128(_mm_or_si128(st0, st1), _mm_or_si128(st2, st3)),
+                       _mm_or_si128(_mm_or_si128(st4, st5), _mm_or_si128(st6, st7)));
+    st8 = _mm_or_si128(_mm_or_si128(_mm_or_si128(st8, st9), _mm_or_si128(st10, st11)),
+                       _mm_or_si128(_mm_or_si128(st12, st13), _mm_or_si128(st14, st15)));
+    __m128i st = _mm_or_si128(*s, st0);
+    *conf0 = (u64a)_mm_cvtsi128_si64(st) ^ ~0ULL;
+    st = _mm_or_si128(_mm_srli_si128(st, 8), st8);
+    *conf8 = (u64a)_mm_cvtsi128_si64(st) ^ ~0ULL;
+    *s = _mm_srli_si128(st, 8);
+}
+
 static int fdr_run(const struct o_FDR *fdr, const rtargs *a, u64a control) {
     size_t len = a->len, start = a->start;
     if (start >= len) return 0;
@@ -593,6 +640,9 @@ static int fdr_run(const struct o_FDR *fdr, const rtargs *a, u64a control) {
         u128 orm = 0;
         for (int k = 0; k < z->shift; k++) orm |= (u128)0xff << (8 * k);
         state |= orm;
+        const int fast = a->simd && main_zone && fdr->stride == 1;
+        __m128i sv = _mm_setzero_si128();
+        if (fast) memcpy(&sv, &state, 16);
         for (long it = z->zstart; it + 16 <= z->zend; it += 16) {
             if (main_zone && (size_t)it > tfd) {
                 u32 fsz;
@@ -605,7 +655,8 @@ static int fdr_run(const struct o_FDR *fdr, const rtargs *a, u64a control) {
                 if (!control) return 1;
             }
             u64a c0, c8;
-            get_conf(z, it, fdr->stride, fdr->domainMask, ft, &c0, &c8, &state);
+            if (fast) get_conf_m128(a->buf + it, fdr->domainMask, ft, &c0, &c8, &sv);
+            else get_conf(z, it, fdr->stride, fdr->domainMask, ft, &c0, &c8, &state);
             for (int half = 0; half < 2; half++) {
                 u64a conf = half ? c8 : c0;
                 while (conf) {
@@ -625,6 +676,7 @@ static int fdr_run(const struct o_FDR *fdr, const rtargs *a, u64a control) {
                 if (!control) return 1;
             }
         }
+        if (fast) memcpy(&state, &sv, 16);
     }
     return 0;
 }
@@ -808,10 +860,23 @@ static int fdr_dispatch_a(const void *eng, rtargs a, u64a groups) {
     return 2;
 }
 
+static int fdr_dispatch_s(const void *eng, const u8 *buf, size_t len, size_t start,
+                          u64a groups, cbctx *cb, int simd) {
+    rtargs a = {buf, len, start, cb, NULL, 0, 0, simd};
+    return fdr_dispatch_a(eng, a, groups);
+}
+
 static int fdr_dispatch(const void *eng, const u8 *buf, size_t len,
                         size_t start, u64a groups, cbctx *cb) {
-    rtargs a = {buf, len, start, cb, NULL, 0, 0};
-    return fdr_dispatch_a(eng, a, groups);
+    return fdr_dispatch_s(eng, buf, len, start, groups, cb, 0);
+}
+
+/* fdrExec through the SIMD main loop (the CPU baseline engine) */
+long orc_fdr_exec_simd(const void *eng, const u8 *buf, size_t len, size_t start,
+                       u64a groups, orc_match *out, size_t cap, int *status) {
+    cbctx cb = {out, cap, 0, -1, ~0ULL};
+    *status = fdr_dispatch_s(eng, buf, len, start, groups, &cb, 1);
+    return (long)cb.n;
 }
 
 /* fdrExecStreaming fdr.c:827-855 */
@@ -819,7 +884,7 @@ long orc_fdr_exec_stream(const void *eng, const u8 *hend, size_t hlen, const u8 
                          size_t len, size_t start, u64a groups, orc_match *out, size_t cap,
                          long term_after, u64a cb_ret, int *status) {
     cbctx cb = {out, cap, 0, term_after, cb_ret};
-    rtargs a = {buf, len, start, &cb, hend, hlen, 1};
+    rtargs a = {buf, len, start, &cb, hend, hlen, 1, 0};
     *status = fdr_dispatch_a(eng, a, groups);
     return (long)cb.n;
 }
@@ -1021,7 +1086,7 @@ u64a orc_fdr_candidates(const void *eng, const u8 *buf, size_t len) {
 
 typedef struct {
     const void *eng;
-    int nood;
+    int nood, simd;
     const u8 *buf;
     size_t len;
     cbctx cb;
@@ -1031,13 +1096,22 @@ typedef struct {
 static void *orc_mt_run(void *p) {
     orc_mt_job *j = (orc_mt_job *)p;
     if (j->nood) j->status = nood_run((const struct o_nood *)j->eng, j->buf, j->len, 0, &j->cb);
-    else j->status = fdr_dispatch(j->eng, j->buf, j->len, 0, ~0ULL, &j->cb);
+    else j->status = fdr_dispatch_s(j->eng, j->buf, j->len, 0, ~0ULL, &j->cb, j->simd);
     return NULL;
 }
 
-/* eng: the engine inside an HWLM blob; nood != 0 for a noodle table */
+/* eng: the engine inside an HWLM blob; nood != 0 for a noodle table; simd:
+ * the FDR main zone through get_conf_m128 (bench.py's cpu_baseline) */
+long orc_digest_mt2(const void *eng, int nood, int simd, const u8 *buf, size_t len,
+                    int nthreads, u64a out[2]);
+
 long orc_digest_mt(const void *eng, int nood, const u8 *buf, size_t len, int nthreads,
                    u64a out[2]) {
+    return orc_digest_mt2(eng, nood, 0, buf, len, nthreads, out);
+}
+
+long orc_digest_mt2(const void *eng, int nood, int simd, const u8 *buf, size_t len,
+                    int nthreads, u64a out[2]) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     if ((size_t)nthreads > len / 64 + 1) nthreads = (int)(len / 64 + 1);
@@ -1048,7 +1122,7 @@ long orc_digest_mt(const void *eng, int nood, const u8 *buf, size_t len, int nth
         const size_t lo = (size_t)t * s, hi = t == nthreads - 1 ? len : lo + s;
         const size_t blo = lo >= 7 ? lo - 7 : 0;
         cbctx cb = {NULL, 0, 0, -1, ~0ULL, 1, lo - blo, blo, 0, 0};
-        jobs[t] = (orc_mt_job){eng, nood, buf + blo, hi - blo, cb, 0};
+        jobs[t] = (orc_mt_job){eng, nood, simd, buf + blo, hi - blo, cb, 0};
         if (pthread_create(&th[t], NULL, orc_mt_run, &jobs[t]) != 0) return -1;
     }
     long n = 0;

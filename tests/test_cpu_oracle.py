@@ -490,3 +490,32 @@ def test_derived_first_stage_no_false_negatives(nlits, hint, minlen):
     assert not missing, missing[:10]
     if minlen >= 4:
         assert len(cand) < 0.05 * len(data), len(cand)
+
+
+# ------------------------------------------------- SIMD CPU baseline ---
+
+@pytest.mark.parametrize("hint", [0, -1])
+def test_simd_fdr_equals_scalar_oracle(hint):
+    """oracle.c's SSE2 get_conf_stride_1 port (bench.py's cpu_baseline
+    engine) == the scalar restatement: the reference's known answers
+    (fdr.cpp fixtures, FDR engine) and random sets / buffers / starts."""
+    for c in load("fdr.json"):
+        blob = build_or_none(lits_of(c), 0)
+        if blob is None or blob.engine_id != 0 or c["expected"] is None:
+            continue
+        data = bytes.fromhex(c["data"])
+        st, m = oracle.fdr_exec_simd(vsa.engine_blob(blob), data, start=c["start"])
+        assert st == 0 and [list(x) for x in m] == c["expected"], c["src"]
+    rng = random.Random(77 + hint)
+    for trial in range(12):
+        lits = rand_lits(rng, rng.choice([50, 300, 2000]), minlen=rng.choice([1, 3, 5]),
+                         msk_frac=0.1)
+        blob = build_or_none(lits, hint)
+        if blob is None or blob.is_noodle or blob.engine_id != 0:
+            continue
+        for ln in (17, 40, 300, 5000, 70000):
+            data = rand_data(rng, ln, alphabet=b"abcdefgh" + bytes([rng.randrange(256)]) * 4)
+            for start in (0, 5, ln // 3):
+                a = oracle.fdr_exec(vsa.engine_blob(blob), data, start=start, cap=1 << 18)
+                b = oracle.fdr_exec_simd(vsa.engine_blob(blob), data, start=start, cap=1 << 18)
+                assert a == b, (trial, ln, start)

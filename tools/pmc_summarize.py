@@ -7,7 +7,7 @@ FETCH_SIZE / WRITE_SIZE are in KiB.  MI355X_MICROARCH.md (HBM section):
 on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced streaming
 read, so it is doubled; WRITE_SIZE is exact for 16-B stores.  The first
 launch of each pass is the bench's parity launch on a 64 MiB sample and is
-excluded (only full 4 GiB launches are averaged)."""
+excluded (only full 4 GiB launches, > 0.5 ms, are averaged)."""
 import csv
 import json
 import os
@@ -32,7 +32,7 @@ for pass_ in ("fetch", "write"):
         dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         rows_out.append([r["Dispatch_Id"], r["Kernel_Name"], r["Counter_Name"],
                          r["Counter_Value"], dur])
-        if dur > 1_000_000:  # full-size launches only (ns)
+        if dur > 500_000:  # full-size 4 GiB launches only (ns)
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 with open(os.path.join(dst, tag + "_pmc_lit_scan.csv"), "w", newline="") as f:
     w = csv.writer(f)
@@ -65,6 +65,32 @@ with open(os.path.join(dst, tag + "_vsa_dispatches.csv"), "w", newline="") as f:
         dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         w.writerow([r["Dispatch_Id"], r["Kernel_Name"], r["Grid_Size_X"], r["Workgroup_Size_X"],
                     r["LDS_Block_Size"], r["VGPR_Count"], r["SGPR_Count"], r["Scratch_Size"], dur])
-        if KERNEL in r["Kernel_Name"] and dur > 1_000_000:
+        if KERNEL in r["Kernel_Name"] and dur > 500_000:
             full.append(dur)
 print("full-size %s launches: %d, avg %.1f us" % (KERNEL, len(full), sum(full) / len(full) / 1e3))
+
+# SQ / LDS counters pass (tools/profile.sh), per full-size launch
+sqf = os.path.join(src, "sq", "run_counter_collection.csv")
+if os.path.exists(sqf):
+    sq = {}
+    for r in csv.DictReader(open(sqf)):
+        if KERNEL not in r["Kernel_Name"]:
+            continue
+        if int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) > 500_000:
+            sq.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    sq = {k: sum(v) / len(v) for k, v in sq.items()}
+    if sq:
+        sq["lds_cycles_per_lds_instr"] = sq["SQ_LDS_IDX_ACTIVE"] / sq["SQ_INSTS_LDS"]
+        sq["bank_conflict_share"] = sq["SQ_LDS_BANK_CONFLICT"] / sq["SQ_LDS_IDX_ACTIVE"]
+        json.dump(sq, open(os.path.join(dst, tag + "_sq_lds.json"), "w"), indent=1)
+        print(json.dumps(sq))
+# configs 1-3 / streaming lines
+cl = os.path.join(src, "configs_trace.log")
+if os.path.exists(cl):
+    lines = [l for l in open(cl) if l.startswith("{")]
+    open(os.path.join(dst, tag + "_configs.jsonl"), "w").writelines(lines)
+    shutil.copy(os.path.join(src, "cfg", "run_kernel_stats.csv"),
+                os.path.join(dst, tag + "_cfg_kernel_stats.csv"))
+bl = [l for l in open(os.path.join(src, "bench_trace.log")) if l.startswith("{")]
+if bl:
+    open(os.path.join(dst, tag + "_bench.json"), "w").write(bl[-1])
