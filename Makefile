@@ -16,6 +16,10 @@ $(CSRC)/compile.o: $(CSRC)/compile.cpp $(CSRC)/hs_layout.h $(CSRC)/vsa_internal.
 $(CSRC)/flood.o: $(CSRC)/flood.cpp $(CSRC)/hs_layout.h $(CSRC)/vsa_internal.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(CSRC)/hs_lit.o: $(CSRC)/hs_lit.cpp $(CSRC)/hs_layout.h $(CSRC)/vsa_internal.h \
+                  include/vectorscan_amd.h include/vectorscan_amd_hs.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(CSRC)/kernels.o: $(CSRC)/kernels.hip $(CSRC)/kernels.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -23,7 +27,7 @@ $(CSRC)/runtime.o: $(CSRC)/runtime.hip $(CSRC)/kernels.h $(CSRC)/hs_layout.h \
                    $(CSRC)/vsa_internal.h include/vectorscan_amd.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(CSRC)/compile.o $(CSRC)/flood.o $(CSRC)/kernels.o $(CSRC)/runtime.o
+$(LIB): $(CSRC)/compile.o $(CSRC)/flood.o $(CSRC)/hs_lit.o $(CSRC)/kernels.o $(CSRC)/runtime.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
 
 $(ORACLE): oracle/oracle.c

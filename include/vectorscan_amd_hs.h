@@ -1,0 +1,126 @@
+/*
+ * vectorscan_amd_hs.h — the pure-literal database API over the GPU literal
+ * matcher: hs_compile_lit_multi / hs_scan / hs_scan_vector / streams, as
+ * the reference runs them when a database holds only pure literals
+ * (ROSE_RUNTIME_PURE_LITERAL, src/rose/rose_build_bytecode.cpp:258-303).
+ *
+ * Each entry point mirrors the reference function named beside it (same
+ * arguments, return codes and callback contract); a maintainer binds the
+ * reference's names to these.  Matches are found by the
+ * HWLM scan of vectorscan_amd.h (one GPU launch per call: per write for a
+ * stream, all pieces of a vector at once) and delivered in the reference
+ * order: increasing `to`; at one `to`, literal fragments in HWLM confirm
+ * order, then patterns in compile order.
+ *
+ * Host buffers are copied to the GPU on every call; for device-resident
+ * corpora use vsa_scan_blocks* directly.
+ */
+#ifndef VECTORSCAN_AMD_HS_H
+#define VECTORSCAN_AMD_HS_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* hs_common.h:478-584 */
+#define VSA_HS_SUCCESS 0
+#define VSA_HS_INVALID (-1)
+#define VSA_HS_NOMEM (-2)
+#define VSA_HS_SCAN_TERMINATED (-3)
+#define VSA_HS_COMPILER_ERROR (-4)
+#define VSA_HS_DB_MODE_ERROR (-7)
+#define VSA_HS_SCRATCH_IN_USE (-10)
+#define VSA_HS_UNKNOWN_ERROR (-13)
+
+/* hs_compile.h:869-1005, 1156-1171 */
+#define VSA_HS_FLAG_CASELESS 1u
+#define VSA_HS_FLAG_DOTALL 2u
+#define VSA_HS_FLAG_MULTILINE 4u
+#define VSA_HS_FLAG_SINGLEMATCH 8u
+#define VSA_HS_FLAG_ALLOWEMPTY 16u
+#define VSA_HS_FLAG_UTF8 32u
+#define VSA_HS_FLAG_UCP 64u
+#define VSA_HS_FLAG_PREFILTER 128u
+#define VSA_HS_FLAG_SOM_LEFTMOST 256u
+#define VSA_HS_FLAG_COMBINATION 512u
+#define VSA_HS_FLAG_QUIET 1024u
+#define VSA_HS_MODE_BLOCK 1u
+#define VSA_HS_MODE_STREAM 2u
+#define VSA_HS_MODE_VECTORED 4u
+#define VSA_HS_MODE_SOM_HORIZON_LARGE (1u << 24)
+#define VSA_HS_MODE_SOM_HORIZON_MEDIUM (1u << 25)
+#define VSA_HS_MODE_SOM_HORIZON_SMALL (1u << 26)
+
+typedef struct vsa_hs_database vsa_hs_database_t;
+typedef struct vsa_hs_scratch vsa_hs_scratch_t;
+typedef struct vsa_hs_stream vsa_hs_stream_t;
+
+/* hs_compile_error_t, hs_compile.h:112-130 */
+typedef struct {
+    char *message;
+    int expression;
+} vsa_hs_compile_error_t;
+
+/* match_event_handler, hs_runtime.h:125-128: nonzero stops matching */
+typedef int (*vsa_hs_match_event_handler)(unsigned int id, unsigned long long from,
+                                          unsigned long long to, unsigned int flags,
+                                          void *context);
+
+/* hs_compile_lit_multi, hs_compile.h:690-697 (checks of hs.cpp:290-400 and
+ * compiler.cpp:391-433).  `platform` is accepted for signature parity and
+ * ignored. */
+int vsa_hs_compile_lit_multi(const char *const *expressions, const unsigned *flags,
+                             const unsigned *ids, const size_t *lens, unsigned elements,
+                             unsigned mode, const void *platform, vsa_hs_database_t **db,
+                             vsa_hs_compile_error_t **error);
+/* hs_compile_lit, hs_compile.h:608-611 */
+int vsa_hs_compile_lit(const char *expression, unsigned flags, size_t len, unsigned mode,
+                       const void *platform, vsa_hs_database_t **db,
+                       vsa_hs_compile_error_t **error);
+int vsa_hs_free_compile_error(vsa_hs_compile_error_t *error); /* hs_compile.h:710 */
+int vsa_hs_free_database(vsa_hs_database_t *db);              /* hs_common.h:80 */
+
+/* hs_alloc_scratch / hs_free_scratch, hs_runtime.h:555 / :609: one scratch per
+ * thread; it holds a GPU context and the device copies of the databases it
+ * was allocated for. */
+int vsa_hs_alloc_scratch(const vsa_hs_database_t *db, vsa_hs_scratch_t **scratch);
+int vsa_hs_free_scratch(vsa_hs_scratch_t *scratch);
+
+/* hs_scan, hs_runtime.h:479-482 (runtime.c:316-470; pureLiteralBlockExec
+ * runtime.c:204-230) */
+int vsa_hs_scan(const vsa_hs_database_t *db, const char *data, unsigned int length,
+                unsigned int flags, vsa_hs_scratch_t *scratch,
+                vsa_hs_match_event_handler onEvent, void *context);
+/* hs_scan_vector, hs_runtime.h:522-527 (runtime.c:1106-1180): all pieces
+ * in one GPU launch, each a stream write with the previous pieces as
+ * history */
+int vsa_hs_scan_vector(const vsa_hs_database_t *db, const char *const *data,
+                       const unsigned int *length, unsigned int count, unsigned int flags,
+                       vsa_hs_scratch_t *scratch, vsa_hs_match_event_handler onEvent,
+                       void *context);
+
+/* streams: hs_open_stream / hs_scan_stream / hs_close_stream /
+ * hs_reset_stream, hs_runtime.h:148, :188, :232, :273 (runtime.c:560-1000, pureLiteralStreamExec
+ * runtime.c:802-831) */
+int vsa_hs_open_stream(const vsa_hs_database_t *db, unsigned int flags,
+                       vsa_hs_stream_t **stream);
+int vsa_hs_scan_stream(vsa_hs_stream_t *id, const char *data, unsigned int length,
+                       unsigned int flags, vsa_hs_scratch_t *scratch,
+                       vsa_hs_match_event_handler onEvent, void *ctxt);
+int vsa_hs_close_stream(vsa_hs_stream_t *id, vsa_hs_scratch_t *scratch,
+                        vsa_hs_match_event_handler onEvent, void *ctxt);
+int vsa_hs_reset_stream(vsa_hs_stream_t *id, unsigned int flags, vsa_hs_scratch_t *scratch,
+                        vsa_hs_match_event_handler onEvent, void *context);
+
+/* Introspection for tests: the database's HWLM blob (fragment id = HWLM
+ * literal id) and the number of literal fragments. */
+int vsa_hs_database_hwlm(const vsa_hs_database_t *db, const void **hwlm, size_t *size,
+                         unsigned *fragments);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

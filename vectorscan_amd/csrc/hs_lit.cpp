@@ -1,0 +1,579 @@
+/*
+ * hs_lit.cpp — pure-literal databases: hs_compile_lit_multi, hs_scan,
+ * hs_scan_vector and streams (include/vectorscan_amd_hs.h) over the GPU
+ * HWLM scan (runtime.hip vsa::exec_pieces: one launch per call).
+ *
+ * Compile — what the reference's build does for pure literals
+ * (compiler.cpp:391-433 addLitExpression, :121-150 ParsedLitExpression,
+ * ng.cpp:578-625 NG::addLiteral, rose_build_matchers.cpp:700-743
+ * addFragmentLiteral):
+ *   - a caseless pattern is a ue2_literal with every position nocase
+ *     (ue2_literal::push_back upper-cases and marks it), so its HWLM
+ *     literal is nocase;
+ *   - patterns with the same literal tail and case share one fragment; the
+ *     fragment's HWLM literal is the last ROSE_SHORT_LITERAL_LEN_MAX = 8
+ *     bytes, the rest of a longer literal is checked when the tail matches
+ *     (CHECK_LONG_LIT / CHECK_MED_LIT);
+ *   - NOREPEAT only where every pattern of the fragment is <= 8 bytes and
+ *     single-match (isNoRunsLiteral :511-557);
+ *   - ids: SINGLEMATCH must agree across patterns of one id
+ *     (report_manager.cpp:212-236); one exhaustion key per single-match id.
+ * Run — pureLiteralBlockExec (runtime.c:204-230) / pureLiteralStreamExec
+ * (:802-831) with roseCallback (match.c): an HWLM end e in a write at stream
+ * offset o is `to` = o + e + 1 (lit_offset_adjust = offset + 1); each
+ * pattern of the fragment, in compile order, reports unless its long-literal
+ * check fails, its id is exhausted, or its id was already reported at this
+ * `to` (dedupe keys are per external id); from = to - len under
+ * HS_FLAG_SOM_LEFTMOST (makeSomRelativeCallback), else 0.  A nonzero
+ * callback return ends the scan: HS_SCAN_TERMINATED, and a terminated
+ * stream stays terminated (runtime.c:883-893).
+ */
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "vectorscan_amd.h"
+#include "vectorscan_amd_hs.h"
+#include "vsa_internal.h"
+
+namespace {
+
+constexpr uint32_t DB_MAGIC = 0x56534c44u;      /* "VSLD" */
+constexpr uint32_t SCRATCH_MAGIC = 0x56534c53u; /* "VSLS" */
+constexpr uint32_t STREAM_MAGIC = 0x5653534du;  /* "VSSM" */
+constexpr size_t SHORT_LIT = 8;                 /* ROSE_SHORT_LITERAL_LEN_MAX */
+constexpr size_t HIST_MIN = 16;                 /* history handed to the GPU */
+constexpr size_t LIMIT_PATTERN_LENGTH = 16000;  /* grey.cpp:148 */
+constexpr unsigned LIMIT_PATTERN_COUNT = 8000000; /* grey.cpp:147 */
+constexpr uint32_t NO_EKEY = ~0u;
+
+std::atomic<uint64_t> g_serial{1};
+
+struct Pattern {
+    uint32_t id = 0;
+    uint32_t ekey = NO_EKEY; /* exhaustion key (single-match ids) */
+    bool som = false;
+    bool caseless = false;
+    std::string s; /* as compiled: upper-cased when caseless */
+};
+
+inline uint8_t upper(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
+
+} // namespace
+
+struct vsa_hs_database {
+    uint32_t magic = DB_MAGIC;
+    uint32_t mode = 0;
+    uint64_t serial = 0;
+    uint8_t *hwlm = nullptr;
+    size_t hwlm_size = 0;
+    std::vector<Pattern> pats;
+    std::vector<std::vector<uint32_t>> frags; /* fragment -> patterns */
+    uint32_t n_ekeys = 0;
+    uint32_t min_width = 0;
+    size_t max_len = 0;
+    bool dedupe = false; /* some id belongs to more than one pattern */
+};
+
+struct vsa_hs_scratch {
+    uint32_t magic = SCRATCH_MAGIC;
+    std::atomic<bool> in_use{false};
+    vsa_ctx_t *ctx = nullptr;
+    std::vector<std::pair<uint64_t, vsa_db_t *>> dbs; /* serial -> device copy */
+};
+
+/* per-stream state: stream offset, the last bytes written (history), the
+ * exhaustion vector and the terminated status */
+struct vsa_hs_stream {
+    uint32_t magic = STREAM_MAGIC;
+    const vsa_hs_database *db = nullptr;
+    uint64_t offset = 0;
+    std::vector<uint8_t> hist;
+    std::vector<uint8_t> exhausted;
+    bool terminated = false;
+};
+
+namespace {
+
+vsa_hs_compile_error_t *make_error(const std::string &msg, int expression) {
+    vsa_hs_compile_error_t *e = (vsa_hs_compile_error_t *)malloc(sizeof(*e));
+    if (!e) return nullptr;
+    e->message = strdup(msg.c_str());
+    e->expression = expression;
+    return e;
+}
+
+bool valid_db(const vsa_hs_database_t *db) { return db && db->magic == DB_MAGIC; }
+
+vsa_db_t *device_db(vsa_hs_scratch_t *s, const vsa_hs_database_t *db) {
+    for (auto &e : s->dbs)
+        if (e.first == db->serial) return e.second;
+    return nullptr;
+}
+
+/* one call's view of the stream: the writes of this call after the
+ * history, and the match callback state */
+struct Run {
+    const vsa_hs_database *db;
+    vsa_hs_stream *st;
+    vsa_hs_match_event_handler cb;
+    void *ctx;
+    const uint8_t *const *bufs;
+    const size_t *lens;
+    std::vector<uint64_t> pos; /* stream offset of each write */
+    size_t cur = 0;
+    uint64_t last_to = ~0ULL;
+    std::vector<uint32_t> at_to; /* ids reported at last_to */
+    bool terminated = false;
+};
+
+uint8_t byte_at(const Run &r, uint64_t p) {
+    if (p < r.pos[0]) return r.st->hist[r.st->hist.size() - (size_t)(r.pos[0] - p)];
+    size_t j = r.cur;
+    while (p < r.pos[j]) j--; /* earlier writes of this call */
+    return r.bufs[j][p - r.pos[j]];
+}
+
+/* CHECK_LONG_LIT: the bytes of the literal before its matched 8-byte tail */
+bool long_ok(const Run &r, uint64_t to, const Pattern &p) {
+    const size_t len = p.s.size();
+    if (to < len || to - len + r.st->hist.size() < r.st->offset) return false;
+    const uint64_t start = to - len;
+    for (size_t k = 0; k + SHORT_LIT < len; k++) {
+        uint8_t b = byte_at(r, start + k);
+        if (p.caseless) b = upper(b);
+        if (b != (uint8_t)p.s[k]) return false;
+    }
+    return true;
+}
+
+u64a on_fragment(size_t end, u32 frag, hs_scratch *sc) {
+    Run &r = *(Run *)sc;
+    const uint64_t to = r.pos[r.cur] + end + 1; /* lit_offset_adjust */
+    if (to != r.last_to) {
+        r.last_to = to;
+        r.at_to.clear();
+    }
+    for (uint32_t pi : r.db->frags[frag]) {
+        const Pattern &p = r.db->pats[pi];
+        if (p.s.size() > SHORT_LIT && !long_ok(r, to, p)) continue;
+        if (p.ekey != NO_EKEY && r.st->exhausted[p.ekey]) continue;
+        if (r.db->dedupe) {
+            if (std::find(r.at_to.begin(), r.at_to.end(), p.id) != r.at_to.end()) continue;
+            r.at_to.push_back(p.id);
+        }
+        if (p.ekey != NO_EKEY) r.st->exhausted[p.ekey] = 1;
+        const uint64_t from = p.som ? to - p.s.size() : 0;
+        if (r.cb && r.cb(p.id, from, to, 0, r.ctx)) {
+            r.terminated = true;
+            return HWLM_TERMINATE_MATCHING;
+        }
+    }
+    return HWLM_CONTINUE_MATCHING;
+}
+
+void on_piece(void *p, size_t i) { ((Run *)p)->cur = i; }
+
+/* keep the last max(16, longest literal - 1) bytes of the stream */
+void push_history(vsa_hs_stream *st, const uint8_t *const *bufs, const size_t *lens, size_t n) {
+    const size_t keep = std::max(HIST_MIN, st->db->max_len ? st->db->max_len - 1 : 0);
+    for (size_t i = 0; i < n; i++) {
+        const size_t l = lens[i];
+        if (!l) continue;
+        if (l >= keep) {
+            st->hist.assign(bufs[i] + l - keep, bufs[i] + l);
+        } else {
+            st->hist.insert(st->hist.end(), bufs[i], bufs[i] + l);
+            if (st->hist.size() > keep)
+                st->hist.erase(st->hist.begin(), st->hist.end() - keep);
+        }
+    }
+}
+
+/* the writes bufs[0, n) of one stream, in one GPU launch */
+int scan_writes(vsa_hs_stream *st, vsa_hs_scratch_t *s, const uint8_t *const *bufs,
+                const size_t *lens, size_t n, vsa_hs_match_event_handler cb, void *ctx) {
+    vsa_db_t *ddb = device_db(s, st->db);
+    if (!ddb) return VSA_HS_INVALID;
+    Run r{st->db, st, cb, ctx, bufs, lens, {}, 0};
+    r.pos.resize(n);
+    uint64_t o = st->offset;
+    for (size_t i = 0; i < n; i++) {
+        r.pos[i] = o;
+        o += lens[i];
+    }
+    const int rc = vsa::exec_pieces(s->ctx, ddb, st->hist.data(), st->hist.size(), bufs, lens,
+                                    n, on_fragment, &r, on_piece);
+    push_history(st, bufs, lens, n);
+    st->offset = o;
+    if (r.terminated) {
+        st->terminated = true;
+        return VSA_HS_SCAN_TERMINATED;
+    }
+    return rc == HWLM_SUCCESS ? VSA_HS_SUCCESS : VSA_HS_UNKNOWN_ERROR;
+}
+
+void init_stream(vsa_hs_stream *st, const vsa_hs_database *db) {
+    st->db = db;
+    st->offset = 0;
+    st->hist.clear();
+    st->exhausted.assign(db->n_ekeys, 0);
+    st->terminated = false;
+}
+
+/* common entry checks: scratch valid for db, then marked in use */
+int enter(const vsa_hs_database_t *db, vsa_hs_scratch_t *s) {
+    if (!s || s->magic != SCRATCH_MAGIC || !device_db(s, db)) return VSA_HS_INVALID;
+    if (s->in_use.exchange(true)) return VSA_HS_SCRATCH_IN_USE;
+    return VSA_HS_SUCCESS;
+}
+
+void leave(vsa_hs_scratch_t *s) { s->in_use.store(false); }
+
+} // namespace
+
+extern "C" {
+
+int vsa_hs_compile_lit_multi(const char *const *expressions, const unsigned *flags,
+                             const unsigned *ids, const size_t *lens, unsigned elements,
+                             unsigned mode, const void *platform, vsa_hs_database_t **db,
+                             vsa_hs_compile_error_t **error) {
+    (void)platform;
+    /* hs.cpp:296-352 */
+    if (!error) {
+        if (db) *db = nullptr;
+        return VSA_HS_COMPILER_ERROR;
+    }
+    auto fail = [&](const std::string &m, int idx) {
+        if (db) *db = nullptr;
+        *error = make_error(m, idx);
+        return VSA_HS_COMPILER_ERROR;
+    };
+    if (!db) return fail("Invalid parameter: db is NULL", -1);
+    if (!expressions) return fail("Invalid parameter: expressions is NULL", -1);
+    if (!lens) return fail("Invalid parameter: len is NULL", -1);
+    if (elements == 0) return fail("Invalid parameter: elements is zero", -1);
+    const unsigned horizons = VSA_HS_MODE_SOM_HORIZON_LARGE | VSA_HS_MODE_SOM_HORIZON_MEDIUM |
+                              VSA_HS_MODE_SOM_HORIZON_SMALL;
+    const unsigned kinds = VSA_HS_MODE_BLOCK | VSA_HS_MODE_STREAM | VSA_HS_MODE_VECTORED;
+    if (mode & ~(kinds | horizons))
+        return fail("Invalid parameter: unrecognised mode flags.", -1);
+    const unsigned kind = mode & kinds;
+    if (!kind || (kind & (kind - 1)))
+        return fail("Invalid parameter: mode must have one (and only one) of HS_MODE_BLOCK, "
+                    "HS_MODE_STREAM or HS_MODE_VECTORED set.", -1);
+    const unsigned som_mode = mode & horizons;
+    if (som_mode) {
+        if (!(mode & VSA_HS_MODE_STREAM))
+            return fail("Invalid parameter: the HS_MODE_SOM_HORIZON_ mode flags may only be "
+                        "set in streaming mode.", -1);
+        if (som_mode & (som_mode - 1))
+            return fail("Invalid parameter: only one HS_MODE_SOM_HORIZON_ mode flag can be "
+                        "set.", -1);
+    }
+    if (elements > LIMIT_PATTERN_COUNT) return fail("Number of patterns too large", -1);
+
+    vsa_hs_database *out = new (std::nothrow) vsa_hs_database;
+    if (!out) return fail("Unable to allocate memory.", -1);
+    out->mode = kind;
+    out->serial = g_serial.fetch_add(1);
+    std::map<uint32_t, std::pair<bool, unsigned>> ext; /* id -> (single, first index) */
+    std::map<uint32_t, uint32_t> ekeys;
+    std::map<std::pair<std::string, bool>, uint32_t> frag_of;
+    std::vector<vsa::Literal> lits;
+    std::vector<bool> frag_noruns;
+    const unsigned allowed = VSA_HS_FLAG_CASELESS | VSA_HS_FLAG_SINGLEMATCH |
+                             VSA_HS_FLAG_SOM_LEFTMOST;
+    const unsigned all_flags = 0x7ffu; /* HS_FLAG_ALL, hs_internal.h:75-85 */
+    size_t min_len = ~(size_t)0;
+    for (unsigned i = 0; i < elements; i++) {
+        const unsigned f = flags ? flags[i] : 0;
+        const uint32_t id = ids ? ids[i] : 0;
+        const char *e = expressions[i];
+        const int idx = (int)i;
+        if (!e) {
+            delete out;
+            return fail("Invalid parameter: expression is NULL", idx);
+        }
+        /* compiler.cpp:406-423 */
+        if (lens[i] > LIMIT_PATTERN_LENGTH) {
+            delete out;
+            return fail("Pattern length exceeds limit.", idx);
+        }
+        if (f & ~allowed & all_flags) {
+            delete out;
+            return fail("Only HS_FLAG_CASELESS, HS_FLAG_SINGLEMATCH and HS_FLAG_SOM_LEFTMOST "
+                        "are supported in literal API.", idx);
+        }
+        if (e[0] == '\0' || lens[i] == 0) {
+            delete out;
+            return fail("Pure literal API doesn't support empty string.", idx);
+        }
+        /* compiler.cpp:130-139 */
+        if (f & ~all_flags) {
+            delete out;
+            return fail("Unrecognised flag.", idx);
+        }
+        const bool single = f & VSA_HS_FLAG_SINGLEMATCH;
+        if (single && (f & VSA_HS_FLAG_SOM_LEFTMOST)) {
+            delete out;
+            return fail("HS_FLAG_SINGLEMATCH is not supported in combination with "
+                        "HS_FLAG_SOM_LEFTMOST.", idx);
+        }
+        /* report_manager.cpp:212-236 */
+        auto it = ext.find(id);
+        if (it == ext.end()) {
+            ext.emplace(id, std::make_pair(single, i));
+        } else {
+            out->dedupe = true;
+            if (it->second.first != single) {
+                std::string m = "Expression (index " + std::to_string(i) + ") with match ID " +
+                                std::to_string(id) + " " +
+                                (single ? "specified " : "did not specify ") +
+                                "HS_FLAG_SINGLEMATCH whereas previous expression (index " +
+                                std::to_string(it->second.second) +
+                                ") with the same match ID did" + (single ? " not" : "") + ".";
+                delete out;
+                return fail(m, idx);
+            }
+        }
+        Pattern p;
+        p.id = id;
+        p.som = f & VSA_HS_FLAG_SOM_LEFTMOST;
+        p.caseless = f & VSA_HS_FLAG_CASELESS;
+        p.s.assign(e, lens[i]);
+        if (p.caseless)
+            for (auto &c : p.s) c = (char)upper((uint8_t)c);
+        if (single) {
+            auto ek = ekeys.find(id);
+            if (ek == ekeys.end()) ek = ekeys.emplace(id, (uint32_t)ekeys.size()).first;
+            p.ekey = ek->second;
+        }
+        const std::string tail = p.s.size() > SHORT_LIT ? p.s.substr(p.s.size() - SHORT_LIT) : p.s;
+        const auto key = std::make_pair(tail, p.caseless);
+        auto fr = frag_of.find(key);
+        if (fr == frag_of.end()) {
+            fr = frag_of.emplace(key, (uint32_t)out->frags.size()).first;
+            out->frags.emplace_back();
+            frag_noruns.push_back(true);
+            lits.push_back(vsa::makeLiteral((const u8 *)tail.data(), tail.size(), p.caseless,
+                                            false, fr->second, HWLM_ALL_GROUPS, nullptr,
+                                            nullptr, 0));
+        }
+        if (!single || p.s.size() > SHORT_LIT) frag_noruns[fr->second] = false;
+        out->frags[fr->second].push_back((uint32_t)out->pats.size());
+        out->max_len = std::max(out->max_len, p.s.size());
+        min_len = std::min(min_len, p.s.size());
+        out->pats.push_back(std::move(p));
+    }
+    for (size_t k = 0; k < lits.size(); k++) lits[k].noruns = frag_noruns[k];
+    out->n_ekeys = (uint32_t)ekeys.size();
+    out->min_width = (uint32_t)min_len;
+    vsa::BuildOptions opt;
+    if (vsa::buildHwlm(lits, opt, &out->hwlm, &out->hwlm_size) != VSA_OK) {
+        delete out;
+        return fail("Internal error.", -1);
+    }
+    *db = out;
+    *error = nullptr;
+    return VSA_HS_SUCCESS;
+}
+
+int vsa_hs_compile_lit(const char *expression, unsigned flags, size_t len, unsigned mode,
+                       const void *platform, vsa_hs_database_t **db,
+                       vsa_hs_compile_error_t **error) {
+    const unsigned id = 0;
+    return vsa_hs_compile_lit_multi(&expression, &flags, &id, &len, 1, mode, platform, db,
+                                    error);
+}
+
+int vsa_hs_free_compile_error(vsa_hs_compile_error_t *error) {
+    if (error) {
+        free(error->message);
+        free(error);
+    }
+    return VSA_HS_SUCCESS;
+}
+
+int vsa_hs_free_database(vsa_hs_database_t *db) {
+    if (db && db->magic != DB_MAGIC) return VSA_HS_INVALID;
+    if (db) {
+        db->magic = 0;
+        vsa_blob_free(db->hwlm);
+        delete db;
+    }
+    return VSA_HS_SUCCESS;
+}
+
+int vsa_hs_database_hwlm(const vsa_hs_database_t *db, const void **hwlm, size_t *size,
+                         unsigned *fragments) {
+    if (!valid_db(db)) return VSA_HS_INVALID;
+    if (hwlm) *hwlm = db->hwlm;
+    if (size) *size = db->hwlm_size;
+    if (fragments) *fragments = (unsigned)db->frags.size();
+    return VSA_HS_SUCCESS;
+}
+
+/* scratch.c:242-300: grows an existing scratch to serve db as well */
+int vsa_hs_alloc_scratch(const vsa_hs_database_t *db, vsa_hs_scratch_t **scratch) {
+    if (!db || !scratch) return VSA_HS_INVALID;
+    if (!valid_db(db)) return VSA_HS_INVALID;
+    vsa_hs_scratch_t *s = *scratch;
+    if (s) {
+        if (s->magic != SCRATCH_MAGIC) return VSA_HS_INVALID;
+        if (s->in_use.exchange(true)) return VSA_HS_SCRATCH_IN_USE;
+    } else {
+        s = new (std::nothrow) vsa_hs_scratch;
+        if (!s) return VSA_HS_NOMEM;
+        s->in_use.store(true);
+        const char *e = getenv("VSA_DEVICE");
+        if (vsa_ctx_create(e ? atoi(e) : 0, &s->ctx) != VSA_OK) {
+            delete s;
+            return VSA_HS_NOMEM;
+        }
+    }
+    if (!device_db(s, db)) {
+        vsa_db_t *d = nullptr;
+        if (vsa_db_load(s->ctx, db->hwlm, db->hwlm_size, &d) != VSA_OK) {
+            s->in_use.store(false);
+            if (!*scratch) vsa_hs_free_scratch(s);
+            return VSA_HS_NOMEM;
+        }
+        s->dbs.emplace_back(db->serial, d);
+    }
+    s->in_use.store(false);
+    *scratch = s;
+    return VSA_HS_SUCCESS;
+}
+
+int vsa_hs_free_scratch(vsa_hs_scratch_t *scratch) {
+    if (!scratch) return VSA_HS_SUCCESS;
+    if (scratch->magic != SCRATCH_MAGIC) return VSA_HS_INVALID;
+    if (scratch->in_use.exchange(true)) return VSA_HS_SCRATCH_IN_USE;
+    for (auto &e : scratch->dbs) vsa_db_free(e.second);
+    if (scratch->ctx) vsa_ctx_destroy(scratch->ctx);
+    scratch->magic = 0;
+    delete scratch;
+    return VSA_HS_SUCCESS;
+}
+
+/* runtime.c:316-470 */
+int vsa_hs_scan(const vsa_hs_database_t *db, const char *data, unsigned int length,
+                unsigned int flags, vsa_hs_scratch_t *scratch,
+                vsa_hs_match_event_handler onEvent, void *context) {
+    (void)flags;
+    if (!scratch || !data) return VSA_HS_INVALID;
+    if (!valid_db(db)) return VSA_HS_INVALID;
+    if (db->mode != VSA_HS_MODE_BLOCK) return VSA_HS_DB_MODE_ERROR;
+    int rc = enter(db, scratch);
+    if (rc != VSA_HS_SUCCESS) return rc;
+    if (db->min_width > length) {
+        leave(scratch);
+        return VSA_HS_SUCCESS;
+    }
+    vsa_hs_stream st;
+    init_stream(&st, db);
+    const uint8_t *b = (const uint8_t *)data;
+    const size_t l = length;
+    rc = scan_writes(&st, scratch, &b, &l, 1, onEvent, context);
+    leave(scratch);
+    return rc;
+}
+
+/* runtime.c:1106-1180: pieces up to the first NULL one are scanned (its
+ * hs_scan_stream_internal call fails with HS_INVALID) */
+int vsa_hs_scan_vector(const vsa_hs_database_t *db, const char *const *data,
+                       const unsigned int *length, unsigned int count, unsigned int flags,
+                       vsa_hs_scratch_t *scratch, vsa_hs_match_event_handler onEvent,
+                       void *context) {
+    (void)flags;
+    if (!scratch || !data || !length) return VSA_HS_INVALID;
+    if (!valid_db(db)) return VSA_HS_INVALID;
+    if (db->mode != VSA_HS_MODE_VECTORED) return VSA_HS_DB_MODE_ERROR;
+    int rc = enter(db, scratch);
+    if (rc != VSA_HS_SUCCESS) return rc;
+    unsigned n = 0;
+    while (n < count && data[n]) n++;
+    std::vector<size_t> lens(length, length + n);
+    vsa_hs_stream st;
+    init_stream(&st, db);
+    rc = scan_writes(&st, scratch, (const uint8_t *const *)data, lens.data(), n, onEvent,
+                     context);
+    leave(scratch);
+    if (rc != VSA_HS_SUCCESS) return rc;
+    return n < count ? VSA_HS_INVALID : VSA_HS_SUCCESS;
+}
+
+/* runtime.c:545-575 */
+int vsa_hs_open_stream(const vsa_hs_database_t *db, unsigned int flags,
+                       vsa_hs_stream_t **stream) {
+    (void)flags;
+    if (!stream) return VSA_HS_INVALID;
+    if (!valid_db(db)) return VSA_HS_INVALID;
+    if (db->mode != VSA_HS_MODE_STREAM) return VSA_HS_DB_MODE_ERROR;
+    vsa_hs_stream *s = new (std::nothrow) vsa_hs_stream;
+    if (!s) return VSA_HS_NOMEM;
+    init_stream(s, db);
+    *stream = s;
+    return VSA_HS_SUCCESS;
+}
+
+/* runtime.c:868-996 */
+int vsa_hs_scan_stream(vsa_hs_stream_t *id, const char *data, unsigned int length,
+                       unsigned int flags, vsa_hs_scratch_t *scratch,
+                       vsa_hs_match_event_handler onEvent, void *ctxt) {
+    (void)flags;
+    if (!id || id->magic != STREAM_MAGIC || !scratch || !data) return VSA_HS_INVALID;
+    int rc = enter(id->db, scratch);
+    if (rc != VSA_HS_SUCCESS) return rc;
+    if (id->terminated) {
+        leave(scratch);
+        return VSA_HS_SCAN_TERMINATED;
+    }
+    if (!length) {
+        leave(scratch);
+        return VSA_HS_SUCCESS;
+    }
+    const uint8_t *b = (const uint8_t *)data;
+    const size_t l = length;
+    rc = scan_writes(id, scratch, &b, &l, 1, onEvent, ctxt);
+    leave(scratch);
+    return rc;
+}
+
+/* runtime.c:999-1025: pure literal databases have no end-of-data matches */
+int vsa_hs_close_stream(vsa_hs_stream_t *id, vsa_hs_scratch_t *scratch,
+                        vsa_hs_match_event_handler onEvent, void *ctxt) {
+    (void)ctxt;
+    if (!id || id->magic != STREAM_MAGIC) return VSA_HS_INVALID;
+    if (onEvent) {
+        if (!scratch || scratch->magic != SCRATCH_MAGIC || !device_db(scratch, id->db))
+            return VSA_HS_INVALID;
+        if (scratch->in_use.load()) return VSA_HS_SCRATCH_IN_USE;
+    }
+    id->magic = 0;
+    delete id;
+    return VSA_HS_SUCCESS;
+}
+
+/* runtime.c:1028-1055 */
+int vsa_hs_reset_stream(vsa_hs_stream_t *id, unsigned int flags, vsa_hs_scratch_t *scratch,
+                        vsa_hs_match_event_handler onEvent, void *context) {
+    (void)flags;
+    (void)context;
+    if (!id || id->magic != STREAM_MAGIC) return VSA_HS_INVALID;
+    if (onEvent) {
+        if (!scratch || scratch->magic != SCRATCH_MAGIC || !device_db(scratch, id->db))
+            return VSA_HS_INVALID;
+        if (scratch->in_use.load()) return VSA_HS_SCRATCH_IN_USE;
+    }
+    init_stream(id, id->db);
+    return VSA_HS_SUCCESS;
+}
+
+} // extern "C"

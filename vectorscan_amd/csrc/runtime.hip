@@ -693,10 +693,11 @@ bool emit_flood(const vsa::FloodEvent &ev, HWLMCallback cb, hs_scratch *scratch,
  * the ends they skip. */
 hwlm_error_t replay_lit(const vsa_db *db, const uint64_t *keys, uint64_t n,
                         HWLMCallback cb, hs_scratch *scratch, hwlm_group_t groups,
-                        const std::vector<vsa::FloodEvent> *floods = nullptr) {
+                        const std::vector<vsa::FloodEvent> *floods = nullptr,
+                        bool scratch_is_real = true) {
     const uint8_t *eng = db->hblob + VSA_ROUNDUP_CL(sizeof(HWLM));
     const uint8_t *confBase = eng + ((const uint32_t *)eng)[4];
-    const bool squash_ok = scratch && db->mode == VSA_MODE_FDR;
+    const bool squash_ok = scratch && scratch_is_real && db->mode == VSA_MODE_FDR;
     const long co = g_fdr_conf_off.load(), coo = g_fdr_conf_offset_off.load();
     const size_t nf = floods ? floods->size() : 0;
     size_t fe = 0;
@@ -1592,6 +1593,85 @@ hwlm_error_t hwlmExecStreaming(const struct HWLM *tab, size_t len, size_t start,
     start = hwlm_accel_stream(aa, hbuf, hlen, buf, len, start);
     return fdrExecStreaming((const FDR *)eng, hbuf, hlen, buf, len, start, cb, scratch, groups);
 }
+
+/* The writes of one logical stream (hs_scan: one block-mode write;
+ * hs_scan_vector: all pieces) scanned in ONE launch: the history bytes and
+ * the writes laid end to end in the context's input buffer, each write a
+ * block whose history is what precedes it (<= 16 bytes, enough for the
+ * 8-byte HWLM literals); then each write's records replayed in order with
+ * its own flood events and ends relative to it.  cbctx is an opaque
+ * callback context (no Rose scratch: no INCLUDED_JUMP squash). */
+} // extern "C"
+
+namespace vsa {
+hwlm_error_t exec_pieces(vsa_ctx *c, const vsa_db *db, const u8 *hist, size_t hist_len,
+                         const u8 *const *bufs, const size_t *lens, size_t n,
+                         LitCallback cb, void *cbctx, void (*on_piece)(void *, size_t)) {
+    if (!c || !db) return HWLM_ERROR_UNKNOWN;
+    size_t total = 0;
+    for (size_t i = 0; i < n; i++) total += lens[i];
+    if (!total) return HWLM_SUCCESS;
+    const size_t pre = 16, hl0 = std::min<size_t>(hist_len, 16);
+    if (ensure_in(c, pre + total + 16) != VSA_OK) return HWLM_ERROR_UNKNOWN;
+    if (hl0 && hipMemcpyAsync(c->ws.d_in + pre - hl0, hist + hist_len - hl0, hl0,
+                              hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return HWLM_ERROR_UNKNOWN;
+    std::vector<uint64_t> off, len, st, hl;
+    std::vector<size_t> which;
+    size_t pos = pre, seen = hist_len;
+    for (size_t i = 0; i < n; i++) {
+        if (!lens[i]) continue;
+        if (hipMemcpyAsync(c->ws.d_in + pos, bufs[i], lens[i], hipMemcpyHostToDevice,
+                           c->stream) != hipSuccess)
+            return HWLM_ERROR_UNKNOWN;
+        off.push_back(pos);
+        len.push_back(lens[i]);
+        st.push_back(0);
+        hl.push_back(std::min<size_t>(seen, 16));
+        which.push_back(i);
+        pos += lens[i];
+        seen += lens[i];
+    }
+    uint64_t nm = 0;
+    if (scan_blocks_impl(c, db, c->ws.d_in, off.data(), len.data(), st.data(),
+                         (uint32_t)off.size(), 0, &nm, hl.data()) != VSA_OK)
+        return HWLM_ERROR_UNKNOWN;
+    std::vector<uint64_t> keys(nm);
+    std::vector<uint32_t> ids(nm);
+    if (nm) {
+        if (hipMemcpyAsync(keys.data(), c->ws.d_keys[c->cur], nm * 8, hipMemcpyDeviceToHost,
+                           c->stream) != hipSuccess ||
+            hipMemcpyAsync(ids.data(), c->ws.d_ids[c->cur], nm * 4, hipMemcpyDeviceToHost,
+                           c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+            return HWLM_ERROR_UNKNOWN;
+    }
+    hs_scratch *sc = (hs_scratch *)cbctx;
+    std::vector<vsa::FloodEvent> ev;
+    uint64_t k = 0;
+    for (size_t b = 0; b < off.size(); b++) {
+        const uint64_t hi = off[b] + len[b];
+        uint64_t k2 = k;
+        while (k2 < nm && (keys[k2] >> VSA_KEY_END_SHIFT) < hi) {
+            keys[k2] -= off[b] << VSA_KEY_END_SHIFT; /* end relative to the write */
+            k2++;
+        }
+        if (on_piece) on_piece(cbctx, which[b]);
+        hwlm_error_t r;
+        if (db->type == HWLM_ENGINE_NOOD) {
+            r = replay_nood(keys.data() + k, ids.data() + k, k2 - k, cb, sc);
+        } else {
+            r = replay_lit(db, keys.data() + k, k2 - k, cb, sc, HWLM_ALL_GROUPS,
+                           floods_for(db, bufs[which[b]], len[b], 0, ev), false);
+        }
+        if (r != HWLM_SUCCESS) return r;
+        k = k2;
+    }
+    return HWLM_SUCCESS;
+}
+} // namespace vsa
+
+extern "C" {
 
 int vsa_scan_blocks_ex(vsa_ctx_t *c, const vsa_db_t *db, const uint8_t *d_data,
                        const uint64_t *offsets, const uint64_t *lens, const uint64_t *starts,

@@ -55,6 +55,25 @@ struct FloodEvent {
 void flood_events(const u8 *buf, size_t len, size_t start, const u8 *eng, u32 vsize,
                   std::vector<FloodEvent> &out);
 
+} // namespace vsa
+
+struct hs_scratch;
+struct vsa_ctx;
+struct vsa_db;
+
+namespace vsa {
+
+/* HWLMCallback (hwlm.h:63-73) */
+typedef u64a (*LitCallback)(size_t end, u32 id, ::hs_scratch *scratch);
+
+/* runtime.hip: the writes of one stream (history hist[0, hist_len) before
+ * the first) scanned in one GPU launch and replayed write by write through
+ * cb(end relative to the write, HWLM literal id, cbctx); on_piece(cbctx, i)
+ * runs before write i's records.  Zero-length writes are skipped. */
+int exec_pieces(vsa_ctx *c, const vsa_db *db, const u8 *hist, size_t hist_len,
+                const u8 *const *bufs, const size_t *lens, size_t n, LitCallback cb,
+                void *cbctx, void (*on_piece)(void *, size_t));
+
 Literal makeLiteral(const u8 *s, size_t len, bool nocase, bool noruns, u32 id,
                     u64a groups, const u8 *msk, const u8 *cmp, size_t mlen);
 int buildHwlm(std::vector<Literal> lits, const BuildOptions &opt, u8 **out,

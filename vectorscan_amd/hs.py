@@ -1,0 +1,241 @@
+"""Pure-literal database API (include/vectorscan_amd_hs.h) — the Python
+mirror of the reference's hs_compile_lit_multi / hs_scan / hs_scan_vector /
+stream calls (src/hs_compile.h:608-697, src/hs_runtime.h:148-609) for
+databases of pure literals, over the GPU literal matcher.
+
+Callbacks take ``(id, from, to, flags)`` and return a truthy value to stop
+matching (match_event_handler, hs_runtime.h:125-128).  Every scan runs on
+the GPU; there is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+
+from . import lib, _sig, _as_buf
+
+SUCCESS = 0
+INVALID = -1
+NOMEM = -2
+SCAN_TERMINATED = -3
+COMPILER_ERROR = -4
+DB_MODE_ERROR = -7
+SCRATCH_IN_USE = -10
+UNKNOWN_ERROR = -13
+
+FLAG_CASELESS = 1
+FLAG_DOTALL = 2
+FLAG_MULTILINE = 4
+FLAG_SINGLEMATCH = 8
+FLAG_ALLOWEMPTY = 16
+FLAG_UTF8 = 32
+FLAG_UCP = 64
+FLAG_PREFILTER = 128
+FLAG_SOM_LEFTMOST = 256
+FLAG_COMBINATION = 512
+FLAG_QUIET = 1024
+MODE_BLOCK = 1
+MODE_STREAM = 2
+MODE_VECTORED = 4
+MODE_SOM_HORIZON_LARGE = 1 << 24
+MODE_SOM_HORIZON_MEDIUM = 1 << 25
+MODE_SOM_HORIZON_SMALL = 1 << 26
+
+
+class _CompileError(ctypes.Structure):
+    _fields_ = [("message", ctypes.c_char_p), ("expression", ctypes.c_int)]
+
+
+EventHandler = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_uint, ctypes.c_ulonglong,
+                                ctypes.c_ulonglong, ctypes.c_uint, ctypes.c_void_p)
+
+_vp = ctypes.c_void_p
+_sig("vsa_hs_compile_lit_multi", ctypes.c_int, _vp, _vp, _vp, _vp, ctypes.c_uint,
+     ctypes.c_uint, _vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.POINTER(_CompileError)))
+_sig("vsa_hs_free_compile_error", ctypes.c_int, ctypes.POINTER(_CompileError))
+_sig("vsa_hs_free_database", ctypes.c_int, _vp)
+_sig("vsa_hs_database_hwlm", ctypes.c_int, _vp, ctypes.POINTER(_vp),
+     ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_uint))
+_sig("vsa_hs_alloc_scratch", ctypes.c_int, _vp, ctypes.POINTER(_vp))
+_sig("vsa_hs_free_scratch", ctypes.c_int, _vp)
+_sig("vsa_hs_scan", ctypes.c_int, _vp, _vp, ctypes.c_uint, ctypes.c_uint, _vp, EventHandler,
+     _vp)
+_sig("vsa_hs_scan_vector", ctypes.c_int, _vp, _vp, _vp, ctypes.c_uint, ctypes.c_uint, _vp,
+     EventHandler, _vp)
+_sig("vsa_hs_open_stream", ctypes.c_int, _vp, ctypes.c_uint, ctypes.POINTER(_vp))
+_sig("vsa_hs_scan_stream", ctypes.c_int, _vp, _vp, ctypes.c_uint, ctypes.c_uint, _vp,
+     EventHandler, _vp)
+_sig("vsa_hs_close_stream", ctypes.c_int, _vp, _vp, EventHandler, _vp)
+_sig("vsa_hs_reset_stream", ctypes.c_int, _vp, ctypes.c_uint, _vp, EventHandler, _vp)
+
+
+class HsError(RuntimeError):
+    def __init__(self, code, message="", expression=-1):
+        super().__init__("hs error %d%s" % (code, (": " + message) if message else ""))
+        self.code = code
+        self.message = message
+        self.expression = expression
+
+
+class Database:
+    """hs_database_t of pure literals (hs_compile_lit_multi)."""
+
+    def __init__(self, handle, mode):
+        self.handle = handle
+        self.mode = mode
+
+    def hwlm(self):
+        """(address, size, fragments) of the database's HWLM blob."""
+        p, n, f = _vp(), ctypes.c_size_t(), ctypes.c_uint()
+        rc = lib.vsa_hs_database_hwlm(self.handle, ctypes.byref(p), ctypes.byref(n),
+                                      ctypes.byref(f))
+        if rc:
+            raise HsError(rc)
+        return p.value, n.value, f.value
+
+    def hwlm_bytes(self):
+        p, n, _ = self.hwlm()
+        return ctypes.string_at(p, n)
+
+    def close(self):
+        if self.handle:
+            lib.vsa_hs_free_database(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def compile_lit_multi(expressions, flags=None, ids=None, mode=MODE_BLOCK):
+    """hs_compile_lit_multi (hs_compile.h:690).  Raises HsError(code,
+    message, expression) as the reference reports a compile error."""
+    n = len(expressions)
+    bufs = [ctypes.create_string_buffer(bytes(e), max(1, len(e))) for e in expressions]
+    exprs = (ctypes.c_void_p * max(1, n))(*[ctypes.addressof(b) for b in bufs])
+    lens = (ctypes.c_size_t * max(1, n))(*[len(e) for e in expressions])
+    fl = (ctypes.c_uint * max(1, n))(*flags) if flags is not None else None
+    idv = (ctypes.c_uint * max(1, n))(*ids) if ids is not None else None
+    db = _vp()
+    err = ctypes.POINTER(_CompileError)()
+    rc = lib.vsa_hs_compile_lit_multi(exprs, fl, idv, lens, n, mode, None, ctypes.byref(db),
+                                      ctypes.byref(err))
+    if rc != SUCCESS:
+        msg, idx = "", -1
+        if err:
+            msg = err.contents.message.decode()
+            idx = err.contents.expression
+            lib.vsa_hs_free_compile_error(err)
+        raise HsError(rc, msg, idx)
+    return Database(db.value, mode)
+
+
+def compile_lit(expression, flags=0, mode=MODE_BLOCK):
+    """hs_compile_lit (hs_compile.h:608): id 0."""
+    return compile_lit_multi([expression], [flags], [0], mode)
+
+
+class Scratch:
+    """hs_scratch_t: one per thread; grows to serve every database passed."""
+
+    def __init__(self, db):
+        self.handle = None
+        self.grow(db)
+
+    def grow(self, db):
+        h = _vp(self.handle)
+        rc = lib.vsa_hs_alloc_scratch(db.handle, ctypes.byref(h))
+        if rc:
+            raise HsError(rc)
+        self.handle = h.value
+
+    def close(self):
+        if self.handle:
+            lib.vsa_hs_free_scratch(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _handler(on_event, out):
+    def cb(id_, frm, to, flags, ctx):
+        if on_event is None:
+            out.append((id_, frm, to))
+            return 0
+        return 1 if on_event(id_, frm, to, flags) else 0
+    return EventHandler(cb)
+
+
+def scan(db, data, scratch, on_event=None, flags=0):
+    """hs_scan (hs_runtime.h:479).  Returns (rc, [(id, from, to)]) — the list
+    collects the matches when no on_event is given."""
+    keep, ptr, n = _as_buf(data)
+    out = []
+    rc = lib.vsa_hs_scan(db.handle, ptr, n, flags, scratch.handle if scratch else None,
+                         _handler(on_event, out), None)
+    return rc, out
+
+
+def scan_vector(db, pieces, scratch, on_event=None, flags=0):
+    """hs_scan_vector (hs_runtime.h:522).  A piece of None is a NULL data
+    pointer (the call returns HS_INVALID after the pieces before it)."""
+    keeps, ptrs, lens = [], [], []
+    for p in pieces:
+        if p is None:
+            ptrs.append(None)
+            lens.append(0)
+            continue
+        k, ptr, n = _as_buf(p)
+        keeps.append(k)
+        ptrs.append(ptr)
+        lens.append(n)
+    cnt = len(pieces)
+    pv = (ctypes.c_void_p * max(1, cnt))(*ptrs)
+    lv = (ctypes.c_uint * max(1, cnt))(*lens)
+    out = []
+    rc = lib.vsa_hs_scan_vector(db.handle, pv, lv, cnt, flags,
+                                scratch.handle if scratch else None, _handler(on_event, out),
+                                None)
+    return rc, out
+
+
+class Stream:
+    """hs_stream_t (hs_open_stream / hs_scan_stream / hs_close_stream /
+    hs_reset_stream)."""
+
+    def __init__(self, db, flags=0):
+        h = _vp()
+        rc = lib.vsa_hs_open_stream(db.handle, flags, ctypes.byref(h))
+        if rc:
+            raise HsError(rc)
+        self.handle = h.value
+        self._keep = []
+
+    def scan(self, data, scratch, on_event=None, flags=0):
+        keep, ptr, n = _as_buf(data)
+        out = []
+        rc = lib.vsa_hs_scan_stream(self.handle, ptr, n, flags,
+                                    scratch.handle if scratch else None,
+                                    _handler(on_event, out), None)
+        return rc, out
+
+    def reset(self, scratch=None, on_event=None, flags=0):
+        out = []
+        h = _handler(on_event, out) if on_event else EventHandler()
+        return lib.vsa_hs_reset_stream(self.handle, flags, scratch.handle if scratch else None,
+                                       h, None)
+
+    def close(self, scratch=None, on_event=None):
+        if not self.handle:
+            return SUCCESS
+        out = []
+        h = _handler(on_event, out) if on_event else EventHandler()
+        rc = lib.vsa_hs_close_stream(self.handle, scratch.handle if scratch else None, h, None)
+        if rc == SUCCESS:
+            self.handle = None
+        return rc
