@@ -19,7 +19,10 @@ real end = end + lit_offset_adjust, lit_offset_adjust = offset + 1) and
 min(offset, history required), runtime.c:78), with the Rose report program
 of a literal: CHECK_LONG_LIT on the bytes before the 8-byte tail, exhaustion
 (isExhausted / markAsMatched) for single-match ids, dedupe of one external
-id per offset, SOM from = to - len (ng.cpp:600-604 makeSomRelativeCallback).
+id per offset, SOM from = to - len (ng.cpp:600-604 makeSomRelativeCallback);
+SOM reports of an id with several patterns are held in the SOM dedupe log
+and flushed (leftmost start per id, id order) when the offset moves on or
+the write ends (flushStoredSomMatches).
 
 The HWLM scan is oracle.hwlm_exec / hwlm_exec_stream (oracle.c), over the
 HWLM blob built from `hwlm_literals()` by the product's builder (the same
@@ -124,6 +127,23 @@ class _Run:
         self.exhausted = [False] * db.n_ekeys
         self.stream = b""  # every byte written so far
         self.terminated = False
+        self.som_log = {}  # id -> leftmost from at the current offset
+        self.som_to = None
+        counts = {}
+        for p in db.pats:
+            counts[p["id"]] = counts.get(p["id"], 0) + 1
+        self.som_dedupe = [p["som"] and counts[p["id"]] > 1 for p in db.pats]
+
+    def flush(self, out, stop_after):
+        """flushStoredSomMatches: leftmost start per id, in id order."""
+        for i in sorted(self.som_log):
+            if self.terminated:
+                break
+            out.append((i, self.som_log[i], self.som_to))
+            if stop_after is not None and len(out) >= stop_after:
+                self.terminated = True
+        self.som_log = {}
+        return not self.terminated
 
     def deliver(self, frag, to, out, at_to, stop_after):
         for pi in self.db.frags[frag][2]:
@@ -138,6 +158,11 @@ class _Run:
                 if seg != s[:-SHORT]:
                     continue
             if p["ekey"] is not None and self.exhausted[p["ekey"]]:
+                continue
+            if self.som_dedupe[pi]:
+                f = to - len(s)
+                self.som_log[p["id"]] = min(self.som_log.get(p["id"], f), f)
+                self.som_to = to
                 continue
             if self.db.dedupe:
                 if p["id"] in at_to:
@@ -168,9 +193,12 @@ class _Run:
         for end, frag in recs:
             to = off + end + 1
             if to != last_to:
+                if self.som_log and not self.flush(out, stop_after):
+                    return
                 last_to, at_to = to, set()
             if not self.deliver(frag, to, out, at_to, stop_after):
                 return
+        self.flush(out, stop_after)
 
 
 def scan(db, blob_ptr, data, stop_after=None):
@@ -209,17 +237,19 @@ def brute_force(db, data):
             hits.append((start + len(s), pi))
             start = hay.find(s, start + 1)
     hits.sort()
-    out, seen_at, last, exhausted = [], set(), None, set()
+    out, seen_at, last, exhausted = {}, set(), None, set()
     for to, pi in hits:
         p = db.pats[pi]
         if to != last:
             last, seen_at = to, set()
         if p["single"] and p["id"] in exhausted:
             continue
-        if p["id"] in seen_at:
+        frm = to - len(p["s"]) if p["som"] else 0
+        key = (p["id"], to)
+        if key in out:  # one report per id per offset, the leftmost start
+            out[key] = min(out[key], frm)
             continue
-        seen_at.add(p["id"])
         if p["single"]:
             exhausted.add(p["id"])
-        out.append((p["id"], to - len(p["s"]) if p["som"] else 0, to))
-    return out
+        out[key] = frm
+    return [(i, f, t) for (i, t), f in out.items()]

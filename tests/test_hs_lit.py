@@ -42,6 +42,24 @@ def corpus(rng, n, exprs, alphabet=b"abcd", plants=20, runs=True):
     return a
 
 
+def normalize(flags, ids):
+    """SINGLEMATCH agrees per id (a compile error otherwise) and, where an id
+    has several patterns, so does SOM_LEFTMOST: which of two same-offset
+    reports of one id survives dedupe is the first delivered, and with mixed
+    SOM the reference's separate SOM dedupe (DEDUPE_SOM) is not restated."""
+    single, som = {}, {}
+    out = []
+    for i, f in enumerate(flags):
+        s = single.setdefault(ids[i], bool(f & hs.FLAG_SINGLEMATCH))
+        f = (f | hs.FLAG_SINGLEMATCH) if s else (f & ~hs.FLAG_SINGLEMATCH)
+        if s:
+            f &= ~hs.FLAG_SOM_LEFTMOST
+        m = som.setdefault(ids[i], bool(f & hs.FLAG_SOM_LEFTMOST))
+        f = (f | hs.FLAG_SOM_LEFTMOST) if m else (f & ~hs.FLAG_SOM_LEFTMOST)
+        out.append(f)
+    return out
+
+
 def build_pair(exprs, flags, ids=None, mode=hs.MODE_BLOCK):
     db = hs.compile_lit_multi(exprs, flags, ids, mode)
     odb = ohs.compile_lit_multi(exprs, flags, ids)
@@ -104,13 +122,7 @@ def test_fragments_match_oracle(seed):
                                  (0, hs.FLAG_CASELESS, hs.FLAG_SINGLEMATCH,
                                   hs.FLAG_SOM_LEFTMOST, hs.FLAG_CASELESS | hs.FLAG_SINGLEMATCH))
     ids = [rng.randrange(0, max(1, n // 2)) for _ in range(n)]
-    # SINGLEMATCH must agree per id
-    single = {}
-    for i, f in enumerate(flags):
-        s = single.setdefault(ids[i], bool(f & hs.FLAG_SINGLEMATCH))
-        flags[i] = (f | hs.FLAG_SINGLEMATCH) if s else (f & ~hs.FLAG_SINGLEMATCH)
-        if s:
-            flags[i] &= ~hs.FLAG_SOM_LEFTMOST
+    flags = normalize(flags, ids)
     db, odb = build_pair(exprs, flags, ids)
     _, _, nfrag = db.hwlm()
     assert nfrag == len(odb.frags)
@@ -127,11 +139,7 @@ def test_oracle_equals_brute_force(seed):
                                  (0, hs.FLAG_CASELESS, hs.FLAG_SINGLEMATCH,
                                   hs.FLAG_SOM_LEFTMOST))
     ids = list(range(n)) if seed % 2 else [rng.randrange(0, n) for _ in range(n)]
-    single = {}
-    for i, f in enumerate(flags):
-        s = single.setdefault(ids[i], bool(f & hs.FLAG_SINGLEMATCH))
-        flags[i] = ((f | hs.FLAG_SINGLEMATCH) & ~hs.FLAG_SOM_LEFTMOST) if s else \
-            (f & ~hs.FLAG_SINGLEMATCH)
+    flags = normalize(flags, ids)
     odb = ohs.compile_lit_multi(exprs, flags, ids)
     blob = oracle_blob(odb)
     data = corpus(rng, 3000, exprs, b"abcdABCD")
@@ -193,11 +201,7 @@ def make_set(k, seed=0):
     rng = random.Random(1000 * k + seed)
     exprs, flags = rand_patterns(rng, n, lo, hi, alpha, mix)
     ids = [rng.randrange(0, max(1, n // 3)) for _ in range(n)] if dup else list(range(n))
-    single = {}
-    for i, f in enumerate(flags):
-        s = single.setdefault(ids[i], bool(f & hs.FLAG_SINGLEMATCH))
-        flags[i] = ((f | hs.FLAG_SINGLEMATCH) & ~hs.FLAG_SOM_LEFTMOST) if s else \
-            (f & ~hs.FLAG_SINGLEMATCH)
+    flags = normalize(flags, ids)
     return rng, exprs, flags, ids, alpha
 
 

@@ -24,7 +24,10 @@
  * pattern of the fragment, in compile order, reports unless its long-literal
  * check fails, its id is exhausted, or its id was already reported at this
  * `to` (dedupe keys are per external id); from = to - len under
- * HS_FLAG_SOM_LEFTMOST (makeSomRelativeCallback), else 0.  A nonzero
+ * HS_FLAG_SOM_LEFTMOST (makeSomRelativeCallback), else 0.  The SOM reports
+ * of an id with several patterns go through the SOM dedupe log instead: the
+ * leftmost start per id at one offset, delivered when the offset moves on
+ * or the write ends (flushStoredSomMatches).  A nonzero
  * callback return ends the scan: HS_SCAN_TERMINATED, and a terminated
  * stream stays terminated (runtime.c:883-893).
  */
@@ -58,6 +61,7 @@ struct Pattern {
     uint32_t id = 0;
     uint32_t ekey = NO_EKEY; /* exhaustion key (single-match ids) */
     bool som = false;
+    bool som_dedupe = false; /* SOM report of an id with several patterns */
     bool caseless = false;
     std::string s; /* as compiled: upper-cased when caseless */
 };
@@ -129,8 +133,24 @@ struct Run {
     size_t cur = 0;
     uint64_t last_to = ~0ULL;
     std::vector<uint32_t> at_to; /* ids reported at last_to */
+    std::map<uint32_t, uint64_t> som_log; /* id -> leftmost from at last_to */
     bool terminated = false;
 };
+
+/* flushStoredSomMatches (src/som/som_runtime.c, report.h): the SOM reports
+ * of deduped ids held for the current offset, leftmost start per id, in
+ * dedupe-key (id) order */
+bool flush_som(Run &r) {
+    bool ok = true;
+    for (const auto &e : r.som_log) {
+        if (ok && r.cb && r.cb(e.first, e.second, r.last_to, 0, r.ctx)) {
+            r.terminated = true;
+            ok = false;
+        }
+    }
+    r.som_log.clear();
+    return ok;
+}
 
 uint8_t byte_at(const Run &r, uint64_t p) {
     if (p < r.pos[0]) return r.st->hist[r.st->hist.size() - (size_t)(r.pos[0] - p)];
@@ -156,6 +176,7 @@ u64a on_fragment(size_t end, u32 frag, hs_scratch *sc) {
     Run &r = *(Run *)sc;
     const uint64_t to = r.pos[r.cur] + end + 1; /* lit_offset_adjust */
     if (to != r.last_to) {
+        if (!r.som_log.empty() && !flush_som(r)) return HWLM_TERMINATE_MATCHING;
         r.last_to = to;
         r.at_to.clear();
     }
@@ -163,6 +184,13 @@ u64a on_fragment(size_t end, u32 frag, hs_scratch *sc) {
         const Pattern &p = r.db->pats[pi];
         if (p.s.size() > SHORT_LIT && !long_ok(r, to, p)) continue;
         if (p.ekey != NO_EKEY && r.st->exhausted[p.ekey]) continue;
+        if (p.som_dedupe) {
+            const uint64_t from = to - p.s.size();
+            auto it = r.som_log.find(p.id);
+            if (it == r.som_log.end()) r.som_log.emplace(p.id, from);
+            else it->second = std::min(it->second, from);
+            continue;
+        }
         if (r.db->dedupe) {
             if (std::find(r.at_to.begin(), r.at_to.end(), p.id) != r.at_to.end()) continue;
             r.at_to.push_back(p.id);
@@ -209,6 +237,7 @@ int scan_writes(vsa_hs_stream *st, vsa_hs_scratch_t *s, const uint8_t *const *bu
     }
     const int rc = vsa::exec_pieces(s->ctx, ddb, st->hist.data(), st->hist.size(), bufs, lens,
                                     n, on_fragment, &r, on_piece);
+    if (rc == HWLM_SUCCESS && !r.terminated) flush_som(r); /* end of the write */
     push_history(st, bufs, lens, n);
     st->offset = o;
     if (r.terminated) {
@@ -284,6 +313,7 @@ int vsa_hs_compile_lit_multi(const char *const *expressions, const unsigned *fla
     out->serial = g_serial.fetch_add(1);
     std::map<uint32_t, std::pair<bool, unsigned>> ext; /* id -> (single, first index) */
     std::map<uint32_t, uint32_t> ekeys;
+    std::map<uint32_t, uint32_t> ext_count; /* patterns per id */
     std::map<std::pair<std::string, bool>, uint32_t> frag_of;
     std::vector<vsa::Literal> lits;
     std::vector<bool> frag_noruns;
@@ -342,6 +372,7 @@ int vsa_hs_compile_lit_multi(const char *const *expressions, const unsigned *fla
                 return fail(m, idx);
             }
         }
+        ext_count[id]++;
         Pattern p;
         p.id = id;
         p.som = f & VSA_HS_FLAG_SOM_LEFTMOST;
@@ -372,6 +403,8 @@ int vsa_hs_compile_lit_multi(const char *const *expressions, const unsigned *fla
         out->pats.push_back(std::move(p));
     }
     for (size_t k = 0; k < lits.size(); k++) lits[k].noruns = frag_noruns[k];
+    for (auto &p : out->pats)
+        if (p.som && ext.count(p.id) && ext_count[p.id] > 1) p.som_dedupe = true;
     out->n_ekeys = (uint32_t)ekeys.size();
     out->min_width = (uint32_t)min_len;
     vsa::BuildOptions opt;
