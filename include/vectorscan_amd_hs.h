@@ -19,6 +19,7 @@
 #define VECTORSCAN_AMD_HS_H
 
 #include <stddef.h>
+#include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -113,6 +114,21 @@ int vsa_hs_close_stream(vsa_hs_stream_t *id, vsa_hs_scratch_t *scratch,
                         vsa_hs_match_event_handler onEvent, void *ctxt);
 int vsa_hs_reset_stream(vsa_hs_stream_t *id, unsigned int flags, vsa_hs_scratch_t *scratch,
                         vsa_hs_match_event_handler onEvent, void *context);
+
+/* hsbench's corpus loop (tools/hsbench/main.cpp:487-511 block mode,
+ * :520-600 streaming / vectored) in ONE launch over device-resident blocks
+ * (d_data on the scratch's device).  Block database: each block is one
+ * hs_scan.  Stream / vectored database: blocks sharing a stream_ids value
+ * are, in array order, the writes of one stream and lie back to back in
+ * d_data.  counts[nblocks] (optional) gets each block's match count, *total
+ * their sum (matches as delivered to a callback: after long-literal checks,
+ * exhaustion and dedupe).  h_data = host copy of the same bytes, required
+ * only when some literal is longer than 8 bytes; `threads` host threads
+ * replay the records where one record is not exactly one match. */
+int vsa_hs_scan_corpus(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch,
+                       const uint8_t *d_data, const uint8_t *h_data, const uint64_t *offsets,
+                       const uint64_t *lens, const uint32_t *stream_ids, uint32_t nblocks,
+                       uint64_t *counts, uint64_t *total, unsigned threads);
 
 /* Introspection for tests: the database's HWLM blob (fragment id = HWLM
  * literal id) and the number of literal fragments. */

@@ -38,6 +38,7 @@
 #include <map>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "vectorscan_amd.h"
@@ -54,6 +55,7 @@ constexpr size_t HIST_MIN = 16;                 /* history handed to the GPU */
 constexpr size_t LIMIT_PATTERN_LENGTH = 16000;  /* grey.cpp:148 */
 constexpr unsigned LIMIT_PATTERN_COUNT = 8000000; /* grey.cpp:147 */
 constexpr uint32_t NO_EKEY = ~0u;
+constexpr int KEY_END_SHIFT = 24; /* vsa_match_t.key: end << 24 */
 
 std::atomic<uint64_t> g_serial{1};
 
@@ -82,6 +84,7 @@ struct vsa_hs_database {
     uint32_t min_width = 0;
     size_t max_len = 0;
     bool dedupe = false; /* some id belongs to more than one pattern */
+    bool simple = false; /* one report per HWLM record (see vsa_hs_scan_corpus) */
 };
 
 struct vsa_hs_scratch {
@@ -206,6 +209,11 @@ u64a on_fragment(size_t end, u32 frag, hs_scratch *sc) {
 }
 
 void on_piece(void *p, size_t i) { ((Run *)p)->cur = i; }
+
+int count_match(unsigned, unsigned long long, unsigned long long, unsigned, void *ctx) {
+    ++*(uint64_t *)ctx;
+    return 0;
+}
 
 /* keep the last max(16, longest literal - 1) bytes of the stream */
 void push_history(vsa_hs_stream *st, const uint8_t *const *bufs, const size_t *lens, size_t n) {
@@ -406,6 +414,9 @@ int vsa_hs_compile_lit_multi(const char *const *expressions, const unsigned *fla
     for (auto &p : out->pats)
         if (p.som && ext.count(p.id) && ext_count[p.id] > 1) p.som_dedupe = true;
     out->n_ekeys = (uint32_t)ekeys.size();
+    out->simple = !out->dedupe && out->n_ekeys == 0 && out->max_len <= SHORT_LIT &&
+                  std::all_of(out->frags.begin(), out->frags.end(),
+                              [](const std::vector<uint32_t> &f) { return f.size() == 1; });
     out->min_width = (uint32_t)min_len;
     vsa::BuildOptions opt;
     if (vsa::buildHwlm(lits, opt, &out->hwlm, &out->hwlm_size) != VSA_OK) {
@@ -540,6 +551,151 @@ int vsa_hs_scan_vector(const vsa_hs_database_t *db, const char *const *data,
     leave(scratch);
     if (rc != VSA_HS_SUCCESS) return rc;
     return n < count ? VSA_HS_INVALID : VSA_HS_SUCCESS;
+}
+
+/* The corpus loop of hsbench (tools/hsbench/main.cpp:487-511 block mode,
+ * :520-600 streaming / vectored) as ONE launch over device-resident blocks.
+ * Block database: every block is one hs_scan.  Stream / vectored database:
+ * the blocks of one stream_ids value, in array order, are the writes of one
+ * stream and must lie back to back in d_data (each block's history is what
+ * precedes it).  counts[b] (optional) = matches of block b after the report
+ * program; *total = their sum.  h_data = host copy of d_data's bytes (needed
+ * only for literals longer than 8 bytes).  A database where every HWLM
+ * record is exactly one report (distinct ids, literals <= 8 bytes, no
+ * SINGLEMATCH) takes *total from the GPU's record count without copying the
+ * records back; otherwise the records are replayed through the report
+ * program on `threads` host threads (streams are independent).  No match
+ * callbacks: this is the benchmark path. */
+int vsa_hs_scan_corpus(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch,
+                       const uint8_t *d_data, const uint8_t *h_data, const uint64_t *offsets,
+                       const uint64_t *lens, const uint32_t *stream_ids, uint32_t nblocks,
+                       uint64_t *counts, uint64_t *total, unsigned threads) {
+    if (!valid_db(db) || !offsets || !lens || !total || (nblocks && !d_data))
+        return VSA_HS_INVALID;
+    if (db->max_len > SHORT_LIT && !h_data) return VSA_HS_INVALID;
+    int rc = enter(db, scratch);
+    if (rc != VSA_HS_SUCCESS) return rc;
+    vsa_db_t *ddb = device_db(scratch, db);
+    const bool streams = db->mode != VSA_HS_MODE_BLOCK && stream_ids;
+    /* streams: block lists in array order; history lengths */
+    std::map<uint32_t, std::vector<uint32_t>> by_stream;
+    std::vector<uint64_t> hl(nblocks, 0);
+    std::vector<uint32_t> live; /* non-empty blocks */
+    for (uint32_t b = 0; b < nblocks; b++) {
+        if (streams) {
+            auto &v = by_stream[stream_ids[b]];
+            if (!v.empty()) {
+                const uint32_t p = v.back();
+                if (offsets[b] != offsets[p] + lens[p]) {
+                    leave(scratch);
+                    return VSA_HS_INVALID;
+                }
+                hl[b] = std::min<uint64_t>(16, hl[p] + lens[p]);
+            }
+            v.push_back(b);
+        }
+        if (lens[b]) live.push_back(b);
+    }
+    std::vector<uint64_t> lo(live.size()), ln(live.size()), lh(live.size());
+    for (size_t i = 0; i < live.size(); i++) {
+        lo[i] = offsets[live[i]];
+        ln[i] = lens[live[i]];
+        lh[i] = hl[live[i]];
+    }
+    if (counts) std::fill(counts, counts + nblocks, 0);
+    *total = 0;
+    const bool fast = db->simple && !counts;
+    std::vector<uint64_t> keys;
+    std::vector<uint32_t> ids;
+    uint64_t nm = 0;
+    if (!live.empty() &&
+        vsa::scan_records(scratch->ctx, ddb, d_data, lo.data(), ln.data(),
+                          streams ? lh.data() : nullptr, (uint32_t)live.size(),
+                          fast ? nullptr : &keys, fast ? nullptr : &ids, &nm) != VSA_OK) {
+        leave(scratch);
+        return VSA_HS_UNKNOWN_ERROR;
+    }
+    if (fast) {
+        *total = nm;
+        leave(scratch);
+        return VSA_HS_SUCCESS;
+    }
+    /* records -> blocks (ends are d_data offsets, sorted) */
+    std::vector<uint32_t> order(live);
+    std::sort(order.begin(), order.end(),
+              [&](uint32_t a, uint32_t b) { return offsets[a] < offsets[b]; });
+    std::vector<uint64_t> rb(nblocks, 0), re(nblocks, 0);
+    uint64_t k = 0;
+    for (uint32_t b : order) {
+        const uint64_t hi = offsets[b] + lens[b];
+        while (k < nm && (keys[k] >> KEY_END_SHIFT) < offsets[b]) k++;
+        rb[b] = k;
+        while (k < nm && (keys[k] >> KEY_END_SHIFT) < hi) {
+            keys[k] -= offsets[b] << KEY_END_SHIFT;
+            k++;
+        }
+        re[b] = k;
+    }
+    std::vector<std::vector<uint32_t>> units; /* streams (or single blocks) */
+    if (streams) {
+        for (auto &e : by_stream) units.push_back(std::move(e.second));
+    } else {
+        for (uint32_t b = 0; b < nblocks; b++) units.push_back({b});
+    }
+    const unsigned T = std::max(1u, std::min<unsigned>(threads ? threads : 1,
+                                                        (unsigned)units.size()));
+    std::vector<uint64_t> part(T, 0);
+    std::vector<int> status(T, VSA_HS_SUCCESS);
+    auto work = [&](unsigned t) {
+        for (size_t u = t; u < units.size(); u += T) {
+            const auto &bl = units[u];
+            vsa_hs_stream st;
+            init_stream(&st, db);
+            uint64_t cnt = 0;
+            std::vector<const uint8_t *> bufs(bl.size());
+            std::vector<size_t> bl_len(bl.size());
+            for (size_t j = 0; j < bl.size(); j++) {
+                bufs[j] = h_data ? h_data + offsets[bl[j]] : nullptr;
+                bl_len[j] = lens[bl[j]];
+            }
+            Run r{db, &st, count_match, &cnt, bufs.data(), bl_len.data(), {}, 0};
+            r.pos.resize(bl.size());
+            uint64_t o = 0;
+            for (size_t j = 0; j < bl.size(); j++) {
+                r.pos[j] = o;
+                o += bl_len[j];
+            }
+            for (size_t j = 0; j < bl.size(); j++) {
+                const uint32_t b = bl[j];
+                const uint64_t before = cnt;
+                r.cur = j;
+                if (re[b] > rb[b] &&
+                    vsa::replay_records(ddb, keys.data() + rb[b], ids.data() + rb[b],
+                                        re[b] - rb[b], on_fragment, &r) != HWLM_SUCCESS) {
+                    status[t] = VSA_HS_UNKNOWN_ERROR;
+                    return;
+                }
+                flush_som(r);
+                if (streams && h_data) push_history(&st, &bufs[j], &bl_len[j], 1);
+                st.offset += bl_len[j];
+                if (counts) counts[b] = cnt - before;
+            }
+            part[t] += cnt;
+        }
+    };
+    if (T == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> pool;
+        for (unsigned t = 0; t < T; t++) pool.emplace_back(work, t);
+        for (auto &th : pool) th.join();
+    }
+    leave(scratch);
+    for (unsigned t = 0; t < T; t++) {
+        if (status[t] != VSA_HS_SUCCESS) return status[t];
+        *total += part[t];
+    }
+    return VSA_HS_SUCCESS;
 }
 
 /* runtime.c:545-575 */

@@ -1669,6 +1669,37 @@ hwlm_error_t exec_pieces(vsa_ctx *c, const vsa_db *db, const u8 *hist, size_t hi
     }
     return HWLM_SUCCESS;
 }
+/* One launch over device-resident blocks (hlens NULL: block mode) and the
+ * sorted records copied to the host (want_records) or only counted. */
+int scan_records(vsa_ctx *c, const vsa_db *db, const u8 *d_data, const uint64_t *offsets,
+                 const uint64_t *lens, const uint64_t *hlens, uint32_t nblocks,
+                 std::vector<uint64_t> *keys, std::vector<uint32_t> *ids, uint64_t *n_out) {
+    std::vector<uint64_t> st(nblocks, 0);
+    uint64_t nm = 0;
+    int r = scan_blocks_impl(c, db, d_data, offsets, lens, st.data(), nblocks, 0, &nm, hlens);
+    if (r != VSA_OK) return r;
+    *n_out = nm;
+    if (!keys) return VSA_OK;
+    keys->resize(nm);
+    ids->resize(nm);
+    if (nm) {
+        VSA_CHECK(hipMemcpyAsync(keys->data(), c->ws.d_keys[c->cur], nm * 8,
+                                 hipMemcpyDeviceToHost, c->stream));
+        VSA_CHECK(hipMemcpyAsync(ids->data(), c->ws.d_ids[c->cur], nm * 4,
+                                 hipMemcpyDeviceToHost, c->stream));
+        VSA_CHECK(hipStreamSynchronize(c->stream));
+    }
+    return VSA_OK;
+}
+
+/* The records of one call (ends relative to that call's buffer) through
+ * the callback, without flood emulation (no host buffer address) */
+int replay_records(const vsa_db *db, const uint64_t *keys, const uint32_t *ids, uint64_t n,
+                   LitCallback cb, void *cbctx) {
+    hs_scratch *sc = (hs_scratch *)cbctx;
+    if (db->type == HWLM_ENGINE_NOOD) return replay_nood(keys, ids, n, cb, sc);
+    return replay_lit(db, keys, n, cb, sc, HWLM_ALL_GROUPS, nullptr, false);
+}
 } // namespace vsa
 
 extern "C" {

@@ -74,6 +74,15 @@ int exec_pieces(vsa_ctx *c, const vsa_db *db, const u8 *hist, size_t hist_len,
                 const u8 *const *bufs, const size_t *lens, size_t n, LitCallback cb,
                 void *cbctx, void (*on_piece)(void *, size_t));
 
+/* runtime.hip: one launch over device blocks (hlens NULL = block mode);
+ * the sorted records to the host when keys != NULL, else only counted */
+int scan_records(vsa_ctx *c, const vsa_db *db, const u8 *d_data, const uint64_t *offsets,
+                 const uint64_t *lens, const uint64_t *hlens, uint32_t nblocks,
+                 std::vector<uint64_t> *keys, std::vector<uint32_t> *ids, uint64_t *n);
+/* one call's records (ends relative to its buffer) through cb, no floods */
+int replay_records(const vsa_db *db, const uint64_t *keys, const uint32_t *ids, uint64_t n,
+                   LitCallback cb, void *cbctx);
+
 Literal makeLiteral(const u8 *s, size_t len, bool nocase, bool noruns, u32 id,
                     u64a groups, const u8 *msk, const u8 *cmp, size_t mlen);
 int buildHwlm(std::vector<Literal> lits, const BuildOptions &opt, u8 **out,

@@ -239,3 +239,29 @@ class Stream:
         if rc == SUCCESS:
             self.handle = None
         return rc
+
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_sig("vsa_hs_scan_corpus", ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32,
+     _vp, _u64p, ctypes.c_uint)
+
+
+def scan_corpus(db, scratch, d_data, offsets, lens, stream_ids=None, h_data=None,
+                counts=False, threads=16):
+    """vsa_hs_scan_corpus: hsbench's corpus loop as one launch over
+    device-resident blocks.  Returns (rc, total, per-block counts or None)."""
+    offs = np.ascontiguousarray(offsets, np.uint64)
+    ln = np.ascontiguousarray(lens, np.uint64)
+    n = len(offs)
+    sid = np.ascontiguousarray(stream_ids, np.uint32) if stream_ids is not None else None
+    cnt = np.zeros(n, np.uint64) if counts else None
+    hk = None
+    hp = None
+    if h_data is not None:
+        hk, hp, _ = _as_buf(h_data)
+    total = ctypes.c_uint64()
+    rc = lib.vsa_hs_scan_corpus(db.handle, scratch.handle, d_data, hp, offs.ctypes.data,
+                                ln.ctypes.data, sid.ctypes.data if sid is not None else None,
+                                n, cnt.ctypes.data if cnt is not None else None,
+                                ctypes.byref(total), threads)
+    return rc, total.value, cnt
