@@ -1,0 +1,33 @@
+"""Per-block overhead of the batch scan: 1 GiB cut into blocks of 2 KiB ..
+1 MiB, wall time of vsa_scan_blocks vs its kernel time (cfg-4 FDR set)."""
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, ".")
+import bench  # noqa: E402
+import vectorscan_amd as vsa  # noqa: E402
+
+lits = bench.make_literals(5000, seed=12)
+blob = vsa.hwlm_build(lits)
+ctx = vsa.Context(0)
+db = vsa.Database(ctx, blob)
+total = 1 << 30
+data = bench.make_corpus(total, lits, seed=5, plant_every=64 << 10)
+d = ctx.malloc(total)
+ctx.h2d(d, data)
+for chunk in [2 << 10, 4 << 10, 16 << 10, 64 << 10, 1 << 20, 256 << 20]:
+    n = total // chunk
+    offs = np.arange(n, dtype=np.uint64) * chunk
+    lens = np.full(n, chunk, np.uint64)
+    for _ in range(3):
+        ctx.scan_blocks(db, d, offs, lens)
+    walls, ks = [], []
+    for _ in range(10):
+        t0 = time.perf_counter()
+        m = ctx.scan_blocks(db, d, offs, lens)
+        walls.append(time.perf_counter() - t0)
+        ks.append(ctx.kernel_ms())
+    print("chunk %8d blocks %7d matches %6d wall %.3f ms kernel %.3f ms" %
+          (chunk, n, m, min(walls) * 1e3, min(ks)), flush=True)

@@ -114,6 +114,10 @@ struct vsa_ctx {
     /* kernel-only timing of the last scan (hipEvents on the scan stream) */
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_kernel_ms = 0.0;
+    /* host bytes already in ws.d_in (set only inside one drop-in call, so the
+     * accel pre-skip and the literal scan share one upload) */
+    const uint8_t *res_host = nullptr;
+    size_t res_len = 0;
 };
 
 struct vsa_db {
@@ -774,11 +778,13 @@ int scan_host(vsa_db *db, const uint8_t *buf, size_t len, size_t start,
     vsa_ctx *c = db->ctx;
     int r;
     const size_t pre = hend ? 16 : 0;
+    const bool resident = !pre && c->res_host == buf && c->res_len == len;
+    if (!resident) c->res_host = nullptr;
     if ((r = ensure_in(c, pre + len + 16)) != VSA_OK) return r;
     if (pre) {
         VSA_CHECK(hipMemcpyAsync(c->ws.d_in, hend - 16, 16, hipMemcpyHostToDevice, c->stream));
     }
-    if (len) {
+    if (len && !resident) {
         VSA_CHECK(hipMemcpyAsync(c->ws.d_in + pre, buf, len, hipMemcpyHostToDevice, c->stream));
     }
     uint64_t off = 0, l = len, st = start, n = 0, hl = hlen;
@@ -802,12 +808,18 @@ int class_host(const uint8_t cls[32], const uint8_t *cls2, const uint8_t *buf, s
                uint64_t *first, uint64_t *last) {
     vsa_ctx *c = default_ctx();
     if (!c) return VSA_E_DEVICE;
+    uint64_t cnt;
+    if (c->res_host && buf >= c->res_host && buf + len <= c->res_host + c->res_len) {
+        /* inside the buffer this drop-in call already uploaded */
+        return vsa_class_scan(c, cls, cls2, c->ws.d_in + (buf - c->res_host), len, nullptr,
+                              first, last, &cnt, 0);
+    }
+    c->res_host = nullptr;
     int r;
     if ((r = ensure_in(c, len + 16)) != VSA_OK) return r;
     if (len) {
         VSA_CHECK(hipMemcpyAsync(c->ws.d_in, buf, len, hipMemcpyHostToDevice, c->stream));
     }
-    uint64_t cnt;
     return vsa_class_scan(c, cls, cls2, c->ws.d_in, len, nullptr, first, last, &cnt, 0);
 }
 
@@ -1497,13 +1509,27 @@ hwlm_error_t hwlmExec(const struct HWLM *tab, const uint8_t *buf, size_t len, si
         if (scan_host(db, buf, len, start, keys, ids) != VSA_OK) return HWLM_ERROR_UNKNOWN;
         return replay_nood(keys.data(), ids.data(), keys.size(), cb, scratch);
     }
-    /* accel pre-skip (hwlm.c:85-105, 191-201) on the GPU */
+    /* accel pre-skip (hwlm.c:85-105, 191-201) on the GPU, on the same
+     * upload as the literal scan */
     const HWLM *h = (const HWLM *)db->hblob;
     const union AccelAux *aa = &h->accel0;
     if ((groups & ~h->accel1_groups) == 0) aa = &h->accel1;
-    start = hwlm_accel_block(aa, buf, len, start);
-    if (start >= len) return HWLM_SUCCESS;
-    if (scan_host(db, buf, len, start, keys, ids) != VSA_OK) return HWLM_ERROR_UNKNOWN;
+    if (aa->accel_type != ACCEL_NONE && len - start >= 16) {
+        vsa_ctx *c = db->ctx;
+        if (ensure_in(c, len + 16) != VSA_OK ||
+            hipMemcpyAsync(c->ws.d_in, buf, len, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+            return HWLM_ERROR_UNKNOWN;
+        c->res_host = buf;
+        c->res_len = len;
+        start = hwlm_accel_block(aa, buf, len, start);
+    }
+    if (start >= len) {
+        db->ctx->res_host = nullptr;
+        return HWLM_SUCCESS;
+    }
+    const int sr = scan_host(db, buf, len, start, keys, ids);
+    db->ctx->res_host = nullptr;
+    if (sr != VSA_OK) return HWLM_ERROR_UNKNOWN;
     std::vector<vsa::FloodEvent> ev;
     return replay_lit(db, keys.data(), keys.size(), cb, scratch, groups,
                       floods_for(db, buf, len, start, ev));
