@@ -810,9 +810,17 @@ int class_host(const uint8_t cls[32], const uint8_t *cls2, const uint8_t *buf, s
     if (!c) return VSA_E_DEVICE;
     uint64_t cnt;
     if (c->res_host && buf >= c->res_host && buf + len <= c->res_host + c->res_len) {
-        /* inside the buffer this drop-in call already uploaded */
-        return vsa_class_scan(c, cls, cls2, c->ws.d_in + (buf - c->res_host), len, nullptr,
-                              first, last, &cnt, 0);
+        /* inside the buffer this drop-in call already uploaded (hwlmExec
+         * reserved twice its size): scan it in place when 16-B aligned,
+         * else from an aligned device-side copy behind it */
+        const uint8_t *d = c->ws.d_in + (buf - c->res_host);
+        if ((uintptr_t)d & 15) {
+            uint8_t *cp = c->ws.d_in + ((c->res_len + 16 + 15) & ~(size_t)15);
+            if (cp + len > c->ws.d_in + c->ws.in_cap) return VSA_E_INVALID;
+            VSA_CHECK(hipMemcpyAsync(cp, d, len, hipMemcpyDeviceToDevice, c->stream));
+            d = cp;
+        }
+        return vsa_class_scan(c, cls, cls2, d, len, nullptr, first, last, &cnt, 0);
     }
     c->res_host = nullptr;
     int r;
@@ -1516,7 +1524,7 @@ hwlm_error_t hwlmExec(const struct HWLM *tab, const uint8_t *buf, size_t len, si
     if ((groups & ~h->accel1_groups) == 0) aa = &h->accel1;
     if (aa->accel_type != ACCEL_NONE && len - start >= 16) {
         vsa_ctx *c = db->ctx;
-        if (ensure_in(c, len + 16) != VSA_OK ||
+        if (ensure_in(c, 2 * len + 48) != VSA_OK ||
             hipMemcpyAsync(c->ws.d_in, buf, len, hipMemcpyHostToDevice, c->stream) != hipSuccess)
             return HWLM_ERROR_UNKNOWN;
         c->res_host = buf;
