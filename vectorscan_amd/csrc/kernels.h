@@ -89,6 +89,8 @@ struct VsaLitParams {
     uint64_t pf_mult;            /* FDRConfirm.mult shared by the prefiltered
                                     buckets (fdr_confirm_compile.cpp) */
     uint32_t qcap;               /* per-wave LDS confirm-queue entries */
+    uint32_t nconf;              /* confirm waves per workgroup (1..4); the
+                                    other LIT_WAVES - nconf waves scan */
     uint32_t dbg;                /* debug: bit0 verify queued keys against HBM
                                     (mismatches -> counters[3]); bit1 drop all
                                     candidates (filter-only timing); bit3 stop

@@ -231,7 +231,6 @@ struct QEnt {
 #define ENT_BLK_SHIFT 40
 #define ENT_LAP_SHIFT 60
 #define ENT_P0_MASK ((1ULL << ENT_BLK_SHIFT) - 1)
-#define RING_SLOTS 4 /* slots of each ring read per gather */
 struct LitShared {
     const void *tab;
     u32 tab_lds;     /* LDS byte address of tab (LDS tables) */
@@ -261,7 +260,7 @@ __device__ __forceinline__ u32 conf_hash(u64 key, u64 andmsk, u64 mult, u32 nbit
  * v whose start lies inside the block.  The candidates' global loads
  * (litIndex slot, block record, each chain step) are independent, so they
  * are issued together: one memory latency per chain step for all of them. */
-#define CONF_U 4
+template <int CONF_U>
 __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfLds &cl,
                                               const QEnt (&q)[CONF_U], const bool (&valid)[CONF_U],
                                               u32 mis) {
@@ -796,44 +795,62 @@ __device__ __forceinline__ uint4 load_wave_kib(const u8 *base, u32 off) {
 
 #define LIT_DEPTH 4
 
-/* The workgroup's confirm wave: gathers up to 64 chunk entries per round
- * from the scanning waves' rings (each consumed in order), expands their
- * candidate bits one per lane per round, drops the candidates whose litIndex
- * slot is empty (LDS slot bitmap: litIndex[hash] == 0 means no LitInfo
- * chain, fdr_confirm_runtime.h:55-58), queues the rest in its private LDS
- * queue and runs the exact confirm 64 at a time.  Its global-memory latency
+/* A workgroup's confirm wave (one, or several for large literal sets, each
+ * serving every nc-th ring): gathers up to 64 chunk entries per round from
+ * its rings (each consumed in order), expands their candidate bits one per
+ * lane per round, drops the candidates whose litIndex slot is empty (LDS
+ * slot bitmap: litIndex[hash] == 0 means no LitInfo chain,
+ * fdr_confirm_runtime.h:55-58), queues the rest in its private LDS queue and
+ * runs the exact confirm CONF_U x 64 at a time.  Its global-memory latency
  * never stalls a scanning wave.  Exits once every scanning wave has finished
  * (q_done, read before the heads), every ring is empty and the queue is
- * drained. */
-#define LIT_SCANNERS (LIT_WAVES - 1)
-#define EXP_U 1     /* candidate bits per lane per expansion round (4 measured
-                       slower: the expansion is VALU-bound, not latency-bound) */
-#define PQ_CAP 512  /* >= CONF_U * 64 + EXP_U * 64 - 1 */
-template <int MODE>
+ * drained.  (A two-step expansion -- all bits written as keys to a
+ * pre-filter queue by their lanes, then filtered 64 at a time with every
+ * lane busy -- measured slower: 10.4 vs 9.4 ms at 20k literals.) */
+#define MAX_CONF_WAVES 4
+#define EXP_U 1 /* candidate bits per lane per expansion round (2 and 4 measured
+                   slower at 5k and at 20k literals) */
+/* confirm queue entries of a confirm wave confirming CU per lane per batch:
+ * >= CU * 64 + EXP_U * 64 - 1 (a round adds <= EXP_U * 64), a power of two */
+#define PQ_ENTRIES(CU) ((CU) == 4 ? 512 : 256)
+template <int MODE, int CONF_U>
 __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLds &cl,
                                              const uint4 *rings, u32 lg, u32 *tails,
                                              const u32 *heads, const u32 *q_done, u32 mis,
-                                             const u32 *slots, QEnt *pq) {
+                                             const u32 *slots, QEnt *pq, u32 cw, u32 nc,
+                                             u64 *pcl) {
     typedef LitTraits<MODE> T;
     constexpr int EW = T::EW;
     constexpr int CW = T::CW;
+    constexpr u32 PQ_CAP = PQ_ENTRIES(CONF_U);
+    static_assert(PQ_CAP >= CONF_U * 64 + EXP_U * 64 - 1, "confirm queue too small");
     const u32 lane = lane_id();
     const u32 cap = 1u << lg;
-    /* lane 4 r + k reads slot tail_r + k of ring r (r < LIT_SCANNERS) */
-    const u32 rr = lane >> 2, rk = lane & 3;
-    const bool ring_lane = rr < LIT_SCANNERS;
+    /* confirm wave cw of nc serves rings cw, cw + nc, ... (nr of them): lane
+     * sl * i + k reads slot tail + k of ring rr = cw + nc i, sl = the slots
+     * per ring one gather reads (64 / nr lanes, at most the ring size) */
+    const u32 nscan = LIT_WAVES - nc;
+    const u32 nr = (nscan - cw + nc - 1) / nc;
+    const u32 sl0 = nr <= 4 ? 16u : nr <= 8 ? 8u : 4u;
+    const u32 sl = sl0 < cap ? sl0 : cap;
+    const u32 ri = lane / sl;
+    const u32 rr = cw + nc * ri, rk = lane - ri * sl;
+    const bool ring_lane = ri < nr;
     u32 tail = 0; /* ring rr's consumed position (same in its 4 lanes) */
     u32 filled = 0;
     u32 consumed = 0;
-    u32 pq_head = 0, pq_tail = 0; /* private queue cursors (wave-uniform) */
-    /* VSA_DEBUG_FLAGS bit 6: cycles per phase + counts -> counters[4..11] */
+    u32 pq_head = 0, pq_tail = 0; /* confirm queue cursors (wave-uniform) */
+    /* VSA_DEBUG_FLAGS bit 6: cycles per phase + counts -> counters[4..11],
+     * kept in LDS (pcl, this wave's 8 slots) so they hold no registers */
     const bool prof = (P.dbg & 64) != 0;
-    u64 pc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     u64 tmark = prof ? __builtin_amdgcn_s_memtime() : 0;
+    auto pcount = [&](int i, u64 v) {
+        if (prof && lane == 0) pcl[i] += v;
+    };
     auto phase = [&](int i) {
         if (prof) {
             const u64 now = __builtin_amdgcn_s_memtime();
-            pc[i] += now - tmark;
+            pcount(i, now - tmark);
             tmark = now;
         }
     };
@@ -849,17 +866,17 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
             valid[i] = j < k;
             q[i] = valid[i] ? pq[(pq_tail + j) & (PQ_CAP - 1)] : QEnt{0, 0};
         }
-        confirm_multi(P, cl, q, valid, mis); /* every lane: wave-uniform inside */
+        confirm_multi<CONF_U>(P, cl, q, valid, mis); /* every lane: wave-uniform inside */
         asm volatile("" ::: "memory");
         pq_tail += k;
         consumed += k;
-        pc[7]++;
+        pcount(7, 1);
         phase(2);
     };
     for (;;) {
-        const bool all_done = lds_ld32(q_done) == LIT_SCANNERS;
+        const bool all_done = lds_ld32(q_done) == nscan;
         asm volatile("" ::: "memory");
-        /* poll: the 15 heads in one broadcast read */
+        /* poll: the served rings' heads in one read */
         const u32 avail = ring_lane ? lds_ld32(&heads[rr]) - tail : 0u;
         const bool valid = rk < avail;
         u32 e[4 * EW];
@@ -867,7 +884,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
         for (int i = 0; i < 4 * EW; i++) e[i] = 0;
         filled = (u32)__popcll(__ballot(valid));
         if (filled) {
-            /* gather the available slots (up to RING_SLOTS per ring) */
+            /* gather the available slots (up to sl per ring) */
             if (valid) {
                 const uint4 *q = rings + ((size_t)rr * cap + ((tail + rk) & (cap - 1))) * EW;
 #pragma unroll
@@ -880,12 +897,12 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                 }
             }
             asm volatile("" ::: "memory"); /* entries read before they are freed */
-            const u32 run = avail < RING_SLOTS ? avail : RING_SLOTS;
+            const u32 run = avail < sl ? avail : sl;
             tail += run;
             if (rk == 0 && ring_lane && run) lds_st32(&tails[rr], tail);
         }
-        pc[4]++;
-        pc[5] += filled;
+        pcount(4, 1);
+        pcount(5, filled);
         phase(0);
         if (filled == 0) {
             if (pq_head != pq_tail) {
@@ -968,7 +985,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                     }
                 }
                 if (!__any(have[0])) break;
-                pc[6]++;
+                pcount(6, 1);
                 u64 key[EXP_U];
                 PfRec pf[EXP_U];
 #pragma unroll
@@ -1025,7 +1042,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
         atomicAdd(&P.counters[2], (unsigned long long)consumed);
     if (prof && lane == 0) {
         phase(1);
-        for (int i = 0; i < 8; i++) atomicAdd(&P.counters[4 + i], (unsigned long long)pc[i]);
+        for (int i = 0; i < 8; i++) atomicAdd(&P.counters[4 + i], (unsigned long long)pcl[i]);
     }
 }
 
@@ -1037,7 +1054,7 @@ vsa_lit_scan(VsaLitParams P) {
     extern __shared__ __align__(16) u8 smem[];
     __shared__ ConfLds cl;
     __shared__ u32 q_tails[16], q_heads[16], q_done;
-    __shared__ QEnt pq[PQ_CAP]; /* the confirm wave's private queue */
+    __shared__ u64 prof_lds[8 * MAX_CONF_WAVES]; /* confirm-wave profile (dbg & 64) */
     const u32 tid = threadIdx.x;
     const u32 lane = lane_id();
     /* provably wave-uniform: the confirm wave's s_setprio is a scalar
@@ -1069,9 +1086,13 @@ vsa_lit_scan(VsaLitParams P) {
         for (u32 i = tid; i < 256 * 32; i += LIT_THREADS) dst[i] = P.table[i >> 5];
         tab = tb;
     }
-    /* LIT_SCANNERS rings of qcap entries each, then the slot bitmaps */
+    /* one ring of qcap entries per scanning wave, the slot bitmaps, then the
+     * confirm waves' private queues (one of 512 entries, or nconf of 256) */
+    const u32 NC = P.nconf;
+    const u32 NS = LIT_WAVES - NC;
     uint4 *rings = (uint4 *)(smem + ((tab_bytes + 15) & ~15u));
-    u32 *slots = (u32 *)(rings + (size_t)LIT_SCANNERS * P.qcap * T::EW);
+    u32 *slots = (u32 *)(rings + (size_t)NS * P.qcap * T::EW);
+    QEnt *pqx = (QEnt *)(slots + ((P.slot_words + 3) & ~3u));
     for (u32 i = tid; i < P.slot_words; i += LIT_THREADS) slots[i] = P.slotmap[i];
     if (tid < 16) {
         const u32 off = P.conf_off[tid];
@@ -1100,14 +1121,20 @@ vsa_lit_scan(VsaLitParams P) {
         q_heads[tid] = 0;
     }
     if (tid == 0) q_done = 0;
+    if (tid < 8 * MAX_CONF_WAVES) prof_lds[tid] = 0;
     __syncthreads();
 
     const u32 mis = (u32)((uintptr_t)P.data & 15);
-    if (wave == LIT_WAVES - 1) {
-
+    if (wave >= NS) {
+        const u32 cw = wave - NS;
 #ifndef VSA_EXP_NO_CONFIRM /* experiment: VGPR use of the scanning path alone */
-        confirm_wave<MODE>(P, cl, rings, 31 - __clz(P.qcap), q_tails, q_heads, &q_done, mis,
-                           slots, pq);
+        if (NC == 1)
+            confirm_wave<MODE, 4>(P, cl, rings, 31 - __clz(P.qcap), q_tails, q_heads, &q_done,
+                                  mis, slots, pqx, 0, 1, prof_lds);
+        else
+            confirm_wave<MODE, 2>(P, cl, rings, 31 - __clz(P.qcap), q_tails, q_heads, &q_done,
+                                  mis, slots, pqx + (size_t)cw * PQ_ENTRIES(2), cw, NC,
+                                  prof_lds + 8 * cw);
 #endif
         return;
     }
@@ -1151,7 +1178,7 @@ vsa_lit_scan(VsaLitParams P) {
      * grid (a single-address ticket capped streaming at ~4.4 TB/s,
      * tools/probe_stream.hip).  P.dynamic == 0: plain static assignment
      * (wave g takes g, g + G, ...). */
-    const u64 G = (u64)gridDim.x * LIT_SCANNERS;
+    const u64 G = (u64)gridDim.x * NS;
     const u32 nreg = P.dynamic ? P.nregions : 1u;
     u32 reg_i = 0; /* regions tried so far */
     u32 reg = blockIdx.x % nreg;
@@ -1175,7 +1202,7 @@ vsa_lit_scan(VsaLitParams P) {
             t = ((u64)readlane_u32((u32)(t1 >> 32), 0) << 32) | readlane_u32((u32)t1, 0);
         }
     };
-    u64 seg = P.dynamic ? resolve(take()) : (u64)blockIdx.x * LIT_SCANNERS + wave;
+    u64 seg = P.dynamic ? resolve(take()) : (u64)blockIdx.x * NS + wave;
     while (seg < P.nsegs) {
         unsigned long long t_next = 0;
         bool have_next = false;

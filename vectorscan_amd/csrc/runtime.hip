@@ -56,8 +56,8 @@ namespace {
 
 const int LIT_WAVES = 16;
 const int LIT_THREADS = 1024;
-const size_t LDS_BUDGET = 160 * 1024 - 12288; /* minus static LDS (confirm params,
-                                                 ring cursors, 8 KiB confirm queue) */
+const size_t LDS_BUDGET = 160 * 1024 - 4096; /* minus static LDS (confirm params,
+                                                ring cursors) */
 const uint32_t SLOT_WORDS_MAX = 3072;        /* 12 KiB of slot bitmaps (coarsened
                                                 beyond, see vsa_db_load) */
 
@@ -110,6 +110,7 @@ struct vsa_ctx {
         uint32_t seg_bytes = 0;
         int end_bits = 0;
         uint32_t flags = 0;
+        uint64_t bytes = 0; /* scanned bytes (len - start summed) */
     } launch;
     /* kernel-only timing of the last scan (hipEvents on the scan stream) */
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -142,7 +143,21 @@ struct vsa_db {
     uint8_t slot_bits[16] = {0}; /* prefilter hash bits per bucket (<= nBits) */
     uint64_t pf_mult = 0;
     bool flood_live = false;     /* some FDRFlood record can fire (idCount < max) */
+    /* confirm waves per workgroup for the next launch, adapted to the
+     * confirm-candidate rate the previous launches measured */
+    mutable uint32_t nconf = 1;
 };
+
+/* confirm waves for a measured confirm-candidate rate (candidates per
+ * scanned byte): one confirm wave keeps up with ~1e-4 (cfg 4); past that it
+ * becomes the bound and more waves (fewer scanners) pay off */
+static uint32_t nconf_for_rate(double rate) {
+    /* measured (4 GiB, FDR): 5k literals (5e-5) best at 1; 10k (2.5e-4)
+     * equal; 20k (5.7e-3) 9.4 -> 5.2 ms at 2; 50k (0.26) 124 -> 68 ms at 2.
+     * 3-4 waves leave too little LDS for rings of useful size beside a
+     * domain-14 table */
+    return rate > 1e-3 ? 2u : 1u;
+}
 
 /* VECTORSIZE of the reference build emulated where results depend on it:
  * shuftiDoubleExec's per-block lanes and the Teddy loop shape of the flood
@@ -269,14 +284,27 @@ int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds) {
  * noodle; a push of up to 64 lanes is split into ring-sized batches) + slot
  * bitmaps */
 size_t plan_lds(size_t tab, uint32_t slot_words, size_t ent, uint32_t *qcap,
-                size_t budget = LDS_BUDGET) {
-    const size_t waves = LIT_WAVES - 1;
+                size_t budget = LDS_BUDGET, uint32_t nconf = 1) {
+    const size_t waves = LIT_WAVES - nconf;
+    /* the confirm waves' private queues (kernels.hip PQ_ENTRIES x 16 B) */
+    const size_t extra = nconf == 1 ? 512 * 16 : (size_t)nconf * 256 * 16;
+    const size_t slots = ((size_t)slot_words * 4 + 15) & ~(size_t)15;
     tab = (tab + 15) & ~(size_t)15;
-    size_t rest = budget > tab + slot_words * 4 ? budget - tab - slot_words * 4 : 0;
+    size_t rest = budget > tab + slots + extra ? budget - tab - slots - extra : 0;
     uint32_t q = 4;
     while (q < 64 && waves * (size_t)(2 * q) * ent <= rest) q *= 2;
     *qcap = q;
-    return tab + waves * (size_t)q * ent + (size_t)slot_words * 4;
+    return tab + waves * (size_t)q * ent + slots + extra;
+}
+
+/* the confirm-wave count of a launch: the db's adapted value (or
+ * VSA_NCONF), lowered until the LDS plan fits */
+uint32_t launch_nconf(const vsa_db *db, size_t tab, size_t ent, size_t budget) {
+    uint32_t nc = db->nconf;
+    if (const char *e = getenv("VSA_NCONF")) nc = (uint32_t)std::min(4, std::max(1, atoi(e)));
+    uint32_t q;
+    while (nc > 1 && plan_lds(tab, db->slot_words, ent, &q, budget, nc) > budget) nc--;
+    return nc;
 }
 
 int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
@@ -321,6 +349,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
             P.dbg = e ? (uint32_t)atoi(e) : 0u;
         }
         for (int b = 0; b < 16; b++) P.slot_off[b] = 0xffffffffu;
+        P.nconf = 1;
         size_t lds = plan_lds(0, 0, 32, &P.qcap);
         return launch_lit<VSA_MODE_NOOD, false>(c, P, lds);
     }
@@ -363,10 +392,12 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     if (db->mode == VSA_MODE_FDR) {
         size_t tb = (size_t)db->table_entries * 8;
         if (tb <= 128 * 1024) {
-            size_t lds = plan_lds(tb, db->slot_words, 48, &P.qcap);
+            P.nconf = launch_nconf(db, tb, 48, LDS_BUDGET);
+            size_t lds = plan_lds(tb, db->slot_words, 48, &P.qcap, LDS_BUDGET, P.nconf);
             if (lds <= LDS_BUDGET) return launch_lit<VSA_MODE_FDR, true>(c, P, lds);
         }
-        size_t lds = plan_lds(0, db->slot_words, 48, &P.qcap);
+        P.nconf = launch_nconf(db, 0, 48, LDS_BUDGET);
+        size_t lds = plan_lds(0, db->slot_words, 48, &P.qcap, LDS_BUDGET, P.nconf);
         return launch_lit<VSA_MODE_FDR, false>(c, P, lds);
     }
     /* Teddy / Fat Teddy: the 64 KiB table sits at LDS 0x10000 (kernels.hip
@@ -374,10 +405,12 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     const size_t below = 0x10000 - (160 * 1024 - LDS_BUDGET);
     const size_t teddy_dyn = 128 * 1024;
     if (db->mode == VSA_MODE_TEDDY) {
-        if (plan_lds(0, db->slot_words, 48, &P.qcap, below) > below) return VSA_E_INVALID;
+        P.nconf = launch_nconf(db, 0, 48, below);
+        if (plan_lds(0, db->slot_words, 48, &P.qcap, below, P.nconf) > below) return VSA_E_INVALID;
         return launch_lit<VSA_MODE_TEDDY, true>(c, P, teddy_dyn);
     }
-    if (plan_lds(0, db->slot_words, 64, &P.qcap, below) > below) return VSA_E_INVALID;
+    P.nconf = launch_nconf(db, 0, 64, below);
+    if (plan_lds(0, db->slot_words, 64, &P.qcap, below, P.nconf) > below) return VSA_E_INVALID;
     size_t lds = teddy_dyn;
     return launch_lit<VSA_MODE_FAT, true>(c, P, lds);
 }
@@ -389,6 +422,10 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     VSA_CHECK(hipStreamSynchronize(c->stream));
     uint64_t n = w.h_counters[0];
     c->last_cand = w.h_counters[2];
+    /* adapt the db's confirm-wave count to the measured candidate rate
+     * (over a representative launch; not under diagnostic flags) */
+    if (c->launch.db && c->launch.bytes >= (16u << 20) && !getenv("VSA_DEBUG_FLAGS"))
+        c->launch.db->nconf = nconf_for_rate((double)c->last_cand / (double)c->launch.bytes);
     if (getenv("VSA_DEBUG_FLAGS") && w.h_counters[3]) {
         fprintf(stderr, "vsa: %llu queued confirm keys differ from HBM\n",
                 (unsigned long long)w.h_counters[3]);
@@ -441,7 +478,7 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         const int64_t org = (blo + std::max<int64_t>(0, st - 16)) & ~(int64_t)1023;
         if (st < len) spans.push_back(blo + len - org);
     }
-    const uint64_t waves = (uint64_t)c->num_cus * (LIT_WAVES - 1);
+    const uint64_t waves = (uint64_t)c->num_cus * (LIT_WAVES - db->nconf);
     uint64_t seg_bytes = spans.empty() ? (64u << 10) : pick_seg_bytes(spans, waves);
     if (const char *e = getenv("VSA_SEG_KB")) seg_bytes = (uint64_t)std::max(1, atoi(e)) << 10;
     uint64_t segs = 0;
@@ -494,6 +531,14 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
     c->launch.segs = segs;
     c->launch.seg_bytes = (uint32_t)seg_bytes;
     c->launch.end_bits = end_bits;
+    {
+        uint64_t by = 0;
+        for (uint32_t i = 0; i < nb; i++) {
+            const uint64_t st = starts ? starts[i] : 0;
+            if (st < lens[i]) by += lens[i] - st;
+        }
+        c->launch.bytes = by;
+    }
     c->launch.flags = flags;
     if ((r = launch_scan(c, db, d_data, nb, segs, (uint32_t)seg_bytes)) != VSA_OK) return r;
     if (flags & VSA_SCAN_ASYNC) {
