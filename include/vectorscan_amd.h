@@ -190,6 +190,19 @@ int vsa_scan_blocks_stream(vsa_ctx_t *ctx, const vsa_db_t *db, const uint8_t *d_
                            const uint64_t *offsets, const uint64_t *lens,
                            const uint64_t *starts, const uint64_t *hlens, uint32_t nblocks,
                            uint32_t flags, uint64_t *n_matches);
+/* A batch's block table and segment map built and uploaded once for
+ * repeated scans of the same device blocks (e.g. hsbench's repeats): the
+ * arguments of vsa_scan_blocks_ex / _stream (starts, hlens, report_lo may
+ * be NULL).  At most 2^20 blocks per batch.  A plan belongs to its context
+ * and must outlive the scans that use it. */
+typedef struct vsa_plan vsa_plan_t;
+int vsa_plan_create(vsa_ctx_t *ctx, const uint8_t *d_data, const uint64_t *offsets,
+                    const uint64_t *lens, const uint64_t *starts, const uint64_t *hlens,
+                    const uint64_t *report_lo, uint32_t nblocks, vsa_plan_t **plan);
+int vsa_plan_free(vsa_plan_t *plan);
+/* vsa_scan_blocks over a plan (same flags, results and waiting) */
+int vsa_scan_plan(vsa_ctx_t *ctx, const vsa_db_t *db, const vsa_plan_t *plan, uint32_t flags,
+                  uint64_t *n_matches);
 int vsa_scan_wait(vsa_ctx_t *ctx, uint64_t *n_matches);
 /* Device pointers to the last scan's sorted keys (u64) and ids (u32). */
 int vsa_scan_results(vsa_ctx_t *ctx, const uint64_t **d_keys,

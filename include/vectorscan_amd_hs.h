@@ -130,6 +130,20 @@ int vsa_hs_scan_corpus(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch,
                        const uint64_t *lens, const uint32_t *stream_ids, uint32_t nblocks,
                        uint64_t *counts, uint64_t *total, unsigned threads);
 
+/* The same corpus prepared once (launch plan on the device, stream
+ * grouping on the host) and scanned many times, as hsbench's repeats do.
+ * The scratch must stay allocated (and not be used concurrently) for the
+ * corpus's life. */
+typedef struct vsa_hs_corpus vsa_hs_corpus_t;
+int vsa_hs_corpus_prepare(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch,
+                          const uint8_t *d_data, const uint8_t *h_data,
+                          const uint64_t *offsets, const uint64_t *lens,
+                          const uint32_t *stream_ids, uint32_t nblocks,
+                          vsa_hs_corpus_t **corpus);
+int vsa_hs_corpus_scan(vsa_hs_corpus_t *corpus, uint64_t *counts, uint64_t *total,
+                       unsigned threads);
+int vsa_hs_corpus_free(vsa_hs_corpus_t *corpus);
+
 /* Introspection for tests: the database's HWLM blob (fragment id = HWLM
  * literal id) and the number of literal fragments. */
 int vsa_hs_database_hwlm(const vsa_hs_database_t *db, const void **hwlm, size_t *size,

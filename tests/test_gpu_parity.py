@@ -395,3 +395,69 @@ def test_gpu_dshufti_random():
                 want = oracle.shufti_double(*m, data, vector_size=vsize, mis=addr % vsize)
                 assert r == want, (trial, vsize, n, mis)
     vsa.set_accel_vector_size(64)
+
+
+@pytest.mark.parametrize("nlits", [1, 30, 500])
+def test_gpu_many_small_blocks(ctx, nlits):
+    """Thousands of small blocks in one launch (hsbench-style corpora): runs
+    of blocks shorter than half a segment are packed whole into one segment
+    (runtime.hip build_plan); every block still scans as its own hwlmExec
+    call.  Same answers with packing disabled (VSA_NO_GROUPS)."""
+    import os
+    rng = random.Random(77 + nlits)
+    lits = rand_lits(rng, nlits, minlen=1 if nlits == 1 else 2, maxlen=8)
+    blob = vsa.hwlm_build(lits)
+    sizes = [0, 1, 2, 7, 15, 16, 17, 100, 1023, 1024, 1025, 2047, 2048, 3000, 9000, 40000]
+    bufs = [rand_data(rng, rng.choice(sizes)) for _ in range(3000)]
+    starts = [rng.choice([0, 0, 0, 1, 5, 17]) if b else 0 for b in bufs]
+    starts = [s if s < max(1, len(b)) else 0 for s, b in zip(starts, bufs)]
+    want = []
+    for b, s in zip(bufs, starts):
+        if s >= len(b):
+            want.append([])
+            continue
+        st, m = oracle.hwlm_exec(blob.ptr, b, start=s, cap=1 << 16)
+        want.append(m)
+    for mis in (0, 5):
+        assert batch_run(ctx, blob, bufs, starts=starts, misalign=mis) == want
+    os.environ["VSA_NO_GROUPS"] = "1"
+    try:
+        assert batch_run(ctx, blob, bufs, starts=starts) == want
+    finally:
+        del os.environ["VSA_NO_GROUPS"]
+
+
+def test_gpu_plan_reuse(ctx):
+    """vsa_plan_create / vsa_scan_plan: the tables built once give the same
+    records as vsa_scan_blocks, scan after scan and for another database."""
+    rng = random.Random(5)
+    lits = rand_lits(rng, 200, minlen=2, maxlen=8)
+    blob = vsa.hwlm_build(lits)
+    blob2 = vsa.hwlm_build(rand_lits(rng, 20, minlen=2, maxlen=8))
+    bufs = [rand_data(rng, rng.choice([1, 17, 1000, 3000, 20000])) for _ in range(500)]
+    offs, pos = [], 3
+    for b in bufs:
+        offs.append(pos)
+        pos += len(b) + 1
+    host = np.zeros(pos + 16, np.uint8)
+    for o, b in zip(offs, bufs):
+        host[o:o + len(b)] = np.frombuffer(b, np.uint8)
+    d = ctx.malloc(len(host))
+    try:
+        ctx.h2d(d, host)
+        lens = [len(b) for b in bufs]
+        for bl in (blob, blob2):
+            db = vsa.Database(ctx, bl)
+            n = ctx.scan_blocks(db, d, offs, lens)
+            want = ctx.results(n)
+            plan = ctx.plan(d, offs, lens)
+            for _ in range(3):
+                m = ctx.scan_plan(db, plan)
+                got = ctx.results(m)
+                assert m == n
+                assert np.array_equal(got["key"], want["key"])
+                assert np.array_equal(got["id"], want["id"])
+            plan.close()
+            db.close()
+    finally:
+        ctx.free(d)

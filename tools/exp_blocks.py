@@ -1,5 +1,6 @@
 """Per-block overhead of the batch scan: 1 GiB cut into blocks of 2 KiB ..
-1 MiB, wall time of vsa_scan_blocks vs its kernel time (cfg-4 FDR set)."""
+1 MiB, wall time of vsa_scan_blocks (tables built per call) and of
+vsa_scan_plan (tables built once) vs the kernel time (cfg-4 FDR set)."""
 import sys
 import time
 
@@ -29,5 +30,13 @@ for chunk in [2 << 10, 4 << 10, 16 << 10, 64 << 10, 1 << 20, 256 << 20]:
         m = ctx.scan_blocks(db, d, offs, lens)
         walls.append(time.perf_counter() - t0)
         ks.append(ctx.kernel_ms())
-    print("chunk %8d blocks %7d matches %6d wall %.3f ms kernel %.3f ms" %
-          (chunk, n, m, min(walls) * 1e3, min(ks)), flush=True)
+    plan = ctx.plan(d, offs, lens)
+    pw = []
+    for _ in range(10):
+        t0 = time.perf_counter()
+        m2 = ctx.scan_plan(db, plan)
+        pw.append(time.perf_counter() - t0)
+    plan.close()
+    assert m2 == m
+    print("chunk %8d blocks %7d matches %6d wall %.3f ms plan wall %.3f ms kernel %.3f ms" %
+          (chunk, n, m, min(walls) * 1e3, min(pw) * 1e3, min(ks)), flush=True)

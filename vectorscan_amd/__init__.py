@@ -140,6 +140,12 @@ _sig("vsa_scan_blocks_ex", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
 _sig("vsa_scan_blocks_stream", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_void_p, _u64p, _u64p, ctypes.c_void_p, _u64p, ctypes.c_uint32,
      ctypes.c_uint32, _u64p)
+_sig("vsa_plan_create", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+     ctypes.POINTER(ctypes.c_void_p))
+_sig("vsa_plan_free", ctypes.c_int, ctypes.c_void_p)
+_sig("vsa_scan_plan", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+     ctypes.c_uint32, _u64p)
 _sig("vsa_scan_wait", ctypes.c_int, ctypes.c_void_p, _u64p)
 _sig("vsa_scan_results", ctypes.c_int, ctypes.c_void_p,
      ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p))
@@ -616,6 +622,27 @@ class Context:
             raise RuntimeError("vsa_scan_blocks_stream failed (%d)" % rc)
         return n.value
 
+    def plan(self, d_data, offsets, lens, starts=None, hlens=None, report_lo=None):
+        """vsa_plan_create: the batch's launch tables built once (Plan.scan
+        reuses them)."""
+        arrs = [None if a is None else np.ascontiguousarray(a, np.uint64)
+                for a in (offsets, lens, starts, hlens, report_lo)]
+        h = ctypes.c_void_p()
+        rc = lib.vsa_plan_create(self.ptr, d_data, *[None if a is None else a.ctypes.data
+                                                      for a in arrs], len(arrs[0]),
+                                 ctypes.byref(h))
+        if rc != 0:
+            raise RuntimeError("vsa_plan_create failed (%d)" % rc)
+        return Plan(self, h.value)
+
+    def scan_plan(self, db, plan, sort=True, asynchronous=False):
+        n = ctypes.c_uint64()
+        flags = (0 if sort else 1) | (2 if asynchronous else 0)
+        rc = lib.vsa_scan_plan(self.ptr, db.ptr, plan.ptr, flags, ctypes.byref(n))
+        if rc != 0:
+            raise RuntimeError("vsa_scan_plan failed (%d)" % rc)
+        return n.value
+
     def scan_wait(self):
         n = ctypes.c_uint64()
         _check(lib.vsa_scan_wait(self.ptr, ctypes.byref(n)))
@@ -661,6 +688,25 @@ class Context:
     def close(self):
         if self.ptr:
             lib.vsa_ctx_destroy(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Plan:
+    """vsa_plan_t: a batch's block table and segment map on the device."""
+
+    def __init__(self, ctx, ptr):
+        self.ctx = ctx
+        self.ptr = ptr
+
+    def close(self):
+        if self.ptr:
+            lib.vsa_plan_free(self.ptr)
             self.ptr = None
 
     def __del__(self):

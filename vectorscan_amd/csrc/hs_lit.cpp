@@ -565,53 +565,107 @@ int vsa_hs_scan_vector(const vsa_hs_database_t *db, const char *const *data,
  * SINGLEMATCH) takes *total from the GPU's record count without copying the
  * records back; otherwise the records are replayed through the report
  * program on `threads` host threads (streams are independent).  No match
- * callbacks: this is the benchmark path. */
-int vsa_hs_scan_corpus(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch,
-                       const uint8_t *d_data, const uint8_t *h_data, const uint64_t *offsets,
-                       const uint64_t *lens, const uint32_t *stream_ids, uint32_t nblocks,
-                       uint64_t *counts, uint64_t *total, unsigned threads) {
-    if (!valid_db(db) || !offsets || !lens || !total || (nblocks && !d_data))
+ * callbacks: this is the benchmark path.  A prepared corpus keeps the
+ * launch plan (block table, segment map) and the stream grouping on the
+ * device / host between scans. */
+struct vsa_hs_corpus {
+    const vsa_hs_database *db = nullptr;
+    vsa_hs_scratch *scratch = nullptr;
+    const uint8_t *d_data = nullptr, *h_data = nullptr;
+    std::vector<uint64_t> offsets, lens;
+    bool streams = false;
+    std::vector<std::vector<uint32_t>> units; /* streams (or single blocks) */
+    std::vector<uint32_t> order;              /* live blocks by offset */
+    vsa_plan_t *plan = nullptr;
+};
+
+int vsa_hs_corpus_prepare(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch,
+                          const uint8_t *d_data, const uint8_t *h_data,
+                          const uint64_t *offsets, const uint64_t *lens,
+                          const uint32_t *stream_ids, uint32_t nblocks,
+                          vsa_hs_corpus_t **out) {
+    if (!valid_db(db) || !offsets || !lens || !out || (nblocks && !d_data))
         return VSA_HS_INVALID;
     if (db->max_len > SHORT_LIT && !h_data) return VSA_HS_INVALID;
-    int rc = enter(db, scratch);
-    if (rc != VSA_HS_SUCCESS) return rc;
-    vsa_db_t *ddb = device_db(scratch, db);
-    const bool streams = db->mode != VSA_HS_MODE_BLOCK && stream_ids;
-    /* streams: block lists in array order; history lengths */
+    if (!scratch || scratch->magic != SCRATCH_MAGIC || !device_db(scratch, db))
+        return VSA_HS_INVALID;
+    vsa_hs_corpus *c = new (std::nothrow) vsa_hs_corpus;
+    if (!c) return VSA_HS_NOMEM;
+    c->db = db;
+    c->scratch = scratch;
+    c->d_data = d_data;
+    c->h_data = h_data;
+    c->offsets.assign(offsets, offsets + nblocks);
+    c->lens.assign(lens, lens + nblocks);
+    c->streams = db->mode != VSA_HS_MODE_BLOCK && stream_ids;
     std::map<uint32_t, std::vector<uint32_t>> by_stream;
     std::vector<uint64_t> hl(nblocks, 0);
-    std::vector<uint32_t> live; /* non-empty blocks */
+    std::vector<uint64_t> lo, ln, lh;
     for (uint32_t b = 0; b < nblocks; b++) {
-        if (streams) {
+        if (c->streams) {
             auto &v = by_stream[stream_ids[b]];
             if (!v.empty()) {
                 const uint32_t p = v.back();
                 if (offsets[b] != offsets[p] + lens[p]) {
-                    leave(scratch);
+                    delete c;
                     return VSA_HS_INVALID;
                 }
                 hl[b] = std::min<uint64_t>(16, hl[p] + lens[p]);
             }
             v.push_back(b);
         }
-        if (lens[b]) live.push_back(b);
+        if (lens[b]) {
+            c->order.push_back(b);
+            lo.push_back(offsets[b]);
+            ln.push_back(lens[b]);
+            lh.push_back(hl[b]);
+        }
     }
-    std::vector<uint64_t> lo(live.size()), ln(live.size()), lh(live.size());
-    for (size_t i = 0; i < live.size(); i++) {
-        lo[i] = offsets[live[i]];
-        ln[i] = lens[live[i]];
-        lh[i] = hl[live[i]];
+    if (c->streams) {
+        for (auto &e : by_stream) c->units.push_back(std::move(e.second));
+    } else {
+        for (uint32_t b = 0; b < nblocks; b++) c->units.push_back({b});
     }
+    std::sort(c->order.begin(), c->order.end(),
+              [&](uint32_t a, uint32_t b) { return offsets[a] < offsets[b]; });
+    if (!lo.empty() &&
+        vsa_plan_create(scratch->ctx, d_data, lo.data(), ln.data(), nullptr,
+                        c->streams ? lh.data() : nullptr, nullptr, (uint32_t)lo.size(),
+                        &c->plan) != VSA_OK) {
+        delete c;
+        return VSA_HS_NOMEM;
+    }
+    *out = c;
+    return VSA_HS_SUCCESS;
+}
+
+int vsa_hs_corpus_free(vsa_hs_corpus_t *c) {
+    if (!c) return VSA_HS_SUCCESS;
+    vsa_plan_free(c->plan);
+    delete c;
+    return VSA_HS_SUCCESS;
+}
+
+int vsa_hs_corpus_scan(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *total,
+                       unsigned threads) {
+    if (!cp || !total || !valid_db(cp->db)) return VSA_HS_INVALID;
+    const vsa_hs_database *db = cp->db;
+    vsa_hs_scratch *scratch = cp->scratch;
+    int rc = enter(db, scratch);
+    if (rc != VSA_HS_SUCCESS) return rc;
+    vsa_db_t *ddb = device_db(scratch, db);
+    const uint32_t nblocks = (uint32_t)cp->offsets.size();
+    const uint64_t *offsets = cp->offsets.data(), *lens = cp->lens.data();
     if (counts) std::fill(counts, counts + nblocks, 0);
     *total = 0;
     const bool fast = db->simple && !counts;
     std::vector<uint64_t> keys;
     std::vector<uint32_t> ids;
     uint64_t nm = 0;
-    if (!live.empty() &&
-        vsa::scan_records(scratch->ctx, ddb, d_data, lo.data(), ln.data(),
-                          streams ? lh.data() : nullptr, (uint32_t)live.size(),
-                          fast ? nullptr : &keys, fast ? nullptr : &ids, &nm) != VSA_OK) {
+    if (cp->plan &&
+        vsa::scan_records(scratch->ctx, ddb, cp->d_data, nullptr, nullptr, nullptr, 0,
+                          fast ? nullptr : &keys, fast ? nullptr : &ids, &nm,
+                          cp->plan) != VSA_OK) {
         leave(scratch);
         return VSA_HS_UNKNOWN_ERROR;
     }
@@ -621,12 +675,9 @@ int vsa_hs_scan_corpus(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch,
         return VSA_HS_SUCCESS;
     }
     /* records -> blocks (ends are d_data offsets, sorted) */
-    std::vector<uint32_t> order(live);
-    std::sort(order.begin(), order.end(),
-              [&](uint32_t a, uint32_t b) { return offsets[a] < offsets[b]; });
     std::vector<uint64_t> rb(nblocks, 0), re(nblocks, 0);
     uint64_t k = 0;
-    for (uint32_t b : order) {
+    for (uint32_t b : cp->order) {
         const uint64_t hi = offsets[b] + lens[b];
         while (k < nm && (keys[k] >> KEY_END_SHIFT) < offsets[b]) k++;
         rb[b] = k;
@@ -636,12 +687,9 @@ int vsa_hs_scan_corpus(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch,
         }
         re[b] = k;
     }
-    std::vector<std::vector<uint32_t>> units; /* streams (or single blocks) */
-    if (streams) {
-        for (auto &e : by_stream) units.push_back(std::move(e.second));
-    } else {
-        for (uint32_t b = 0; b < nblocks; b++) units.push_back({b});
-    }
+    const auto &units = cp->units;
+    const uint8_t *h_data = cp->h_data;
+    const bool streams = cp->streams;
     const unsigned T = std::max(1u, std::min<unsigned>(threads ? threads : 1,
                                                         (unsigned)units.size()));
     std::vector<uint64_t> part(T, 0);
@@ -696,6 +744,20 @@ int vsa_hs_scan_corpus(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch,
         *total += part[t];
     }
     return VSA_HS_SUCCESS;
+}
+
+int vsa_hs_scan_corpus(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch,
+                       const uint8_t *d_data, const uint8_t *h_data, const uint64_t *offsets,
+                       const uint64_t *lens, const uint32_t *stream_ids, uint32_t nblocks,
+                       uint64_t *counts, uint64_t *total, unsigned threads) {
+    if (!total) return VSA_HS_INVALID;
+    vsa_hs_corpus_t *c = nullptr;
+    int rc = vsa_hs_corpus_prepare(db, scratch, d_data, h_data, offsets, lens, stream_ids,
+                                   nblocks, &c);
+    if (rc != VSA_HS_SUCCESS) return rc;
+    rc = vsa_hs_corpus_scan(c, counts, total, threads);
+    vsa_hs_corpus_free(c);
+    return rc;
 }
 
 /* runtime.c:545-575 */

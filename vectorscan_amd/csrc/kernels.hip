@@ -1206,14 +1206,22 @@ vsa_lit_scan(VsaLitParams P) {
     while (seg < P.nsegs) {
         unsigned long long t_next = 0;
         bool have_next = false;
+        bool lastb = true;
         auto prefetch_ticket = [&]() {
-            if (P.dynamic && !have_next) {
+            if (P.dynamic && !have_next && lastb) {
                 t_next = take();
                 have_next = true;
             }
         };
-        /* block of the segment: host-built segment -> block table */
-        const u32 blk = readfirstlane_u32(P.seg_blk[seg]);
+        /* the segment's blocks: host-built segment -> block map, first block
+         * | count << 24; count 0 = a part of one block, else `count` whole
+         * consecutive blocks (runtime.hip build_plan) */
+        const u32 sbv = readfirstlane_u32(P.seg_blk[seg]);
+        const u32 gcount = sbv >> 24;
+        const u32 nblk = gcount ? gcount : 1u;
+        for (u32 gi = 0; gi < nblk; gi++) {
+        lastb = gi + 1 == nblk;
+        const u32 blk = (sbv & 0xffffffu) + gi;
         const VsaBlock B = P.blocks[blk];
         SegCtx S;
         S.blk = blk;
@@ -1232,8 +1240,8 @@ vsa_lit_scan(VsaLitParams P) {
         S.len = (int64_t)B.len;
         S.zbase = B.zbase;
         S.rlo = B.rlo > S.start ? B.rlo : S.start;
-        const int64_t s_lo = B.org + (int64_t)(seg - B.seg_first) * SEG;
-        const int64_t s_hi = (s_lo + SEG < S.bhi) ? s_lo + SEG : S.bhi;
+        const int64_t s_lo = gcount ? B.org : B.org + (int64_t)(seg - B.seg_first) * SEG;
+        const int64_t s_hi = (!gcount && s_lo + SEG < S.bhi) ? s_lo + SEG : S.bhi;
         const u32 niters = (u32)((s_hi - s_lo + 1023) >> 10);
         const int64_t zlo = (MODE == VSA_MODE_FDR) ? B.zbase : S.qlo;
 
@@ -1255,6 +1263,34 @@ vsa_lit_scan(VsaLitParams P) {
         const int64_t fb = s_lo + 1024 * (int64_t)f0;
         uint4 ring[LIT_DEPTH];
         u32 after = 0;
+        /* The range's first loads are issued together: the prologue bytes,
+         * the first checked iteration's chunk (ring[0]) and, when there is
+         * no sweep, the last checked iteration's chunk (ring[1]), so a small
+         * block costs one memory round trip before its first lookup, not
+         * one per step (hsbench corpora).  The sweep's chunks follow the
+         * first checked iteration (issuing them earlier keeps 16 more VGPRs
+         * live through it and spills). */
+        const bool pro1 = lane < (u32)(T::NL - 1);
+        const int64_t pp = s_lo - (T::NL - 1) + (int64_t)lane;
+        const bool pro1_in = pro1 && pp - S.blo >= zlo && pp - S.blo < (int64_t)B.len;
+        const u8 pb0 = pro1_in ? load_byte_masked(A, pp, S.vlo, S.bhi) : (u8)0;
+        const u8 pb1 = (T::KEY16 && pro1_in) ? load_byte_masked(A, pp + 1, S.vlo, S.bhi) : (u8)0;
+        const u32 pbb = lane < 8 ? load_byte_masked(A, s_lo - 8 + (int64_t)lane, S.vlo, S.bhi) : 0u;
+        u32 nxt_f = 0, nxt_t = 0;
+        ring[0] = make_uint4(0, 0, 0, 0);
+        ring[1] = make_uint4(0, 0, 0, 0);
+        if (f0 > 0) {
+            ring[0] = load_chunk(A, s_lo + 16 * (int64_t)lane, S.bhi);
+            nxt_f = load_byte_masked(A, s_lo + 1024, S.vlo, S.bhi);
+        }
+        /* the tail's first chunk is preloaded only without a sweep (f1 is
+         * then max(f0, ...) and the tail starts right after the f0 loop) */
+        const bool tail_pre = nf == 0 && f1 < niters && f1 > 0;
+        if (tail_pre) {
+            const int64_t ibt = s_lo + 1024 * (int64_t)f1;
+            ring[1] = load_chunk(A, ibt + 16 * (int64_t)lane, S.bhi);
+            nxt_t = load_byte_masked(A, ibt + 1024, S.vlo, S.bhi);
+        }
         /* prologue 1: table spill from positions s_lo-NL+1 .. s_lo-1 */
         IterState is;
         is.ncand = ncand_total;
@@ -1262,21 +1298,12 @@ vsa_lit_scan(VsaLitParams P) {
         is.head = ring_head;
         {
             S_t x = 0;
-            if (lane < (u32)(T::NL - 1)) {
-                const int64_t p = s_lo - (T::NL - 1) + (int64_t)lane;
-                const int64_t q = p - S.blo;
-                if (q >= zlo && q < (int64_t)B.len) {
-                    const u8 b0 = load_byte_masked(A, p, S.vlo, S.bhi);
-                    u32 key;
-                    if constexpr (T::KEY16) {
-                        const u8 b1 = load_byte_masked(A, p + 1, S.vlo, S.bhi);
-                        key = vsa_fdr_key(b0, b1, P.dmask);
-                    } else {
-                        key = b0;
-                    }
-                    x = (S_t)lit_lookup<MODE, LDS_TABLE>(tab, key, lane);
-                    x >>= T::LB * (s_lo - p);
-                }
+            if (pro1_in) {
+                u32 key;
+                if constexpr (T::KEY16) key = vsa_fdr_key(pb0, pb1, P.dmask);
+                else key = pb0;
+                x = (S_t)lit_lookup<MODE, LDS_TABLE>(tab, key, lane);
+                x >>= T::LB * (s_lo - pp);
             }
             u64 xv = (u64)x;
 #pragma unroll
@@ -1287,9 +1314,7 @@ vsa_lit_scan(VsaLitParams P) {
             }
             is.carry = ((u64)shfl_u32((u32)(xv >> 32), 0) << 32) | shfl_u32((u32)xv, 0);
             /* prologue 2: the 8 bytes before s_lo (keys of the first ends) */
-            u32 bb = 0;
-            if (lane < 8) bb = load_byte_masked(A, s_lo - 8 + (int64_t)lane, S.vlo, S.bhi);
-            u64 pb = (u64)bb << (8 * (lane & 7));
+            u64 pb = (u64)pbb << (8 * (lane & 7));
 #pragma unroll
             for (int dd = 1; dd < 8; dd <<= 1) {
                 const u32 lo = shfl_down_u32((u32)pb, dd);
@@ -1300,8 +1325,12 @@ vsa_lit_scan(VsaLitParams P) {
         }
         for (u32 it = 0; it < f0; it++) {
             const int64_t ib = s_lo + 1024 * (int64_t)it;
-            const uint4 cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
-            const u32 nxt0 = load_byte_masked(A, ib + 1024, S.vlo, S.bhi);
+            uint4 cur = ring[0];
+            u32 nxt0 = nxt_f;
+            if (it > 0) {
+                cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
+                nxt0 = load_byte_masked(A, ib + 1024, S.vlo, S.bhi);
+            }
             is = scan_iter<MODE, LDS_TABLE, true>(P, cl, L, S, mis, ib, cur, nxt0, is,
                                                  bucket_mask);
         }
@@ -1349,14 +1378,19 @@ vsa_lit_scan(VsaLitParams P) {
         prefetch_ticket();
         for (u32 it = f1; it < niters; it++) {
             const int64_t ib = s_lo + 1024 * (int64_t)it;
-            const uint4 cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
-            const u32 nxt0 = load_byte_masked(A, ib + 1024, S.vlo, S.bhi);
+            uint4 cur = ring[1];
+            u32 nxt0 = nxt_t;
+            if (it > f1 || !tail_pre) {
+                cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
+                nxt0 = load_byte_masked(A, ib + 1024, S.vlo, S.bhi);
+            }
             is = scan_iter<MODE, LDS_TABLE, true>(P, cl, L, S, mis, ib, cur, nxt0, is,
                                                  bucket_mask);
         }
         ncand_total = is.ncand;
         ring_tail_cache = is.tail_cache;
         ring_head = is.head;
+        } /* blocks of the segment */
         seg = P.dynamic ? resolve(t_next) : seg + G;
     }
     /* every push of this wave precedes this (LDS order) */

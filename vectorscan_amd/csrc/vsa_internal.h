@@ -60,6 +60,7 @@ void flood_events(const u8 *buf, size_t len, size_t start, const u8 *eng, u32 vs
 struct hs_scratch;
 struct vsa_ctx;
 struct vsa_db;
+struct vsa_plan;
 
 namespace vsa {
 
@@ -78,7 +79,8 @@ int exec_pieces(vsa_ctx *c, const vsa_db *db, const u8 *hist, size_t hist_len,
  * the sorted records to the host when keys != NULL, else only counted */
 int scan_records(vsa_ctx *c, const vsa_db *db, const u8 *d_data, const uint64_t *offsets,
                  const uint64_t *lens, const uint64_t *hlens, uint32_t nblocks,
-                 std::vector<uint64_t> *keys, std::vector<uint32_t> *ids, uint64_t *n);
+                 std::vector<uint64_t> *keys, std::vector<uint32_t> *ids, uint64_t *n,
+                 const vsa_plan *plan = nullptr);
 /* one call's records (ends relative to its buffer) through cb, no floods */
 int replay_records(const vsa_db *db, const uint64_t *keys, const uint32_t *ids, uint64_t n,
                    LitCallback cb, void *cbctx);

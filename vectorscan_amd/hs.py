@@ -265,3 +265,51 @@ def scan_corpus(db, scratch, d_data, offsets, lens, stream_ids=None, h_data=None
                                 n, cnt.ctypes.data if cnt is not None else None,
                                 ctypes.byref(total), threads)
     return rc, total.value, cnt
+
+
+_sig("vsa_hs_corpus_prepare", ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32,
+     ctypes.POINTER(_vp))
+_sig("vsa_hs_corpus_scan", ctypes.c_int, _vp, _vp, _u64p, ctypes.c_uint)
+_sig("vsa_hs_corpus_free", ctypes.c_int, _vp)
+
+
+class Corpus:
+    """vsa_hs_corpus_t: device-resident blocks prepared once (launch plan,
+    stream grouping) for repeated vsa_hs_corpus_scan calls."""
+
+    def __init__(self, db, scratch, d_data, offsets, lens, stream_ids=None, h_data=None):
+        self._offs = np.ascontiguousarray(offsets, np.uint64)
+        self._lens = np.ascontiguousarray(lens, np.uint64)
+        self._sid = (np.ascontiguousarray(stream_ids, np.uint32)
+                     if stream_ids is not None else None)
+        self._hk, hp = None, None
+        if h_data is not None:
+            self._hk, hp, _ = _as_buf(h_data)
+        self.n = len(self._offs)
+        h = _vp()
+        rc = lib.vsa_hs_corpus_prepare(db.handle, scratch.handle, d_data, hp,
+                                       self._offs.ctypes.data, self._lens.ctypes.data,
+                                       self._sid.ctypes.data if self._sid is not None else None,
+                                       self.n, ctypes.byref(h))
+        if rc:
+            raise HsError(rc)
+        self.handle = h.value
+        self._db, self._scratch = db, scratch  # keep alive
+
+    def scan(self, counts=False, threads=16):
+        cnt = np.zeros(self.n, np.uint64) if counts else None
+        total = ctypes.c_uint64()
+        rc = lib.vsa_hs_corpus_scan(self.handle, cnt.ctypes.data if cnt is not None else None,
+                                    ctypes.byref(total), threads)
+        return rc, total.value, cnt
+
+    def close(self):
+        if self.handle:
+            lib.vsa_hs_corpus_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -15,11 +15,12 @@ id, stream_id, data FROM chunk ORDER BY id`` (data_corpus.cpp:72-110).
 Default mode is streaming (every stream's chunks in id order are its
 writes); -N block mode (every chunk one hs_scan); -V vectored.
 
-Difference by design: the corpus is uploaded to HBM once and every repeat
-(the block loop of main.cpp:487-511, or the stream loops) runs as ONE GPU
-launch through vsa_hs_scan_corpus over all chunks, instead of one hs_scan
-call per chunk on a CPU thread.  The timed region of a repeat is that call
-(launch, device sort, count / record replay, synchronisation); the report
+Difference by design: the corpus is uploaded to HBM and prepared once
+(vsa_hs_corpus_prepare: launch plan on the device), and every repeat (the
+block loop of main.cpp:487-511, or the stream loops) runs as ONE GPU launch
+over all chunks (vsa_hs_corpus_scan), instead of one hs_scan call per chunk
+on a CPU thread.  The timed region of a repeat is that call (launch, device
+sort, count / record replay, synchronisation); the report
 lines and calc_mbps (main.cpp:705-708: bytes / (seconds * 125000)) are the
 reference's, with "per core" meaning per GPU.
 """
@@ -194,17 +195,18 @@ class GpuCorpus:
         self.d_data = self.ctx.malloc(max(1, self.image.nbytes))
         self.ctx.h2d(self.d_data, self.image)
         self.long = any(len(e) > 8 for e in exprs)
+        self.corpus = hs.Corpus(self.db, self.scratch, self.d_data, self.offs, self.lens,
+                                self.sids if mode != hs.MODE_BLOCK else None,
+                                self.image if self.long else None)
 
     def scan(self, counts=False, threads=16):
-        rc, total, cnt = hs.scan_corpus(
-            self.db, self.scratch, self.d_data, self.offs, self.lens,
-            self.sids if self.mode != hs.MODE_BLOCK else None,
-            self.image if self.long else None, counts, threads)
+        rc, total, cnt = self.corpus.scan(counts, threads)
         if rc != hs.SUCCESS:
             raise hs.HsError(rc)
         return total, cnt
 
     def close(self):
+        self.corpus.close()
         if self.d_data:
             self.ctx.free(self.d_data)
             self.d_data = None
