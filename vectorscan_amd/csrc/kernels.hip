@@ -488,6 +488,38 @@ __device__ __forceinline__ void conf_accumulate(const typename LitTraits<MODE>::
     }
 }
 
+/* Block-edge masks: position j (0..16) of a lane's chunk is end / byte
+ * q0 + j (block-relative).  rel32 clamps a bound X to the chunk's
+ * coordinates; range_mask gives bits j in [lo, hi) over 17 positions, so an
+ * edge iteration's per-position tests are a handful of 32-bit ops instead
+ * of 16 x 64-bit compares each. */
+__device__ __forceinline__ int rel32(int64_t x, int64_t q0) {
+    const int64_t d = x - q0;
+    return d < -1 ? -1 : (d > 17 ? 17 : (int)d);
+}
+__device__ __forceinline__ u32 range_mask(int lo, int hi) {
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > 17 ? 17 : hi;
+    return hi <= lo ? 0u : ((0xffffffffu << lo) & ((1u << hi) - 1u));
+}
+/* bits 0..3 of t -> bytes 0..3 of 0xff / 0 (no carries: the shifted copies
+ * of t do not overlap) */
+__device__ __forceinline__ u32 nib_to_bytes(u32 t) {
+    return (((t & 0xfu) * 0x00204081u) & 0x01010101u) * 0xffu;
+}
+/* 4 bytes at signed byte offset o of the zero-padded 16-byte s[0..3] */
+__device__ __forceinline__ u32 window4(const u32 (&s)[4], int o) {
+    const int a = o >> 2; /* floor */
+    const u32 b = (u32)o & 3u;
+    auto W = [&](int i) -> u32 {
+        u32 v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) v = i == k ? s[k] : v;
+        return v;
+    };
+    return __builtin_amdgcn_alignbyte(W(a + 1), W(a), b);
+}
+
 /* One 1 KiB iteration at aoff `ib`: lane l owns bytes [ib + 16 l, +16).
  * d = the lane's 16 bytes, nxt0 = first byte of the following chunk (for
  * lane 63's last 2-byte key). */
@@ -506,18 +538,15 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     /* next byte (only byte 0 of d[4] reaches a key: the 16-bit key of
      * position 15 is bytes 15..16, masked to <= 16 bits) */
     d[4] = writelane_u32<WAVE - 1>(lane_down1(d[0]), nxt0);
+    /* edge iterations: readable bytes [vlo, bhi) and looked-up positions */
+    u32 look_m = 0xffffu;
     if (EDGE) {
+        const int r_len = rel32(S.len, q0);
+        const u32 bm = range_mask(rel32(S.vlo - S.blo, q0), r_len);
 #pragma unroll
-        for (int w = 0; w < 4; w++) {
-            u32 m = 0;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                int64_t p = p0 + 4 * w + k;
-                if (p >= S.vlo && p < S.bhi) m |= 0xffu << (8 * k);
-            }
-            d[w] &= m;
-        }
-        if (p0 + 16 < S.vlo || p0 + 16 >= S.bhi) d[4] = 0;
+        for (int w = 0; w < 4; w++) d[w] &= nib_to_bytes(bm >> (4 * w));
+        if (!((bm >> 16) & 1u)) d[4] = 0;
+        look_m = range_mask(rel32(MODE == VSA_MODE_FDR ? S.zbase : S.qlo, q0), r_len);
     }
 
     /* own contributions: the lane's 16 lookups ... */
@@ -548,14 +577,7 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
             x[j] = (S_t)lit_lookup<MODE, LDS_TABLE>(L.tab, key, lane);
         }
         if (EDGE) {
-            int64_t q = q0 + j;
-            bool valid;
-            if constexpr (MODE == VSA_MODE_FDR) {
-                valid = q >= S.zbase && q < S.len;
-            } else {
-                valid = q >= S.qlo && q < S.len;
-            }
-            if (!valid) x[j] = 0;
+            if (!((look_m >> j) & 1u)) x[j] = 0;
         }
     }
 #ifdef VSA_EXTRA_VALU
@@ -586,23 +608,26 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
         if constexpr (MODE == VSA_MODE_FDR) if (!S.stream) {
             /* start state: byte i applies to end start + i (the short zone
              * shifts fdr->start by 16 - (len - start) against a scan from
-             * len - 16, fdr.c:372-440 and :712-720, landing on start too) */
+             * len - 16, fdr.c:372-440 and :712-720, landing on start too):
+             * end q0 + j takes byte q0 + j - start of the zero-padded state */
+            const int64_t r0 = q0 - S.start;
+            if (r0 > -16 && r0 < 16) {
+                const u32 sv[4] = {(u32)P.state_lo, (u32)(P.state_lo >> 32), (u32)P.state_hi,
+                                   (u32)(P.state_hi >> 32)};
 #pragma unroll
-            for (int j = 0; j < 16; j++) {
-                int64_t r = q0 + j - S.start;
-                if (r >= 0 && r < 16) {
-                    u64 sv = r < 8 ? P.state_lo : P.state_hi;
-                    c[j >> 2] |= ((u32)(sv >> (8 * (r & 7))) & 0xff) << (8 * (j & 3));
-                }
+                for (int w = 0; w < 4; w++) c[w] |= window4(sv, (int)r0 + 4 * w);
             }
         }
         /* only ends in [max(start, rlo), len) are reported */
+        const u32 out_m = ~range_mask(rel32(S.rlo, q0), rel32(S.len, q0)) & 0xffffu;
+        if constexpr (T::LB == 8) {
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            int64_t q = q0 + j;
-            if (q < S.rlo || q >= S.len) {
-                if constexpr (T::LB == 8) c[j >> 2] |= 0xffu << (8 * (j & 3));
-                else c[j >> 1] |= 0xffffu << (16 * (j & 1));
+            for (int w = 0; w < 4; w++) c[w] |= nib_to_bytes(out_m >> (4 * w));
+        } else {
+#pragma unroll
+            for (int w = 0; w < 8; w++) {
+                const u32 t = out_m >> (2 * w);
+                c[w] |= ((t & 1u) ? 0xffffu : 0u) | ((t & 2u) ? 0xffff0000u : 0u);
             }
         }
     }
@@ -669,16 +694,9 @@ __device__ __forceinline__ IterState nood_iter(const VsaLitParams &P, const LitS
     const int64_t q0 = p0 - S.blo;
     u32 d[4] = {chunk.x, chunk.y, chunk.z, chunk.w};
     if (EDGE) {
+        const u32 bm = range_mask(rel32(S.vlo - S.blo, q0), rel32(S.len, q0));
 #pragma unroll
-        for (int w = 0; w < 4; w++) {
-            u32 m = 0;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                int64_t p = p0 + 4 * w + k;
-                if (p >= S.vlo && p < S.bhi) m |= 0xffu << (8 * k);
-            }
-            d[w] &= m;
-        }
+        for (int w = 0; w < 4; w++) d[w] &= nib_to_bytes(bm >> (4 * w));
     }
     u32 pv2 = lane_up1(d[2]), pv3 = lane_up1(d[3]);
     if (lane == 0) {
@@ -731,11 +749,7 @@ __device__ __forceinline__ IterState nood_iter(const VsaLitParams &P, const LitS
          * min(hlen, msk_len - 1) bytes into the history (noodle_engine.cpp:
          * 149-180) -- S.qlo carries that (0 in block mode) */
         const int64_t elo = S.start + (int64_t)P.nood_len - 1 + S.qlo;
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const int64_t q = q0 + j;
-            if (q < elo || q < S.rlo || q >= S.len) hits &= ~(1u << j);
-        }
+        hits &= range_mask(rel32(elo > S.rlo ? elo : S.rlo, q0), rel32(S.len, q0));
     }
     if (!__any(hits != 0)) return out;
     const u64 meta = (u64)p0 | ((u64)S.blk << ENT_BLK_SHIFT);
