@@ -137,7 +137,13 @@ struct vsa_ctx {
     const uint8_t *res_host = nullptr;
     size_t res_len = 0;
     BatchPlan plan; /* the per-call batch plan (reused storage) */
+    bool host_sort = false; /* the last scan's records are left unsorted */
 };
+
+/* drop-in scans: results of at most HOST_SORT_MAX records are sorted on the
+ * host after the copy back (internal scan flag) */
+constexpr uint32_t SCAN_HOST_SORT_SMALL = 1u << 16;
+constexpr uint64_t HOST_SORT_MAX = 1024;
 
 struct vsa_db {
     vsa_ctx *ctx = nullptr;
@@ -485,7 +491,10 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     }
     if (n > w.out_cap) return VSA_E_OVERFLOW;
     c->cur = 0;
-    if (n > 1 && !(flags & VSA_SCAN_UNSORTED)) {
+    /* internal: a few records are sorted by the host caller after its copy
+     * (the device sort's launches cost more than sorting them there) */
+    c->host_sort = (flags & SCAN_HOST_SORT_SMALL) && n <= HOST_SORT_MAX;
+    if (n > 1 && !(flags & VSA_SCAN_UNSORTED) && !c->host_sort) {
         hipcub::DoubleBuffer<uint64_t> kb(w.d_keys[0], w.d_keys[1]);
         hipcub::DoubleBuffer<uint32_t> vb(w.d_ids[0], w.d_ids[1]);
         size_t bytes = w.tmp_bytes;
@@ -938,8 +947,8 @@ int scan_host(vsa_db *db, const uint8_t *buf, size_t len, size_t start,
         VSA_CHECK(hipMemcpyAsync(c->ws.d_in + pre, buf, len, hipMemcpyHostToDevice, c->stream));
     }
     uint64_t off = 0, l = len, st = start, n = 0, hl = hlen;
-    if ((r = scan_blocks_impl(c, db, c->ws.d_in + pre, &off, &l, &st, 1, 0, &n,
-                              pre ? &hl : nullptr)) != VSA_OK)
+    if ((r = scan_blocks_impl(c, db, c->ws.d_in + pre, &off, &l, &st, 1, SCAN_HOST_SORT_SMALL,
+                              &n, pre ? &hl : nullptr)) != VSA_OK)
         return r;
     keys.resize(n);
     ids.resize(n);
@@ -949,6 +958,16 @@ int scan_host(vsa_db *db, const uint8_t *buf, size_t len, size_t start,
         VSA_CHECK(hipMemcpyAsync(ids.data(), c->ws.d_ids[c->cur], n * 4,
                                  hipMemcpyDeviceToHost, c->stream));
         VSA_CHECK(hipStreamSynchronize(c->stream));
+    }
+    if (c->host_sort && n > 1) {
+        /* keys are unique (end, bucket, LitInfo) */
+        std::vector<std::pair<uint64_t, uint32_t>> kv(n);
+        for (uint64_t i = 0; i < n; i++) kv[i] = {keys[i], ids[i]};
+        std::sort(kv.begin(), kv.end());
+        for (uint64_t i = 0; i < n; i++) {
+            keys[i] = kv[i].first;
+            ids[i] = kv[i].second;
+        }
     }
     return VSA_OK;
 }
@@ -1818,7 +1837,7 @@ hwlm_error_t exec_pieces(vsa_ctx *c, const vsa_db *db, const u8 *hist, size_t hi
     }
     uint64_t nm = 0;
     if (scan_blocks_impl(c, db, c->ws.d_in, off.data(), len.data(), st.data(),
-                         (uint32_t)off.size(), 0, &nm, hl.data()) != VSA_OK)
+                         (uint32_t)off.size(), SCAN_HOST_SORT_SMALL, &nm, hl.data()) != VSA_OK)
         return HWLM_ERROR_UNKNOWN;
     std::vector<uint64_t> keys(nm);
     std::vector<uint32_t> ids(nm);
@@ -1829,6 +1848,15 @@ hwlm_error_t exec_pieces(vsa_ctx *c, const vsa_db *db, const u8 *hist, size_t hi
                            c->stream) != hipSuccess ||
             hipStreamSynchronize(c->stream) != hipSuccess)
             return HWLM_ERROR_UNKNOWN;
+    }
+    if (c->host_sort && nm > 1) {
+        std::vector<std::pair<uint64_t, uint32_t>> kv(nm);
+        for (uint64_t i = 0; i < nm; i++) kv[i] = {keys[i], ids[i]};
+        std::sort(kv.begin(), kv.end());
+        for (uint64_t i = 0; i < nm; i++) {
+            keys[i] = kv[i].first;
+            ids[i] = kv[i].second;
+        }
     }
     hs_scratch *sc = (hs_scratch *)cbctx;
     std::vector<vsa::FloodEvent> ev;
