@@ -260,6 +260,17 @@ __device__ __forceinline__ u32 conf_hash(u64 key, u64 andmsk, u64 mult, u32 nbit
  * v whose start lies inside the block.  The candidates' global loads
  * (litIndex slot, block record, each chain step) are independent, so they
  * are issued together: one memory latency per chain step for all of them. */
+/* the binned sort's histogram (runtime.hip finish_scan): one count per
+ * record written, by its end's top bits; a bin past VSA_SORT_BIN_MAX flags
+ * the launch for the library sort instead */
+__device__ __forceinline__ void bin_count(const VsaLitParams &P, u64 end) {
+    if (!P.bins) return;
+    const u32 old = atomicAdd(&P.bins[(u32)(end >> P.bin_shift)], 1u);
+    if (old == VSA_SORT_BIN_MAX)
+        __hip_atomic_store(&P.counters[VSA_CTR_BIN_OVERFLOW], 1ULL, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int CONF_U>
 __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfLds &cl,
                                               const QEnt (&q)[CONF_U], const bool (&valid)[CONF_U],
@@ -335,6 +346,7 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
                                        ((u64)b[i] << VSA_KEY_BUCKET_SHIFT) | lidx;
                     P.out_ids[slot] = w1[i].z;
                 }
+                if (mt[i]) bin_count(P, base[i] + (u64)e[i]);
             }
         }
 #pragma unroll
@@ -959,6 +971,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                         P.out_keys[slot] = (p0 + j - mis) << VSA_KEY_END_SHIFT;
                         P.out_ids[slot] = P.nood_id;
                     }
+                    bin_count(P, p0 + j - mis);
                 }
             }
             continue;
@@ -1418,6 +1431,92 @@ template __global__ void vsa_lit_scan<VSA_MODE_FDR, false>(VsaLitParams);
 template __global__ void vsa_lit_scan<VSA_MODE_TEDDY, true>(VsaLitParams);
 template __global__ void vsa_lit_scan<VSA_MODE_FAT, true>(VsaLitParams);
 template __global__ void vsa_lit_scan<VSA_MODE_NOOD, false>(VsaLitParams);
+
+/* ====================================================== binned sort === */
+
+/* Match records sorted in three short launches instead of a library sort's
+ * dozen (runtime.hip finish_scan): bins = VSA_SORT_BINS ranges of end
+ * positions counted by the scan kernel (bin_count); (1) exclusive scan of the
+ * counts, (2) scatter into bin order, (3) one wave sorts each bin (<= 64
+ * records: a register bitonic sort on the full key).  Keys are unique (end,
+ * bucket, LitInfo), so the result equals the full sort. */
+__global__ void __launch_bounds__(1024) vsa_bin_scan(const uint32_t *counts, uint32_t *cursor) {
+    __shared__ uint32_t part[1024];
+    const uint32_t t = threadIdx.x;
+    constexpr uint32_t PER = VSA_SORT_BINS / 1024;
+    uint32_t v[PER], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++) {
+        v[k] = counts[t * PER + k];
+        sum += v[k];
+    }
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint32_t x = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - sum; /* exclusive prefix of this thread's bins */
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++) {
+        cursor[t * PER + k] = run;
+        run += v[k];
+    }
+}
+
+__global__ void __launch_bounds__(256) vsa_bin_scatter(const uint64_t *keys, const uint32_t *ids,
+                                                       uint64_t n, uint32_t bin_shift,
+                                                       uint32_t *cursor, uint64_t *okeys,
+                                                       uint32_t *oids) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * 256) {
+        const uint64_t k = keys[i];
+        const uint32_t pos = atomicAdd(&cursor[(uint32_t)((k >> VSA_KEY_END_SHIFT) >> bin_shift)], 1u);
+        okeys[pos] = k;
+        oids[pos] = ids[i];
+    }
+}
+
+/* one wave per bin; after the scatter cursor[b] = the bin's end */
+__global__ void __launch_bounds__(256) vsa_bin_sort(const uint32_t *counts,
+                                                    const uint32_t *cursor, uint64_t *keys,
+                                                    uint32_t *ids) {
+    const uint32_t bin = blockIdx.x * 4 + threadIdx.x / WAVE;
+    const u32 lane = lane_id();
+    const uint32_t m = counts[bin];
+    if (m < 2) return;
+    const uint32_t base = cursor[bin] - m;
+    u64 k = ~0ULL;
+    u32 id = 0;
+    if (lane < m) {
+        k = keys[base + lane];
+        id = ids[base + lane];
+    }
+#pragma unroll
+    for (u32 size = 2; size <= WAVE; size <<= 1) {
+#pragma unroll
+        for (u32 j = size >> 1; j > 0; j >>= 1) {
+            const u32 plo = shfl_xor_u32((u32)k, (int)j);
+            const u32 phi = shfl_xor_u32((u32)(k >> 32), (int)j);
+            const u32 pid = shfl_xor_u32(id, (int)j);
+            const u64 pk = ((u64)phi << 32) | plo;
+            const bool up = (lane & size) == 0;
+            const bool lower = (lane & j) == 0;
+            /* keep the smaller key where (lower == up) */
+            const bool take = (lower == up) ? (pk < k) : (pk > k);
+            if (take) {
+                k = pk;
+                id = pid;
+            }
+        }
+    }
+    if (lane < m) {
+        keys[base + lane] = k;
+        ids[base + lane] = id;
+    }
+}
 
 /* ======================================================= class scan === */
 

@@ -38,6 +38,12 @@
 template <int MODE, bool LDS_TABLE>
 __global__ void vsa_lit_scan(VsaLitParams P);
 __global__ void vsa_class_scan(VsaClassParams P);
+__global__ void vsa_bin_scan(const uint32_t *counts, uint32_t *cursor);
+__global__ void vsa_bin_scatter(const uint64_t *keys, const uint32_t *ids, uint64_t n,
+                                uint32_t bin_shift, uint32_t *cursor, uint64_t *okeys,
+                                uint32_t *oids);
+__global__ void vsa_bin_sort(const uint32_t *counts, const uint32_t *cursor, uint64_t *keys,
+                             uint32_t *ids);
 __global__ void vsa_class_scan_lut(VsaClassParams P, uint64_t span);
 __global__ void vsa_pair_scan(VsaPairParams P);
 
@@ -79,6 +85,7 @@ struct Workspace {
     void *d_tmp = nullptr;
     size_t tmp_bytes = 0;
     unsigned long long *d_counters = nullptr; /* layout above */
+    uint32_t *d_bins = nullptr; /* binned sort: counts[VSA_SORT_BINS], cursor[..] */
     unsigned long long *h_counters = nullptr; /* pinned mirror */
     VsaBlock *d_blocks = nullptr;
     VsaBlock *h_blocks = nullptr;
@@ -125,6 +132,7 @@ struct vsa_ctx {
         uint32_t seg_bytes = 0;
         int end_bits = 0;
         uint32_t flags = 0;
+        bool bins = false;  /* the scan counts records into the sort bins */
         uint64_t bytes = 0; /* scanned bytes (len - start summed) */
         const VsaBlock *d_blocks = nullptr;
         const uint32_t *d_segblk = nullptr;
@@ -132,6 +140,7 @@ struct vsa_ctx {
     /* kernel-only timing of the last scan (hipEvents on the scan stream) */
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_kernel_ms = 0.0;
+    uint32_t bin_skip = 0; /* launches left without the binned sort */
     /* host bytes already in ws.d_in (set only inside one drop-in call, so the
      * accel pre-skip and the literal scan share one upload) */
     const uint8_t *res_host = nullptr;
@@ -362,12 +371,27 @@ uint32_t launch_nconf(const vsa_db *db, size_t tab, size_t ent, size_t budget) {
     return nc;
 }
 
+/* the binned sort (kernels.hip) replaces the library sort unless the
+ * caller wants the records unsorted or VSA_LIB_SORT is set */
+bool use_bins(const vsa_ctx *c) {
+    static const bool lib_sort = getenv("VSA_LIB_SORT") != nullptr;
+    return !lib_sort && !(c->launch.flags & VSA_SCAN_UNSORTED) && c->bin_skip == 0;
+}
+
+/* bins of 2^bin_shift end positions, at most VSA_SORT_BINS over the span */
+uint32_t bin_shift_for(int end_bits) {
+    return end_bits > (int)VSA_SORT_BIN_BITS ? (uint32_t)end_bits - VSA_SORT_BIN_BITS : 0u;
+}
+
 int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
                        uint64_t nsegs, uint32_t seg_bytes);
 
 int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
                 uint64_t nsegs, uint32_t seg_bytes) {
     VSA_CHECK(hipMemsetAsync(c->ws.d_counters, 0, 144 * sizeof(unsigned long long), c->stream));
+    c->launch.bins = use_bins(c);
+    if (c->launch.bins)
+        VSA_CHECK(hipMemsetAsync(c->ws.d_bins, 0, VSA_SORT_BINS * sizeof(uint32_t), c->stream));
     VSA_CHECK(hipEventRecord(c->ev0, c->stream));
     int r = launch_scan_kernel(c, db, d_data, nb, nsegs, seg_bytes);
     if (r != VSA_OK) return r;
@@ -399,6 +423,8 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         P.out_ids = w.d_ids[0];
         P.out_cap = w.out_cap;
         P.counters = w.d_counters;
+        P.bins = c->launch.bins ? w.d_bins : nullptr;
+        P.bin_shift = bin_shift_for(c->launch.end_bits);
         {
             const char *e = getenv("VSA_DEBUG_FLAGS");
             P.dbg = e ? (uint32_t)atoi(e) : 0u;
@@ -435,6 +461,8 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.out_ids = w.d_ids[0];
     P.out_cap = w.out_cap;
     P.counters = w.d_counters;
+    P.bins = c->launch.bins ? w.d_bins : nullptr;
+    P.bin_shift = bin_shift_for(c->launch.end_bits);
     {
         const char *e = getenv("VSA_DEBUG_FLAGS");
         P.dbg = e ? (uint32_t)atoi(e) : 0u;
@@ -472,7 +500,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
 
 int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     Workspace &w = c->ws;
-    VSA_CHECK(hipMemcpyAsync(w.h_counters, w.d_counters, 4 * sizeof(unsigned long long),
+    VSA_CHECK(hipMemcpyAsync(w.h_counters, w.d_counters, 16 * sizeof(unsigned long long),
                              hipMemcpyDeviceToHost, c->stream));
     VSA_CHECK(hipStreamSynchronize(c->stream));
     uint64_t n = w.h_counters[0];
@@ -494,7 +522,26 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     /* internal: a few records are sorted by the host caller after its copy
      * (the device sort's launches cost more than sorting them there) */
     c->host_sort = (flags & SCAN_HOST_SORT_SMALL) && n <= HOST_SORT_MAX;
-    if (n > 1 && !(flags & VSA_SCAN_UNSORTED) && !c->host_sort) {
+    /* a launch whose records crowd one bin sorts with the library; the next
+     * few launches (likely as dense) skip the histogram */
+    if (c->bin_skip) c->bin_skip--;
+    if (c->launch.bins && w.h_counters[VSA_CTR_BIN_OVERFLOW]) c->bin_skip = 16;
+    if (n > 1 && !(flags & VSA_SCAN_UNSORTED) && !c->host_sort && c->launch.bins &&
+        !w.h_counters[VSA_CTR_BIN_OVERFLOW]) {
+        /* binned sort: bins of <= VSA_SORT_BIN_MAX records (kernels.hip) */
+        uint32_t *counts = w.d_bins, *cursor = w.d_bins + VSA_SORT_BINS;
+        const uint32_t shift = bin_shift_for(end_bits);
+        hipLaunchKernelGGL(vsa_bin_scan, dim3(1), dim3(1024), 0, c->stream, counts, cursor);
+        const uint64_t want = (n + 255) / 256;
+        const uint32_t grid =
+            (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * 8));
+        hipLaunchKernelGGL(vsa_bin_scatter, dim3(grid), dim3(256), 0, c->stream, w.d_keys[0],
+                           w.d_ids[0], n, shift, cursor, w.d_keys[1], w.d_ids[1]);
+        hipLaunchKernelGGL(vsa_bin_sort, dim3(VSA_SORT_BINS / 4), dim3(256), 0, c->stream,
+                           counts, cursor, w.d_keys[1], w.d_ids[1]);
+        VSA_CHECK(hipGetLastError());
+        c->cur = 1;
+    } else if (n > 1 && !(flags & VSA_SCAN_UNSORTED) && !c->host_sort) {
         hipcub::DoubleBuffer<uint64_t> kb(w.d_keys[0], w.d_keys[1]);
         hipcub::DoubleBuffer<uint32_t> vb(w.d_ids[0], w.d_ids[1]);
         size_t bytes = w.tmp_bytes;
@@ -1090,6 +1137,7 @@ int vsa_ctx_create(int device, vsa_ctx_t **out) {
     VSA_CHECK(hipEventCreate(&c->ev0));
     VSA_CHECK(hipEventCreate(&c->ev1));
     VSA_CHECK(hipMalloc(&c->ws.d_counters, N_COUNTERS * sizeof(unsigned long long)));
+    VSA_CHECK(hipMalloc(&c->ws.d_bins, 2 * VSA_SORT_BINS * sizeof(uint32_t)));
     VSA_CHECK(hipHostMalloc((void **)&c->ws.h_counters, N_COUNTERS * sizeof(unsigned long long),
                             hipHostMallocDefault));
     *out = c.release();
@@ -1108,6 +1156,7 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (w.d_tmp) (void)hipFree(w.d_tmp);
     if (w.d_in) (void)hipFree(w.d_in);
     if (w.d_counters) (void)hipFree(w.d_counters);
+    if (w.d_bins) (void)hipFree(w.d_bins);
     if (w.h_counters) (void)hipHostFree(w.h_counters);
     if (w.d_blocks) (void)hipFree(w.d_blocks);
     if (w.h_blocks) (void)hipHostFree(w.h_blocks);
