@@ -1466,10 +1466,19 @@ __global__ void __launch_bounds__(1024) vsa_bin_scan(const uint32_t *counts, uin
     }
 }
 
+/* the scan's record count and overflow flag, read on the device (the sort
+ * is queued before the host has seen them): 0 when the launch overflowed its
+ * output (it runs again) or a bin (the library sort runs instead) */
+__device__ __forceinline__ uint64_t bin_records(const uint64_t *ctr, uint64_t cap) {
+    const uint64_t n = ctr[0];
+    return (n > cap || ctr[VSA_CTR_BIN_OVERFLOW]) ? 0 : n;
+}
+
 __global__ void __launch_bounds__(256) vsa_bin_scatter(const uint64_t *keys, const uint32_t *ids,
-                                                       uint64_t n, uint32_t bin_shift,
-                                                       uint32_t *cursor, uint64_t *okeys,
-                                                       uint32_t *oids) {
+                                                       const uint64_t *ctr, uint64_t cap,
+                                                       uint32_t bin_shift, uint32_t *cursor,
+                                                       uint64_t *okeys, uint32_t *oids) {
+    const uint64_t n = bin_records(ctr, cap);
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * 256) {
         const uint64_t k = keys[i];
@@ -1480,12 +1489,15 @@ __global__ void __launch_bounds__(256) vsa_bin_scatter(const uint64_t *keys, con
 }
 
 /* one wave per bin; after the scatter cursor[b] = the bin's end */
-__global__ void __launch_bounds__(256) vsa_bin_sort(const uint32_t *counts,
+__global__ void __launch_bounds__(256) vsa_bin_sort(const uint64_t *ctr, uint64_t cap,
+                                                    uint32_t *counts,
                                                     const uint32_t *cursor, uint64_t *keys,
                                                     uint32_t *ids) {
+    if (bin_records(ctr, cap) < 2) return;
     const uint32_t bin = blockIdx.x * 4 + threadIdx.x / WAVE;
     const u32 lane = lane_id();
     const uint32_t m = counts[bin];
+    if (lane_id() == 0) counts[bin] = 0; /* ready for the next scan */
     if (m < 2) return;
     const uint32_t base = cursor[bin] - m;
     u64 k = ~0ULL;

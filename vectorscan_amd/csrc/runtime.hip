@@ -39,11 +39,11 @@ template <int MODE, bool LDS_TABLE>
 __global__ void vsa_lit_scan(VsaLitParams P);
 __global__ void vsa_class_scan(VsaClassParams P);
 __global__ void vsa_bin_scan(const uint32_t *counts, uint32_t *cursor);
-__global__ void vsa_bin_scatter(const uint64_t *keys, const uint32_t *ids, uint64_t n,
-                                uint32_t bin_shift, uint32_t *cursor, uint64_t *okeys,
-                                uint32_t *oids);
-__global__ void vsa_bin_sort(const uint32_t *counts, const uint32_t *cursor, uint64_t *keys,
-                             uint32_t *ids);
+__global__ void vsa_bin_scatter(const uint64_t *keys, const uint32_t *ids, const uint64_t *ctr,
+                                uint64_t cap, uint32_t bin_shift, uint32_t *cursor,
+                                uint64_t *okeys, uint32_t *oids);
+__global__ void vsa_bin_sort(const uint64_t *ctr, uint64_t cap, uint32_t *counts,
+                             const uint32_t *cursor, uint64_t *keys, uint32_t *ids);
 __global__ void vsa_class_scan_lut(VsaClassParams P, uint64_t span);
 __global__ void vsa_pair_scan(VsaPairParams P);
 
@@ -132,7 +132,8 @@ struct vsa_ctx {
         uint32_t seg_bytes = 0;
         int end_bits = 0;
         uint32_t flags = 0;
-        bool bins = false;  /* the scan counts records into the sort bins */
+        bool bins = false;     /* the scan counts records into the sort bins */
+        bool dev_sort = false; /* ... and the binned sort is queued behind it */
         uint64_t bytes = 0; /* scanned bytes (len - start summed) */
         const VsaBlock *d_blocks = nullptr;
         const uint32_t *d_segblk = nullptr;
@@ -140,7 +141,8 @@ struct vsa_ctx {
     /* kernel-only timing of the last scan (hipEvents on the scan stream) */
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_kernel_ms = 0.0;
-    uint32_t bin_skip = 0; /* launches left without the binned sort */
+    uint32_t bin_skip = 0;   /* launches left without the binned sort */
+    bool bins_clean = false; /* the bin counts are zero (no memset needed) */
     /* host bytes already in ws.d_in (set only inside one drop-in call, so the
      * accel pre-skip and the literal scan share one upload) */
     const uint8_t *res_host = nullptr;
@@ -236,29 +238,32 @@ int ensure_in(vsa_ctx *c, size_t need) {
     return VSA_OK;
 }
 
-int ensure_segblk(vsa_ctx *c, uint64_t n) {
-    Workspace &w = c->ws;
-    if (n <= w.segblk_cap) return VSA_OK;
-    if (w.d_segblk) (void)hipFree(w.d_segblk);
-    if (w.h_segblk) (void)hipHostFree(w.h_segblk);
-    w.d_segblk = nullptr;
-    w.h_segblk = nullptr;
-    const uint64_t cap = std::max<uint64_t>(n, 1024);
-    VSA_CHECK(hipMalloc(&w.d_segblk, cap * sizeof(uint32_t)));
-    VSA_CHECK(hipHostMalloc((void **)&w.h_segblk, cap * sizeof(uint32_t), hipHostMallocDefault));
-    w.segblk_cap = cap;
-    return VSA_OK;
+/* the per-call block table and segment map share one device allocation and
+ * one pinned mirror, so a call uploads them with a single copy */
+constexpr size_t TAB_ALIGN = 256;
+
+size_t tab_seg_off(uint32_t blocks_cap) {
+    return ((size_t)blocks_cap * sizeof(VsaBlock) + TAB_ALIGN - 1) & ~(TAB_ALIGN - 1);
 }
 
-int ensure_blocks(vsa_ctx *c, uint32_t n) {
+int ensure_tables(vsa_ctx *c, uint32_t nb, uint64_t nsegs) {
     Workspace &w = c->ws;
-    if (n <= w.blocks_cap) return VSA_OK;
+    if (nb <= w.blocks_cap && nsegs <= w.segblk_cap) return VSA_OK;
     if (w.d_blocks) (void)hipFree(w.d_blocks);
     if (w.h_blocks) (void)hipHostFree(w.h_blocks);
-    uint32_t cap = std::max<uint32_t>(n, 64);
-    VSA_CHECK(hipMalloc(&w.d_blocks, cap * sizeof(VsaBlock)));
-    VSA_CHECK(hipHostMalloc((void **)&w.h_blocks, cap * sizeof(VsaBlock), hipHostMallocDefault));
-    w.blocks_cap = cap;
+    const uint32_t bcap = std::max<uint32_t>({nb, 64u, w.blocks_cap});
+    const uint64_t scap = std::max<uint64_t>({nsegs, (uint64_t)1024, w.segblk_cap});
+    w.d_blocks = w.h_blocks = nullptr;
+    w.d_segblk = w.h_segblk = nullptr;
+    w.blocks_cap = 0;
+    w.segblk_cap = 0;
+    const size_t bytes = tab_seg_off(bcap) + scap * sizeof(uint32_t);
+    VSA_CHECK(hipMalloc(&w.d_blocks, bytes));
+    VSA_CHECK(hipHostMalloc((void **)&w.h_blocks, bytes, hipHostMallocDefault));
+    w.d_segblk = (uint32_t *)((uint8_t *)w.d_blocks + tab_seg_off(bcap));
+    w.h_segblk = (uint32_t *)((uint8_t *)w.h_blocks + tab_seg_off(bcap));
+    w.blocks_cap = bcap;
+    w.segblk_cap = scap;
     return VSA_OK;
 }
 
@@ -383,6 +388,24 @@ uint32_t bin_shift_for(int end_bits) {
     return end_bits > (int)VSA_SORT_BIN_BITS ? (uint32_t)end_bits - VSA_SORT_BIN_BITS : 0u;
 }
 
+/* the binned sort's three launches (kernels.hip): they read the record
+ * count and the overflow flag from d_counters, so they may be queued before
+ * the host has seen either (an overflowed launch leaves them idle) */
+int queue_bin_sort(vsa_ctx *c) {
+    Workspace &w = c->ws;
+    uint32_t *counts = w.d_bins, *cursor = w.d_bins + VSA_SORT_BINS;
+    const uint32_t shift = bin_shift_for(c->launch.end_bits);
+    hipLaunchKernelGGL(vsa_bin_scan, dim3(1), dim3(1024), 0, c->stream, counts, cursor);
+    hipLaunchKernelGGL(vsa_bin_scatter, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, c->stream,
+                       w.d_keys[0], w.d_ids[0], (const uint64_t *)w.d_counters,
+                       (uint64_t)w.out_cap, shift, cursor, w.d_keys[1], w.d_ids[1]);
+    hipLaunchKernelGGL(vsa_bin_sort, dim3(VSA_SORT_BINS / 4), dim3(256), 0, c->stream,
+                       (const uint64_t *)w.d_counters, (uint64_t)w.out_cap, counts, cursor,
+                       w.d_keys[1], w.d_ids[1]);
+    VSA_CHECK(hipGetLastError());
+    return VSA_OK;
+}
+
 int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
                        uint64_t nsegs, uint32_t seg_bytes);
 
@@ -390,12 +413,19 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
                 uint64_t nsegs, uint32_t seg_bytes) {
     VSA_CHECK(hipMemsetAsync(c->ws.d_counters, 0, 144 * sizeof(unsigned long long), c->stream));
     c->launch.bins = use_bins(c);
-    if (c->launch.bins)
+    if (c->launch.bins && !c->bins_clean)
         VSA_CHECK(hipMemsetAsync(c->ws.d_bins, 0, VSA_SORT_BINS * sizeof(uint32_t), c->stream));
+    c->bins_clean = false;
     VSA_CHECK(hipEventRecord(c->ev0, c->stream));
     int r = launch_scan_kernel(c, db, d_data, nb, nsegs, seg_bytes);
     if (r != VSA_OK) return r;
     VSA_CHECK(hipEventRecord(c->ev1, c->stream));
+    /* the binned sort queues behind the scan with no host round trip: its
+     * kernels read the record count and the overflow flag on the device
+     * (finish_scan falls back to the library sort if a bin overflowed).  Not
+     * for the drop-in calls, whose few records the host sorts. */
+    c->launch.dev_sort = c->launch.bins && !(c->launch.flags & SCAN_HOST_SORT_SMALL);
+    if (c->launch.dev_sort) return queue_bin_sort(c);
     return VSA_OK;
 }
 
@@ -528,19 +558,13 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     if (c->launch.bins && w.h_counters[VSA_CTR_BIN_OVERFLOW]) c->bin_skip = 16;
     if (n > 1 && !(flags & VSA_SCAN_UNSORTED) && !c->host_sort && c->launch.bins &&
         !w.h_counters[VSA_CTR_BIN_OVERFLOW]) {
-        /* binned sort: bins of <= VSA_SORT_BIN_MAX records (kernels.hip) */
-        uint32_t *counts = w.d_bins, *cursor = w.d_bins + VSA_SORT_BINS;
-        const uint32_t shift = bin_shift_for(end_bits);
-        hipLaunchKernelGGL(vsa_bin_scan, dim3(1), dim3(1024), 0, c->stream, counts, cursor);
-        const uint64_t want = (n + 255) / 256;
-        const uint32_t grid =
-            (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * 8));
-        hipLaunchKernelGGL(vsa_bin_scatter, dim3(grid), dim3(256), 0, c->stream, w.d_keys[0],
-                           w.d_ids[0], n, shift, cursor, w.d_keys[1], w.d_ids[1]);
-        hipLaunchKernelGGL(vsa_bin_sort, dim3(VSA_SORT_BINS / 4), dim3(256), 0, c->stream,
-                           counts, cursor, w.d_keys[1], w.d_ids[1]);
-        VSA_CHECK(hipGetLastError());
+        /* queued in launch_scan already, except for the drop-in calls */
+        if (!c->launch.dev_sort) {
+            int r = queue_bin_sort(c);
+            if (r != VSA_OK) return r;
+        }
         c->cur = 1;
+        c->bins_clean = true; /* vsa_bin_sort zeroes the counts it read */
     } else if (n > 1 && !(flags & VSA_SCAN_UNSORTED) && !c->host_sort) {
         hipcub::DoubleBuffer<uint64_t> kb(w.d_keys[0], w.d_keys[1]);
         hipcub::DoubleBuffer<uint32_t> vb(w.d_ids[0], w.d_ids[1]);
@@ -694,18 +718,16 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
     int r = build_plan(d_data, offs, lens, starts, hlens, rlos, nb,
                        (uint64_t)c->num_cus * (LIT_WAVES - db->nconf), pl);
     if (r != VSA_OK) return r;
-    if ((r = ensure_blocks(c, nb)) != VSA_OK) return r;
-    if (!pl.segblk.empty() && (r = ensure_segblk(c, pl.segblk.size())) != VSA_OK) return r;
-    /* through the pinned mirrors (pageable copies stage synchronously) */
-    memcpy(c->ws.h_blocks, pl.blocks.data(), nb * sizeof(VsaBlock));
-    VSA_CHECK(hipMemcpyAsync(c->ws.d_blocks, c->ws.h_blocks, nb * sizeof(VsaBlock),
-                             hipMemcpyHostToDevice, c->stream));
-    if (!pl.segblk.empty()) {
-        memcpy(c->ws.h_segblk, pl.segblk.data(), pl.segblk.size() * sizeof(uint32_t));
-        VSA_CHECK(hipMemcpyAsync(c->ws.d_segblk, c->ws.h_segblk,
-                                 pl.segblk.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                                 c->stream));
-    }
+    if ((r = ensure_tables(c, nb, pl.segblk.size())) != VSA_OK) return r;
+    /* through the pinned mirror (pageable copies stage synchronously), one
+     * copy from the table's start to the segment map's end */
+    Workspace &w = c->ws;
+    memcpy(w.h_blocks, pl.blocks.data(), nb * sizeof(VsaBlock));
+    memcpy(w.h_segblk, pl.segblk.data(), pl.segblk.size() * sizeof(uint32_t));
+    const size_t tab_bytes =
+        (size_t)((uint8_t *)(w.h_segblk + pl.segblk.size()) - (uint8_t *)w.h_blocks);
+    VSA_CHECK(hipMemcpyAsync(w.d_blocks, w.h_blocks, tab_bytes, hipMemcpyHostToDevice,
+                             c->stream));
     return launch_planned(c, db, d_data, c->ws.d_blocks, c->ws.d_segblk, nb, pl.segblk.size(),
                           pl.seg_bytes, pl.end_bits, pl.bytes, flags, n_out);
 }
@@ -1160,8 +1182,6 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (w.h_counters) (void)hipHostFree(w.h_counters);
     if (w.d_blocks) (void)hipFree(w.d_blocks);
     if (w.h_blocks) (void)hipHostFree(w.h_blocks);
-    if (w.d_segblk) (void)hipFree(w.d_segblk);
-    if (w.h_segblk) (void)hipHostFree(w.h_segblk);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     (void)hipStreamDestroy(c->stream);
