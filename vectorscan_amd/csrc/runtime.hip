@@ -29,6 +29,7 @@
 #include <memory>
 #include <mutex>
 #include <vector>
+#include <chrono>
 
 #include "../../include/vectorscan_amd.h"
 #include "hs_layout.h"
@@ -87,12 +88,11 @@ struct Workspace {
     unsigned long long *d_counters = nullptr; /* layout above */
     uint32_t *d_bins = nullptr; /* binned sort: counts[VSA_SORT_BINS], cursor[..] */
     unsigned long long *h_counters = nullptr; /* pinned mirror */
-    VsaBlock *d_blocks = nullptr;
-    VsaBlock *h_blocks = nullptr;
-    uint32_t blocks_cap = 0;
-    uint32_t *d_segblk = nullptr; /* block of each segment */
+    VsaBlock *d_blocks = nullptr; /* this call's block table, then its segment map */
+    VsaBlock *h_blocks = nullptr; /* pinned mirror */
+    size_t tab_cap = 0;           /* bytes of both */
+    uint32_t *d_segblk = nullptr; /* block of each segment (inside d_blocks) */
     uint32_t *h_segblk = nullptr;
-    uint64_t segblk_cap = 0;
 };
 
 } // namespace
@@ -110,6 +110,7 @@ struct BatchPlan {
     uint32_t seg_bytes = 0;
     int end_bits = 0;
     uint64_t bytes = 0; /* scanned bytes (len - start summed) */
+    std::vector<int64_t> spans, live; /* build_plan scratch */
 };
 
 struct vsa_ctx {
@@ -140,6 +141,7 @@ struct vsa_ctx {
     } launch;
     /* kernel-only timing of the last scan (hipEvents on the scan stream) */
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_done = nullptr; /* polled by wait_stream */
     double last_kernel_ms = 0.0;
     uint32_t bin_skip = 0;   /* launches left without the binned sort */
     bool bins_clean = false; /* the bin counts are zero (no memset needed) */
@@ -239,31 +241,29 @@ int ensure_in(vsa_ctx *c, size_t need) {
 }
 
 /* the per-call block table and segment map share one device allocation and
- * one pinned mirror, so a call uploads them with a single copy */
+ * one pinned mirror, laid out per call (the map right after this call's
+ * blocks), so a call uploads them with a single copy of just their bytes */
 constexpr size_t TAB_ALIGN = 256;
 
-size_t tab_seg_off(uint32_t blocks_cap) {
-    return ((size_t)blocks_cap * sizeof(VsaBlock) + TAB_ALIGN - 1) & ~(TAB_ALIGN - 1);
-}
-
-int ensure_tables(vsa_ctx *c, uint32_t nb, uint64_t nsegs) {
+int ensure_tables(vsa_ctx *c, uint32_t nb, uint64_t nsegs, bool keep_blocks = false) {
     Workspace &w = c->ws;
-    if (nb <= w.blocks_cap && nsegs <= w.segblk_cap) return VSA_OK;
-    if (w.d_blocks) (void)hipFree(w.d_blocks);
-    if (w.h_blocks) (void)hipHostFree(w.h_blocks);
-    const uint32_t bcap = std::max<uint32_t>({nb, 64u, w.blocks_cap});
-    const uint64_t scap = std::max<uint64_t>({nsegs, (uint64_t)1024, w.segblk_cap});
-    w.d_blocks = w.h_blocks = nullptr;
-    w.d_segblk = w.h_segblk = nullptr;
-    w.blocks_cap = 0;
-    w.segblk_cap = 0;
-    const size_t bytes = tab_seg_off(bcap) + scap * sizeof(uint32_t);
-    VSA_CHECK(hipMalloc(&w.d_blocks, bytes));
-    VSA_CHECK(hipHostMalloc((void **)&w.h_blocks, bytes, hipHostMallocDefault));
-    w.d_segblk = (uint32_t *)((uint8_t *)w.d_blocks + tab_seg_off(bcap));
-    w.h_segblk = (uint32_t *)((uint8_t *)w.h_blocks + tab_seg_off(bcap));
-    w.blocks_cap = bcap;
-    w.segblk_cap = scap;
+    const size_t seg_off = ((size_t)nb * sizeof(VsaBlock) + TAB_ALIGN - 1) & ~(TAB_ALIGN - 1);
+    const size_t need = seg_off + nsegs * sizeof(uint32_t);
+    if (need > w.tab_cap) {
+        VsaBlock *old = w.h_blocks;
+        if (w.d_blocks) (void)hipFree(w.d_blocks);
+        w.d_blocks = w.h_blocks = nullptr;
+        w.tab_cap = 0;
+        const size_t cap = std::max<size_t>(need + need / 4, 64 << 10);
+        VSA_CHECK(hipMalloc(&w.d_blocks, cap));
+        VSA_CHECK(hipHostMalloc((void **)&w.h_blocks, cap, hipHostMallocDefault));
+        /* the block table already written into the old mirror */
+        if (keep_blocks && old) memcpy(w.h_blocks, old, (size_t)nb * sizeof(VsaBlock));
+        if (old) (void)hipHostFree(old);
+        w.tab_cap = cap;
+    }
+    w.d_segblk = (uint32_t *)((uint8_t *)w.d_blocks + seg_off);
+    w.h_segblk = (uint32_t *)((uint8_t *)w.h_blocks + seg_off);
     return VSA_OK;
 }
 
@@ -272,31 +272,52 @@ int ensure_tables(vsa_ctx *c, uint32_t nb, uint64_t nsegs) {
  * segment count is just under a multiple of the scanning-wave count
  * (every wave gets k or k-1 segments, no long tail).  spans[] are the
  * per-block byte spans from their 1 KiB-aligned origins. */
-uint64_t pick_seg_bytes(const std::vector<int64_t> &spans, uint64_t waves) {
-    /* segments of a candidate size, blocks of at most half a segment packed
-     * whole (up to 255 per segment) as build_plan does */
-    auto count = [&](uint64_t seg) {
-        uint64_t n = 0, gn = 0;
-        int64_t gs = 0;
-        for (int64_t sp : spans) {
-            if (2 * sp <= (int64_t)seg) {
-                if (gn && (gs + sp > (int64_t)seg || gn == 255)) {
-                    n++;
-                    gn = 0;
-                    gs = 0;
-                }
-                gn++;
-                gs += sp;
-                continue;
-            }
-            if (gn) {
-                n++;
+/* segments build_plan makes of spans[first, first + n) at segment size seg */
+uint64_t count_range(const std::vector<int64_t> &spans, size_t first, size_t n, uint64_t seg) {
+    uint64_t cnt = 0, gn = 0;
+    int64_t gs = 0;
+    for (size_t i = first; i < first + n; i++) {
+        const int64_t sp = spans[i];
+        if (2 * sp <= (int64_t)seg) {
+            if (gn && (gs + sp > (int64_t)seg || gn == 255)) {
+                cnt++;
                 gn = 0;
                 gs = 0;
             }
-            n += (uint64_t)((sp + (int64_t)seg - 1) / (int64_t)seg);
+            gn++;
+            gs += sp;
+            continue;
         }
-        return n + (gn ? 1 : 0);
+        if (gn) {
+            cnt++;
+            gn = 0;
+            gs = 0;
+        }
+        cnt += (uint64_t)((sp + (int64_t)seg - 1) / (int64_t)seg);
+    }
+    return cnt + (gn ? 1 : 0);
+}
+
+uint64_t pick_seg_bytes(const std::vector<int64_t> &spans, uint64_t waves) {
+    /* segments of a candidate size, blocks of at most half a segment packed
+     * whole (up to 255 per segment) as build_plan does.  Past 64 Ki blocks
+     * the count is estimated from 64 runs of 1024 consecutive blocks spread
+     * over the batch, scaled by bytes (it only balances the schedule) */
+    const size_t ns = spans.size();
+    const size_t RUNS = 64, RUN = 1024;
+    const bool sampled = ns > 65536;
+    uint64_t all_bytes = 0, sample_bytes = 0;
+    if (sampled) {
+        for (int64_t sp : spans) all_bytes += (uint64_t)sp;
+        for (size_t r = 0; r < RUNS; r++)
+            for (size_t i = r * (ns / RUNS); i < r * (ns / RUNS) + RUN; i++)
+                sample_bytes += (uint64_t)spans[i];
+    }
+    auto count = [&](uint64_t seg) {
+        if (!sampled) return count_range(spans, 0, ns, seg);
+        uint64_t n = 0;
+        for (size_t r = 0; r < RUNS; r++) n += count_range(spans, r * (ns / RUNS), RUN, seg);
+        return (uint64_t)((double)n * (double)all_bytes / (double)std::max<uint64_t>(1, sample_bytes));
     };
     uint64_t total = 0;
     for (int64_t sp : spans) total += (uint64_t)sp;
@@ -528,11 +549,31 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     return launch_lit<VSA_MODE_FAT, true>(c, P, lds);
 }
 
+/* wait for the scan stream by polling an event: a blocking wait wakes on a
+ * coarse tick (measured ~1 ms after a 0.3 ms scan), which would set the
+ * wall time of every scan shorter than that.  Past 50 ms of polling the
+ * wait blocks (long scans do not need the precision).  VSA_SYNC_BLOCK:
+ * always block. */
+hipError_t wait_stream(vsa_ctx *c) {
+    static const bool block = getenv("VSA_SYNC_BLOCK") != nullptr;
+    if (block) return hipStreamSynchronize(c->stream);
+    hipError_t e = hipEventRecord(c->ev_done, c->stream);
+    if (e != hipSuccess) return e;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0;; i++) {
+        e = hipEventQuery(c->ev_done);
+        if (e != hipErrorNotReady) return e;
+        if ((i & 255) == 255 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
+            return hipStreamSynchronize(c->stream);
+    }
+}
+
 int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     Workspace &w = c->ws;
     VSA_CHECK(hipMemcpyAsync(w.h_counters, w.d_counters, 16 * sizeof(unsigned long long),
                              hipMemcpyDeviceToHost, c->stream));
-    VSA_CHECK(hipStreamSynchronize(c->stream));
+    VSA_CHECK(wait_stream(c));
     uint64_t n = w.h_counters[0];
     c->last_cand = w.h_counters[2];
     /* adapt the db's confirm-wave count to the measured candidate rate
@@ -587,19 +628,26 @@ constexpr uint32_t PLAN_MAX_BLOCKS = 1u << 20; /* 20-bit block field of the keys
 
 int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens,
                const uint64_t *starts, const uint64_t *hlens, const uint64_t *rlos,
-               uint32_t nb, uint64_t waves, BatchPlan &pl) {
+               uint32_t nb, uint64_t waves, BatchPlan &pl, VsaBlock *out = nullptr) {
     if (nb > PLAN_MAX_BLOCKS) return VSA_E_INVALID;
-    pl.blocks.resize(nb);
+    /* the block table goes to `out` (a pinned mirror) or pl.blocks */
+    if (!out) {
+        pl.blocks.resize(nb);
+        out = pl.blocks.data();
+    }
     pl.segblk.clear();
     uint64_t span = 0;
     for (uint32_t i = 0; i < nb; i++) span = std::max(span, offs[i] + lens[i]);
     const int64_t mis = (int64_t)((uintptr_t)d_data & 15);
-    std::vector<int64_t> spans(nb, -1); /* -1: nothing to scan */
-    std::vector<int64_t> live;
+    /* scratch kept in the plan: a fresh multi-MB vector per call costs its
+     * page faults every call */
+    std::vector<int64_t> &spans = pl.spans, &live = pl.live;
+    spans.assign(nb, -1); /* -1: nothing to scan */
+    live.clear();
     live.reserve(nb);
     pl.bytes = 0;
     for (uint32_t i = 0; i < nb; i++) {
-        VsaBlock &b = pl.blocks[i];
+        VsaBlock &b = out[i];
         b.base = offs[i];
         b.len = lens[i];
         b.start = starts ? starts[i] : 0;
@@ -642,13 +690,13 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
         if (group && 2 * sp <= (int64_t)seg) {
             if (g_n && (g_span + sp > (int64_t)seg || g_n == SEG_GROUP_MAX)) flush();
             if (!g_n) g_first = i;
-            pl.blocks[i].seg_first = pl.segblk.size();
+            out[i].seg_first = pl.segblk.size();
             g_n++;
             g_span += sp;
             continue;
         }
         flush();
-        pl.blocks[i].seg_first = pl.segblk.size();
+        out[i].seg_first = pl.segblk.size();
         const uint64_t k = (uint64_t)((sp + (int64_t)seg - 1) / (int64_t)seg);
         for (uint64_t j = 0; j < k; j++) pl.segblk.push_back(i);
     }
@@ -715,21 +763,36 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         VSA_CHECK(hipStreamSynchronize(c->stream));
     }
     BatchPlan &pl = c->plan;
-    int r = build_plan(d_data, offs, lens, starts, hlens, rlos, nb,
-                       (uint64_t)c->num_cus * (LIT_WAVES - db->nconf), pl);
-    if (r != VSA_OK) return r;
-    if ((r = ensure_tables(c, nb, pl.segblk.size())) != VSA_OK) return r;
-    /* through the pinned mirror (pageable copies stage synchronously), one
-     * copy from the table's start to the segment map's end */
+    auto T0 = std::chrono::steady_clock::now();
+    /* the block table is built straight into the pinned mirror (pageable
+     * copies stage synchronously), the segment map after it; one copy of
+     * both */
+    int r;
+    if ((r = ensure_tables(c, nb, 0)) != VSA_OK) return r;
     Workspace &w = c->ws;
-    memcpy(w.h_blocks, pl.blocks.data(), nb * sizeof(VsaBlock));
+    if ((r = build_plan(d_data, offs, lens, starts, hlens, rlos, nb,
+                        (uint64_t)c->num_cus * (LIT_WAVES - db->nconf), pl, w.h_blocks)) !=
+        VSA_OK)
+        return r;
+    auto T1 = std::chrono::steady_clock::now();
+    if ((r = ensure_tables(c, nb, pl.segblk.size(), true)) != VSA_OK) return r;
     memcpy(w.h_segblk, pl.segblk.data(), pl.segblk.size() * sizeof(uint32_t));
     const size_t tab_bytes =
         (size_t)((uint8_t *)(w.h_segblk + pl.segblk.size()) - (uint8_t *)w.h_blocks);
+    auto T2 = std::chrono::steady_clock::now();
     VSA_CHECK(hipMemcpyAsync(w.d_blocks, w.h_blocks, tab_bytes, hipMemcpyHostToDevice,
                              c->stream));
-    return launch_planned(c, db, d_data, c->ws.d_blocks, c->ws.d_segblk, nb, pl.segblk.size(),
+    int rr = launch_planned(c, db, d_data, c->ws.d_blocks, c->ws.d_segblk, nb, pl.segblk.size(),
                           pl.seg_bytes, pl.end_bits, pl.bytes, flags, n_out);
+    auto T3 = std::chrono::steady_clock::now();
+    /* diagnostic: host-side cost of a per-call plan (tools/exp_host.py) */
+    static const bool timing = getenv("VSA_HOST_TIMING") != nullptr;
+    if (timing)
+        fprintf(stderr, "host: nb %u segs %zu build %.3f memcpy %.3f launch+wait %.3f ms (kernel %.3f)\n", nb, pl.segblk.size(),
+                std::chrono::duration<double, std::milli>(T1 - T0).count(),
+                std::chrono::duration<double, std::milli>(T2 - T1).count(),
+                std::chrono::duration<double, std::milli>(T3 - T2).count(), c->last_kernel_ms);
+    return rr;
 }
 
 /* Count + sort of the last launch; on an output overflow the buffers grow
@@ -1158,6 +1221,7 @@ int vsa_ctx_create(int device, vsa_ctx_t **out) {
     VSA_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     VSA_CHECK(hipEventCreate(&c->ev0));
     VSA_CHECK(hipEventCreate(&c->ev1));
+    VSA_CHECK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
     VSA_CHECK(hipMalloc(&c->ws.d_counters, N_COUNTERS * sizeof(unsigned long long)));
     VSA_CHECK(hipMalloc(&c->ws.d_bins, 2 * VSA_SORT_BINS * sizeof(uint32_t)));
     VSA_CHECK(hipHostMalloc((void **)&c->ws.h_counters, N_COUNTERS * sizeof(unsigned long long),
@@ -1184,6 +1248,7 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (w.h_blocks) (void)hipHostFree(w.h_blocks);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     (void)hipStreamDestroy(c->stream);
     if (t_ctx == c) t_ctx = nullptr;
     delete c;
