@@ -167,13 +167,20 @@ def run(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    dev = torch.device("cuda", local)
+    # VSA_BENCH_BACKEND=gloo rehearses the N > 1 path on fewer GPUs than
+    # ranks (ranks share devices round-robin); the driver's runs use RCCL
+    backend = os.environ.get("VSA_BENCH_BACKEND", "nccl")
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count())
+                       if backend != "nccl" else local)
     torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
-    ctx = vsa.Context(local)
+    ctx = vsa.Context(dev.index)
     lits = make_literals(args.lits, seed=12)
     blob = vsa.hwlm_build(lits)
     db = vsa.Database(ctx, blob)
@@ -196,42 +203,52 @@ def run(args):
     rlos = [w.rlo for w in wins]
     local_bytes = g1 - cuts[rank]
 
-    # N > 1: RCCL gather of the ranks' sorted records to rank 0 (device to
-    # device over xGMI), padded to the largest count
-    st = {"cap": 0, "gk": None, "gi": None, "keys": None, "ids": None}
+    # N > 1: ONE RCCL all-gather per step of every rank's sorted records
+    # (device to device over xGMI) in a packed int64 buffer [count | keys |
+    # ids], sized from the previous steps' largest count (grown, and the
+    # gather repeated, when a rank's count passes it); rank 0 merges the
+    # valid prefixes in rank order = global end order
+    st = {"cap": 0, "pk": None, "ag": None, "keys": None, "ids": None}
     g0s = None
     if dist is not None:
         t = torch.tensor([g0], dtype=torch.int64, device=dev)
         g0s_t = torch.zeros(world, dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(g0s_t, t)
         g0s = g0s_t.cpu().tolist()
+        koff = (g0s_t << 24).view(world, 1)
+
+    def gather(n_local):
+        cap = st["cap"]
+        pk = st["pk"]
+        ids32 = pk.view(torch.int32)
+        pk[0:1].fill_(n_local)
+        ctx.results_to_device(pk[1:].data_ptr(), ids32[2 * (1 + cap):].data_ptr(), cap)
+        ctx.sync()
+        dist.all_gather_into_tensor(st["ag"], pk)
+        return st["ag"].view(world, -1)[:, 0].cpu().tolist()
+
+    def grow(m):
+        st["cap"] = cap = max(1024, m + m // 4)
+        st["pk"] = torch.zeros(1 + 2 * cap, dtype=torch.int64, device=dev)
+        st["ag"] = torch.zeros(world * (1 + 2 * cap), dtype=torch.int64, device=dev)
 
     def step():
         n_local = ctx.scan_blocks_ex(db, dptr, offs, lens, None, rlos)
         if dist is None:
             return n_local
-        cnt = torch.tensor([n_local], dtype=torch.int64, device=dev)
-        counts = torch.zeros(world, dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(counts, cnt)
-        cl = counts.cpu().tolist()
-        m = max(max(cl), 1)
-        if m > st["cap"]:
-            st["cap"] = m + m // 4
-            st["gk"] = torch.zeros(st["cap"], dtype=torch.int64, device=dev)
-            st["gi"] = torch.zeros(st["cap"], dtype=torch.int32, device=dev)
-            st["ak"] = torch.zeros(world * st["cap"], dtype=torch.int64, device=dev)
-            st["ai"] = torch.zeros(world * st["cap"], dtype=torch.int32, device=dev)
-        ctx.results_to_device(st["gk"].data_ptr(), st["gi"].data_ptr(), st["cap"])
-        ctx.sync()
-        ak, ai = st["ak"][:world * m], st["ai"][:world * m]
-        dist.all_gather_into_tensor(ak, st["gk"][:m])
-        dist.all_gather_into_tensor(ai, st["gi"][:m])
+        if st["pk"] is None:
+            grow(0)  # the same size on every rank; the gathered counts set it
+        cl = gather(n_local)
+        if max(cl) > st["cap"]:
+            grow(max(cl))
+            cl = gather(n_local)
         if rank == 0:
-            # merge in end order: ranks own increasing end ranges; keys
-            # become global corpus offsets
-            st["keys"] = torch.cat([ak[r * m:r * m + cl[r]] + (g0s[r] << 24)
-                                    for r in range(world)])
-            st["ids"] = torch.cat([ai[r * m:r * m + cl[r]] for r in range(world)])
+            cap = st["cap"]
+            ag = st["ag"].view(world, 1 + 2 * cap)
+            k2 = ag[:, 1:1 + cap] + koff
+            i2 = ag.view(torch.int32)[:, 2 * (1 + cap):2 * (1 + cap) + cap]
+            st["keys"] = torch.cat([k2[r, :cl[r]] for r in range(world)])
+            st["ids"] = torch.cat([i2[r, :cl[r]] for r in range(world)])
         return int(sum(cl))
 
     for _ in range(args.warmup):

@@ -1,1 +1,4 @@
-for v in "VSA_NCONF=2 VSA_DEBUG_FLAGS=64" "VSA_NCONF=2 VSA_DEBUG_FLAGS=32" "VSA_FDR_DOMAIN=13 VSA_NCONF=2" "VSA_FDR_DOMAIN=13 VSA_NCONF=3" "VSA_FDR_DOMAIN=13 VSA_NCONF=4" "VSA_FDR_DOMAIN=14 VSA_NCONF=3"; do echo "$v"; env $v LITS=20000 timeout -k 10 200 python3 tools/exp_counters.py || exit 1; done
+#!/bin/bash
+# parity of the literal-scan kernel, then kernel time vs literal-set size
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/par.log 2>&1; rc=$?; echo par rc=$rc; tail -2 gpurun_out/par.log; [ $rc -eq 0 ] || exit $rc
+for n in 5000 10000 20000 50000; do LITS=$n timeout -k 10 200 python3 tools/exp_counters.py | grep lits || exit 1; done
