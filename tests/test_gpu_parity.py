@@ -493,3 +493,38 @@ def test_gpu_binned_sort(ctx):
             db.close()
     finally:
         ctx.free(d)
+
+
+def test_gpu_plan_memo(ctx):
+    """A repeated block list reuses the device tables of the previous call;
+    any change (an offset, a length, a start, the buffer) rebuilds them."""
+    rng = random.Random(23)
+    db = vsa.Database(ctx, vsa.hwlm_build(rand_lits(rng, 150, minlen=2, maxlen=8)))
+    host = np.frombuffer(rand_data(rng, 1 << 20), np.uint8).copy()
+    d = ctx.malloc(len(host) + 64)
+    try:
+        ctx.h2d(d, host)
+        offs = [0, 1000, 5000, 300000]
+        lens = [900, 3000, 200000, 700000]
+
+        def run(o, l, starts=None, ptr=d):
+            n = ctx.scan_blocks(db, ptr, o, l, starts)
+            return ctx.results(n)
+
+        base = run(offs, lens)
+        variants = [(offs, lens[:3] + [600000], None, d), (offs[:3] + [300016], lens, None, d),
+                    (offs, lens, [0, 10, 0, 5], d), (offs, lens, None, d + 16)]
+        for o, l, st, ptr in variants:
+            plan = ctx.plan(ptr, o, l, st)  # tables built from scratch
+            want = ctx.results(ctx.scan_plan(db, plan))
+            plan.close()
+            for _ in range(2):  # a rebuild, then the memoised tables
+                got = run(o, l, st, ptr)
+                assert np.array_equal(got["key"], want["key"])
+                assert np.array_equal(got["id"], want["id"])
+            back = run(offs, lens)
+            assert np.array_equal(back["key"], base["key"])
+            assert np.array_equal(back["id"], base["id"])
+        db.close()
+    finally:
+        ctx.free(d)

@@ -150,6 +150,16 @@ struct vsa_ctx {
     const uint8_t *res_host = nullptr;
     size_t res_len = 0;
     BatchPlan plan; /* the per-call batch plan (reused storage) */
+    /* the inputs of the plan now in ws.d_blocks: a call with the same block
+     * list (a scan repeated over the same buffers) reuses the device tables
+     * instead of rebuilding and uploading them */
+    struct {
+        bool valid = false;
+        const uint8_t *d_data = nullptr;
+        uint64_t waves = 0;
+        uint32_t nb = 0;
+        std::vector<uint64_t> in[5]; /* offs, lens, starts, hlens, rlos ({} = NULL) */
+    } memo;
     bool host_sort = false; /* the last scan's records are left unsorted */
 };
 
@@ -764,24 +774,42 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
     }
     BatchPlan &pl = c->plan;
     auto T0 = std::chrono::steady_clock::now();
-    /* the block table is built straight into the pinned mirror (pageable
-     * copies stage synchronously), the segment map after it; one copy of
-     * both */
+    const uint64_t waves = (uint64_t)c->num_cus * (LIT_WAVES - db->nconf);
+    const uint64_t *in[5] = {offs, lens, starts, hlens, rlos};
+    auto &M = c->memo;
+    bool same = M.valid && M.d_data == d_data && M.nb == nb && M.waves == waves;
+    for (int k = 0; same && k < 5; k++)
+        same = in[k] ? (M.in[k].size() == nb && !memcmp(M.in[k].data(), in[k], nb * 8))
+                     : M.in[k].empty();
     int r;
-    if ((r = ensure_tables(c, nb, 0)) != VSA_OK) return r;
     Workspace &w = c->ws;
-    if ((r = build_plan(d_data, offs, lens, starts, hlens, rlos, nb,
-                        (uint64_t)c->num_cus * (LIT_WAVES - db->nconf), pl, w.h_blocks)) !=
-        VSA_OK)
-        return r;
-    auto T1 = std::chrono::steady_clock::now();
-    if ((r = ensure_tables(c, nb, pl.segblk.size(), true)) != VSA_OK) return r;
-    memcpy(w.h_segblk, pl.segblk.data(), pl.segblk.size() * sizeof(uint32_t));
-    const size_t tab_bytes =
-        (size_t)((uint8_t *)(w.h_segblk + pl.segblk.size()) - (uint8_t *)w.h_blocks);
-    auto T2 = std::chrono::steady_clock::now();
-    VSA_CHECK(hipMemcpyAsync(w.d_blocks, w.h_blocks, tab_bytes, hipMemcpyHostToDevice,
-                             c->stream));
+    auto T1 = T0, T2 = T0;
+    if (!same) {
+        /* the block table is built straight into the pinned mirror (pageable
+         * copies stage synchronously), the segment map after it; one copy of
+         * both */
+        M.valid = false;
+        if ((r = ensure_tables(c, nb, 0)) != VSA_OK) return r;
+        if ((r = build_plan(d_data, offs, lens, starts, hlens, rlos, nb, waves, pl,
+                            w.h_blocks)) != VSA_OK)
+            return r;
+        T1 = std::chrono::steady_clock::now();
+        if ((r = ensure_tables(c, nb, pl.segblk.size(), true)) != VSA_OK) return r;
+        memcpy(w.h_segblk, pl.segblk.data(), pl.segblk.size() * sizeof(uint32_t));
+        const size_t tab_bytes =
+            (size_t)((uint8_t *)(w.h_segblk + pl.segblk.size()) - (uint8_t *)w.h_blocks);
+        T2 = std::chrono::steady_clock::now();
+        VSA_CHECK(hipMemcpyAsync(w.d_blocks, w.h_blocks, tab_bytes, hipMemcpyHostToDevice,
+                                 c->stream));
+        M.d_data = d_data;
+        M.nb = nb;
+        M.waves = waves;
+        for (int k = 0; k < 5; k++) {
+            if (in[k]) M.in[k].assign(in[k], in[k] + nb);
+            else M.in[k].clear();
+        }
+        M.valid = true;
+    }
     int rr = launch_planned(c, db, d_data, c->ws.d_blocks, c->ws.d_segblk, nb, pl.segblk.size(),
                           pl.seg_bytes, pl.end_bits, pl.bytes, flags, n_out);
     auto T3 = std::chrono::steady_clock::now();
