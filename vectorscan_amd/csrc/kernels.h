@@ -68,7 +68,7 @@ enum VsaLitMode {
 #define VSA_SORT_BIN_BITS 14
 #define VSA_SORT_BINS (1u << VSA_SORT_BIN_BITS)
 #define VSA_SORT_BIN_MAX 64
-#define VSA_CTR_BIN_OVERFLOW 12
+#define VSA_CTR_BIN_OVERFLOW 12 /* counters[12]: some bin passed VSA_SORT_BIN_MAX */
 
 struct VsaLitParams {
     const uint8_t *data;
@@ -110,11 +110,6 @@ struct VsaLitParams {
     uint64_t *out_keys;
     uint32_t *out_ids;
     uint64_t out_cap;
-    uint32_t *bins;              /* VSA_SORT_BINS record counts by end >> bin_shift
-                                    (the binned sort, runtime.hip finish_scan);
-                                    NULL: none.  counters[12] set when a bin
-                                    passes VSA_SORT_BIN_MAX records */
-    uint32_t bin_shift;
     unsigned long long *counters; /* [0] matches, [16 + 16 r] region tickets,
                                      [2] candidates handed to confirm (after
                                      the slot prefilter; diagnostic) */

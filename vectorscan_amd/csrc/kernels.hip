@@ -260,17 +260,6 @@ __device__ __forceinline__ u32 conf_hash(u64 key, u64 andmsk, u64 mult, u32 nbit
  * v whose start lies inside the block.  The candidates' global loads
  * (litIndex slot, block record, each chain step) are independent, so they
  * are issued together: one memory latency per chain step for all of them. */
-/* the binned sort's histogram (runtime.hip finish_scan): one count per
- * record written, by its end's top bits; a bin past VSA_SORT_BIN_MAX flags
- * the launch for the library sort instead */
-__device__ __forceinline__ void bin_count(const VsaLitParams &P, u64 end) {
-    if (!P.bins) return;
-    const u32 old = atomicAdd(&P.bins[(u32)(end >> P.bin_shift)], 1u);
-    if (old == VSA_SORT_BIN_MAX)
-        __hip_atomic_store(&P.counters[VSA_CTR_BIN_OVERFLOW], 1ULL, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
 template <int CONF_U>
 __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfLds &cl,
                                               const QEnt (&q)[CONF_U], const bool (&valid)[CONF_U],
@@ -346,7 +335,6 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
                                        ((u64)b[i] << VSA_KEY_BUCKET_SHIFT) | lidx;
                     P.out_ids[slot] = w1[i].z;
                 }
-                if (mt[i]) bin_count(P, base[i] + (u64)e[i]);
             }
         }
 #pragma unroll
@@ -971,7 +959,6 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                         P.out_keys[slot] = (p0 + j - mis) << VSA_KEY_END_SHIFT;
                         P.out_ids[slot] = P.nood_id;
                     }
-                    bin_count(P, p0 + j - mis);
                 }
             }
             continue;
@@ -1073,6 +1060,26 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
     }
 }
 
+/* dst[i] = src(i) for i < n, thread tid of LIT_THREADS: UNR loads issued
+ * before their LDS stores (a plain strided loop waits out one memory round
+ * trip per step: ~8 of them for a 128 KiB table at every launch) */
+template <int UNR, typename TV, typename F>
+__device__ __forceinline__ void stage_lds(TV *dst, u32 n, u32 tid, F &&src) {
+    for (u32 base = 0; base < n; base += UNR * LIT_THREADS) {
+        TV v[UNR];
+#pragma unroll
+        for (int k = 0; k < UNR; k++) {
+            const u32 i = base + (u32)k * LIT_THREADS + tid;
+            if (i < n) v[k] = src(i);
+        }
+#pragma unroll
+        for (int k = 0; k < UNR; k++) {
+            const u32 i = base + (u32)k * LIT_THREADS + tid;
+            if (i < n) dst[i] = v[k];
+        }
+    }
+}
+
 template <int MODE, bool LDS_TABLE>
 __global__ void __launch_bounds__(LIT_THREADS)
 vsa_lit_scan(VsaLitParams P) {
@@ -1095,8 +1102,7 @@ vsa_lit_scan(VsaLitParams P) {
         if (LDS_TABLE) {
             tab_bytes = P.table_entries * 8;
             const uint4 *src = (const uint4 *)P.table;
-            uint4 *dst = (uint4 *)smem;
-            for (u32 i = tid; i < tab_bytes / 16; i += LIT_THREADS) dst[i] = src[i];
+            stage_lds<8>((uint4 *)smem, tab_bytes / 16, tid, [&](u32 i) { return src[i]; });
             tab = smem;
         } else {
             tab = P.table;
@@ -1109,8 +1115,7 @@ vsa_lit_scan(VsaLitParams P) {
          * bank pairs and the address of byte c is 0x10000 | c << 8 |
          * (lane & 31) << 3: one v_perm (TEDDY_TAB_LDS) */
         u8 *tb = smem + (TEDDY_TAB_LDS - (u32)(uintptr_t)(lds_u8_t *)smem);
-        u64 *dst = (u64 *)tb;
-        for (u32 i = tid; i < 256 * 32; i += LIT_THREADS) dst[i] = P.table[i >> 5];
+        stage_lds<8>((u64 *)tb, 256 * 32, tid, [&](u32 i) { return P.table[i >> 5]; });
         tab = tb;
     }
     /* one ring of qcap entries per scanning wave, the slot bitmaps, then the
@@ -1120,7 +1125,7 @@ vsa_lit_scan(VsaLitParams P) {
     uint4 *rings = (uint4 *)(smem + ((tab_bytes + 15) & ~15u));
     u32 *slots = (u32 *)(rings + (size_t)NS * P.qcap * T::EW);
     QEnt *pqx = (QEnt *)(slots + ((P.slot_words + 3) & ~3u));
-    for (u32 i = tid; i < P.slot_words; i += LIT_THREADS) slots[i] = P.slotmap[i];
+    stage_lds<4>(slots, P.slot_words, tid, [&](u32 i) { return P.slotmap[i]; });
     if (tid < 16) {
         const u32 off = P.conf_off[tid];
         cl.off[tid] = off;
@@ -1434,22 +1439,39 @@ template __global__ void vsa_lit_scan<VSA_MODE_NOOD, false>(VsaLitParams);
 
 /* ====================================================== binned sort === */
 
-/* Match records sorted in three short launches instead of a library sort's
+/* Match records sorted in four short launches instead of a library sort's
  * dozen (runtime.hip finish_scan): bins = VSA_SORT_BINS ranges of end
- * positions counted by the scan kernel (bin_count); (1) exclusive scan of the
- * counts, (2) scatter into bin order, (3) one wave sorts each bin (<= 64
- * records: a register bitonic sort on the full key).  Keys are unique (end,
+ * positions; (1) a histogram of the records' bins (outside the scan kernel,
+ * whose confirm loop then carries no per-record atomic), (2) exclusive scan
+ * of the counts, (3) scatter into bin order, (4) one wave sorts each bin
+ * (<= 64 records: a register bitonic sort on the full key).  Keys are unique (end,
  * bucket, LitInfo), so the result equals the full sort. */
-__global__ void __launch_bounds__(1024) vsa_bin_scan(const uint32_t *counts, uint32_t *cursor) {
+__global__ void __launch_bounds__(256) vsa_bin_hist(const uint64_t *keys, const uint64_t *ctr,
+                                                    uint64_t cap, uint32_t bin_shift,
+                                                    uint32_t *counts) {
+    const uint64_t n0 = ctr[0];
+    const uint64_t n = n0 > cap ? 0 : n0; /* an overflowed launch runs again */
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * 256)
+        __hip_atomic_fetch_add(&counts[(uint32_t)((keys[i] >> VSA_KEY_END_SHIFT) >> bin_shift)],
+                               1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(1024) vsa_bin_scan(const uint32_t *counts, uint32_t *cursor,
+                                                    uint64_t *ctr) {
     __shared__ uint32_t part[1024];
     const uint32_t t = threadIdx.x;
     constexpr uint32_t PER = VSA_SORT_BINS / 1024;
-    uint32_t v[PER], sum = 0;
+    uint32_t v[PER], sum = 0, big = 0;
 #pragma unroll
     for (uint32_t k = 0; k < PER; k++) {
         v[k] = counts[t * PER + k];
         sum += v[k];
+        big |= v[k] > VSA_SORT_BIN_MAX;
     }
+    /* a crowded bin: the scatter and sort stand down (bin_records) and the
+     * host sorts with the library */
+    if (big) ctr[VSA_CTR_BIN_OVERFLOW] = 1;
     part[t] = sum;
     __syncthreads();
     for (uint32_t d = 1; d < 1024; d <<= 1) {

@@ -39,7 +39,9 @@
 template <int MODE, bool LDS_TABLE>
 __global__ void vsa_lit_scan(VsaLitParams P);
 __global__ void vsa_class_scan(VsaClassParams P);
-__global__ void vsa_bin_scan(const uint32_t *counts, uint32_t *cursor);
+__global__ void vsa_bin_hist(const uint64_t *keys, const uint64_t *ctr, uint64_t cap,
+                             uint32_t bin_shift, uint32_t *counts);
+__global__ void vsa_bin_scan(const uint32_t *counts, uint32_t *cursor, uint64_t *ctr);
 __global__ void vsa_bin_scatter(const uint64_t *keys, const uint32_t *ids, const uint64_t *ctr,
                                 uint64_t cap, uint32_t bin_shift, uint32_t *cursor,
                                 uint64_t *okeys, uint32_t *oids);
@@ -426,7 +428,11 @@ int queue_bin_sort(vsa_ctx *c) {
     Workspace &w = c->ws;
     uint32_t *counts = w.d_bins, *cursor = w.d_bins + VSA_SORT_BINS;
     const uint32_t shift = bin_shift_for(c->launch.end_bits);
-    hipLaunchKernelGGL(vsa_bin_scan, dim3(1), dim3(1024), 0, c->stream, counts, cursor);
+    hipLaunchKernelGGL(vsa_bin_hist, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, c->stream,
+                       w.d_keys[0], (const uint64_t *)w.d_counters, (uint64_t)w.out_cap, shift,
+                       counts);
+    hipLaunchKernelGGL(vsa_bin_scan, dim3(1), dim3(1024), 0, c->stream, counts, cursor,
+                       (uint64_t *)w.d_counters);
     hipLaunchKernelGGL(vsa_bin_scatter, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, c->stream,
                        w.d_keys[0], w.d_ids[0], (const uint64_t *)w.d_counters,
                        (uint64_t)w.out_cap, shift, cursor, w.d_keys[1], w.d_ids[1]);
@@ -443,7 +449,9 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
 int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
                 uint64_t nsegs, uint32_t seg_bytes) {
     VSA_CHECK(hipMemsetAsync(c->ws.d_counters, 0, 144 * sizeof(unsigned long long), c->stream));
-    c->launch.bins = use_bins(c);
+    /* not for the drop-in calls, whose few records the host sorts (a
+     * larger result takes the library sort) */
+    c->launch.bins = use_bins(c) && !(c->launch.flags & SCAN_HOST_SORT_SMALL);
     if (c->launch.bins && !c->bins_clean)
         VSA_CHECK(hipMemsetAsync(c->ws.d_bins, 0, VSA_SORT_BINS * sizeof(uint32_t), c->stream));
     c->bins_clean = false;
@@ -453,9 +461,8 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
     VSA_CHECK(hipEventRecord(c->ev1, c->stream));
     /* the binned sort queues behind the scan with no host round trip: its
      * kernels read the record count and the overflow flag on the device
-     * (finish_scan falls back to the library sort if a bin overflowed).  Not
-     * for the drop-in calls, whose few records the host sorts. */
-    c->launch.dev_sort = c->launch.bins && !(c->launch.flags & SCAN_HOST_SORT_SMALL);
+     * (finish_scan falls back to the library sort if a bin overflowed) */
+    c->launch.dev_sort = c->launch.bins;
     if (c->launch.dev_sort) return queue_bin_sort(c);
     return VSA_OK;
 }
@@ -484,8 +491,6 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         P.out_ids = w.d_ids[0];
         P.out_cap = w.out_cap;
         P.counters = w.d_counters;
-        P.bins = c->launch.bins ? w.d_bins : nullptr;
-        P.bin_shift = bin_shift_for(c->launch.end_bits);
         {
             const char *e = getenv("VSA_DEBUG_FLAGS");
             P.dbg = e ? (uint32_t)atoi(e) : 0u;
@@ -522,8 +527,6 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.out_ids = w.d_ids[0];
     P.out_cap = w.out_cap;
     P.counters = w.d_counters;
-    P.bins = c->launch.bins ? w.d_bins : nullptr;
-    P.bin_shift = bin_shift_for(c->launch.end_bits);
     {
         const char *e = getenv("VSA_DEBUG_FLAGS");
         P.dbg = e ? (uint32_t)atoi(e) : 0u;
@@ -606,14 +609,11 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     /* a launch whose records crowd one bin sorts with the library; the next
      * few launches (likely as dense) skip the histogram */
     if (c->bin_skip) c->bin_skip--;
-    if (c->launch.bins && w.h_counters[VSA_CTR_BIN_OVERFLOW]) c->bin_skip = 16;
-    if (n > 1 && !(flags & VSA_SCAN_UNSORTED) && !c->host_sort && c->launch.bins &&
+    if (c->launch.dev_sort && w.h_counters[VSA_CTR_BIN_OVERFLOW]) c->bin_skip = 16;
+    if (n > 1 && !(flags & VSA_SCAN_UNSORTED) && !c->host_sort && c->launch.dev_sort &&
         !w.h_counters[VSA_CTR_BIN_OVERFLOW]) {
-        /* queued in launch_scan already, except for the drop-in calls */
-        if (!c->launch.dev_sort) {
-            int r = queue_bin_sort(c);
-            if (r != VSA_OK) return r;
-        }
+        /* sorted by the binned sort queued in launch_scan (its overflow
+         * flag, set by vsa_bin_scan, is in the counters just read) */
         c->cur = 1;
         c->bins_clean = true; /* vsa_bin_sort zeroes the counts it read */
     } else if (n > 1 && !(flags & VSA_SCAN_UNSORTED) && !c->host_sort) {
