@@ -133,3 +133,32 @@ def test_gpu_report_lo_keeps_start_state(ctx):
     finally:
         ctx.free(d)
         db.close()
+
+
+@pytest.mark.parametrize("nlits", [20000, 50000])
+def test_gpu_large_literal_sets(ctx, nlits, monkeypatch):
+    """Large FDR sets, where the confirm stage is the bound: the first launch
+    (>= 16 MiB) measures the confirm-candidate rate and the next ones run
+    with two confirm waves per workgroup; one launch also forces a single
+    confirm wave and one three (VSA_NCONF).  Every launch == the oracle."""
+    lits = bench.make_literals(nlits, seed=12)
+    blob = vsa.hwlm_build(lits)
+    data = bench.make_corpus(24 << 20, lits, seed=5, plant_every=16 << 10)
+    st, want = oracle.fdr_exec(vsa.engine_blob(blob), data, cap=1 << 23)
+    assert st == 0 and len(want) >= len(data) // (16 << 10)
+    n = len(data)
+    d = ctx.malloc(n + 64)
+    db = vsa.Database(ctx, blob)
+    try:
+        ctx.h2d(d, data)
+        for nconf in (None, None, "1", "3"):
+            if nconf:
+                monkeypatch.setenv("VSA_NCONF", nconf)
+            k = ctx.scan_blocks(db, d, [0], [n])
+            res = ctx.results(k)
+            got = list(zip((res["key"] >> np.uint64(24)).tolist(), res["id"].tolist()))
+            assert got == want, nconf
+    finally:
+        monkeypatch.delenv("VSA_NCONF", raising=False)
+        db.close()
+        ctx.free(d)
