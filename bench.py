@@ -193,12 +193,16 @@ def run(args):
     cuts, plan = stripe.plan_corpus_stripes(total, bl, world)
     wins = plan[rank]
     # this rank's bytes: its windows (own range + 7-byte halo), from g0
-    g0 = min((w.wlo for w in wins), default=cuts[rank]) & ~255
+    g0 = min((w.wlo for w in wins), default=cuts[rank]) & ~1023
     g1 = cuts[rank + 1]
     data = make_corpus_device(torch, g0, g1, total, lits, 5, plant_every, dev, pplan)
     torch.cuda.synchronize()
-    dptr = data.data_ptr()
-    offs = [w.wlo - g0 for w in wins]
+    # the rank's buffer holds corpus bytes [g0, g1): blocks are addressed in
+    # corpus coordinates from data_ptr - g0, so the match keys come out as
+    # global end offsets.  g0 is 1 KiB-aligned like the kernel's segment
+    # origins, so no read falls below the buffer.
+    dptr = data.data_ptr() - g0
+    offs = [w.wlo for w in wins]
     lens = [w.wlen for w in wins]
     rlos = [w.rlo for w in wins]
     local_bytes = g1 - cuts[rank]
@@ -209,13 +213,10 @@ def run(args):
     # gather repeated, when a rank's count passes it); rank 0 merges the
     # valid prefixes in rank order = global end order
     st = {"cap": 0, "pk": None, "ag": None, "keys": None, "ids": None}
-    g0s = None
     if dist is not None:
-        t = torch.tensor([g0], dtype=torch.int64, device=dev)
-        g0s_t = torch.zeros(world, dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(g0s_t, t)
-        g0s = g0s_t.cpu().tolist()
-        koff = (g0s_t << 24).view(world, 1)
+        # the context's stream, so the gather waits for the record copies on
+        # the GPU (no host sync)
+        ctx_stream = torch.cuda.ExternalStream(ctx.stream, device=dev)
 
     def gather(n_local):
         cap = st["cap"]
@@ -223,7 +224,7 @@ def run(args):
         ids32 = pk.view(torch.int32)
         pk[0:1].fill_(n_local)
         ctx.results_to_device(pk[1:].data_ptr(), ids32[2 * (1 + cap):].data_ptr(), cap)
-        ctx.sync()
+        torch.cuda.current_stream().wait_stream(ctx_stream)
         dist.all_gather_into_tensor(st["ag"], pk)
         return st["ag"].view(world, -1)[:, 0].cpu().tolist()
 
@@ -245,7 +246,7 @@ def run(args):
         if rank == 0:
             cap = st["cap"]
             ag = st["ag"].view(world, 1 + 2 * cap)
-            k2 = ag[:, 1:1 + cap] + koff
+            k2 = ag[:, 1:1 + cap]
             i2 = ag.view(torch.int32)[:, 2 * (1 + cap):2 * (1 + cap) + cap]
             st["keys"] = torch.cat([k2[r, :cl[r]] for r in range(world)])
             st["ids"] = torch.cat([i2[r, :cl[r]] for r in range(world)])
