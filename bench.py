@@ -208,48 +208,28 @@ def run(args):
     local_bytes = g1 - cuts[rank]
 
     # N > 1: ONE RCCL all-gather per step of every rank's sorted records
-    # (device to device over xGMI) in a packed int64 buffer [count | keys |
-    # ids], sized from the previous steps' largest count (grown, and the
-    # gather repeated, when a rank's count passes it); rank 0 merges the
-    # valid prefixes in rank order = global end order
-    st = {"cap": 0, "pk": None, "ag": None, "keys": None, "ids": None}
+    # (device to device over xGMI), stripe.PackedGather; rank 0 concatenates
+    # the ranks' valid prefixes = global end order (keys are corpus offsets)
+    st = {"keys": None, "ids": None}
     if dist is not None:
-        # the context's stream, so the gather waits for the record copies on
+        # the context's stream: the gather waits for the record copies on
         # the GPU (no host sync)
         ctx_stream = torch.cuda.ExternalStream(ctx.stream, device=dev)
+        pg = stripe.PackedGather(dist, world, dev)
 
-    def gather(n_local):
-        cap = st["cap"]
-        pk = st["pk"]
-        ids32 = pk.view(torch.int32)
-        pk[0:1].fill_(n_local)
-        ctx.results_to_device(pk[1:].data_ptr(), ids32[2 * (1 + cap):].data_ptr(), cap)
-        torch.cuda.current_stream().wait_stream(ctx_stream)
-        dist.all_gather_into_tensor(st["ag"], pk)
-        return st["ag"].view(world, -1)[:, 0].cpu().tolist()
+        def fill(kv, iv, cap):
+            ctx.results_to_device(kv.data_ptr(), iv.data_ptr(), cap)
 
-    def grow(m):
-        st["cap"] = cap = max(1024, m + m // 4)
-        st["pk"] = torch.zeros(1 + 2 * cap, dtype=torch.int64, device=dev)
-        st["ag"] = torch.zeros(world * (1 + 2 * cap), dtype=torch.int64, device=dev)
+        def wait():
+            torch.cuda.current_stream().wait_stream(ctx_stream)
 
     def step():
         n_local = ctx.scan_blocks_ex(db, dptr, offs, lens, None, rlos)
         if dist is None:
             return n_local
-        if st["pk"] is None:
-            grow(0)  # the same size on every rank; the gathered counts set it
-        cl = gather(n_local)
-        if max(cl) > st["cap"]:
-            grow(max(cl))
-            cl = gather(n_local)
+        cl = pg.gather(n_local, fill, wait)
         if rank == 0:
-            cap = st["cap"]
-            ag = st["ag"].view(world, 1 + 2 * cap)
-            k2 = ag[:, 1:1 + cap]
-            i2 = ag.view(torch.int32)[:, 2 * (1 + cap):2 * (1 + cap) + cap]
-            st["keys"] = torch.cat([k2[r, :cl[r]] for r in range(world)])
-            st["ids"] = torch.cat([i2[r, :cl[r]] for r in range(world)])
+            st["keys"], st["ids"] = pg.merged(cl)
         return int(sum(cl))
 
     for _ in range(args.warmup):

@@ -221,3 +221,55 @@ def test_digest_matches_oracle_list():
     want = oracle.digest_of([e for e, _ in m], [i for _, i in m])
     for t in (1, 2, 7, 16):
         assert oracle.digest_mt(vsa.engine_blob(blob), data, t) == want
+
+
+def _packed_worker(rank, world, port, q):
+    import torch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pg = st.PackedGather(dist, world)
+        out = []
+        # step 1 fits the initial 1,024; step 2 passes it on rank 1 (grow +
+        # repeat); step 3 has an empty rank
+        for n in ([3, 7, 0][rank], [10, 1500, 4][rank], [0, 0, 9][rank]):
+            keys = torch.arange(n, dtype=torch.int64) * 5 + (rank << 40)
+            ids = torch.arange(n, dtype=torch.int32) + 1000 * rank
+
+            def fill(kv, iv, cap):
+                m = min(n, cap)
+                kv[:m].copy_(keys[:m])
+                iv[:m].copy_(ids[:m])
+
+            counts = pg.gather(n, fill)
+            k, i = pg.merged(counts)
+            out.append((counts, k.tolist(), i.tolist(), pg.cap))
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_packed_gather_world3():
+    """bench.py's per-step exchange (stripe.PackedGather): one all-gather,
+    the buffer grown from the gathered counts when a rank passes it."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_packed_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for counts, keys, ids, cap in out:
+        want_k, want_i = [], []
+        for r, n in enumerate(counts):
+            want_k += [j * 5 + (r << 40) for j in range(n)]
+            want_i += [j + 1000 * r for j in range(n)]
+        assert keys == want_k and ids == want_i
+    assert [o[0] for o in out] == [[3, 7, 0], [10, 1500, 4], [0, 0, 9]]
+    assert out[0][3] == 1024 and out[1][3] == 1875

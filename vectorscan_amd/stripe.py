@@ -163,3 +163,57 @@ def gather_to_root(dist, keys, ids, n, root=0):
         if rank == root:
             out.append(torch.cat([r[:c] for r, c in zip(recv, counts)]))
     return tuple(out) if rank == root else None
+
+
+class PackedGather:
+    """bench.py's per-step exchange: ONE all-gather of every rank's sorted
+    records in a packed int64 buffer ``[count | keys (cap) | ids (cap int32)]``.
+
+    The buffer size must agree across ranks, so it starts at 1,024 records.
+    It grows to 1.25x the largest count every rank sees in the gathered
+    headers, and the gather is then repeated once.  ``fill(keys, ids, cap)``
+    writes this rank's first ``min(n, cap)`` records into the two views.
+    On device tensors it uses RCCL; on CPU tensors (tests) it uses gloo.
+    ``wait()``, if given, runs between the fill and the collective (bench.py:
+    the current stream waits on the scan context's stream)."""
+
+    def __init__(self, dist, world, device=None):
+        self.dist, self.world, self.device = dist, world, device
+        self.cap = 0
+        self.pk = self.ag = None
+        self._grow(0)
+
+    def _grow(self, m):
+        import torch
+        self.cap = cap = max(1024, m + m // 4)
+        self.pk = torch.zeros(1 + 2 * cap, dtype=torch.int64, device=self.device)
+        self.ag = torch.zeros(self.world * (1 + 2 * cap), dtype=torch.int64, device=self.device)
+
+    def _once(self, n, fill, wait):
+        cap = self.cap
+        self.pk[0:1].fill_(n)
+        import torch
+        ids32 = self.pk.view(torch.int32)
+        fill(self.pk[1:1 + cap], ids32[2 * (1 + cap):2 * (1 + cap) + cap], cap)
+        if wait is not None:
+            wait()
+        self.dist.all_gather_into_tensor(self.ag, self.pk)
+        return self.ag.view(self.world, -1)[:, 0].cpu().tolist()
+
+    def gather(self, n, fill, wait=None):
+        """every rank's record count (the records land in self.ag)"""
+        counts = self._once(n, fill, wait)
+        if max(counts) > self.cap:
+            self._grow(max(counts))
+            counts = self._once(n, fill, wait)
+        return counts
+
+    def merged(self, counts):
+        """the gathered records concatenated in rank order: (keys, ids)"""
+        import torch
+        cap = self.cap
+        ag = self.ag.view(self.world, 1 + 2 * cap)
+        keys = ag[:, 1:1 + cap]
+        ids = ag.view(torch.int32)[:, 2 * (1 + cap):2 * (1 + cap) + cap]
+        return (torch.cat([keys[r, :c] for r, c in enumerate(counts)]),
+                torch.cat([ids[r, :c] for r, c in enumerate(counts)]))
