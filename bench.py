@@ -62,6 +62,33 @@ def make_literals(n, seed=12, minlen=4, maxlen=8, nocase_frac=0.02):
     return lits
 
 
+def make_mixed_set(n, seed=21, minlen=4, maxlen=16, shared_ids=True):
+    """cfg-5-shaped pure-literal database (the regex mix of cfg 5 needs the
+    reference's full compiler, out of scope): n printable literals of length
+    minlen-maxlen (the ones past 8 bytes confirmed on the host), flags mixed
+    70 % plain / 10 % CASELESS / 10 % SINGLEMATCH / 10 % SOM_LEFTMOST, ~10 %
+    of ids shared by two patterns (SINGLEMATCH and SOM made consistent per
+    id, as hs_compile requires; hsbench expression files need unique ids:
+    shared_ids=False).  Returns (exprs, flags, ids)."""
+    from vectorscan_amd import hs
+    r = random.Random(seed)
+    mix = [0] * 7 + [hs.FLAG_CASELESS, hs.FLAG_SINGLEMATCH, hs.FLAG_SOM_LEFTMOST]
+    exprs, flags, ids = [], [], []
+    single, som = {}, {}
+    for i in range(n):
+        ln = r.randint(minlen, maxlen)
+        exprs.append(bytes(r.randint(0x20, 0x7E) for _ in range(ln)))
+        ident = r.randrange(i) if i and r.random() < 0.1 and shared_ids else i
+        f = r.choice(mix)
+        s = single.setdefault(ident, bool(f & hs.FLAG_SINGLEMATCH))
+        f = ((f | hs.FLAG_SINGLEMATCH) & ~hs.FLAG_SOM_LEFTMOST) if s else \
+            (f & ~hs.FLAG_SINGLEMATCH)
+        m = som.setdefault(ident, bool(f & hs.FLAG_SOM_LEFTMOST))
+        flags.append((f | hs.FLAG_SOM_LEFTMOST) if m else (f & ~hs.FLAG_SOM_LEFTMOST))
+        ids.append(ident)
+    return exprs, flags, ids
+
+
 def plant_plan(n, lits, seed, plant_every):
     """positions + literal bytes planted once per `plant_every` bytes."""
     r = np.random.default_rng(seed + 1)

@@ -200,3 +200,50 @@ def test_hsbench_main(tmp_path, capsys, mode_flag):
     blocks = [(i, s, d) for i, (s, d) in enumerate(chunks)]
     assert res["matches"] == sum(oracle_counts(exprs, [0] * len(exprs), ids, blocks, mode))
     assert "Mean throughput (overall):" in out and "WARNING" not in out
+
+
+def cfg5_case(nbytes, nstreams=8):
+    """the cfg-5-shaped pure-literal set (bench.make_mixed_set: 10k
+    literals, length 4-16, CASELESS / SINGLEMATCH / SOM_LEFTMOST mixed, shared
+    ids) planted once per 4 KiB in printable bytes, cut into 16 KiB chunks"""
+    import bench
+    exprs, flags, ids = bench.make_mixed_set(10000)
+    lits = [vsa.HwlmLiteral(e, False, i) for i, e in enumerate(exprs)]
+    data = bench.make_corpus(nbytes, lits, seed=9, plant_every=4 << 10)
+    chunks = [(k % nstreams, data[o:o + (16 << 10)].tobytes())
+              for k, o in enumerate(range(0, nbytes, 16 << 10))]
+    return exprs, flags, ids, [(i, s, d) for i, (s, d) in enumerate(chunks)]
+
+
+def test_cfg5_set_blob_and_oracle():
+    """CPU: the product's HWLM blob for the cfg-5-shaped set is the one built
+    from the oracle's fragment list, and the oracle's run over a chunk equals
+    the engine-free brute force"""
+    exprs, flags, ids, blocks = cfg5_case(64 << 10)
+    db = hs.compile_lit_multi(exprs, flags, ids, hs.MODE_BLOCK)
+    odb = ohs.compile_lit_multi(exprs, flags, ids)
+    lits = [vsa.HwlmLiteral(t, nc, f, noruns=nr) for t, nc, f, nr in odb.hwlm_literals()]
+    blob = vsa.hwlm_build(lits)
+    assert db.hwlm_bytes() == blob.tobytes()
+    data = np.frombuffer(blocks[1][2], np.uint8).copy()
+    got = ohs.scan(odb, blob.ptr, data)
+    assert len(got) > 0
+    assert sorted(got) == sorted(ohs.brute_force(odb, data))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [hs.MODE_BLOCK, hs.MODE_STREAM, hs.MODE_VECTORED])
+def test_cfg5_mixed_literal_db(mode):
+    """cfg-5-shaped database on 4 MiB of 16 KiB chunks: per-chunk match
+    counts of the one-launch corpus scan + host report replay vs the oracle"""
+    exprs, flags, ids, blocks = cfg5_case(4 << 20)
+    g = hsbench.GpuCorpus(exprs, ids, flags, blocks, mode)
+    try:
+        want = oracle_counts(exprs, flags, ids, blocks, mode)
+        total, counts = g.scan(counts=True)
+        assert list(counts) == want
+        assert total == sum(want) > 1000
+        t2, _ = g.scan()
+        assert t2 == total
+    finally:
+        g.close()

@@ -3,6 +3,16 @@
 set -o pipefail
 mkdir -p gpurun_out
 D=/tmp/hsb_$$
+if [ "$1" = "cfg5" ] || [ "$1" = "all" ]; then
+  # cfg-5-shaped: 10k mixed-flag pure literals (bench.make_mixed_set), block mode
+  python tools/make_hsbench_corpus.py --out ${D}_c5 --lits 10000 --bytes 1G --chunk 16K \
+      --streams 64 --mixed > gpurun_out/hsbench_gen.log 2>&1 || exit 1
+  echo "== mode block, cfg-5-shaped 10k mixed literals" >> gpurun_out/hsbench.log
+  timeout -k 10 300 python -u -m vectorscan_amd.hsbench -e ${D}_c5/sigs -c ${D}_c5/corpus.db \
+      -n 10 --literal-on --json -N >> gpurun_out/hsbench.log 2>&1 || exit 1
+  rm -rf ${D}_c5
+  [ "$1" = "cfg5" ] && { cat gpurun_out/hsbench.log; exit 0; }
+fi
 python tools/make_hsbench_corpus.py --out $D --lits 5000 --bytes 1G --chunk 16K --streams 64 \
     > gpurun_out/hsbench_gen.log 2>&1 || exit 1
 for m in -N -V ""; do

@@ -33,6 +33,11 @@
  */
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -116,6 +121,61 @@ vsa_hs_compile_error_t *make_error(const std::string &msg, int expression) {
 }
 
 bool valid_db(const vsa_hs_database_t *db) { return db && db->magic == DB_MAGIC; }
+
+/* Persistent workers for the corpus replay: starting 16 threads per call
+ * cost as much as the replay itself.  run(T, fn) runs fn(1..T-1) on the
+ * workers and fn(0) on the caller, and returns when all are done.  One job
+ * at a time (callers serialize on `call`); the pool is never destroyed (its
+ * idle threads end with the process). */
+struct ReplayPool {
+    std::mutex call, m;
+    std::condition_variable go, done;
+    std::vector<std::thread> th;
+    std::function<void(unsigned)> job;
+    unsigned njob = 0, pending = 0;
+    uint64_t gen = 0;
+
+    void run(unsigned T, const std::function<void(unsigned)> &fn) {
+        std::lock_guard<std::mutex> serial(call);
+        {
+            std::unique_lock<std::mutex> lk(m);
+            while (th.size() + 1 < T) {
+                const unsigned id = (unsigned)th.size() + 1;
+                th.emplace_back([this, id] { loop(id); });
+                th.back().detach();
+            }
+            job = fn;
+            njob = T;
+            pending = T - 1;
+            gen++;
+        }
+        go.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> lk(m);
+        done.wait(lk, [&] { return pending == 0; });
+        job = nullptr;
+    }
+    void loop(unsigned id) {
+        uint64_t seen = 0;
+        for (;;) {
+            std::function<void(unsigned)> f;
+            {
+                std::unique_lock<std::mutex> lk(m);
+                go.wait(lk, [&] { return gen != seen; });
+                seen = gen;
+                if (id >= njob) continue;
+                f = job;
+            }
+            f(id);
+            std::lock_guard<std::mutex> lk(m);
+            if (--pending == 0) done.notify_one();
+        }
+    }
+};
+ReplayPool &replay_pool() {
+    static ReplayPool *p = new ReplayPool();
+    return *p;
+}
 
 vsa_db_t *device_db(vsa_hs_scratch_t *s, const vsa_hs_database_t *db) {
     for (auto &e : s->dbs)
@@ -574,8 +634,15 @@ struct vsa_hs_corpus {
     const uint8_t *d_data = nullptr, *h_data = nullptr;
     std::vector<uint64_t> offsets, lens;
     bool streams = false;
-    std::vector<std::vector<uint32_t>> units; /* streams (or single blocks) */
-    std::vector<uint32_t> order;              /* live blocks by offset */
+    /* units = streams (or single blocks), CSR: unit u is blocks
+     * unit_blk[unit_off[u] .. unit_off[u + 1]) in write order */
+    std::vector<uint32_t> unit_off, unit_blk, blk_unit;
+    std::vector<uint32_t> order;  /* non-empty blocks by offset */
+    std::vector<uint64_t> so, se; /* their [offset, end) in that order */
+    /* per-scan record ranges, valid where bstamp == gen (no clearing) */
+    std::vector<uint64_t> rb, re;
+    std::vector<uint32_t> bstamp, ustamp;
+    uint32_t gen = 0;
     vsa_plan_t *plan = nullptr;
 };
 
@@ -621,13 +688,33 @@ int vsa_hs_corpus_prepare(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch
             lh.push_back(hl[b]);
         }
     }
+    c->blk_unit.assign(nblocks, 0);
+    c->unit_off.push_back(0);
     if (c->streams) {
-        for (auto &e : by_stream) c->units.push_back(std::move(e.second));
+        for (auto &e : by_stream) {
+            for (uint32_t b : e.second) {
+                c->blk_unit[b] = (uint32_t)c->unit_off.size() - 1;
+                c->unit_blk.push_back(b);
+            }
+            c->unit_off.push_back((uint32_t)c->unit_blk.size());
+        }
     } else {
-        for (uint32_t b = 0; b < nblocks; b++) c->units.push_back({b});
+        for (uint32_t b = 0; b < nblocks; b++) {
+            c->blk_unit[b] = b;
+            c->unit_blk.push_back(b);
+            c->unit_off.push_back(b + 1);
+        }
     }
-    std::sort(c->order.begin(), c->order.end(),
-              [&](uint32_t a, uint32_t b) { return offsets[a] < offsets[b]; });
+    std::stable_sort(c->order.begin(), c->order.end(),
+                     [&](uint32_t a, uint32_t b) { return offsets[a] < offsets[b]; });
+    for (uint32_t b : c->order) {
+        c->so.push_back(offsets[b]);
+        c->se.push_back(offsets[b] + lens[b]);
+    }
+    c->rb.assign(nblocks, 0);
+    c->re.assign(nblocks, 0);
+    c->bstamp.assign(nblocks, 0);
+    c->ustamp.assign(c->unit_off.size() - 1, 0);
     if (!lo.empty() &&
         vsa_plan_create(scratch->ctx, d_data, lo.data(), ln.data(), nullptr,
                         c->streams ? lh.data() : nullptr, nullptr, (uint32_t)lo.size(),
@@ -659,6 +746,13 @@ int vsa_hs_corpus_scan(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *total,
     if (counts) std::fill(counts, counts + nblocks, 0);
     *total = 0;
     const bool fast = db->simple && !counts;
+    /* VSA_HOST_TIMING: per-phase wall times on stderr */
+    static const bool timing = getenv("VSA_HOST_TIMING") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto t0 = now();
     std::vector<uint64_t> keys;
     std::vector<uint32_t> ids;
     uint64_t nm = 0;
@@ -674,50 +768,105 @@ int vsa_hs_corpus_scan(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *total,
         leave(scratch);
         return VSA_HS_SUCCESS;
     }
-    /* records -> blocks (ends are d_data offsets, sorted) */
-    std::vector<uint64_t> rb(nblocks, 0), re(nblocks, 0);
-    uint64_t k = 0;
-    for (uint32_t b : cp->order) {
-        const uint64_t hi = offsets[b] + lens[b];
-        while (k < nm && (keys[k] >> KEY_END_SHIFT) < offsets[b]) k++;
-        rb[b] = k;
-        while (k < nm && (keys[k] >> KEY_END_SHIFT) < hi) {
-            keys[k] -= offsets[b] << KEY_END_SHIFT;
-            k++;
-        }
-        re[b] = k;
+    const auto t1 = now();
+    /* records -> blocks: the records are sorted by end (d_data offsets),
+     * the non-empty blocks by offset; each run of records is placed with one
+     * binary search, so the cost follows the records, not the block count.
+     * Units holding records are the live ones (the others report nothing,
+     * their counts stay 0). */
+    if (++cp->gen == 0) {
+        std::fill(cp->bstamp.begin(), cp->bstamp.end(), 0);
+        std::fill(cp->ustamp.begin(), cp->ustamp.end(), 0);
+        cp->gen = 1;
     }
-    const auto &units = cp->units;
+    const uint32_t gen = cp->gen;
+    uint64_t *rb = cp->rb.data(), *re = cp->re.data();
+    const uint32_t *bstamp = cp->bstamp.data();
+    std::vector<uint32_t> live;
+    uint64_t live_recs = 0;
+    {
+        const auto &so = cp->so, &se = cp->se;
+        uint64_t k = 0;
+        size_t at = 0; /* search start: the runs come in increasing order */
+        while (k < nm) {
+            const uint64_t e = keys[k] >> KEY_END_SHIFT;
+            /* gallop from the previous run's block, then binary search */
+            size_t lo = at, step = 1;
+            while (lo + step < so.size() && so[lo + step] <= e) {
+                lo += step;
+                step <<= 1;
+            }
+            const size_t oi = (size_t)(std::upper_bound(so.begin() + lo,
+                                                        so.begin() + std::min(so.size(), lo + step),
+                                                        e) - so.begin());
+            at = oi ? oi - 1 : 0;
+            if (oi == 0 || e >= se[oi - 1]) { /* outside every block: not reported */
+                k++;
+                continue;
+            }
+            const uint32_t b = cp->order[oi - 1];
+            const uint64_t o = so[oi - 1], hi = se[oi - 1];
+            const uint64_t k0 = k;
+            while (k < nm && (keys[k] >> KEY_END_SHIFT) < hi) {
+                keys[k] -= o << KEY_END_SHIFT;
+                k++;
+            }
+            rb[b] = k0;
+            re[b] = k;
+            cp->bstamp[b] = gen;
+            const uint32_t u = cp->blk_unit[b];
+            if (cp->ustamp[u] != gen) {
+                cp->ustamp[u] = gen;
+                live.push_back(u);
+            }
+            live_recs += k - k0;
+        }
+    }
+    const uint32_t *unit_off = cp->unit_off.data(), *unit_blk = cp->unit_blk.data();
     const uint8_t *h_data = cp->h_data;
     const bool streams = cp->streams;
-    const unsigned T = std::max(1u, std::min<unsigned>(threads ? threads : 1,
-                                                        (unsigned)units.size()));
+    /* a thread per ~2k records (thread start-up costs more than replaying a
+     * few hundred) */
+    const unsigned T = (unsigned)std::max<uint64_t>(
+        1, std::min<uint64_t>({threads ? threads : 1u, live.size(), 1 + live_recs / 2048}));
     std::vector<uint64_t> part(T, 0);
     std::vector<int> status(T, VSA_HS_SUCCESS);
     auto work = [&](unsigned t) {
-        for (size_t u = t; u < units.size(); u += T) {
-            const auto &bl = units[u];
-            vsa_hs_stream st;
+        /* per-thread state, reused across units */
+        vsa_hs_stream st;
+        std::vector<const uint8_t *> bufs;
+        std::vector<size_t> bl_len;
+        uint64_t cnt = 0;
+        Run r{db, &st, count_match, &cnt, nullptr, nullptr, {}, 0};
+        for (size_t i = t; i < live.size(); i += T) {
+            const uint32_t *bl = unit_blk + unit_off[live[i]];
+            const size_t nbl = unit_off[live[i] + 1] - unit_off[live[i]];
             init_stream(&st, db);
-            uint64_t cnt = 0;
-            std::vector<const uint8_t *> bufs(bl.size());
-            std::vector<size_t> bl_len(bl.size());
-            for (size_t j = 0; j < bl.size(); j++) {
+            cnt = 0;
+            bufs.resize(nbl);
+            bl_len.resize(nbl);
+            for (size_t j = 0; j < nbl; j++) {
                 bufs[j] = h_data ? h_data + offsets[bl[j]] : nullptr;
                 bl_len[j] = lens[bl[j]];
             }
-            Run r{db, &st, count_match, &cnt, bufs.data(), bl_len.data(), {}, 0};
-            r.pos.resize(bl.size());
+            r.bufs = bufs.data();
+            r.lens = bl_len.data();
+            r.cur = 0;
+            r.last_to = ~0ULL;
+            r.at_to.clear();
+            r.som_log.clear();
+            r.terminated = false;
+            r.pos.resize(nbl);
             uint64_t o = 0;
-            for (size_t j = 0; j < bl.size(); j++) {
+            for (size_t j = 0; j < nbl; j++) {
                 r.pos[j] = o;
                 o += bl_len[j];
             }
-            for (size_t j = 0; j < bl.size(); j++) {
+            for (size_t j = 0; j < nbl; j++) {
                 const uint32_t b = bl[j];
                 const uint64_t before = cnt;
                 r.cur = j;
-                if (re[b] > rb[b] &&
+                if (bstamp[b] == gen && re[b] > rb[b] &&
                     vsa::replay_records(ddb, keys.data() + rb[b], ids.data() + rb[b],
                                         re[b] - rb[b], on_fragment, &r) != HWLM_SUCCESS) {
                     status[t] = VSA_HS_UNKNOWN_ERROR;
@@ -731,13 +880,14 @@ int vsa_hs_corpus_scan(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *total,
             part[t] += cnt;
         }
     };
-    if (T == 1) {
-        work(0);
-    } else {
-        std::vector<std::thread> pool;
-        for (unsigned t = 0; t < T; t++) pool.emplace_back(work, t);
-        for (auto &th : pool) th.join();
-    }
+    const auto t2 = now();
+    if (T == 1) work(0);
+    else replay_pool().run(T, work);
+    if (timing)
+        fprintf(stderr, "vsa_hs_corpus_scan: scan+copy %.3f ms, map %.3f ms, replay %.3f ms "
+                        "(%u threads, %zu live units, %llu records)\n",
+                ms(t0, t1), ms(t1, t2), ms(t2, now()), T, live.size(),
+                (unsigned long long)nm);
     leave(scratch);
     for (unsigned t = 0; t < T; t++) {
         if (status[t] != VSA_HS_SUCCESS) return status[t];
