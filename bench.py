@@ -299,6 +299,9 @@ def run(args):
     torch.cuda.empty_cache()
 
     out = None
+    # the CPU baseline is timed at N = 1 only (on rank 0); N > 1 runs check
+    # parity alone
+    with_cpu = not args.no_cpu and world == 1
     if rank == 0:
         import oracle
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
@@ -314,7 +317,7 @@ def run(args):
                 host = make_corpus_device(torch, lo, hi, total, lits, 5, plant_every, dev,
                                           pplan).cpu().numpy()
                 want.append(oracle.digest_mt(eng, host, threads))
-                if not args.no_cpu:
+                if with_cpu:
                     # CPU baseline: the SSE2 port of fdr.c's main loop
                     # (get_conf_stride_1 :145-213 + confirm), same bytes,
                     # same host threads; its result must match as well
@@ -328,7 +331,7 @@ def run(args):
             if not parity:
                 print("bench: PARITY FAILURE got %s want %s sorted %s" % (got, want, sorted_ok),
                       file=sys.stderr, flush=True)
-            if not args.no_cpu:
+            if with_cpu:
                 cpu = {"value": round(parity_bytes / t_cpu / 1e9, 4), "unit": "GB/s",
                        "cores": threads, "kind": "port", "match_set_equal": cpu_ok,
                        "sample": "the whole %d-byte corpus, 4 x 1 GiB blocks: oracle/oracle.c "

@@ -549,22 +549,37 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
         look_m = range_mask(rel32(MODE == VSA_MODE_FDR ? S.zbase : S.qlo, q0), r_len);
     }
 
+    /* FDR (LDS table): the lane looks up positions -1 .. 14, keyed by the
+     * byte pairs (j - 1, j), so no key needs the byte after its chunk and
+     * the sweep never waits on the next chunk's load; byte -1 is the previous
+     * lane's last byte (lane 0: the previous chunk's, in.pbytes).  Position
+     * 15 is the next lane's (or chunk's) position -1.  Only field 0 of end -1
+     * is left out: a one-byte constraint on b[e] that field 1 (b[e - 1],
+     * b[e]) implies (derive_fdr_table) — the filter stays a superset. */
+    constexpr bool FDR_BACK = MODE == VSA_MODE_FDR && LDS_TABLE;
+    u32 pv3 = lane_up1(d[3]);
+    if (lane == 0) pv3 = (u32)(in.pbytes >> 32);
+    if constexpr (FDR_BACK) {
+        if (EDGE) look_m = range_mask(rel32(S.zbase, q0) + 1, rel32(S.len, q0) + 1);
+    }
+
     /* own contributions: the lane's 16 lookups ... */
     S_t x[16];
     u32 km[4], ko[4]; /* FDR/LDS: keys of even / odd positions, two per dword */
-    if constexpr (MODE == VSA_MODE_FDR && LDS_TABLE) {
+    if constexpr (FDR_BACK) {
 #pragma unroll
         for (int w = 0; w < 4; w++) {
+            /* km: positions 4w, 4w + 2; ko: 4w - 1, 4w + 1 */
             km[w] = fdr_key2(d[w], L.kmask2);
-            ko[w] = fdr_key2(__builtin_amdgcn_alignbyte(d[w + 1], d[w], 1), L.kmask2);
+            ko[w] = fdr_key2(__builtin_amdgcn_alignbyte(d[w], w ? d[w - 1] : pv3, 3), L.kmask2);
         }
     }
 #pragma unroll
     for (int j = 0; j < 16; j++) {
-        if constexpr (MODE == VSA_MODE_FDR && LDS_TABLE) {
-            /* position 4w + r: key = 16-bit half r >> 1 of km[w] (r even)
-             * or ko[w] (r odd) */
-            const u32 kw = (j & 1) ? ko[j >> 2] : km[j >> 2];
+        if constexpr (FDR_BACK) {
+            /* x[j] = position j - 1 = 4w + r - 1: ko[w] (r even) or km[w]
+             * (r odd), 16-bit half r >> 1 */
+            const u32 kw = (j & 1) ? km[j >> 2] : ko[j >> 2];
             const u32 a = (j & 2) ? tab_addr16<1>(kw, L.tab_lds) : tab_addr16<0>(kw, L.tab_lds);
             x[j] = lds_ld64(a);
         } else if constexpr (MODE == VSA_MODE_TEDDY || MODE == VSA_MODE_FAT) {
@@ -589,6 +604,20 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     u32 c[T::CW];
     u64 s_out;
     conf_accumulate<MODE>(x, c, s_out);
+    if constexpr (FDR_BACK) {
+        /* x[j] sat at position j - 1: every end one byte down (end -1, the
+         * byte shifted out, held only field 0 of position -1) */
+        const u32 f4 = (u32)s_out, f5 = (u32)(s_out >> 32);
+        const u32 c0 = __builtin_amdgcn_alignbyte(c[1], c[0], 1);
+        const u32 c1 = __builtin_amdgcn_alignbyte(c[2], c[1], 1);
+        const u32 c2 = __builtin_amdgcn_alignbyte(c[3], c[2], 1);
+        const u32 c3 = __builtin_amdgcn_alignbyte(f4, c[3], 1);
+        c[0] = c0;
+        c[1] = c1;
+        c[2] = c2;
+        c[3] = c3;
+        s_out = ((u64)(f5 >> 8) << 32) | __builtin_amdgcn_alignbyte(f5, f4, 1);
+    }
     /* spill from the previous lane (lane 0: from the previous chunk) */
     const u32 s_in_lo = writelane_u32<0>(lane_up1((u32)s_out), (u32)in.carry);
     const u32 s_in_hi = sizeof(S_t) == 8
@@ -657,11 +686,8 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     if (P.dbg & 8) return out;
 
     /* bytes p0-8 .. p0+15 for the 8-byte confirm keys */
-    u32 pv2 = lane_up1(d[2]), pv3 = lane_up1(d[3]);
-    if (lane == 0) {
-        pv2 = (u32)in.pbytes;
-        pv3 = (u32)(in.pbytes >> 32);
-    }
+    u32 pv2 = lane_up1(d[2]);
+    if (lane == 0) pv2 = (u32)in.pbytes;
     /* one chunk entry per lane with candidates; the confirm wave expands it */
     const u64 meta = (u64)p0 | ((u64)S.blk << ENT_BLK_SHIFT);
     u32 w[4 * T::EW];
@@ -807,7 +833,9 @@ __device__ __forceinline__ uint4 load_wave_kib(const u8 *base, u32 off) {
     return make_uint4(t.x, t.y, t.z, t.w);
 }
 
-#define LIT_DEPTH 4
+#ifndef LIT_DEPTH
+#define LIT_DEPTH 4 /* chunks in flight per scanning wave (1 KiB each) */
+#endif
 
 /* A workgroup's confirm wave (one, or several for large literal sets, each
  * serving every nc-th ring): gathers up to 64 chunk entries per round from
