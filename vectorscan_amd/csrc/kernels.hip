@@ -1223,6 +1223,8 @@ vsa_lit_scan(VsaLitParams P) {
     L.lg = 31 - __clz(P.qcap);
     L.dbg = P.dbg;
 
+    if ((P.dbg & 2048) && lane == 0) /* diagnostic: first scanning-wave start */
+        atomicMax(&P.counters[8], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
     const u8 *A = P.data - mis;
     const int64_t SEG = (int64_t)P.seg_bytes;
     u32 ncand_total = 0;
@@ -1453,8 +1455,20 @@ vsa_lit_scan(VsaLitParams P) {
         } /* blocks of the segment */
         seg = P.dynamic ? resolve(t_next) : seg + G;
     }
+    if ((P.dbg & 2048) && lane == 0) {
+        /* diagnostic: earliest / latest scanning-wave end (100 MHz clock):
+         * the schedule's tail */
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        atomicMax(&P.counters[9], ~t);
+        atomicMax(&P.counters[10], t);
+    }
     /* every push of this wave precedes this (LDS order) */
-    if (lane == 0) __hip_atomic_fetch_add(&q_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0) {
+        const u32 prev = __hip_atomic_fetch_add(&q_done, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+        if ((P.dbg & 2048) && prev + 1 == NS) /* diagnostic: earliest CU done */
+            atomicMax(&P.counters[11], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
     if (P.counters && lane_id() == 0 && ncand_total)
         atomicAdd(&P.counters[2], (unsigned long long)ncand_total);
 }
