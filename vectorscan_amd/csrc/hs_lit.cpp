@@ -44,6 +44,7 @@
 #include <new>
 #include <string>
 #include <thread>
+#include <unistd.h>
 #include <vector>
 
 #include "vectorscan_amd.h"
@@ -135,10 +136,17 @@ struct ReplayPool {
     unsigned njob = 0, pending = 0;
     uint64_t gen = 0;
 
+    pid_t owner = getpid();
+
     void run(unsigned T, const std::function<void(unsigned)> &fn) {
         std::lock_guard<std::mutex> serial(call);
         {
             std::unique_lock<std::mutex> lk(m);
+            if (getpid() != owner) {
+                /* a forked child inherits the pool but not its threads */
+                th.clear();
+                owner = getpid();
+            }
             while (th.size() + 1 < T) {
                 const unsigned id = (unsigned)th.size() + 1;
                 th.emplace_back([this, id] { loop(id); });
