@@ -290,6 +290,12 @@ int64_t vsa_shufti_double_find(const uint8_t lo1[16], const uint8_t hi1[16],
 /* VECTORSIZE of the reference build whose shuftiDoubleExec is emulated
  * (16 SSE, 32 AVX2, 64 AVX-512; default 64). */
 void vsa_set_accel_vector_size(uint32_t vsize);
+
+/* Diagnostic: device buffer of 8 x u64 per scanning wave (workgroup * 16 +
+ * wave) that literal scans run with VSA_DEBUG_FLAGS bit 4096 fill (start and
+ * end timestamps at 100 MHz, segments, 1 KiB iterations, workgroup, wave,
+ * XCC id, HW_ID); NULL turns it off. */
+void vsa_set_wave_log(void *d_log);
 /* shufticompile.cpp:135 shuftiBuildDoubleMasks: onechar = 256-bit class
  * (may be NULL), pairs = npairs (first, second) bytes.  0 ok, -1 = more
  * than 8 buckets needed. */

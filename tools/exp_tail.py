@@ -3,7 +3,7 @@ first scanning-wave start, earliest and latest scanning-wave end, per launch."""
 import os
 import sys
 
-os.environ["VSA_DEBUG_FLAGS"] = "2048"
+os.environ["VSA_DEBUG_FLAGS"] = str(2048 | int(os.environ.get("EXTRA_DBG", "0")))
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 import bench  # noqa: E402

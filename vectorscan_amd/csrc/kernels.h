@@ -110,6 +110,9 @@ struct VsaLitParams {
     uint64_t *out_keys;
     uint32_t *out_ids;
     uint64_t out_cap;
+    unsigned long long *wave_log; /* diagnostic (dbg bit12): 8 u64 per scanning
+                                     wave: start, end (100 MHz), segments,
+                                     KiB iterations, workgroup, wave, XCC, HW_ID */
     unsigned long long *counters; /* [0] matches, [16 + 16 r] region tickets,
                                      [2] candidates handed to confirm (after
                                      the slot prefilter; diagnostic) */

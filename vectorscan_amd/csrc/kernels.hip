@@ -1223,8 +1223,10 @@ vsa_lit_scan(VsaLitParams P) {
     L.lg = 31 - __clz(P.qcap);
     L.dbg = P.dbg;
 
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    u32 n_seg = 0, n_iter = 0; /* diagnostic (wave_log) */
     if ((P.dbg & 2048) && lane == 0) /* diagnostic: first scanning-wave start */
-        atomicMax(&P.counters[8], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+        atomicMax(&P.counters[8], ~t_start);
     const u8 *A = P.data - mis;
     const int64_t SEG = (int64_t)P.seg_bytes;
     u32 ncand_total = 0;
@@ -1305,6 +1307,7 @@ vsa_lit_scan(VsaLitParams P) {
         const int64_t s_lo = gcount ? B.org : B.org + (int64_t)(seg - B.seg_first) * SEG;
         const int64_t s_hi = (!gcount && s_lo + SEG < S.bhi) ? s_lo + SEG : S.bhi;
         const u32 niters = (u32)((s_hi - s_lo + 1023) >> 10);
+        n_iter += niters;
         const int64_t zlo = (MODE == VSA_MODE_FDR) ? B.zbase : S.qlo;
 
         /* iterations [f0, f1) are interior ("fast"): no byte of the 1 KiB
@@ -1453,7 +1456,20 @@ vsa_lit_scan(VsaLitParams P) {
         ring_tail_cache = is.tail_cache;
         ring_head = is.head;
         } /* blocks of the segment */
+        n_seg++;
         seg = P.dynamic ? resolve(t_next) : seg + G;
+    }
+    if ((P.dbg & 4096) && P.wave_log && lane < 8) {
+        u32 xcc, hwid;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long v[8] = {t_start, t_end, n_seg, n_iter, blockIdx.x, wave,
+                                         xcc, hwid};
+        unsigned long long x = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) x = (u32)k == lane ? v[k] : x;
+        P.wave_log[((size_t)blockIdx.x * LIT_WAVES + wave) * 8 + lane] = x;
     }
     if ((P.dbg & 2048) && lane == 0) {
         /* diagnostic: earliest / latest scanning-wave end (100 MHz clock):

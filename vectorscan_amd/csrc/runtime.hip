@@ -443,6 +443,10 @@ int queue_bin_sort(vsa_ctx *c) {
     return VSA_OK;
 }
 
+/* diagnostic per-wave log (vsa_set_wave_log; the kernel writes it under
+ * debug flag 4096) */
+static unsigned long long *g_wave_log = nullptr;
+
 int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
                        uint64_t nsegs, uint32_t seg_bytes);
 
@@ -491,6 +495,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         P.out_ids = w.d_ids[0];
         P.out_cap = w.out_cap;
         P.counters = w.d_counters;
+        P.wave_log = g_wave_log;
         {
             const char *e = getenv("VSA_DEBUG_FLAGS");
             P.dbg = e ? (uint32_t)atoi(e) : 0u;
@@ -527,6 +532,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.out_ids = w.d_ids[0];
     P.out_cap = w.out_cap;
     P.counters = w.d_counters;
+    P.wave_log = g_wave_log;
     {
         const char *e = getenv("VSA_DEBUG_FLAGS");
         P.dbg = e ? (uint32_t)atoi(e) : 0u;
@@ -2300,6 +2306,8 @@ const uint8_t *shuftiExec(vsa_m128_t mask_lo, vsa_m128_t mask_hi, const uint8_t 
     return fwd_result(vsa_shufti_find(lo, hi, buf, (size_t)(buf_end - buf), 0), buf, buf_end,
                       "shuftiExec");
 }
+
+void vsa_set_wave_log(void *d_log) { g_wave_log = (unsigned long long *)d_log; }
 
 void vsa_set_accel_vector_size(uint32_t vsize) {
     if (vsize == 16 || vsize == 32 || vsize == 64) g_vector_size = vsize;
