@@ -165,7 +165,9 @@ int vsa_sync(vsa_ctx_t *ctx);
  * starts may be NULL (all 0).  Matches are sorted on the device into the
  * reference order; ends are offsets relative to d_data.  flags bit0: skip
  * the sort; bit1: asynchronous (do not wait for the count; *n_matches is
- * filled by vsa_scan_wait). */
+ * filled by vsa_scan_wait).  A scan started while an asynchronous one is
+ * still pending first completes it (count, output-overflow rescan, sort) and
+ * then supersedes its results. */
 #define VSA_SCAN_UNSORTED 1u
 #define VSA_SCAN_ASYNC 2u
 int vsa_scan_blocks(vsa_ctx_t *ctx, const vsa_db_t *db, const uint8_t *d_data,
@@ -205,6 +207,16 @@ int vsa_scan_plan(vsa_ctx_t *ctx, const vsa_db_t *db, const vsa_plan_t *plan, ui
                   uint64_t *n_matches);
 int vsa_scan_wait(vsa_ctx_t *ctx, uint64_t *n_matches);
 /* Device pointers to the last scan's sorted keys (u64) and ids (u32). */
+/* Pack the last scan's sorted records for a collective, into caller device
+ * memory d_dst (u64 words): [header | keys (cap) | ids (cap x u32, i.e.
+ * cap / 2 words)], header = record count, bit 62 set when the records are
+ * not usable as packed (the scan overflowed its output or a crowded bin
+ * needs the host sort: complete the scan with vsa_scan_wait and pack
+ * again), then min(count, cap) records.  After an asynchronous binned scan
+ * the pack is queued on the context's stream behind it with no host wait
+ * (RCCL gathers of stripes, vectorscan_amd/stripe.py); otherwise the scan
+ * is completed first. */
+int vsa_scan_pack(vsa_ctx_t *ctx, void *d_dst, uint64_t cap);
 int vsa_scan_results(vsa_ctx_t *ctx, const uint64_t **d_keys,
                      const uint32_t **d_ids);
 /* Copy up to cap results of the last scan to the host. */

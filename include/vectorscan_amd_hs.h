@@ -142,6 +142,22 @@ int vsa_hs_corpus_prepare(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch
                           vsa_hs_corpus_t **corpus);
 int vsa_hs_corpus_scan(vsa_hs_corpus_t *corpus, uint64_t *counts, uint64_t *total,
                        unsigned threads);
+/* As vsa_hs_corpus_scan, plus digests[nblocks] (optional): per block, the
+ * fold of vsa_hs_seq_digest_step over its callback sequence (id, from, to)
+ * in delivery order, from 0 -- an order-dependent fingerprint of exactly
+ * what hs_scan / hs_scan_stream would have delivered for that block. */
+int vsa_hs_corpus_scan_ex(vsa_hs_corpus_t *corpus, uint64_t *counts, uint64_t *digests,
+                          uint64_t *total, unsigned threads);
+static inline uint64_t vsa_hs_seq_digest_step(uint64_t h, unsigned id, unsigned long long from,
+                                              unsigned long long to) {
+    uint64_t x = h ^ ((uint64_t)id * 0x9E3779B97F4A7C15ULL) ^
+                 ((uint64_t)from * 0xC2B2AE3D27D4EB4FULL) ^ ((uint64_t)to * 0x165667B19E3779F9ULL);
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ULL;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
 int vsa_hs_corpus_free(vsa_hs_corpus_t *corpus);
 
 /* Introspection for tests: the database's HWLM blob (fragment id = HWLM

@@ -66,11 +66,15 @@ class LitDb:
 
     @property
     def min_width(self):
-        return min(len(p["s"]) for p in self.pats)
+        if not hasattr(self, "_min_width"):
+            self._min_width = min(len(p["s"]) for p in self.pats)
+        return self._min_width
 
     @property
     def history_required(self):
-        return max(len(t) for t, _, _ in self.frags) - 1
+        if not hasattr(self, "_hist_req"):
+            self._hist_req = max(len(t) for t, _, _ in self.frags) - 1
+        return self._hist_req
 
 
 def compile_lit_multi(expressions, flags=None, ids=None):
@@ -125,14 +129,22 @@ class _Run:
     def __init__(self, db):
         self.db = db
         self.exhausted = [False] * db.n_ekeys
-        self.stream = b""  # every byte written so far
+        # the stream's bytes as far back as any check reaches: buf holds the
+        # kept tail of earlier writes plus the current write, buf_off is the
+        # stream offset of buf[0], length the bytes written so far
+        self.buf = b""
+        self.buf_off = 0
+        self.length = 0
         self.terminated = False
         self.som_log = {}  # id -> leftmost from at the current offset
         self.som_to = None
-        counts = {}
-        for p in db.pats:
-            counts[p["id"]] = counts.get(p["id"], 0) + 1
-        self.som_dedupe = [p["som"] and counts[p["id"]] > 1 for p in db.pats]
+        if not hasattr(db, "_run_consts"):  # per-database, computed once
+            counts = {}
+            for p in db.pats:
+                counts[p["id"]] = counts.get(p["id"], 0) + 1
+            db._run_consts = (max(db.history_required, max(len(p["s"]) for p in db.pats)),
+                              [p["som"] and counts[p["id"]] > 1 for p in db.pats])
+        self.keep, self.som_dedupe = db._run_consts
 
     def flush(self, out, stop_after):
         """flushStoredSomMatches: leftmost start per id, in id order."""
@@ -152,7 +164,7 @@ class _Run:
             if len(s) > SHORT:
                 if to < len(s):
                     continue
-                seg = self.stream[to - len(s):to - SHORT]
+                seg = self.buf[to - len(s) - self.buf_off:to - SHORT - self.buf_off]
                 if p["caseless"]:
                     seg = _upper(seg)
                 if seg != s[:-SHORT]:
@@ -179,16 +191,19 @@ class _Run:
     def write(self, blob_ptr, data, out, stop_after=None):
         """One write (pureLiteralStreamExec; offset 0 = block mode)."""
         data_b = bytes(data) if not hasattr(data, "tobytes") else data.tobytes()
-        off = len(self.stream)
-        self.stream += data_b
+        off = self.length
+        tail = self.buf[max(0, len(self.buf) - self.keep):]
+        self.buf_off = off - len(tail)
+        self.buf = tail + data_b
+        self.length += len(data_b)
         if not data_b:
             return
         if off == 0:
-            _, recs = oracle.hwlm_exec(blob_ptr, data, cap=1 << 16)
+            _, recs = oracle.hwlm_exec(blob_ptr, data, cap=4096)
         else:
             hl = min(off, self.db.history_required)
-            hist = self.stream[off - hl:off]
-            _, recs = oracle.hwlm_exec_stream(blob_ptr, hist, data, cap=1 << 16)
+            hist = tail[len(tail) - hl:]
+            _, recs = oracle.hwlm_exec_stream(blob_ptr, hist, data, cap=4096)
         last_to, at_to = None, set()
         for end, frag in recs:
             to = off + end + 1

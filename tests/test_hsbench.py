@@ -202,17 +202,40 @@ def test_hsbench_main(tmp_path, capsys, mode_flag):
     assert "Mean throughput (overall):" in out and "WARNING" not in out
 
 
-def cfg5_case(nbytes, nstreams=8):
+def cfg5_case(nbytes, nstreams=8, chunk=16 << 10):
     """the cfg-5-shaped pure-literal set (bench.make_mixed_set: 10k
     literals, length 4-16, CASELESS / SINGLEMATCH / SOM_LEFTMOST mixed, shared
-    ids) planted once per 4 KiB in printable bytes, cut into 16 KiB chunks"""
+    ids) planted once per 4 KiB in printable bytes, cut into `chunk`-byte
+    chunks dealt round-robin over `nstreams` streams"""
     import bench
     exprs, flags, ids = bench.make_mixed_set(10000)
     lits = [vsa.HwlmLiteral(e, False, i) for i, e in enumerate(exprs)]
     data = bench.make_corpus(nbytes, lits, seed=9, plant_every=4 << 10)
-    chunks = [(k % nstreams, data[o:o + (16 << 10)].tobytes())
-              for k, o in enumerate(range(0, nbytes, 16 << 10))]
+    chunks = [(k % nstreams, data[o:o + chunk].tobytes())
+              for k, o in enumerate(range(0, nbytes, chunk))]
     return exprs, flags, ids, [(i, s, d) for i, (s, d) in enumerate(chunks)]
+
+
+def oracle_sequences(exprs, flags, ids, blocks, mode):
+    """per-chunk callback sequences [(id, from, to)] from the oracle's
+    pure-literal restatement (runtime.c:204-230 block, :802-831 streams:
+    each stream's writes in order through one run state), indexed like
+    `blocks`"""
+    odb = ohs.compile_lit_multi(exprs, flags, ids)
+    lits = [vsa.HwlmLiteral(t, nc, f, noruns=nr) for t, nc, f, nr in odb.hwlm_literals()]
+    blob = vsa.hwlm_build(lits)
+    seqs = [None] * len(blocks)
+    runs = {}
+    for i, s, d in blocks:
+        data = np.frombuffer(d, np.uint8)
+        if mode == hs.MODE_BLOCK:
+            seqs[i] = ohs.scan(odb, blob.ptr, data)
+            continue
+        r = runs.setdefault(s, ohs._Run(odb))
+        out = []
+        r.write(blob.ptr, data, out)
+        seqs[i] = out
+    return seqs
 
 
 def test_cfg5_set_blob_and_oracle():
@@ -231,19 +254,57 @@ def test_cfg5_set_blob_and_oracle():
     assert sorted(got) == sorted(ohs.brute_force(odb, data))
 
 
+def test_seq_digest_matches_c():
+    """the Python fold of the sequence digest equals the C one (through a
+    one-block corpus would need a GPU; here the formula on known values)"""
+    assert hs.seq_digest([]) == 0
+    a = hs.seq_digest([(1, 0, 5), (2, 3, 9)])
+    b = hs.seq_digest([(2, 3, 9), (1, 0, 5)])
+    assert a != b and a == hs.seq_digest([(2, 3, 9)], hs.seq_digest([(1, 0, 5)]))
+
+
+def _check_sequences(g, exprs, flags, ids, blocks, mode):
+    want = oracle_sequences(exprs, flags, ids, blocks, mode)
+    total, counts, digests = g.scan_digests()
+    # the layout's scan order (hsbench.layout) -> block index: streams
+    # grouped in order of first appearance
+    first = {}
+    for i, (_, sid, _) in enumerate(blocks):
+        first.setdefault(sid, i)
+    order = list(range(len(blocks))) if mode == hs.MODE_BLOCK else \
+        sorted(range(len(blocks)), key=lambda i: (first[blocks[i][1]], i))
+    bad = [(i, len(want[b]), int(counts[i])) for i, b in enumerate(order)
+           if int(digests[i]) != hs.seq_digest(want[b]) or int(counts[i]) != len(want[b])]
+    assert not bad, "chunks whose callback sequence differs (pos, want n, got n): %s" % bad[:8]
+    assert total == sum(len(w) for w in want)
+    return total
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [hs.MODE_BLOCK, hs.MODE_STREAM, hs.MODE_VECTORED])
 def test_cfg5_mixed_literal_db(mode):
-    """cfg-5-shaped database on 4 MiB of 16 KiB chunks: per-chunk match
-    counts of the one-launch corpus scan + host report replay vs the oracle"""
-    exprs, flags, ids, blocks = cfg5_case(4 << 20)
+    """cfg-5-shaped database (10k mixed literals) on 64 MiB of 16 KiB chunks:
+    every chunk's full callback sequence (id, from, to) out of the one-launch
+    corpus scan + host report replay equals the oracle's (an order-dependent
+    digest per chunk plus the count), in block, stream and vectored mode"""
+    exprs, flags, ids, blocks = cfg5_case(64 << 20)
     g = hsbench.GpuCorpus(exprs, ids, flags, blocks, mode)
     try:
-        want = oracle_counts(exprs, flags, ids, blocks, mode)
-        total, counts = g.scan(counts=True)
-        assert list(counts) == want
-        assert total == sum(want) > 1000
+        total = _check_sequences(g, exprs, flags, ids, blocks, mode)
+        assert total > 10000
         t2, _ = g.scan()
         assert t2 == total
+    finally:
+        g.close()
+
+
+@pytest.mark.gpu
+def test_cfg5_small_chunks_sequences():
+    """the same set on 32 MiB of 2 KiB chunks (hsbench's small-block case),
+    block mode: full callback sequences per chunk"""
+    exprs, flags, ids, blocks = cfg5_case(32 << 20, chunk=2 << 10)
+    g = hsbench.GpuCorpus(exprs, ids, flags, blocks, hs.MODE_BLOCK)
+    try:
+        assert _check_sequences(g, exprs, flags, ids, blocks, hs.MODE_BLOCK) > 2000
     finally:
         g.close()

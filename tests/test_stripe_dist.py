@@ -237,12 +237,29 @@ def _packed_worker(rank, world, port, q):
             keys = torch.arange(n, dtype=torch.int64) * 5 + (rank << 40)
             ids = torch.arange(n, dtype=torch.int32) + 1000 * rank
 
-            def fill(kv, iv, cap):
-                m = min(n, cap)
-                kv[:m].copy_(keys[:m])
-                iv[:m].copy_(ids[:m])
+            counts = pg.gather(st.host_pack(keys, ids, n))
+            if rank == 0:
+                k, i = pg.merged(counts)
+                out.append((counts, k.tolist(), i.tolist(), pg.cap))
+            else:
+                assert pg.merged(counts) is None
+        # step 4: rank 2's first pack is not final (a scan that overflowed
+        # its output): every rank sees the header bit, completes and packs again
+        n = 5
+        keys = torch.arange(n, dtype=torch.int64) * 5 + (rank << 40)
+        ids = torch.arange(n, dtype=torch.int32) + 1000 * rank
+        state = {"final": rank != 2, "packs": 0}
+        base = st.host_pack(keys, ids, n)
 
-            counts = pg.gather(n, fill)
+        def pack(buf, cap):
+            state["packs"] += 1
+            base(buf, cap)
+            if not state["final"]:
+                buf[0] = n | st.NOT_READY
+
+        counts = pg.gather(pack, complete=lambda: state.update(final=True))
+        assert state["packs"] == 2, state
+        if rank == 0:
             k, i = pg.merged(counts)
             out.append((counts, k.tolist(), i.tolist(), pg.cap))
         if rank == 0:
@@ -252,8 +269,9 @@ def _packed_worker(rank, world, port, q):
 
 
 def test_packed_gather_world3():
-    """bench.py's per-step exchange (stripe.PackedGather): one all-gather,
-    the buffer grown from the gathered counts when a rank passes it."""
+    """bench.py's per-step exchange (stripe.PackedGather): the headers
+    all-gathered, the records gathered to rank 0 only, the buffers grown
+    from the gathered headers when a rank passes them."""
     world = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -271,5 +289,5 @@ def test_packed_gather_world3():
             want_k += [j * 5 + (r << 40) for j in range(n)]
             want_i += [j + 1000 * r for j in range(n)]
         assert keys == want_k and ids == want_i
-    assert [o[0] for o in out] == [[3, 7, 0], [10, 1500, 4], [0, 0, 9]]
-    assert out[0][3] == 1024 and out[1][3] == 1875
+    assert [o[0] for o in out] == [[3, 7, 0], [10, 1500, 4], [0, 0, 9], [5, 5, 5]]
+    assert out[0][3] == 1024 and out[1][3] == 1875 and out[3][3] == 1875

@@ -147,6 +147,7 @@ _sig("vsa_plan_free", ctypes.c_int, ctypes.c_void_p)
 _sig("vsa_scan_plan", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_uint32, _u64p)
 _sig("vsa_scan_wait", ctypes.c_int, ctypes.c_void_p, _u64p)
+_sig("vsa_scan_pack", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
 _sig("vsa_scan_results", ctypes.c_int, ctypes.c_void_p,
      ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p))
 _sig("vsa_scan_copy", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -647,6 +648,12 @@ class Context:
         n = ctypes.c_uint64()
         _check(lib.vsa_scan_wait(self.ptr, ctypes.byref(n)))
         return n.value
+
+    def scan_pack(self, d_dst, cap):
+        """vsa_scan_pack: the last scan's sorted records packed into device
+        memory d_dst as [header | keys (cap) | ids (cap x u32)] for a
+        collective (queued behind an asynchronous binned scan, no wait)."""
+        _check(lib.vsa_scan_pack(self.ptr, d_dst, cap))
 
     def results(self, n):
         """Copy the last scan's sorted (key, id) records to the host."""

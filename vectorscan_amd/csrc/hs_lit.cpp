@@ -283,6 +283,18 @@ int count_match(unsigned, unsigned long long, unsigned long long, unsigned, void
     return 0;
 }
 
+/* count + order-dependent digest of the callback sequence (vsa_hs_corpus_scan_ex) */
+struct SeqDigest {
+    uint64_t cnt = 0, h = 0;
+};
+int digest_match(unsigned id, unsigned long long from, unsigned long long to, unsigned,
+                 void *ctx) {
+    SeqDigest &d = *(SeqDigest *)ctx;
+    d.cnt++;
+    d.h = vsa_hs_seq_digest_step(d.h, id, from, to);
+    return 0;
+}
+
 /* keep the last max(16, longest literal - 1) bytes of the stream */
 void push_history(vsa_hs_stream *st, const uint8_t *const *bufs, const size_t *lens, size_t n) {
     const size_t keep = std::max(HIST_MIN, st->db->max_len ? st->db->max_len - 1 : 0);
@@ -743,6 +755,11 @@ int vsa_hs_corpus_free(vsa_hs_corpus_t *c) {
 
 int vsa_hs_corpus_scan(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *total,
                        unsigned threads) {
+    return vsa_hs_corpus_scan_ex(cp, counts, nullptr, total, threads);
+}
+
+int vsa_hs_corpus_scan_ex(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *digests,
+                          uint64_t *total, unsigned threads) {
     if (!cp || !total || !valid_db(cp->db)) return VSA_HS_INVALID;
     const vsa_hs_database *db = cp->db;
     vsa_hs_scratch *scratch = cp->scratch;
@@ -752,8 +769,9 @@ int vsa_hs_corpus_scan(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *total,
     const uint32_t nblocks = (uint32_t)cp->offsets.size();
     const uint64_t *offsets = cp->offsets.data(), *lens = cp->lens.data();
     if (counts) std::fill(counts, counts + nblocks, 0);
+    if (digests) std::fill(digests, digests + nblocks, 0);
     *total = 0;
-    const bool fast = db->simple && !counts;
+    const bool fast = db->simple && !counts && !digests;
     /* VSA_HOST_TIMING: per-phase wall times on stderr */
     static const bool timing = getenv("VSA_HOST_TIMING") != nullptr;
     auto now = [] { return std::chrono::steady_clock::now(); };
@@ -844,8 +862,10 @@ int vsa_hs_corpus_scan(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *total,
         vsa_hs_stream st;
         std::vector<const uint8_t *> bufs;
         std::vector<size_t> bl_len;
-        uint64_t cnt = 0;
-        Run r{db, &st, count_match, &cnt, nullptr, nullptr, {}, 0};
+        SeqDigest dg;
+        uint64_t &cnt = dg.cnt;
+        Run r{db, &st, digests ? digest_match : count_match, digests ? (void *)&dg : (void *)&cnt,
+              nullptr, nullptr, {}, 0};
         for (size_t i = t; i < live.size(); i += T) {
             const uint32_t *bl = unit_blk + unit_off[live[i]];
             const size_t nbl = unit_off[live[i] + 1] - unit_off[live[i]];
@@ -873,6 +893,7 @@ int vsa_hs_corpus_scan(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *total,
             for (size_t j = 0; j < nbl; j++) {
                 const uint32_t b = bl[j];
                 const uint64_t before = cnt;
+                dg.h = 0;
                 r.cur = j;
                 if (bstamp[b] == gen && re[b] > rb[b] &&
                     vsa::replay_records(ddb, keys.data() + rb[b], ids.data() + rb[b],
@@ -884,6 +905,7 @@ int vsa_hs_corpus_scan(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *total,
                 if (streams && h_data) push_history(&st, &bufs[j], &bl_len[j], 1);
                 st.offset += bl_len[j];
                 if (counts) counts[b] = cnt - before;
+                if (digests) digests[b] = dg.h;
             }
             part[t] += cnt;
         }

@@ -46,13 +46,17 @@ struct VsaBlock {
 #define VSA_KEY_LI_MASK 0xfffffu
 
 /* Key of the derived FDR first stage (runtime.hip derive_fdr_table) for the
- * byte pair (b0, b1) at positions (p, p + 1), dmask = 2^bits - 1 (bits 13 or
- * 14): the low 7 bits of b0 and the low bits - 7 bits of b1.  The kernels
- * compute it two keys per dword (kernels.hip fdr_key2). */
+ * byte pair (b0, b1) at positions (p, p + 1), dmask = 2^bits - 1: the low
+ * 7 bits of b0 and the low bits - 7 bits of b1, except at 13 bits: the low
+ * 6 bits of b0 and 7 of b1.  Both are "first byte under a mask, second
+ * byte's low 7 bits shifted up", which the kernels compute two keys per
+ * dword in two packed ops (kernels.hip fdr_key2: v_pk_lshrrev_b16 of the
+ * 7-bit bytes by 1 or 2, v_bfi_b32 with the first-byte mask). */
 #ifdef __HIPCC__
 __host__ __device__
 #endif
 static inline uint32_t vsa_fdr_key(uint32_t b0, uint32_t b1, uint32_t dmask) {
+    if (dmask == 0x1fffu) return (b0 & 0x3fu) | ((b1 & 0x7fu) << 6);
     return (b0 & 0x7fu) | ((b1 << 7) & dmask & ~0x7fu);
 }
 

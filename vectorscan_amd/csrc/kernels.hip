@@ -84,12 +84,18 @@ __device__ __forceinline__ u32 writelane_u32(u32 v, u32 s) {
     asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(readfirstlane_u32(s)), "n"(L));
     return v;
 }
-/* vsa_fdr_key of the byte pairs (0, 1) and (2, 3) of x, one per 16-bit half:
- * the low 7 bits of the first byte, then the second byte's low bits under
- * km = (dmask & ~0x7f) in both halves (the shift's bit 16 -> 15 spill is
- * outside km) */
-__device__ __forceinline__ u32 fdr_key2(u32 x, u32 km) {
-    return (x & 0x007f007fu) | ((x >> 1) & km);
+/* vsa_fdr_key of the byte pairs (0, 1) and (2, 3) of z, one per 16-bit half,
+ * for 14- and 13-bit tables: z = the bytes with bit 7 clear (every byte
+ * AND 0x7f, shared by all keys of a dword); the packed shift moves each
+ * half's second byte down by kshift (1 or 2: its low 7 bits land right
+ * above the first byte's kf bits, its bit 7 is 0 and bit 15 is zero-filled)
+ * and v_bfi_b32 keeps the first byte's bits under kf (0x007f007f or
+ * 0x003f003f).  Two VALU ops per two keys. */
+__device__ __forceinline__ u32 fdr_key2(u32 z, u32 kf, u32 kshift2) {
+    u32 y, r;
+    asm("v_pk_lshrrev_b16 %0, %1, %2" : "=v"(y) : "s"(kshift2), "v"(z));
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(kf), "v"(z), "v"(y));
+    return r;
 }
 /* LDS byte address of an 8-byte table entry: base + 8 * (16-bit half H of
  * w) in one op (v_mad_u32_u16 with op_sel picks the half, no bfe/shift) */
@@ -234,7 +240,8 @@ struct QEnt {
 struct LitShared {
     const void *tab;
     u32 tab_lds;     /* LDS byte address of tab (LDS tables) */
-    u32 kmask2;      /* FDR key mask in both 16-bit halves */
+    u32 kf;          /* FDR key: first-byte mask in both halves (fdr_key2) */
+    u32 kshift2;     /* FDR key: second-byte shift in both halves */
     u32 tsel;        /* Teddy: TEDDY_TAB_LDS | this lane's copy offset */
     uint4 *ring;     /* this wave's ring */
     const u32 *tail; /* this ring's consumed position (written by the confirm wave) */
@@ -488,6 +495,146 @@ __device__ __forceinline__ void conf_accumulate(const typename LitTraits<MODE>::
     }
 }
 
+/* OR-into-place of the FDR entries of the residue groups in RM (bit r: the
+ * slots j = 4 w + r), the LB == 8 case of conf_accumulate split by residue:
+ * F[0..5] = the conf dwords of positions -1 .. 22 (byte i of F[w] = end
+ * 4 w + i - 1; F[4..5] spill into the next lane), before the look-back
+ * shift. */
+template <int RM, bool ACC = false>
+__device__ __forceinline__ void fdr_acc_groups(const u64 (&x)[16], u32 (&F)[6]) {
+    auto lo = [&](int j) { return (u32)x[j]; };
+    auto hi = [&](int j) { return (u32)(x[j] >> 32); };
+    constexpr bool R0 = RM & 1, R1 = RM & 2, R2 = RM & 4, R3 = RM & 8;
+    u32 A[4][5];
+#pragma unroll
+    for (int r = 1; r < 4; r++) {
+        A[r][0] = lo(r);
+        A[r][1] = hi(r) | lo(4 + r);
+        A[r][2] = hi(4 + r) | lo(8 + r);
+        A[r][3] = hi(8 + r) | lo(12 + r);
+        A[r][4] = hi(12 + r);
+    }
+    /* ACC: OR into F (the previous level's dwords ride in the or3's spare
+     * operand) */
+    u32 f0 = ACC ? F[0] : 0u;
+    if (R0) f0 |= lo(0);
+    if (R1) f0 |= A[1][0] << 8;
+    if (R2) f0 |= A[2][0] << 16;
+    if (R3) f0 |= A[3][0] << 24;
+    F[0] = f0;
+#pragma unroll
+    for (int i = 1; i < 5; i++) {
+        u32 a = ACC ? F[i] : 0u, b = 0, c = 0;
+        if (R0) a |= hi(4 * (i - 1)) | (i < 4 ? lo(4 * i) : 0u);
+        if (R1) b = __builtin_amdgcn_alignbyte(A[1][i], A[1][i - 1], 3);
+        if (R2) c = __builtin_amdgcn_alignbyte(A[2][i], A[2][i - 1], 2);
+        if (R3) c |= __builtin_amdgcn_alignbyte(A[3][i], A[3][i - 1], 1);
+        F[i] = or3(a, b, c);
+    }
+    u32 f5 = ACC ? F[5] : 0u;
+    if (R1) f5 |= A[1][4] >> 24;
+    if (R2) f5 |= A[2][4] >> 16;
+    if (R3) f5 |= A[3][4] >> 8;
+    F[5] = f5;
+}
+
+
+/* the look-back shift (lit_iter): byte i of c[w] = end 4 w + i; s = the
+ * spill into ends 16 .. 22 */
+__device__ __forceinline__ void fdr_shift1(const u32 (&F)[6], u32 (&c)[4], u64 &s) {
+#pragma unroll
+    for (int w = 0; w < 4; w++) c[w] = __builtin_amdgcn_alignbyte(F[w + 1], F[w], 1);
+    s = ((u64)(F[5] >> 8) << 32) | __builtin_amdgcn_alignbyte(F[5], F[4], 1);
+}
+
+/* FDR sweep (LDS table, interior iteration): the 16 lookups in two levels.
+ * Level 1 looks up the 8 even slots (positions -1, 1, .., 13).  Level 2
+ * looks up the odd slots (positions 0, 2, .., 14) with their real keys only
+ * in the lanes where a conf dword the pair of slots reaches still has a
+ * live end after level 1; the other lanes look up key 0, one address for
+ * all of them (an LDS broadcast, no bank conflict).  On cfg-4 text 3.5 % of
+ * ends survive the even slots, so ~35 % of level 2's lanes carry real keys
+ * and the model of the LDS array cycles per KiB falls from ~113 to ~90
+ * (tools/sim_lds.py): the random lookups' bank conflicts are what bound
+ * this kernel.  The result is exactly the full filter's: a dead lane's
+ * entry is OR-ed only into ends that are already dead (every bucket bit
+ * set), which stay dead, and lane 63, whose reach crosses into the next
+ * chunk, always looks up. */
+template <bool TWO>
+__device__ __forceinline__ void fdr_sweep_conf(const LitShared &L, const u32 (&d)[4], u32 pv3,
+                                               u64 carry, u32 (&U)[6]) {
+    u64 x[16];
+    u32 ko[4], km[4], z[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) z[w] = d[w] & 0x7f7f7f7fu;
+    /* byte -1 (pv3's top byte) is only ever a first byte: fdr_key2 keeps
+     * its low kf bits, so it needs no mask */
+#pragma unroll
+    for (int w = 0; w < 4; w++)
+        ko[w] = fdr_key2(__builtin_amdgcn_alignbyte(z[w], w ? z[w - 1] : pv3, 3), L.kf, L.kshift2);
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        x[4 * w] = lds_ld64(tab_addr16<0>(ko[w], L.tab_lds));
+        x[4 * w + 2] = lds_ld64(tab_addr16<1>(ko[w], L.tab_lds));
+    }
+    if (!TWO) {
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            km[w] = fdr_key2(z[w], L.kf, L.kshift2);
+            x[4 * w + 1] = lds_ld64(tab_addr16<0>(km[w], L.tab_lds));
+            x[4 * w + 3] = lds_ld64(tab_addr16<1>(km[w], L.tab_lds));
+        }
+    }
+    /* Level 1, before the look-back shift: byte i of U[w] = end 4 w + i - 1,
+     * U[4..5] = ends 15 .. 22 (byte 0 of U[4] is this lane's end 15, the
+     * rest spills into the next lane).  The previous lane's U[4..5] land on
+     * this lane's U[0..1] as they are (its end 15 = this lane's end -1);
+     * lane 0 takes the previous chunk's carry in the same form. */
+    fdr_acc_groups<0x5>(x, U);
+    if (!TWO) fdr_acc_groups<0xA, true>(x, U);
+    const u64 cu = carry << 8; /* the carry (ends 0 .. 6 at bytes 0 .. 6), unshifted */
+    U[0] |= writelane_u32<0>(lane_up1(U[4]), (u32)cu);
+    U[1] |= writelane_u32<0>(lane_up1(U[5]), (u32)(cu >> 32));
+    if (!TWO) return;
+    /* conf dwords with a live end after level 1 (lane masks; an absent
+     * bucket's bit is set in every entry, derive_fdr_table).  The next
+     * lane's U[0] / U[1] cover ends 15 .. 22 (its U[0] byte 0 = this lane's
+     * end 15); lane 63's successor is the next chunk: always live. */
+    const u64 m0 = __ballot(U[0] != 0xffffffffu);
+    const u64 m1 = __ballot(U[1] != 0xffffffffu);
+    const u64 m2 = __ballot(U[2] != 0xffffffffu);
+    const u64 m3 = __ballot(U[3] != 0xffffffffu);
+    const u64 top = 1ULL << 63;
+    const u64 n0 = (m0 >> 1) | top, n1 = (m1 >> 1) | top;
+    /* slots 2 i + 1 and 2 i + 3 (i even: positions 2 i, 2 i + 2, one key
+     * dword km[i / 2]) reach ends 2 i .. 2 i + 9 = U bytes 2 i + 1 .. 2 i + 10:
+     * dwords i / 2 .. i / 2 + 2 */
+    const u64 m12 = m1 | m2, m3n0 = m3 | n0;
+    const u64 act[4] = {m0 | m12, m12 | m3, m2 | m3n0, m3n0 | n1};
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        /* a dead pair reads entry 0 (a broadcast: no bank conflict); any
+         * entry serves a dead end */
+        const u32 k = fdr_key2(z[w], L.kf, L.kshift2);
+        km[w] = __builtin_amdgcn_inverse_ballot_w64(act[w]) ? k : 0u;
+    }
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        x[4 * w + 1] = lds_ld64(tab_addr16<0>(km[w], L.tab_lds));
+        x[4 * w + 3] = lds_ld64(tab_addr16<1>(km[w], L.tab_lds));
+    }
+    fdr_acc_groups<0xA, true>(x, U);
+#ifdef VSA_EXTRA_VALU
+    /* experiment build: VSA_EXTRA_VALU dependent VALU ops per iteration */
+#pragma unroll
+    for (int i = 0; i < VSA_EXTRA_VALU; i++) asm volatile("v_or_b32 %0, %0, %0" : "+v"(U[i & 3]));
+#endif
+    /* spill again: the odd slots' part is new, the even slots' part is
+     * OR-ed twice (lane 0: the carry is in already) */
+    U[0] |= lane_up1(U[4]);
+    U[1] |= lane_up1(U[5]);
+}
+
 /* Block-edge masks: position j (0..16) of a lane's chunk is end / byte
  * q0 + j (block-relative).  rel32 clamps a bound X to the chunk's
  * coordinates; range_mask gives bits j in [lo, hi) over 17 positions, so an
@@ -557,12 +704,39 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
      * is left out: a one-byte constraint on b[e] that field 1 (b[e - 1],
      * b[e]) implies (derive_fdr_table) — the filter stays a superset. */
     constexpr bool FDR_BACK = MODE == VSA_MODE_FDR && LDS_TABLE;
-    u32 pv3 = lane_up1(d[3]);
-    if (lane == 0) pv3 = (u32)(in.pbytes >> 32);
+    const u32 pv3 = writelane_u32<0>(lane_up1(d[3]), (u32)(in.pbytes >> 32));
     if constexpr (FDR_BACK) {
         if (EDGE) look_m = range_mask(rel32(S.zbase, q0) + 1, rel32(S.len, q0) + 1);
     }
 
+    constexpr bool SWEEP = FDR_BACK && !EDGE;
+#ifdef VSA_FDR_ONE_LEVEL /* experiment build: every lookup in every lane */
+    constexpr bool TWO_LVL = false;
+#else
+    constexpr bool TWO_LVL = true;
+#endif
+    u32 c[T::CW];
+    IterState out;
+    out.ncand = in.ncand;
+    out.tail_cache = in.tail_cache;
+    out.head = in.head;
+    out.pbytes = ((u64)readlane_u32(d[3], WAVE - 1) << 32) | readlane_u32(d[2], WAVE - 1);
+    if constexpr (SWEEP) {
+        /* interior FDR iteration (fdr_sweep_conf): the candidate test runs on
+         * the unshifted dwords (this lane's ends are U[0] bytes 1..3, U[1..3]
+         * and U[4] byte 0); the shift to end order is done only for a push */
+        u32 U[6];
+        fdr_sweep_conf<TWO_LVL>(L, {d[0], d[1], d[2], d[3]}, pv3, in.carry, U);
+        out.carry = (((u64)readlane_u32(U[5], WAVE - 1) << 32) | readlane_u32(U[4], WAVE - 1)) >> 8;
+        const u32 nbm = ~bucket_mask;
+        /* this lane's ends: U[0] bytes 1..3 and U[4] byte 0 (one v_bfi) */
+        const u32 a123 = U[1] & U[2] & U[3];
+        u32 a04;
+        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(a04) : "s"(0xffu), "v"(U[4]), "v"(U[0]));
+        if (!__any(((a04 & a123) | nbm) != 0xffffffffu)) return out;
+#pragma unroll
+        for (int w = 0; w < 4; w++) c[w] = __builtin_amdgcn_alignbyte(U[w + 1], U[w], 1);
+    } else {
     /* own contributions: the lane's 16 lookups ... */
     S_t x[16];
     u32 km[4], ko[4]; /* FDR/LDS: keys of even / odd positions, two per dword */
@@ -570,8 +744,10 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
 #pragma unroll
         for (int w = 0; w < 4; w++) {
             /* km: positions 4w, 4w + 2; ko: 4w - 1, 4w + 1 */
-            km[w] = fdr_key2(d[w], L.kmask2);
-            ko[w] = fdr_key2(__builtin_amdgcn_alignbyte(d[w], w ? d[w - 1] : pv3, 3), L.kmask2);
+            const u32 zw = d[w] & 0x7f7f7f7fu;
+            const u32 zp = w ? d[w - 1] & 0x7f7f7f7fu : pv3;
+            km[w] = fdr_key2(zw, L.kf, L.kshift2);
+            ko[w] = fdr_key2(__builtin_amdgcn_alignbyte(zw, zp, 3), L.kf, L.kshift2);
         }
     }
 #pragma unroll
@@ -601,7 +777,6 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     for (int i = 0; i < VSA_EXTRA_VALU; i++) asm volatile("v_or_b32 %0, %0, %0" : "+v"(d[i & 3]));
 #endif
     /* ... OR-ed into place: field k of x[j] lands on end j + k */
-    u32 c[T::CW];
     u64 s_out;
     conf_accumulate<MODE>(x, c, s_out);
     if constexpr (FDR_BACK) {
@@ -624,15 +799,11 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
                             ? writelane_u32<0>(lane_up1((u32)(s_out >> 32)), (u32)(in.carry >> 32))
                             : 0u;
     const u64 s_in = ((u64)s_in_hi << 32) | s_in_lo;
-    IterState out;
-    out.ncand = in.ncand;
-    out.tail_cache = in.tail_cache;
-    out.head = in.head;
     out.carry = ((u64)readlane_u32((u32)(s_out >> 32), WAVE - 1) << 32) |
                 readlane_u32((u32)s_out, WAVE - 1);
-    out.pbytes = ((u64)readlane_u32(d[3], WAVE - 1) << 32) | readlane_u32(d[2], WAVE - 1);
     c[0] |= (u32)s_in;
     if constexpr (sizeof(S_t) == 8) c[1] |= (u32)(s_in >> 32);
+    } /* one-level lookups */
     if (EDGE) {
         if constexpr (MODE == VSA_MODE_FDR) if (!S.stream) {
             /* start state: byte i applies to end start + i (the short zone
@@ -1215,7 +1386,9 @@ vsa_lit_scan(VsaLitParams P) {
     LitShared L;
     L.tab = tab;
     L.tab_lds = (u32)(uintptr_t)(lds_u8_t *)smem;
-    L.kmask2 = (P.dmask & 0xff80u) * 0x10001u;
+    /* fdr_key2's parameters for the table's key width (vsa_fdr_key) */
+    L.kf = P.dmask == 0x1fffu ? 0x003f003fu : 0x007f007fu;
+    L.kshift2 = P.dmask == 0x1fffu ? 0x00020002u : 0x00010001u;
     L.tsel = TEDDY_TAB_LDS | ((lane & 31) << 3);
     L.ring = rings + (size_t)wave * P.qcap * T::EW;
     L.tail = &q_tails[wave];
@@ -1573,11 +1746,13 @@ __global__ void __launch_bounds__(256) vsa_bin_sort(const uint64_t *ctr, uint64_
                                                     uint32_t *counts,
                                                     const uint32_t *cursor, uint64_t *keys,
                                                     uint32_t *ids) {
-    if (bin_records(ctr, cap) < 2) return;
     const uint32_t bin = blockIdx.x * 4 + threadIdx.x / WAVE;
     const u32 lane = lane_id();
     const uint32_t m = counts[bin];
-    if (lane_id() == 0) counts[bin] = 0; /* ready for the next scan */
+    /* ready for the next scan, whether or not this one sorts (an overflowed
+     * or crowded launch leaves its counts behind too) */
+    if (lane_id() == 0) counts[bin] = 0;
+    if (bin_records(ctr, cap) < 2) return;
     if (m < 2) return;
     const uint32_t base = cursor[bin] - m;
     u64 k = ~0ULL;
@@ -1607,6 +1782,51 @@ __global__ void __launch_bounds__(256) vsa_bin_sort(const uint64_t *ctr, uint64_
     if (lane < m) {
         keys[base + lane] = k;
         ids[base + lane] = id;
+    }
+}
+
+/* The last launch of a binned scan: the scan's counters [0, 16) go to
+ * host memory (fine-grained, h[1..16]) and then h[0] = seq with a
+ * system-scope release, which the host polls instead of queueing a copy
+ * and an event; then the scan's counters [0, nzero) are zeroed for the
+ * next launch, which therefore needs no memset. */
+__global__ void __launch_bounds__(256) vsa_publish(unsigned long long *ctr,
+                                                   unsigned long long *h,
+                                                   unsigned long long seq, uint32_t nzero) {
+    const u32 t = threadIdx.x;
+    unsigned long long v = 0;
+    if (t < 16) v = ctr[t];
+    __syncthreads(); /* every read before any zeroing */
+    if (t < 16) {
+        h[1 + t] = v;
+        ctr[nzero + t] = v; /* kept on the device too (vsa_pack) */
+    }
+    for (u32 i = t; i < nzero; i += 256) ctr[i] = 0;
+    if (t == 0) {
+        /* lanes 0..15 are this wave: the fence waits for their stores */
+        __threadfence_system();
+        __hip_atomic_store(&h[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+/* A binned scan's sorted records packed for a collective, on the device
+ * (no host round trip): dst = [header | keys (cap) | ids (cap x u32)], the
+ * header = the record count, with bit 62 set when the records are not
+ * usable as they are (the scan overflowed its output and will run again,
+ * or a crowded bin left them to the library sort); min(count, cap)
+ * records follow.  saved = the counters vsa_publish kept. */
+__global__ void __launch_bounds__(256) vsa_pack(const unsigned long long *saved, uint64_t out_cap,
+                                                const uint64_t *keys, const uint32_t *ids,
+                                                uint64_t cap, uint64_t *dst) {
+    const uint64_t n = saved[0];
+    const bool bad = n > out_cap || saved[VSA_CTR_BIN_OVERFLOW] != 0;
+    const uint64_t m = bad ? 0 : (n < cap ? n : cap);
+    if (blockIdx.x == 0 && threadIdx.x == 0) dst[0] = n | (bad ? (1ULL << 62) : 0ULL);
+    uint32_t *did = (uint32_t *)(dst + 1 + cap);
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m;
+         i += (uint64_t)gridDim.x * 256) {
+        dst[1 + i] = keys[i];
+        did[i] = ids[i];
     }
 }
 

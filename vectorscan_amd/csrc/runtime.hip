@@ -30,6 +30,7 @@
 #include <mutex>
 #include <vector>
 #include <chrono>
+#include <sched.h>
 
 #include "../../include/vectorscan_amd.h"
 #include "hs_layout.h"
@@ -48,6 +49,10 @@ __global__ void vsa_bin_scatter(const uint64_t *keys, const uint32_t *ids, const
 __global__ void vsa_bin_sort(const uint64_t *ctr, uint64_t cap, uint32_t *counts,
                              const uint32_t *cursor, uint64_t *keys, uint32_t *ids);
 __global__ void vsa_class_scan_lut(VsaClassParams P, uint64_t span);
+__global__ void vsa_publish(unsigned long long *ctr, unsigned long long *h, unsigned long long seq,
+                            uint32_t nzero);
+__global__ void vsa_pack(const unsigned long long *saved, uint64_t out_cap, const uint64_t *keys,
+                         const uint32_t *ids, uint64_t cap, uint64_t *dst);
 __global__ void vsa_pair_scan(VsaPairParams P);
 
 #define VSA_CHECK(x)                                                          \
@@ -90,6 +95,9 @@ struct Workspace {
     unsigned long long *d_counters = nullptr; /* layout above */
     uint32_t *d_bins = nullptr; /* binned sort: counts[VSA_SORT_BINS], cursor[..] */
     unsigned long long *h_counters = nullptr; /* pinned mirror */
+    /* fine-grained host memory the device publishes a binned scan's
+     * counters into (vsa_publish): [0] = sequence, [1..16] = counters */
+    unsigned long long *h_pub = nullptr, *d_pub = nullptr;
     VsaBlock *d_blocks = nullptr; /* this call's block table, then its segment map */
     VsaBlock *h_blocks = nullptr; /* pinned mirror */
     size_t tab_cap = 0;           /* bytes of both */
@@ -115,6 +123,8 @@ struct BatchPlan {
     std::vector<int64_t> spans, live; /* build_plan scratch */
 };
 
+struct vsa_plan;
+
 struct vsa_ctx {
     int device = 0;
     int num_cus = 256;
@@ -137,6 +147,8 @@ struct vsa_ctx {
         uint32_t flags = 0;
         bool bins = false;     /* the scan counts records into the sort bins */
         bool dev_sort = false; /* ... and the binned sort is queued behind it */
+        bool published = false; /* ... and vsa_publish after it (finish_scan
+                                   polls h_pub instead of copying) */
         uint64_t bytes = 0; /* scanned bytes (len - start summed) */
         const VsaBlock *d_blocks = nullptr;
         const uint32_t *d_segblk = nullptr;
@@ -163,6 +175,29 @@ struct vsa_ctx {
         std::vector<uint64_t> in[5]; /* offs, lens, starts, hlens, rlos ({} = NULL) */
     } memo;
     bool host_sort = false; /* the last scan's records are left unsorted */
+    /* the scan counters [0, 144) are zero (the last launch published and
+     * cleared them), so the next launch needs no memset */
+    bool ctr_clean = false;
+    uint64_t pub_seq = 0; /* sequence of the last vsa_publish queued */
+    /* live plans of this context (vsa_ctx_destroy detaches them, so a plan
+     * freed after its context never touches it) */
+    std::vector<vsa_plan *> plans;
+};
+
+/* A batch's block table and segment map built and uploaded once, then
+ * reused by every vsa_scan_plan (a corpus scanned repeatedly: hsbench's
+ * repeats, a database swap over the same data). */
+struct vsa_plan {
+    /* the owning context (nullptr once it is destroyed) */
+    vsa_ctx *ctx = nullptr;
+    const uint8_t *d_data = nullptr;
+    uint32_t nb = 0;
+    uint64_t segs = 0;
+    uint32_t seg_bytes = 0;
+    int end_bits = 0;
+    uint64_t bytes = 0;
+    VsaBlock *d_blocks = nullptr;
+    uint32_t *d_segblk = nullptr;
 };
 
 /* drop-in scans: results of at most HOST_SORT_MAX records are sorted on the
@@ -192,9 +227,12 @@ struct vsa_db {
     uint8_t slot_bits[16] = {0}; /* prefilter hash bits per bucket (<= nBits) */
     uint64_t pf_mult = 0;
     bool flood_live = false;     /* some FDRFlood record can fire (idCount < max) */
-    /* confirm waves per workgroup for the next launch, adapted to the
-     * confirm-candidate rate the previous launches measured */
-    mutable uint32_t nconf = 1;
+    /* confirm waves per workgroup, set once from the confirm-candidate rate
+     * of the first representative launch (>= 16 MiB) of the db on any
+     * context; atomic, as dbs are shared by contexts and threads.  It feeds
+     * the segment sizes, so a db's launch plans change at most once. */
+    mutable std::atomic<uint32_t> nconf{1};
+    mutable std::atomic<bool> nconf_set{false};
 };
 
 /* confirm waves for a measured confirm-candidate rate (candidates per
@@ -402,7 +440,7 @@ size_t plan_lds(size_t tab, uint32_t slot_words, size_t ent, uint32_t *qcap,
 /* the confirm-wave count of a launch: the db's adapted value (or
  * VSA_NCONF), lowered until the LDS plan fits */
 uint32_t launch_nconf(const vsa_db *db, size_t tab, size_t ent, size_t budget) {
-    uint32_t nc = db->nconf;
+    uint32_t nc = db->nconf.load(std::memory_order_relaxed);
     if (const char *e = getenv("VSA_NCONF")) nc = (uint32_t)std::min(4, std::max(1, atoi(e)));
     uint32_t q;
     while (nc > 1 && plan_lds(tab, db->slot_words, ent, &q, budget, nc) > budget) nc--;
@@ -452,7 +490,10 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
 
 int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
                 uint64_t nsegs, uint32_t seg_bytes) {
-    VSA_CHECK(hipMemsetAsync(c->ws.d_counters, 0, 144 * sizeof(unsigned long long), c->stream));
+    if (!c->ctr_clean)
+        VSA_CHECK(hipMemsetAsync(c->ws.d_counters, 0, 144 * sizeof(unsigned long long), c->stream));
+    c->ctr_clean = false;
+    c->launch.published = false;
     /* not for the drop-in calls, whose few records the host sorts (a
      * larger result takes the library sort) */
     c->launch.bins = use_bins(c) && !(c->launch.flags & SCAN_HOST_SORT_SMALL);
@@ -467,7 +508,17 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
      * kernels read the record count and the overflow flag on the device
      * (finish_scan falls back to the library sort if a bin overflowed) */
     c->launch.dev_sort = c->launch.bins;
-    if (c->launch.dev_sort) return queue_bin_sort(c);
+    if (!c->launch.dev_sort) return VSA_OK;
+    int r2 = queue_bin_sort(c);
+    if (r2 != VSA_OK) return r2;
+    /* vsa_bin_sort zeroes every bin count; vsa_publish hands the counters
+     * to the host and zeroes them */
+    c->bins_clean = true;
+    hipLaunchKernelGGL(vsa_publish, dim3(1), dim3(256), 0, c->stream, c->ws.d_counters,
+                       c->ws.d_pub, (unsigned long long)++c->pub_seq, 144u);
+    VSA_CHECK(hipGetLastError());
+    c->launch.published = true;
+    c->ctr_clean = true;
     return VSA_OK;
 }
 
@@ -578,27 +629,60 @@ hipError_t wait_stream(vsa_ctx *c) {
     if (block) return hipStreamSynchronize(c->stream);
     hipError_t e = hipEventRecord(c->ev_done, c->stream);
     if (e != hipSuccess) return e;
+    /* spin ~100 us, then yield the core between polls (the host replay
+     * pool and the CPU baseline share the host) */
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 0;; i++) {
         e = hipEventQuery(c->ev_done);
         if (e != hipErrorNotReady) return e;
-        if ((i & 255) == 255 &&
-            std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
-            return hipStreamSynchronize(c->stream);
+        if ((i & 15) == 15) {
+            const auto dt = std::chrono::steady_clock::now() - t0;
+            if (dt > std::chrono::milliseconds(50)) return hipStreamSynchronize(c->stream);
+            if (dt > std::chrono::microseconds(100)) sched_yield();
+        }
     }
+}
+
+/* wait for the vsa_publish of sequence seq (spin ~100 us, then yield;
+ * past 50 ms the stream is synchronized and checked) */
+hipError_t wait_published(vsa_ctx *c, uint64_t seq) {
+    volatile unsigned long long *h = c->ws.h_pub;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0;; i++) {
+        if (h[0] == seq) break;
+        if ((i & 15) == 15) {
+            const auto dt = std::chrono::steady_clock::now() - t0;
+            if (dt > std::chrono::milliseconds(50)) {
+                hipError_t e = hipStreamSynchronize(c->stream);
+                if (e != hipSuccess) return e;
+                if (h[0] != seq) return hipErrorUnknown;
+                break;
+            }
+            if (dt > std::chrono::microseconds(100)) sched_yield();
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return hipSuccess;
 }
 
 int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     Workspace &w = c->ws;
-    VSA_CHECK(hipMemcpyAsync(w.h_counters, w.d_counters, 16 * sizeof(unsigned long long),
-                             hipMemcpyDeviceToHost, c->stream));
-    VSA_CHECK(wait_stream(c));
+    if (c->launch.published) {
+        VSA_CHECK(wait_published(c, c->pub_seq));
+        for (int i = 0; i < 16; i++) w.h_counters[i] = w.h_pub[1 + i];
+    } else {
+        VSA_CHECK(hipMemcpyAsync(w.h_counters, w.d_counters, 16 * sizeof(unsigned long long),
+                                 hipMemcpyDeviceToHost, c->stream));
+        VSA_CHECK(wait_stream(c));
+    }
     uint64_t n = w.h_counters[0];
     c->last_cand = w.h_counters[2];
     /* adapt the db's confirm-wave count to the measured candidate rate
      * (over a representative launch; not under diagnostic flags) */
-    if (c->launch.db && c->launch.bytes >= (16u << 20) && !getenv("VSA_DEBUG_FLAGS"))
-        c->launch.db->nconf = nconf_for_rate((double)c->last_cand / (double)c->launch.bytes);
+    if (c->launch.db && c->launch.bytes >= (16u << 20) && !getenv("VSA_DEBUG_FLAGS") &&
+        !c->launch.db->nconf_set.exchange(true))
+        c->launch.db->nconf.store(
+            nconf_for_rate((double)c->last_cand / (double)c->launch.bytes));
     if (getenv("VSA_DEBUG_FLAGS") && w.h_counters[3]) {
         fprintf(stderr, "vsa: %llu queued confirm keys differ from HBM\n",
                 (unsigned long long)w.h_counters[3]);
@@ -621,7 +705,6 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
         /* sorted by the binned sort queued in launch_scan (its overflow
          * flag, set by vsa_bin_scan, is in the counters just read) */
         c->cur = 1;
-        c->bins_clean = true; /* vsa_bin_sort zeroes the counts it read */
     } else if (n > 1 && !(flags & VSA_SCAN_UNSORTED) && !c->host_sort) {
         hipcub::DoubleBuffer<uint64_t> kb(w.d_keys[0], w.d_keys[1]);
         hipcub::DoubleBuffer<uint32_t> vb(w.d_ids[0], w.d_ids[1]);
@@ -637,6 +720,14 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
 }
 
 int complete_scan(vsa_ctx *c, uint64_t *n_out);
+
+/* complete an asynchronous scan still in flight (as vsa_scan_wait) */
+int finish_pending(vsa_ctx *c) {
+    if (!c->pending) return VSA_OK;
+    c->pending = false;
+    uint64_t n = 0;
+    return complete_scan(c, &n);
+}
 
 constexpr uint32_t SEG_GROUP_SHIFT = 24;
 constexpr uint32_t SEG_GROUP_MAX = 255;
@@ -772,15 +863,12 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
                      const uint64_t *hlens = nullptr, const uint64_t *rlos = nullptr) {
     if (!c || !db || !d_data || !offs || !lens || (!nb)) return VSA_E_INVALID;
     /* an asynchronous scan still in flight may be reading the block and
-     * segment tables rewritten below: let it finish first.  Its results are
-     * superseded by this scan (vsa_scan_wait then reports this one). */
-    if (c->pending) {
-        c->pending = false;
-        VSA_CHECK(hipStreamSynchronize(c->stream));
-    }
+     * segment tables rewritten below: it is completed first (count, overflow
+     * rescan, sort); its results are then superseded by this scan */
+    if (int r0 = finish_pending(c)) return r0;
     BatchPlan &pl = c->plan;
     auto T0 = std::chrono::steady_clock::now();
-    const uint64_t waves = (uint64_t)c->num_cus * (LIT_WAVES - db->nconf);
+    const uint64_t waves = (uint64_t)c->num_cus * (LIT_WAVES - db->nconf.load());
     const uint64_t *in[5] = {offs, lens, starts, hlens, rlos};
     auto &M = c->memo;
     bool same = M.valid && M.d_data == d_data && M.nb == nb && M.waves == waves;
@@ -836,6 +924,8 @@ int complete_scan(vsa_ctx *c, uint64_t *n_out) {
     for (int attempt = 0; attempt < 3; attempt++) {
         int r = finish_scan(c, c->launch.flags, c->launch.end_bits, n_out);
         if (r != VSA_E_OVERFLOW) return r;
+        /* the rescan reads the launch's tables: gone if its plan was freed */
+        if (!c->launch.d_blocks || !c->launch.d_segblk) return VSA_E_INVALID;
         if ((r = ensure_out(c, c->ws.h_counters[0])) != VSA_OK) return r;
         if ((r = launch_scan(c, c->launch.db, c->launch.d_data, c->launch.nb, c->launch.segs,
                              c->launch.seg_bytes)) != VSA_OK)
@@ -1260,6 +1350,10 @@ int vsa_ctx_create(int device, vsa_ctx_t **out) {
     VSA_CHECK(hipMalloc(&c->ws.d_bins, 2 * VSA_SORT_BINS * sizeof(uint32_t)));
     VSA_CHECK(hipHostMalloc((void **)&c->ws.h_counters, N_COUNTERS * sizeof(unsigned long long),
                             hipHostMallocDefault));
+    VSA_CHECK(hipHostMalloc((void **)&c->ws.h_pub, 32 * sizeof(unsigned long long),
+                            hipHostMallocCoherent | hipHostMallocMapped));
+    memset(c->ws.h_pub, 0, 32 * sizeof(unsigned long long));
+    VSA_CHECK(hipHostGetDevicePointer((void **)&c->ws.d_pub, c->ws.h_pub, 0));
     *out = c.release();
     return VSA_OK;
 }
@@ -1268,6 +1362,8 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (!c) return VSA_E_INVALID;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    /* plans outliving the context keep only their own device tables */
+    for (vsa_plan *p : c->plans) p->ctx = nullptr;
     Workspace &w = c->ws;
     for (int i = 0; i < 2; i++) {
         if (w.d_keys[i]) (void)hipFree(w.d_keys[i]);
@@ -1278,6 +1374,7 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (w.d_counters) (void)hipFree(w.d_counters);
     if (w.d_bins) (void)hipFree(w.d_bins);
     if (w.h_counters) (void)hipHostFree(w.h_counters);
+    if (w.h_pub) (void)hipHostFree(w.h_pub);
     if (w.d_blocks) (void)hipFree(w.d_blocks);
     if (w.h_blocks) (void)hipHostFree(w.h_blocks);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1519,7 +1616,7 @@ int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
          * the rings and slot bitmaps, else 13 (see derive_fdr_table) */
         uint32_t qc = 0;
         uint32_t bits = 14;
-        if (getenv("VSA_FDR_DOMAIN")) bits = (uint32_t)std::min(15, std::max(9, atoi(getenv("VSA_FDR_DOMAIN"))));
+        if (getenv("VSA_FDR_DOMAIN")) bits = (uint32_t)std::min(15, std::max(13, atoi(getenv("VSA_FDR_DOMAIN"))));
         else if (plan_lds((size_t)8 << 14, db->slot_words, 48, &qc) > LDS_BUDGET) bits = 13;
         std::vector<uint64_t> T;
         derive_fdr_table(eng, db->conf_off, bits, T);
@@ -1650,6 +1747,35 @@ int vsa_scan_results(vsa_ctx_t *c, const uint64_t **k, const uint32_t **ids) {
     if (!c) return VSA_E_INVALID;
     if (k) *k = c->ws.d_keys[c->cur];
     if (ids) *ids = c->ws.d_ids[c->cur];
+    return VSA_OK;
+}
+
+int vsa_scan_pack(vsa_ctx_t *c, void *d_dst, uint64_t cap) {
+    if (!c || !d_dst) return VSA_E_INVALID;
+    VSA_CHECK(hipSetDevice(c->device));
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((cap + 255) / 256, 256));
+    if (c->pending && c->launch.published && c->launch.dev_sort) {
+        /* the async binned scan's sorted records (buffer 1) and the counters
+         * vsa_publish keeps on the device: queued behind it, no wait */
+        hipLaunchKernelGGL(vsa_pack, dim3(grid), dim3(256), 0, c->stream,
+                           (const unsigned long long *)c->ws.d_counters + 144,
+                           (uint64_t)c->ws.out_cap, (const uint64_t *)c->ws.d_keys[1],
+                           (const uint32_t *)c->ws.d_ids[1], cap, (uint64_t *)d_dst);
+        VSA_CHECK(hipGetLastError());
+        return VSA_OK;
+    }
+    /* otherwise the scan is completed on the host first (library sort,
+     * overflow rescan) and its final records are packed */
+    if (int r = finish_pending(c)) return r;
+    unsigned long long *save = c->ws.d_counters + 144;
+    unsigned long long hv[16] = {c->last_n, 0};
+    VSA_CHECK(hipMemcpyAsync(save, hv, sizeof(hv), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(vsa_pack, dim3(grid), dim3(256), 0, c->stream,
+                       (const unsigned long long *)save, (uint64_t)c->ws.out_cap,
+                       (const uint64_t *)c->ws.d_keys[c->cur], (const uint32_t *)c->ws.d_ids[c->cur],
+                       cap, (uint64_t *)d_dst);
+    VSA_CHECK(hipGetLastError());
+    VSA_CHECK(hipStreamSynchronize(c->stream)); /* hv is on the host stack */
     return VSA_OK;
 }
 
@@ -2108,20 +2234,6 @@ int vsa_scan_blocks_stream(vsa_ctx_t *c, const vsa_db_t *db, const uint8_t *d_da
                             n_matches ? n_matches : &dummy, hlens);
 }
 
-/* A batch's block table and segment map built and uploaded once, then
- * reused by every vsa_scan_plan (a corpus scanned repeatedly: hsbench's
- * repeats, a database swap over the same data). */
-struct vsa_plan {
-    vsa_ctx *ctx = nullptr;
-    const uint8_t *d_data = nullptr;
-    uint32_t nb = 0;
-    uint64_t segs = 0;
-    uint32_t seg_bytes = 0;
-    int end_bits = 0;
-    uint64_t bytes = 0;
-    VsaBlock *d_blocks = nullptr;
-    uint32_t *d_segblk = nullptr;
-};
 
 int vsa_plan_create(vsa_ctx_t *c, const uint8_t *d_data, const uint64_t *offsets,
                     const uint64_t *lens, const uint64_t *starts, const uint64_t *hlens,
@@ -2134,6 +2246,7 @@ int vsa_plan_create(vsa_ctx_t *c, const uint8_t *d_data, const uint64_t *offsets
     vsa_plan *p = new (std::nothrow) vsa_plan;
     if (!p) return VSA_E_NOMEM;
     p->ctx = c;
+    c->plans.push_back(p);
     p->d_data = d_data;
     p->nb = nblocks;
     p->segs = pl.segblk.size();
@@ -2155,26 +2268,28 @@ int vsa_plan_create(vsa_ctx_t *c, const uint8_t *d_data, const uint64_t *offsets
 
 int vsa_plan_free(vsa_plan_t *p) {
     if (!p) return VSA_OK;
-    if (p->ctx) {
-        if (p->ctx->pending) vsa_sync(p->ctx);
-        if (p->ctx->launch.d_blocks == p->d_blocks) {
-            p->ctx->launch.d_blocks = nullptr;
-            p->ctx->launch.d_segblk = nullptr;
+    int r = VSA_OK;
+    if (vsa_ctx *c = p->ctx) {
+        if (c->launch.d_blocks == p->d_blocks) {
+            /* a scan of this plan still in flight is completed while its
+             * tables exist (an overflow rescan reads them) */
+            r = finish_pending(c);
+            c->launch.d_blocks = nullptr;
+            c->launch.d_segblk = nullptr;
         }
+        (void)hipStreamSynchronize(c->stream);
+        c->plans.erase(std::remove(c->plans.begin(), c->plans.end(), p), c->plans.end());
     }
     if (p->d_blocks) (void)hipFree(p->d_blocks);
     if (p->d_segblk) (void)hipFree(p->d_segblk);
     delete p;
-    return VSA_OK;
+    return r;
 }
 
 int vsa_scan_plan(vsa_ctx_t *c, const vsa_db_t *db, const vsa_plan_t *p, uint32_t flags,
                   uint64_t *n_matches) {
     if (!c || !db || !p || p->ctx != c) return VSA_E_INVALID;
-    if (c->pending) {
-        c->pending = false;
-        VSA_CHECK(hipStreamSynchronize(c->stream));
-    }
+    if (int r0 = finish_pending(c)) return r0;
     uint64_t dummy;
     return launch_planned(c, db, p->d_data, p->d_blocks, p->d_segblk, p->nb, p->segs,
                           p->seg_bytes, p->end_bits, p->bytes, flags,

@@ -270,7 +270,24 @@ def scan_corpus(db, scratch, d_data, offsets, lens, stream_ids=None, h_data=None
 _sig("vsa_hs_corpus_prepare", ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32,
      ctypes.POINTER(_vp))
 _sig("vsa_hs_corpus_scan", ctypes.c_int, _vp, _vp, _u64p, ctypes.c_uint)
+_sig("vsa_hs_corpus_scan_ex", ctypes.c_int, _vp, _vp, _vp, _u64p, ctypes.c_uint)
 _sig("vsa_hs_corpus_free", ctypes.c_int, _vp)
+
+_M64 = (1 << 64) - 1
+
+
+def seq_digest(matches, h=0):
+    """vsa_hs_seq_digest_step (vectorscan_amd_hs.h) folded over a callback
+    sequence [(id, from, to)] in delivery order."""
+    for i, f, t in matches:
+        x = h ^ ((i * 0x9E3779B97F4A7C15) & _M64) ^ ((f * 0xC2B2AE3D27D4EB4F) & _M64) ^ \
+            ((t * 0x165667B19E3779F9) & _M64)
+        x ^= x >> 30
+        x = (x * 0xBF58476D1CE4E5B9) & _M64
+        x ^= x >> 27
+        x = (x * 0x94D049BB133111EB) & _M64
+        h = x ^ (x >> 31)
+    return h
 
 
 class Corpus:
@@ -296,11 +313,17 @@ class Corpus:
         self.handle = h.value
         self._db, self._scratch = db, scratch  # keep alive
 
-    def scan(self, counts=False, threads=16):
+    def scan(self, counts=False, threads=16, digests=False):
+        """(rc, total, per-block counts or None[, per-block sequence digests
+        (seq_digest of each block's callback sequence) when digests])"""
         cnt = np.zeros(self.n, np.uint64) if counts else None
+        dg = np.zeros(self.n, np.uint64) if digests else None
         total = ctypes.c_uint64()
-        rc = lib.vsa_hs_corpus_scan(self.handle, cnt.ctypes.data if cnt is not None else None,
-                                    ctypes.byref(total), threads)
+        rc = lib.vsa_hs_corpus_scan_ex(self.handle, cnt.ctypes.data if cnt is not None else None,
+                                       dg.ctypes.data if dg is not None else None,
+                                       ctypes.byref(total), threads)
+        if digests:
+            return rc, total.value, cnt, dg
         return rc, total.value, cnt
 
     def close(self):

@@ -205,6 +205,14 @@ class GpuCorpus:
             raise hs.HsError(rc)
         return total, cnt
 
+    def scan_digests(self, threads=16):
+        """(total, per-block counts, per-block callback-sequence digests,
+        hs.seq_digest) of one corpus scan"""
+        rc, total, cnt, dg = self.corpus.scan(True, threads, digests=True)
+        if rc != hs.SUCCESS:
+            raise hs.HsError(rc)
+        return total, cnt, dg
+
     def close(self):
         self.corpus.close()
         if self.d_data:

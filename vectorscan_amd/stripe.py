@@ -16,7 +16,8 @@ The gathers use torch.distributed (RCCL over xGMI with backend "nccl" and
 device tensors; gloo with CPU tensors in the tests): one all_gather of the
 per-rank counts, then the records padded to the largest count
 (gather_matches: all_gather of host lists; gather_to_root: dist.gather of
-device tensors to one rank, used by bench.py).
+device tensors to one rank; PackedGather: bench.py's per-step exchange,
+packed on the device, headers all-gathered, records gathered to the root).
 """
 from dataclasses import dataclass
 
@@ -165,55 +166,91 @@ def gather_to_root(dist, keys, ids, n, root=0):
     return tuple(out) if rank == root else None
 
 
+NOT_READY = 1 << 62  # packed header bit: the records are not usable as packed
+
+
 class PackedGather:
-    """bench.py's per-step exchange: ONE all-gather of every rank's sorted
-    records in a packed int64 buffer ``[count | keys (cap) | ids (cap int32)]``.
+    """bench.py's per-step exchange, with no host count read before it.
 
-    The buffer size must agree across ranks, so it starts at 1,024 records.
-    It grows to 1.25x the largest count every rank sees in the gathered
-    headers, and the gather is then repeated once.  ``fill(keys, ids, cap)``
-    writes this rank's first ``min(n, cap)`` records into the two views.
-    On device tensors it uses RCCL; on CPU tensors (tests) it uses gloo.
-    ``wait()``, if given, runs between the fill and the collective (bench.py:
-    the current stream waits on the scan context's stream)."""
+    Every rank packs its sorted records into an int64 buffer
+    ``[header | keys (cap) | ids (cap int32)]`` (header = the record count,
+    bit 62 set when the records are not final, e.g. the scan overflowed its
+    output; on the GPU ``vsa_scan_pack`` queues this behind the scan, on the
+    device).  Then ONE all-gather of the 8-byte headers and ONE gather of
+    the packed buffers to the root, both queued before the host looks at
+    anything.  The host reads the gathered headers after that (every rank,
+    so all agree): when some rank's records did not fit ``cap`` or were not
+    final, ``cap`` grows to 1.25x the largest count (at least 1,024) and
+    the pack and both collectives run once more.
 
-    def __init__(self, dist, world, device=None):
-        self.dist, self.world, self.device = dist, world, device
+    ``pack(buf, cap)`` fills this rank's buffer; ``wait()``, if given, runs
+    between the pack and the collectives (bench.py: the collective stream
+    waits on the scan context's stream); ``complete()``, if given, runs
+    after the collectives are queued (bench.py: the rank's own scan is
+    completed, which performs any output-overflow rescan, so a repeated
+    pack is final).  Device tensors use RCCL, CPU tensors gloo (tests)."""
+
+    def __init__(self, dist, world, device=None, root=0):
+        self.dist, self.world, self.device, self.root = dist, world, device, root
+        self.rank = dist.get_rank()
         self.cap = 0
-        self.pk = self.ag = None
+        self.pk = self.hdr = self.recv = None
         self._grow(0)
 
     def _grow(self, m):
         import torch
         self.cap = cap = max(1024, m + m // 4)
-        self.pk = torch.zeros(1 + 2 * cap, dtype=torch.int64, device=self.device)
-        self.ag = torch.zeros(self.world * (1 + 2 * cap), dtype=torch.int64, device=self.device)
+        words = 1 + cap + (cap + 1) // 2
+        self.pk = torch.zeros(words, dtype=torch.int64, device=self.device)
+        self.hdr = torch.zeros(self.world, dtype=torch.int64, device=self.device)
+        self.recv = ([torch.zeros(words, dtype=torch.int64, device=self.device)
+                      for _ in range(self.world)] if self.rank == self.root else None)
 
-    def _once(self, n, fill, wait):
-        cap = self.cap
-        self.pk[0:1].fill_(n)
-        import torch
-        ids32 = self.pk.view(torch.int32)
-        fill(self.pk[1:1 + cap], ids32[2 * (1 + cap):2 * (1 + cap) + cap], cap)
+    def _once(self, pack, wait):
+        pack(self.pk, self.cap)
         if wait is not None:
             wait()
-        self.dist.all_gather_into_tensor(self.ag, self.pk)
-        return self.ag.view(self.world, -1)[:, 0].cpu().tolist()
+        self.dist.all_gather_into_tensor(self.hdr, self.pk[0:1])
+        self.dist.gather(self.pk, self.recv, dst=self.root)
 
-    def gather(self, n, fill, wait=None):
-        """every rank's record count (the records land in self.ag)"""
-        counts = self._once(n, fill, wait)
-        if max(counts) > self.cap:
-            self._grow(max(counts))
-            counts = self._once(n, fill, wait)
+    def gather(self, pack, wait=None, complete=None):
+        """every rank's record count (the records are on the root, merged())"""
+        self._once(pack, wait)
+        if complete is not None:
+            complete()
+        hdr = self.hdr.cpu().tolist()
+        counts = [h & ~NOT_READY for h in hdr]
+        if any(h & NOT_READY for h in hdr) or max(counts) > self.cap:
+            if max(counts) > self.cap:
+                self._grow(max(counts))
+            self._once(pack, wait)
+            hdr = self.hdr.cpu().tolist()
+            counts = [h & ~NOT_READY for h in hdr]
+            if any(h & NOT_READY for h in hdr):
+                raise RuntimeError("PackedGather: records still not final after the rescan")
         return counts
 
     def merged(self, counts):
-        """the gathered records concatenated in rank order: (keys, ids)"""
+        """the root's gathered records concatenated in rank order: (keys,
+        ids); None on the other ranks"""
         import torch
+        if self.rank != self.root:
+            return None
         cap = self.cap
-        ag = self.ag.view(self.world, 1 + 2 * cap)
-        keys = ag[:, 1:1 + cap]
-        ids = ag.view(torch.int32)[:, 2 * (1 + cap):2 * (1 + cap) + cap]
-        return (torch.cat([keys[r, :c] for r, c in enumerate(counts)]),
-                torch.cat([ids[r, :c] for r, c in enumerate(counts)]))
+        keys = [r[1:1 + c] for r, c in zip(self.recv, counts)]
+        ids = [r.view(torch.int32)[2 * (1 + cap):2 * (1 + cap) + c]
+               for r, c in zip(self.recv, counts)]
+        return torch.cat(keys), torch.cat(ids)
+
+
+def host_pack(keys, ids, n):
+    """pack(buf, cap) for records held in torch tensors (CPU tests): the
+    PackedGather layout, header = n"""
+    import torch
+
+    def pack(buf, cap):
+        m = min(n, cap)
+        buf[0] = n
+        buf[1:1 + m].copy_(keys[:m])
+        buf.view(torch.int32)[2 * (1 + cap):2 * (1 + cap) + m].copy_(ids[:m])
+    return pack
