@@ -168,6 +168,8 @@ def main():
     ap.add_argument("--lits", type=int, default=5000)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline timing")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="one scan context: each step completed before the next is queued")
     ap.add_argument("--no-settle", action="store_true",
                     help="skip the clock-settle launches before the warmup steps")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -236,39 +238,71 @@ def run(args):
     rlos = [w.rlo for w in wins]
     local_bytes = g1 - cuts[rank]
 
-    # N > 1 (stripe.PackedGather): each rank's scan runs asynchronously, its
-    # sorted records are packed on the device behind it (vsa_scan_pack: the
-    # count rides in the header, no host read), then ONE RCCL all-gather of
-    # the 8-byte headers and ONE gather of the packed records to rank 0 over
-    # xGMI; the host looks at the headers only after both are queued.  Rank
-    # 0 concatenates the ranks' records = global end order (keys are corpus
+    # Steps are pipelined over two scan contexts (own plan, counters and
+    # output buffers each; one stream and the database shared, so scans run
+    # one at a time in queue order and each kernel time is its own): step
+    # k's scan is queued
+    # before step k-1 is completed on the host, so its sort, count readback
+    # and host turnaround run while step k's scan is on the GPU instead of
+    # between two scans.  Every step still scans the whole corpus, sorts its
+    # records in HBM and has its count read (all timed counts are checked);
+    # the timed region ends after the last step is complete.  --no-pipeline:
+    # one context, each step completed before the next is queued.
+    #
+    # N > 1 (stripe.PackedGather): a rank's sorted records are packed on the
+    # device behind its asynchronous scan (vsa_scan_pack: the count rides in
+    # the header, no host read), then ONE RCCL all-gather of the 8-byte
+    # headers and ONE gather of the packed records to rank 0 over xGMI; the
+    # host reads the headers only when the step is completed.  Rank 0
+    # concatenates the ranks' records = global end order (keys are corpus
     # offsets).
     st = {"keys": None, "ids": None}
-    # the rank's windows as one launch plan (block table + segment map on
-    # the device, built once: vsa_plan_create), scanned every step
-    plan = ctx.plan(dptr, offs, lens, None, None, rlos)
-    if dist is not None:
-        # the context's stream: the collectives wait for the pack on the GPU
-        ctx_stream = torch.cuda.ExternalStream(ctx.stream, device=dev)
-        pg = stripe.PackedGather(dist, world, dev)
+    nslot = 1 if args.no_pipeline else 2
+    ctxs = [ctx] + [vsa.Context(share_stream_with=ctx) for _ in range(nslot - 1)]
+    # the rank's windows as one launch plan per context (block table +
+    # segment map on the device, built once: vsa_plan_create)
+    plans = [c.plan(dptr, offs, lens, None, None, rlos) for c in ctxs]
+    slots = []
+    for c, pl in zip(ctxs, plans):
+        sl = {"ctx": c, "plan": pl}
+        if dist is not None:
+            # the context's stream: the collectives wait for the pack on the GPU
+            cs = torch.cuda.ExternalStream(c.stream, device=dev)
+            sl["pg"] = stripe.PackedGather(dist, world, dev)
+            sl["pack"] = (lambda c_: lambda buf, cap: c_.scan_pack(buf.data_ptr(), cap))(c)
+            sl["wait"] = (lambda s_: lambda: torch.cuda.current_stream().wait_stream(s_))(cs)
+        slots.append(sl)
+    kms = []
 
-        def pack(buf, cap):
-            ctx.scan_pack(buf.data_ptr(), cap)
+    def issue(k):
+        sl = slots[k % nslot]
+        sl["ctx"].scan_plan(db, sl["plan"], asynchronous=True)
+        if dist is not None:
+            sl["pg"].start(sl["pack"], sl["wait"])
 
-        def wait():
-            torch.cuda.current_stream().wait_stream(ctx_stream)
-
-        def complete():
-            ctx.scan_wait()  # the local scan's own completion (overflow rescan)
-
-    def step():
+    def complete(k):
+        sl = slots[k % nslot]
+        c = sl["ctx"]
         if dist is None:
-            return ctx.scan_plan(db, plan)
-        ctx.scan_plan(db, plan, asynchronous=True)
-        cl = pg.gather(pack, wait, complete)
-        if rank == 0:
-            st["keys"], st["ids"] = pg.merged(cl)
-        return int(sum(cl))
+            n = c.scan_wait()
+        else:
+            cl = sl["pg"].finish(sl["pack"], sl["wait"], c.scan_wait)
+            if rank == 0:
+                st["keys"], st["ids"] = sl["pg"].merged(cl)
+            n = int(sum(cl))
+        kms.append(c.kernel_ms())
+        return n
+
+    def run_steps(k_steps):
+        """k_steps steps, pipelined nslot deep; their counts in step order"""
+        counts = []
+        for k in range(k_steps):
+            issue(k)
+            if k >= nslot - 1:
+                counts.append(complete(k - nslot + 1))
+        for k in range(max(0, k_steps - nslot + 1), k_steps):
+            counts.append(complete(k))
+        return counts
 
     # Clock settle (untimed, before the W warmup steps): after an idle
     # period the GPU's power management takes ~30-40 launches (~40 ms of
@@ -282,7 +316,7 @@ def run(args):
         hist = []
         while settle_n < 400 and time.perf_counter() - t_settle < 3.0:
             # the rank's own scan only: ranks settle independently, no collective
-            ctx.scan_plan(db, plan)
+            ctx.scan_plan(db, plans[0])
             settle_n += 1
             hist.append(ctx.kernel_ms())
             if settle_n >= 40 and max(hist[-8:]) <= 1.02 * min(hist[-8:]):
@@ -290,26 +324,24 @@ def run(args):
     t_settle = time.perf_counter() - t_settle
     if dist is not None:
         dist.barrier()
-    for _ in range(args.warmup):
-        step()
+    run_steps(args.warmup)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    kms = []
+    kms.clear()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    nm = 0
-    for _ in range(args.steps):
-        nm = step()
-        kms.append(ctx.kernel_ms())
+    counts = run_steps(args.steps)
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
     el = t1 - t0
-    ncand = int(ctx.candidates())  # rank 0, last timed step
+    nm = counts[-1]
+    last = slots[(args.steps - 1) % nslot]["ctx"]
+    ncand = int(last.candidates())  # rank 0, last timed step
     if dist is not None:
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -320,7 +352,7 @@ def run(args):
     # records of the last timed step, global offsets (rank 0)
     if rank == 0:
         if dist is None:
-            res = ctx.results(nm)
+            res = last.results(nm)
             keys, ids = res["key"], res["id"].astype(np.uint64)
         else:
             keys = st["keys"].cpu().numpy().view(np.uint64)
@@ -358,7 +390,8 @@ def run(args):
                     cpu_ok = cpu_ok and d == want[-1]
                 parity_bytes += hi - lo
                 del host
-            parity = sorted_ok and got == want and sum(w[0] for w in want) == nm
+            parity = (sorted_ok and got == want and sum(w[0] for w in want) == nm and
+                      all(c == nm for c in counts))
             if not parity:
                 print("bench: PARITY FAILURE got %s want %s sorted %s" % (got, want, sorted_ok),
                       file=sys.stderr, flush=True)
@@ -406,6 +439,7 @@ def run(args):
                          "traffic": traffic, "kernel_ms": round(kavg, 4),
                          "scope": "rank 0 scan kernel (%d input bytes)" % local_bytes},
             "cpu_baseline": cpu,
+            "pipeline": nslot,
             "settle": {"launches": settle_n, "s": round(t_settle, 3),
                        "why": "GPU clock ramp after idle (profiles/r03_ramp.jsonl): untimed "
                               "scans until the kernel time is stable, before the warmup"},
@@ -414,9 +448,11 @@ def run(args):
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
-    plan.close()
+    for pl in plans:
+        pl.close()
     db.close()
-    ctx.close()
+    for c in ctxs:
+        c.close()
 
 
 def blob_domain(blob):

@@ -45,6 +45,34 @@ typedef hwlm_group_t hwlmcb_rv_t;     /* hwlm.h:63 */
 typedef hwlmcb_rv_t (*HWLMCallback)(size_t end, uint32_t id,
                                     struct hs_scratch *scratch);
 
+/* The GPU entry points under their own names (same arguments and results
+ * as hwlmExec, hwlmExecStreaming, fdrExec, noodExec above), for a build
+ * that keeps the reference's definitions and routes each call by its
+ * length. */
+hwlm_error_t vsa_gpu_hwlmExec(const struct HWLM *tab, const uint8_t *buf, size_t len,
+                              size_t start, HWLMCallback cb, struct hs_scratch *scratch,
+                              hwlm_group_t groups);
+hwlm_error_t vsa_gpu_hwlmExecStreaming(const struct HWLM *tab, size_t len, size_t start,
+                                       HWLMCallback cb, struct hs_scratch *scratch,
+                                       hwlm_group_t groups);
+hwlm_error_t vsa_gpu_fdrExec(const struct FDR *fdr, const uint8_t *buf, size_t len,
+                             size_t start, HWLMCallback cb, struct hs_scratch *scratch,
+                             hwlm_group_t groups);
+hwlm_error_t vsa_gpu_noodExec(const struct noodTable *n, const uint8_t *buf, size_t len,
+                              size_t start, HWLMCallback cb, struct hs_scratch *scratch);
+
+/* Registration of an immutable bytecode blob for the drop-ins: between
+ * vsa_hwlm_register(blob) and vsa_hwlm_unregister(blob) the bytes at blob
+ * do not change, so the drop-ins' device-copy cache serves them without
+ * comparing the whole blob on every call (unregistered blobs are compared,
+ * ~20 us per call for a 0.4 MB FDR blob).  bare_type -1: an HWLM
+ * (hwlmExec / hwlmExecStreaming); 12 (HWLM_ENGINE_FDR) / 16
+ * (HWLM_ENGINE_NOOD): a bare FDR or noodle engine (fdrExec / noodExec
+ * pointers).  The reference-side call sites are where the database is
+ * loaded and freed. */
+int vsa_hwlm_register(const void *blob, int bare_type);
+int vsa_hwlm_unregister(const void *blob);
+
 /* Replaces hwlmExec, src/hwlm/hwlm.h:116 (impl. src/hwlm/hwlm.c:178).
  * Copies buf to the GPU, scans, replays confirmed matches through cb in the
  * reference order (end, bucket, confirm-chain order) applying groups /
@@ -145,6 +173,12 @@ typedef struct {
 int vsa_device_count(void);
 int vsa_ctx_create(int device, vsa_ctx_t **ctx);
 int vsa_ctx_destroy(vsa_ctx_t *ctx);
+/* A second workspace on `base`'s device and stream: scans queued through
+ * either run in queue order, so a pipelined caller (scan k + 1 queued before
+ * waiting for scan k, VSA_SCAN_ASYNC) keeps one kernel at a time on the GPU
+ * and clean per-scan kernel times.  The stream lives until the last context
+ * using it is destroyed. */
+int vsa_ctx_create_shared(vsa_ctx_t *base, vsa_ctx_t **ctx);
 void *vsa_ctx_stream(vsa_ctx_t *ctx);
 
 /* Upload an HWLM blob (reference layout, 64-byte aligned host copy). */

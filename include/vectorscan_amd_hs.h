@@ -148,6 +148,13 @@ int vsa_hs_corpus_scan(vsa_hs_corpus_t *corpus, uint64_t *counts, uint64_t *tota
  * what hs_scan / hs_scan_stream would have delivered for that block. */
 int vsa_hs_corpus_scan_ex(vsa_hs_corpus_t *corpus, uint64_t *counts, uint64_t *digests,
                           uint64_t *total, unsigned threads);
+/* hsbench's repeat loop: `repeats` scans of the corpus, pass k + 1 on the
+ * GPU while the host replays pass k (the report program of the records
+ * that do not map one to one onto matches).  totals[repeats] = the matches
+ * of each pass; counts / digests (optional, as vsa_hs_corpus_scan_ex) are
+ * those of the last pass. */
+int vsa_hs_corpus_scan_repeats(vsa_hs_corpus_t *corpus, uint32_t repeats, uint64_t *totals,
+                               uint64_t *counts, uint64_t *digests, unsigned threads);
 static inline uint64_t vsa_hs_seq_digest_step(uint64_t h, unsigned id, unsigned long long from,
                                               unsigned long long to) {
     uint64_t x = h ^ ((uint64_t)id * 0x9E3779B97F4A7C15ULL) ^

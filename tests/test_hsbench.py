@@ -277,6 +277,11 @@ def _check_sequences(g, exprs, flags, ids, blocks, mode):
            if int(digests[i]) != hs.seq_digest(want[b]) or int(counts[i]) != len(want[b])]
     assert not bad, "chunks whose callback sequence differs (pos, want n, got n): %s" % bad[:8]
     assert total == sum(len(w) for w in want)
+    # hsbench's pipelined repeat loop (pass k + 1 scanned while pass k
+    # replays): every pass the same total, the last pass's sequences equal
+    rc, tot, cnt2, dg2 = g.corpus.scan_repeats(3, True, 16, True)
+    assert rc == hs.SUCCESS and [int(t) for t in tot] == [total] * 3
+    assert np.array_equal(cnt2, counts) and np.array_equal(dg2, digests)
     return total
 
 

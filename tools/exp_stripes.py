@@ -1,9 +1,11 @@
 """One GPU, the per-rank step of bench.py at N = 1, 2, 4, 8 (verdict r02
 item 4): rank 0's windows of plan_corpus_stripes over the 4 GiB cfg-4
-corpus (4 / 2 / 1 / 0.5 GiB), scanned exactly as a rank's step does
-(vsa_scan_blocks_ex with report_lo, count read back), warm, then K timed
-steps.  Prints one JSON line per N: step ms, kernel ms, step - kernel.
-The collective is not part of this (one GPU); it is what an N-rank run adds.
+corpus (4 / 2 / 1 / 0.5 GiB), scanned as a rank's step does (a plan,
+report_lo, sorted records, count read back), after a clock settle, then K
+timed steps, both one step at a time ("sync") and pipelined over two
+contexts as bench.py does ("pipe").  One JSON line per N and mode: step ms,
+kernel ms, step - kernel.  The collectives are not part of this (one GPU):
+they are what an N-rank run adds.
   python tools/exp_stripes.py [steps] [warmup]"""
 import json
 import os
@@ -19,9 +21,10 @@ from vectorscan_amd import stripe  # noqa: E402
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
 warm = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 dev = torch.device("cuda", 0)
-ctx = vsa.Context(0)
+ctxs = [vsa.Context(0)]
+ctxs.append(vsa.Context(share_stream_with=ctxs[0]))
 lits = bench.make_literals(5000, seed=12)
-db = vsa.Database(ctx, vsa.hwlm_build(lits))
+db = vsa.Database(ctxs[0], vsa.hwlm_build(lits))
 total = 4 << 30
 bl = total // 4
 data = bench.make_corpus_device(torch, 0, total, total, lits, 5, 64 << 10, dev)
@@ -33,19 +36,32 @@ for n in (1, 2, 4, 8):
     offs = [w.wlo for w in wins]
     lens = [w.wlen for w in wins]
     rlos = [w.rlo for w in wins]
-    plan = ctx.plan(dptr, offs, lens, None, None, rlos)
-    for _ in range(warm):
-        ctx.scan_plan(db, plan)
-    ks = []
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        m = ctx.scan_plan(db, plan)
-        ks.append(ctx.kernel_ms())
-    torch.cuda.synchronize()
-    st = (time.perf_counter() - t0) / steps * 1e3
-    k = sum(ks) / len(ks)
-    plan.close()
-    print(json.dumps({"ranks": n, "rank_bytes": cuts[1] - cuts[0], "windows": len(wins),
-                      "step_ms": round(st, 4), "kernel_ms": round(k, 4),
-                      "overhead_us": round((st - k) * 1e3, 1), "matches": m}), flush=True)
+    plans = [c.plan(dptr, offs, lens, None, None, rlos) for c in ctxs]
+    for _ in range(60):  # clock settle + warm
+        ctxs[0].scan_plan(db, plans[0])
+    for mode in ("sync", "pipe"):
+        ks, counts = [], []
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if mode == "sync":
+            for _ in range(steps):
+                counts.append(ctxs[0].scan_plan(db, plans[0]))
+                ks.append(ctxs[0].kernel_ms())
+        else:
+            for k in range(steps):
+                ctxs[k % 2].scan_plan(db, plans[k % 2], asynchronous=True)
+                if k:
+                    counts.append(ctxs[(k - 1) % 2].scan_wait())
+                    ks.append(ctxs[(k - 1) % 2].kernel_ms())
+            counts.append(ctxs[(steps - 1) % 2].scan_wait())
+            ks.append(ctxs[(steps - 1) % 2].kernel_ms())
+        torch.cuda.synchronize()
+        st = (time.perf_counter() - t0) / steps * 1e3
+        k = sum(ks) / len(ks)
+        print(json.dumps({"ranks": n, "mode": mode, "rank_bytes": cuts[1] - cuts[0],
+                          "windows": len(wins), "step_ms": round(st, 4),
+                          "kernel_ms": round(k, 4), "overhead_us": round((st - k) * 1e3, 1),
+                          "matches": counts[-1], "counts_equal": len(set(counts)) == 1}),
+              flush=True)
+    for pl in plans:
+        pl.close()

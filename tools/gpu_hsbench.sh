@@ -10,6 +10,9 @@ if [ "$1" = "cfg5" ] || [ "$1" = "all" ]; then
   echo "== mode block, cfg-5-shaped 10k mixed literals" >> gpurun_out/hsbench.log
   timeout -k 10 300 python -u -m vectorscan_amd.hsbench -e ${D}_c5/sigs -c ${D}_c5/corpus.db \
       -n 10 --literal-on --json -N >> gpurun_out/hsbench.log 2>&1 || exit 1
+  echo "== mode block, cfg-5-shaped, one pass at a time" >> gpurun_out/hsbench.log
+  timeout -k 10 300 python -u -m vectorscan_amd.hsbench -e ${D}_c5/sigs -c ${D}_c5/corpus.db \
+      -n 10 --literal-on --json -N --no-pipeline >> gpurun_out/hsbench.log 2>&1 || exit 1
   rm -rf ${D}_c5
   [ "$1" = "cfg5" ] && { cat gpurun_out/hsbench.log; exit 0; }
 fi

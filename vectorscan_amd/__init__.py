@@ -118,6 +118,7 @@ _sig("vsa_truffle_build_masks", None, ctypes.c_void_p, ctypes.c_void_p,
 _sig("vsa_device_count", ctypes.c_int)
 _sig("vsa_ctx_create", ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p))
 _sig("vsa_ctx_destroy", ctypes.c_int, ctypes.c_void_p)
+_sig("vsa_ctx_create_shared", ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p))
 _sig("vsa_ctx_stream", ctypes.c_void_p, ctypes.c_void_p)
 _sig("vsa_db_load", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
      ctypes.POINTER(ctypes.c_void_p))
@@ -543,9 +544,16 @@ def truffle_build_masks(chars):
 class Context:
     """vsa_ctx: a HIP stream + device workspace on one GPU."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, share_stream_with=None):
+        """share_stream_with: another Context whose stream this one queues
+        on (vsa_ctx_create_shared): a second workspace for pipelined scans
+        that still run one at a time"""
         self.ptr = ctypes.c_void_p()
-        rc = lib.vsa_ctx_create(device, ctypes.byref(self.ptr))
+        if share_stream_with is not None:
+            device = share_stream_with.device
+            rc = lib.vsa_ctx_create_shared(share_stream_with.ptr, ctypes.byref(self.ptr))
+        else:
+            rc = lib.vsa_ctx_create(device, ctypes.byref(self.ptr))
         if rc != 0:
             raise RuntimeError("vsa_ctx_create(%d) failed (%d)" % (device, rc))
         self.device = device

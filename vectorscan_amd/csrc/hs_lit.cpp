@@ -753,48 +753,20 @@ int vsa_hs_corpus_free(vsa_hs_corpus_t *c) {
     return VSA_HS_SUCCESS;
 }
 
-int vsa_hs_corpus_scan(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *total,
-                       unsigned threads) {
-    return vsa_hs_corpus_scan_ex(cp, counts, nullptr, total, threads);
-}
-
-int vsa_hs_corpus_scan_ex(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *digests,
-                          uint64_t *total, unsigned threads) {
-    if (!cp || !total || !valid_db(cp->db)) return VSA_HS_INVALID;
+/* The records of one corpus scan (sorted by d_data end offset; keys are
+ * rebased to their block in place) through the report program on
+ * `threads` host threads: per-block counts / sequence digests (optional)
+ * and the total. */
+static int corpus_replay(vsa_hs_corpus *cp, uint64_t *keys, const uint32_t *ids, uint64_t nm,
+                         uint64_t *counts, uint64_t *digests, uint64_t *total,
+                         unsigned threads) {
     const vsa_hs_database *db = cp->db;
-    vsa_hs_scratch *scratch = cp->scratch;
-    int rc = enter(db, scratch);
-    if (rc != VSA_HS_SUCCESS) return rc;
-    vsa_db_t *ddb = device_db(scratch, db);
+    vsa_db_t *ddb = device_db(cp->scratch, db);
     const uint32_t nblocks = (uint32_t)cp->offsets.size();
     const uint64_t *offsets = cp->offsets.data(), *lens = cp->lens.data();
     if (counts) std::fill(counts, counts + nblocks, 0);
     if (digests) std::fill(digests, digests + nblocks, 0);
     *total = 0;
-    const bool fast = db->simple && !counts && !digests;
-    /* VSA_HOST_TIMING: per-phase wall times on stderr */
-    static const bool timing = getenv("VSA_HOST_TIMING") != nullptr;
-    auto now = [] { return std::chrono::steady_clock::now(); };
-    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
-        return std::chrono::duration<double, std::milli>(b - a).count();
-    };
-    const auto t0 = now();
-    std::vector<uint64_t> keys;
-    std::vector<uint32_t> ids;
-    uint64_t nm = 0;
-    if (cp->plan &&
-        vsa::scan_records(scratch->ctx, ddb, cp->d_data, nullptr, nullptr, nullptr, 0,
-                          fast ? nullptr : &keys, fast ? nullptr : &ids, &nm,
-                          cp->plan) != VSA_OK) {
-        leave(scratch);
-        return VSA_HS_UNKNOWN_ERROR;
-    }
-    if (fast) {
-        *total = nm;
-        leave(scratch);
-        return VSA_HS_SUCCESS;
-    }
-    const auto t1 = now();
     /* records -> blocks: the records are sorted by end (d_data offsets),
      * the non-empty blocks by offset; each run of records is placed with one
      * binary search, so the cost follows the records, not the block count.
@@ -896,7 +868,7 @@ int vsa_hs_corpus_scan_ex(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *diges
                 dg.h = 0;
                 r.cur = j;
                 if (bstamp[b] == gen && re[b] > rb[b] &&
-                    vsa::replay_records(ddb, keys.data() + rb[b], ids.data() + rb[b],
+                    vsa::replay_records(ddb, keys + rb[b], ids + rb[b],
                                         re[b] - rb[b], on_fragment, &r) != HWLM_SUCCESS) {
                     status[t] = VSA_HS_UNKNOWN_ERROR;
                     return;
@@ -910,20 +882,160 @@ int vsa_hs_corpus_scan_ex(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *diges
             part[t] += cnt;
         }
     };
-    const auto t2 = now();
     if (T == 1) work(0);
     else replay_pool().run(T, work);
-    if (timing)
-        fprintf(stderr, "vsa_hs_corpus_scan: scan+copy %.3f ms, map %.3f ms, replay %.3f ms "
-                        "(%u threads, %zu live units, %llu records)\n",
-                ms(t0, t1), ms(t1, t2), ms(t2, now()), T, live.size(),
-                (unsigned long long)nm);
-    leave(scratch);
     for (unsigned t = 0; t < T; t++) {
         if (status[t] != VSA_HS_SUCCESS) return status[t];
         *total += part[t];
     }
     return VSA_HS_SUCCESS;
+}
+
+
+int vsa_hs_corpus_scan(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *total,
+                       unsigned threads) {
+    return vsa_hs_corpus_scan_ex(cp, counts, nullptr, total, threads);
+}
+
+int vsa_hs_corpus_scan_ex(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *digests,
+                          uint64_t *total, unsigned threads) {
+    if (!cp || !total || !valid_db(cp->db)) return VSA_HS_INVALID;
+    const vsa_hs_database *db = cp->db;
+    vsa_hs_scratch *scratch = cp->scratch;
+    int rc = enter(db, scratch);
+    if (rc != VSA_HS_SUCCESS) return rc;
+    vsa_db_t *ddb = device_db(scratch, db);
+    const uint32_t nblocks = (uint32_t)cp->offsets.size();
+    if (counts) std::fill(counts, counts + nblocks, 0);
+    if (digests) std::fill(digests, digests + nblocks, 0);
+    *total = 0;
+    const bool fast = db->simple && !counts && !digests;
+    /* VSA_HOST_TIMING: per-phase wall times on stderr */
+    static const bool timing = getenv("VSA_HOST_TIMING") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto t0 = now();
+    std::vector<uint64_t> keys;
+    std::vector<uint32_t> ids;
+    uint64_t nm = 0;
+    if (cp->plan &&
+        vsa::scan_records(scratch->ctx, ddb, cp->d_data, nullptr, nullptr, nullptr, 0,
+                          fast ? nullptr : &keys, fast ? nullptr : &ids, &nm,
+                          cp->plan) != VSA_OK) {
+        leave(scratch);
+        return VSA_HS_UNKNOWN_ERROR;
+    }
+    if (fast) {
+        *total = nm;
+        leave(scratch);
+        return VSA_HS_SUCCESS;
+    }
+    const auto t1 = now();
+    rc = corpus_replay(cp, keys.data(), ids.data(), nm, counts, digests, total, threads);
+    if (timing)
+        fprintf(stderr, "vsa_hs_corpus_scan: scan+copy %.3f ms, map+replay %.3f ms (%llu records)\n",
+                ms(t0, t1), ms(t1, now()), (unsigned long long)nm);
+    leave(scratch);
+    return rc;
+}
+
+/* hsbench's repeat loop (main.cpp:487-511, `repeats` passes over the
+ * corpus) pipelined: pass k + 1's scan is queued on the GPU behind the copy
+ * of pass k's records, and runs while the host replays pass k through the
+ * report program, so a pass costs max(scan, replay) instead of their sum.
+ * totals[k] = the matches of pass k; counts / digests (optional) are those
+ * of the last pass.  Every pass scans the whole corpus and replays all its
+ * records. */
+int vsa_hs_corpus_scan_repeats(vsa_hs_corpus_t *cp, uint32_t repeats, uint64_t *totals,
+                               uint64_t *counts, uint64_t *digests, unsigned threads) {
+    if (!cp || !totals || !repeats || !valid_db(cp->db)) return VSA_HS_INVALID;
+    const vsa_hs_database *db = cp->db;
+    if (db->simple && !counts && !digests) {
+        /* one record = one match: the GPU's counts, nothing to replay */
+        for (uint32_t k = 0; k < repeats; k++) {
+            int rc = vsa_hs_corpus_scan_ex(cp, nullptr, nullptr, &totals[k], threads);
+            if (rc != VSA_HS_SUCCESS) return rc;
+        }
+        return VSA_HS_SUCCESS;
+    }
+    vsa_hs_scratch *scratch = cp->scratch;
+    int rc = enter(db, scratch);
+    if (rc != VSA_HS_SUCCESS) return rc;
+    vsa_db_t *ddb = device_db(scratch, db);
+    vsa_ctx_t *ctx = scratch->ctx;
+    struct Buf {
+        uint64_t *k = nullptr;
+        uint32_t *i = nullptr;
+        uint64_t cap = 0, n = 0;
+    } buf[2];
+    auto grow = [&](Buf &b, uint64_t n) -> bool {
+        if (n <= b.cap) return true;
+        vsa::host_pinned_free(b.k);
+        vsa::host_pinned_free(b.i);
+        b.cap = n + n / 4 + 1024;
+        b.k = (uint64_t *)vsa::host_pinned_alloc(b.cap * 8);
+        b.i = (uint32_t *)vsa::host_pinned_alloc(b.cap * 4);
+        return b.k && b.i;
+    };
+    static const bool timing = getenv("VSA_HOST_TIMING") != nullptr;
+    using clk = std::chrono::steady_clock;
+    auto ms = [](clk::time_point a, clk::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    rc = VSA_HS_SUCCESS;
+    uint64_t nm = 0;
+    if (!cp->plan) {
+        std::fill(totals, totals + repeats, 0);
+        if (counts) std::fill(counts, counts + cp->offsets.size(), 0);
+        if (digests) std::fill(digests, digests + cp->offsets.size(), 0);
+        leave(scratch);
+        return VSA_HS_SUCCESS;
+    }
+    /* pass 0: scanned, its records on their way to the host */
+    if (vsa_scan_plan(ctx, ddb, cp->plan, 0, &nm) != VSA_OK || !grow(buf[0], nm) ||
+        vsa::records_fetch_async(ctx, nm, buf[0].k, buf[0].i) != VSA_OK)
+        rc = VSA_HS_UNKNOWN_ERROR;
+    buf[0].n = nm;
+    for (uint32_t k = 0; k < repeats && rc == VSA_HS_SUCCESS; k++) {
+        Buf &cur = buf[k & 1], &nxt = buf[(k + 1) & 1];
+        const bool more = k + 1 < repeats;
+        /* pass k + 1 queued behind pass k's copy (the copy read the sorted
+         * records before the scan rewrites them) */
+        if (more && vsa_scan_plan(ctx, ddb, cp->plan, VSA_SCAN_ASYNC, &nm) != VSA_OK) {
+            rc = VSA_HS_UNKNOWN_ERROR;
+            break;
+        }
+        const auto t0 = clk::now();
+        if (vsa::records_wait(ctx) != VSA_OK) {
+            rc = VSA_HS_UNKNOWN_ERROR;
+            break;
+        }
+        const auto t1 = clk::now();
+        const bool last = !more;
+        rc = corpus_replay(cp, cur.k, cur.i, cur.n, last ? counts : nullptr,
+                           last ? digests : nullptr, &totals[k], threads);
+        const auto t2 = clk::now();
+        if (rc != VSA_HS_SUCCESS || !more) break;
+        if (vsa_scan_wait(ctx, &nm) != VSA_OK || !grow(nxt, nm) ||
+            vsa::records_fetch_async(ctx, nm, nxt.k, nxt.i) != VSA_OK) {
+            rc = VSA_HS_UNKNOWN_ERROR;
+            break;
+        }
+        if (timing)
+            fprintf(stderr, "vsa_hs_corpus_scan_repeats: pass %u copy wait %.3f ms, replay %.3f ms, "
+                    "next scan wait %.3f ms (%llu records)\n", k, ms(t0, t1), ms(t1, t2),
+                    ms(t2, clk::now()), (unsigned long long)cur.n);
+        nxt.n = nm;
+    }
+    (void)vsa_sync(ctx);
+    for (Buf &b : buf) {
+        vsa::host_pinned_free(b.k);
+        vsa::host_pinned_free(b.i);
+    }
+    leave(scratch);
+    return rc;
 }
 
 int vsa_hs_scan_corpus(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch,

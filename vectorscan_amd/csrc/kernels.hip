@@ -1792,18 +1792,34 @@ __global__ void __launch_bounds__(256) vsa_bin_sort(const uint64_t *ctr, uint64_
  * next launch, which therefore needs no memset. */
 __global__ void __launch_bounds__(256) vsa_publish(unsigned long long *ctr,
                                                    unsigned long long *h,
-                                                   unsigned long long seq, uint32_t nzero) {
+                                                   unsigned long long seq, uint32_t nzero,
+                                                   const uint64_t *keys, const uint32_t *ids,
+                                                   uint32_t kmax) {
     const u32 t = threadIdx.x;
     unsigned long long v = 0;
     if (t < 16) v = ctr[t];
+    /* small results (drop-in calls): up to kmax raw records go along, at
+     * h[17 ..] (keys) and (u32 *)(h + 17 + kmax) (ids) */
+    if (kmax) {
+        const uint64_t n = ctr[0];
+        const uint32_t m = n < kmax ? (uint32_t)n : kmax;
+        uint32_t *hid = (uint32_t *)(h + 17 + kmax);
+        for (uint32_t i = t; i < m; i += 256) {
+            h[17 + i] = keys[i];
+            hid[i] = ids[i];
+        }
+    }
     __syncthreads(); /* every read before any zeroing */
     if (t < 16) {
         h[1 + t] = v;
         ctr[nzero + t] = v; /* kept on the device too (vsa_pack) */
     }
     for (u32 i = t; i < nzero; i += 256) ctr[i] = 0;
+    /* every storing wave waits for its own stores, then the barrier; lane
+     * 0's system-scope release orders the flag after all of them */
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     if (t == 0) {
-        /* lanes 0..15 are this wave: the fence waits for their stores */
         __threadfence_system();
         __hip_atomic_store(&h[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }

@@ -50,7 +50,8 @@ __global__ void vsa_bin_sort(const uint64_t *ctr, uint64_t cap, uint32_t *counts
                              const uint32_t *cursor, uint64_t *keys, uint32_t *ids);
 __global__ void vsa_class_scan_lut(VsaClassParams P, uint64_t span);
 __global__ void vsa_publish(unsigned long long *ctr, unsigned long long *h, unsigned long long seq,
-                            uint32_t nzero);
+                            uint32_t nzero, const uint64_t *keys, const uint32_t *ids,
+                            uint32_t kmax);
 __global__ void vsa_pack(const unsigned long long *saved, uint64_t out_cap, const uint64_t *keys,
                          const uint32_t *ids, uint64_t cap, uint64_t *dst);
 __global__ void vsa_pair_scan(VsaPairParams P);
@@ -83,10 +84,16 @@ constexpr int CLASS_SLOTS = 64;
 constexpr int PAIR_BASE = 160; /* double-shufti stage results, 16 apart */
 constexpr int CLASS_BASE = 256;
 constexpr int N_COUNTERS = CLASS_BASE + 16 * CLASS_SLOTS;
+/* h_pub (vsa_publish): [0] sequence, [1..16] counters, then up to PUB_RECS
+ * raw records of a drop-in scan (keys, then ids as u32) */
+constexpr uint32_t PUB_RECS = 1024;
+constexpr size_t PUB_WORDS = 17 + PUB_RECS + PUB_RECS / 2;
 
 struct Workspace {
     uint8_t *d_in = nullptr;
     size_t in_cap = 0;
+    uint8_t *h_in = nullptr; /* pinned staging of drop-in inputs (one DMA) */
+    size_t h_in_cap = 0;
     uint64_t *d_keys[2] = {nullptr, nullptr};
     uint32_t *d_ids[2] = {nullptr, nullptr};
     uint64_t out_cap = 0;
@@ -129,6 +136,9 @@ struct vsa_ctx {
     int device = 0;
     int num_cus = 256;
     hipStream_t stream = nullptr;
+    /* the stream's owner: shared by contexts made with vsa_ctx_create_shared,
+     * destroyed with the last of them */
+    std::shared_ptr<void> stream_ref;
     Workspace ws;
     int cur = 0;          /* which key/id buffer holds the last results */
     uint64_t last_n = 0;
@@ -156,6 +166,7 @@ struct vsa_ctx {
     /* kernel-only timing of the last scan (hipEvents on the scan stream) */
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_done = nullptr; /* polled by wait_stream */
+    hipEvent_t ev_rec = nullptr;  /* records_fetch_async's copies done */
     double last_kernel_ms = 0.0;
     uint32_t bin_skip = 0;   /* launches left without the binned sort */
     bool bins_clean = false; /* the bin counts are zero (no memset needed) */
@@ -294,6 +305,22 @@ int ensure_in(vsa_ctx *c, size_t need) {
  * one pinned mirror, laid out per call (the map right after this call's
  * blocks), so a call uploads them with a single copy of just their bytes */
 constexpr size_t TAB_ALIGN = 256;
+
+/* drop-in inputs up to this size are staged through pinned memory: one
+ * host memcpy and one asynchronous DMA instead of a pageable copy */
+constexpr size_t PIN_STAGE_MAX = (size_t)8 << 20;
+
+int ensure_hin(vsa_ctx *c, size_t need) {
+    Workspace &w = c->ws;
+    if (need <= w.h_in_cap) return VSA_OK;
+    if (w.h_in) (void)hipHostFree(w.h_in);
+    w.h_in = nullptr;
+    w.h_in_cap = 0;
+    const size_t cap = std::max<size_t>(need, 64 << 10);
+    VSA_CHECK(hipHostMalloc((void **)&w.h_in, cap, hipHostMallocDefault));
+    w.h_in_cap = cap;
+    return VSA_OK;
+}
 
 int ensure_tables(vsa_ctx *c, uint32_t nb, uint64_t nsegs, bool keep_blocks = false) {
     Workspace &w = c->ws;
@@ -500,9 +527,23 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
     if (c->launch.bins && !c->bins_clean)
         VSA_CHECK(hipMemsetAsync(c->ws.d_bins, 0, VSA_SORT_BINS * sizeof(uint32_t), c->stream));
     c->bins_clean = false;
-    VSA_CHECK(hipEventRecord(c->ev0, c->stream));
+    /* drop-in calls (a few records, sorted by the host) skip the kernel
+     * timing and get their counters and records published (no copies) */
+    const bool small = (c->launch.flags & SCAN_HOST_SORT_SMALL) != 0;
+    if (!small) VSA_CHECK(hipEventRecord(c->ev0, c->stream));
     int r = launch_scan_kernel(c, db, d_data, nb, nsegs, seg_bytes);
     if (r != VSA_OK) return r;
+    if (small) {
+        hipLaunchKernelGGL(vsa_publish, dim3(1), dim3(256), 0, c->stream, c->ws.d_counters,
+                           c->ws.d_pub, (unsigned long long)++c->pub_seq, 144u,
+                           (const uint64_t *)c->ws.d_keys[0], (const uint32_t *)c->ws.d_ids[0],
+                           PUB_RECS);
+        VSA_CHECK(hipGetLastError());
+        c->launch.published = true;
+        c->launch.dev_sort = false;
+        c->ctr_clean = true;
+        return VSA_OK;
+    }
     VSA_CHECK(hipEventRecord(c->ev1, c->stream));
     /* the binned sort queues behind the scan with no host round trip: its
      * kernels read the record count and the overflow flag on the device
@@ -515,7 +556,8 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
      * to the host and zeroes them */
     c->bins_clean = true;
     hipLaunchKernelGGL(vsa_publish, dim3(1), dim3(256), 0, c->stream, c->ws.d_counters,
-                       c->ws.d_pub, (unsigned long long)++c->pub_seq, 144u);
+                       c->ws.d_pub, (unsigned long long)++c->pub_seq, 144u,
+                       (const uint64_t *)nullptr, (const uint32_t *)nullptr, 0u);
     VSA_CHECK(hipGetLastError());
     c->launch.published = true;
     c->ctr_clean = true;
@@ -687,7 +729,7 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
         fprintf(stderr, "vsa: %llu queued confirm keys differ from HBM\n",
                 (unsigned long long)w.h_counters[3]);
     }
-    {
+    if (!(flags & SCAN_HOST_SORT_SMALL)) {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_kernel_ms = ms;
     }
@@ -948,10 +990,22 @@ vsa_ctx *default_ctx() {
     return t_ctx;
 }
 
-/* Keyed by (pointer, size); every lookup also compares the whole blob with
- * the cached host copy, so a database freed and re-allocated at the same
- * address is never served from a stale device copy (memcmp runs at memory
- * speed, ~20 us for a 0.4 MB FDR blob). */
+/* Keyed by (pointer, size); a lookup of an unregistered blob also compares
+ * the whole blob with the cached host copy, so a database freed and
+ * re-allocated at the same address is never served from a stale device
+ * copy (memcmp runs at memory speed, ~20 us for a 0.4 MB FDR blob).  A blob
+ * registered with vsa_hwlm_register is immutable until its unregister (the
+ * integration registers it where the database is loaded),
+ * so its lookups skip the compare. */
+std::mutex g_reg_mu;
+std::map<const void *, size_t> g_registered; /* pointer -> size */
+
+bool is_registered(const void *p, size_t size) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_registered.find(p);
+    return it != g_registered.end() && it->second == size;
+}
+
 struct RegKey {
     const void *p;
     size_t size;
@@ -988,7 +1042,7 @@ vsa_db *registry_get(const void *ptr, int bare_type) {
     if (it != t_registry.end()) {
         vsa_db *old = it->second;
         const uint8_t *cached = old->hblob + (bare_type < 0 ? 0 : VSA_ROUNDUP_CL(sizeof(HWLM)));
-        if (memcmp(cached, p, size) == 0) return old;
+        if (is_registered(ptr, size) || memcmp(cached, p, size) == 0) return old;
         vsa_db_free(old); /* erases the registry entry */
     }
     vsa_db *db = nullptr;
@@ -1183,32 +1237,19 @@ const std::vector<vsa::FloodEvent> *floods_for(const vsa_db *db, const uint8_t *
     return ev.empty() ? nullptr : &ev;
 }
 
-/* scan one host buffer with the default context */
-/* One hwlmExec-equivalent scan of a host buffer.  hend != NULL: streaming
- * with history (the 16 bytes before hend are copied in front of buf, as
- * the reference reads them, fdr.c:380-560). */
-int scan_host(vsa_db *db, const uint8_t *buf, size_t len, size_t start,
-              std::vector<uint64_t> &keys, std::vector<uint32_t> &ids,
-              const uint8_t *hend = nullptr, size_t hlen = 0) {
-    vsa_ctx *c = db->ctx;
-    int r;
-    const size_t pre = hend ? 16 : 0;
-    const bool resident = !pre && c->res_host == buf && c->res_len == len;
-    if (!resident) c->res_host = nullptr;
-    if ((r = ensure_in(c, pre + len + 16)) != VSA_OK) return r;
-    if (pre) {
-        VSA_CHECK(hipMemcpyAsync(c->ws.d_in, hend - 16, 16, hipMemcpyHostToDevice, c->stream));
-    }
-    if (len && !resident) {
-        VSA_CHECK(hipMemcpyAsync(c->ws.d_in + pre, buf, len, hipMemcpyHostToDevice, c->stream));
-    }
-    uint64_t off = 0, l = len, st = start, n = 0, hl = hlen;
-    if ((r = scan_blocks_impl(c, db, c->ws.d_in + pre, &off, &l, &st, 1, SCAN_HOST_SORT_SMALL,
-                              &n, pre ? &hl : nullptr)) != VSA_OK)
-        return r;
+/* the last drop-in scan's n records on the host, in reference order: from
+ * the published copy (vsa_publish, <= PUB_RECS records) or the device */
+int fetch_records(vsa_ctx *c, uint64_t n, std::vector<uint64_t> &keys,
+                  std::vector<uint32_t> &ids) {
     keys.resize(n);
     ids.resize(n);
-    if (n) {
+    if (!n) return VSA_OK;
+    if (c->launch.published && (c->launch.flags & SCAN_HOST_SORT_SMALL) && c->host_sort &&
+        n <= PUB_RECS) {
+        const unsigned long long *h = c->ws.h_pub;
+        memcpy(keys.data(), h + 17, n * 8);
+        memcpy(ids.data(), (const uint32_t *)(h + 17 + PUB_RECS), n * 4);
+    } else {
         VSA_CHECK(hipMemcpyAsync(keys.data(), c->ws.d_keys[c->cur], n * 8,
                                  hipMemcpyDeviceToHost, c->stream));
         VSA_CHECK(hipMemcpyAsync(ids.data(), c->ws.d_ids[c->cur], n * 4,
@@ -1226,6 +1267,43 @@ int scan_host(vsa_db *db, const uint8_t *buf, size_t len, size_t start,
         }
     }
     return VSA_OK;
+}
+
+/* scan one host buffer with the default context */
+/* One hwlmExec-equivalent scan of a host buffer.  hend != NULL: streaming
+ * with history (the 16 bytes before hend are copied in front of buf, as
+ * the reference reads them, fdr.c:380-560). */
+int scan_host(vsa_db *db, const uint8_t *buf, size_t len, size_t start,
+              std::vector<uint64_t> &keys, std::vector<uint32_t> &ids,
+              const uint8_t *hend = nullptr, size_t hlen = 0) {
+    vsa_ctx *c = db->ctx;
+    int r;
+    const size_t pre = hend ? 16 : 0;
+    const bool resident = !pre && c->res_host == buf && c->res_len == len;
+    if (!resident) c->res_host = nullptr;
+    if ((r = ensure_in(c, pre + len + 16)) != VSA_OK) return r;
+    if (!resident && pre + len <= PIN_STAGE_MAX) {
+        /* history + block staged in pinned memory, one DMA */
+        if ((r = ensure_hin(c, pre + len)) != VSA_OK) return r;
+        if (pre) memcpy(c->ws.h_in, hend - 16, 16);
+        if (len) memcpy(c->ws.h_in + pre, buf, len);
+        VSA_CHECK(hipMemcpyAsync(c->ws.d_in, c->ws.h_in, pre + len, hipMemcpyHostToDevice,
+                                 c->stream));
+    } else {
+        if (pre) {
+            VSA_CHECK(hipMemcpyAsync(c->ws.d_in, hend - 16, 16, hipMemcpyHostToDevice,
+                                     c->stream));
+        }
+        if (len && !resident) {
+            VSA_CHECK(hipMemcpyAsync(c->ws.d_in + pre, buf, len, hipMemcpyHostToDevice,
+                                     c->stream));
+        }
+    }
+    uint64_t off = 0, l = len, st = start, n = 0, hl = hlen;
+    if ((r = scan_blocks_impl(c, db, c->ws.d_in + pre, &off, &l, &st, 1, SCAN_HOST_SORT_SMALL,
+                              &n, pre ? &hl : nullptr)) != VSA_OK)
+        return r;
+    return fetch_records(c, n, keys, ids);
 }
 
 /* class scan over a host buffer: returns first / last+1 */
@@ -1343,6 +1421,7 @@ int vsa_ctx_create(int device, vsa_ctx_t **out) {
     VSA_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     c->num_cus = cus > 0 ? cus : 256;
     VSA_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->stream_ref.reset((void *)c->stream, [](void *st) { (void)hipStreamDestroy((hipStream_t)st); });
     VSA_CHECK(hipEventCreate(&c->ev0));
     VSA_CHECK(hipEventCreate(&c->ev1));
     VSA_CHECK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
@@ -1350,9 +1429,9 @@ int vsa_ctx_create(int device, vsa_ctx_t **out) {
     VSA_CHECK(hipMalloc(&c->ws.d_bins, 2 * VSA_SORT_BINS * sizeof(uint32_t)));
     VSA_CHECK(hipHostMalloc((void **)&c->ws.h_counters, N_COUNTERS * sizeof(unsigned long long),
                             hipHostMallocDefault));
-    VSA_CHECK(hipHostMalloc((void **)&c->ws.h_pub, 32 * sizeof(unsigned long long),
+    VSA_CHECK(hipHostMalloc((void **)&c->ws.h_pub, PUB_WORDS * sizeof(unsigned long long),
                             hipHostMallocCoherent | hipHostMallocMapped));
-    memset(c->ws.h_pub, 0, 32 * sizeof(unsigned long long));
+    memset(c->ws.h_pub, 0, PUB_WORDS * sizeof(unsigned long long));
     VSA_CHECK(hipHostGetDevicePointer((void **)&c->ws.d_pub, c->ws.h_pub, 0));
     *out = c.release();
     return VSA_OK;
@@ -1375,14 +1454,27 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (w.d_bins) (void)hipFree(w.d_bins);
     if (w.h_counters) (void)hipHostFree(w.h_counters);
     if (w.h_pub) (void)hipHostFree(w.h_pub);
+    if (w.h_in) (void)hipHostFree(w.h_in);
     if (w.d_blocks) (void)hipFree(w.d_blocks);
     if (w.h_blocks) (void)hipHostFree(w.h_blocks);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
-    (void)hipStreamDestroy(c->stream);
+    if (c->ev_rec) (void)hipEventDestroy(c->ev_rec);
     if (t_ctx == c) t_ctx = nullptr;
-    delete c;
+    delete c; /* drops its hold on the stream */
+    return VSA_OK;
+}
+
+int vsa_ctx_create_shared(vsa_ctx_t *base, vsa_ctx_t **out) {
+    if (!base || !out) return VSA_E_INVALID;
+    vsa_ctx_t *c = nullptr;
+    int rc = vsa_ctx_create(base->device, &c);
+    if (rc != VSA_OK) return rc;
+    (void)hipStreamSynchronize(c->stream);
+    c->stream_ref = base->stream_ref; /* releases the stream it made */
+    c->stream = base->stream;
+    *out = c;
     return VSA_OK;
 }
 
@@ -2091,6 +2183,30 @@ hwlm_error_t hwlmExecStreaming(const struct HWLM *tab, size_t len, size_t start,
     return fdrExecStreaming((const FDR *)eng, hbuf, hlen, buf, len, start, cb, scratch, groups);
 }
 
+/* The same entry points under vsa_gpu_* names, for an integration that
+ * keeps the reference's own definitions and routes each call by length
+ * (the CPU below the measured break-even, the GPU
+ * above it). */
+hwlm_error_t vsa_gpu_hwlmExec(const struct HWLM *tab, const uint8_t *buf, size_t len,
+                              size_t start, HWLMCallback cb, struct hs_scratch *scratch,
+                              hwlm_group_t groups) {
+    return hwlmExec(tab, buf, len, start, cb, scratch, groups);
+}
+hwlm_error_t vsa_gpu_hwlmExecStreaming(const struct HWLM *tab, size_t len, size_t start,
+                                       HWLMCallback cb, struct hs_scratch *scratch,
+                                       hwlm_group_t groups) {
+    return hwlmExecStreaming(tab, len, start, cb, scratch, groups);
+}
+hwlm_error_t vsa_gpu_fdrExec(const struct FDR *fdr, const uint8_t *buf, size_t len,
+                             size_t start, HWLMCallback cb, struct hs_scratch *scratch,
+                             hwlm_group_t groups) {
+    return fdrExec(fdr, buf, len, start, cb, scratch, groups);
+}
+hwlm_error_t vsa_gpu_noodExec(const struct noodTable *n, const uint8_t *buf, size_t len,
+                              size_t start, HWLMCallback cb, struct hs_scratch *scratch) {
+    return noodExec(n, buf, len, start, cb, scratch);
+}
+
 /* The writes of one logical stream (hs_scan: one block-mode write;
  * hs_scan_vector: all pieces) scanned in ONE launch: the history bytes and
  * the writes laid end to end in the context's input buffer, each write a
@@ -2110,17 +2226,26 @@ hwlm_error_t exec_pieces(vsa_ctx *c, const vsa_db *db, const u8 *hist, size_t hi
     if (!total) return HWLM_SUCCESS;
     const size_t pre = 16, hl0 = std::min<size_t>(hist_len, 16);
     if (ensure_in(c, pre + total + 16) != VSA_OK) return HWLM_ERROR_UNKNOWN;
-    if (hl0 && hipMemcpyAsync(c->ws.d_in + pre - hl0, hist + hist_len - hl0, hl0,
-                              hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    /* the history and every piece staged in pinned memory, one DMA (past
+     * PIN_STAGE_MAX: a copy per piece) */
+    const bool staged = pre + total <= PIN_STAGE_MAX && ensure_hin(c, pre + total) == VSA_OK;
+    if (staged) {
+        if (hl0) memcpy(c->ws.h_in + pre - hl0, hist + hist_len - hl0, hl0);
+    } else if (hl0 && hipMemcpyAsync(c->ws.d_in + pre - hl0, hist + hist_len - hl0, hl0,
+                                     hipMemcpyHostToDevice, c->stream) != hipSuccess) {
         return HWLM_ERROR_UNKNOWN;
+    }
     std::vector<uint64_t> off, len, st, hl;
     std::vector<size_t> which;
     size_t pos = pre, seen = hist_len;
     for (size_t i = 0; i < n; i++) {
         if (!lens[i]) continue;
-        if (hipMemcpyAsync(c->ws.d_in + pos, bufs[i], lens[i], hipMemcpyHostToDevice,
-                           c->stream) != hipSuccess)
+        if (staged) {
+            memcpy(c->ws.h_in + pos, bufs[i], lens[i]);
+        } else if (hipMemcpyAsync(c->ws.d_in + pos, bufs[i], lens[i], hipMemcpyHostToDevice,
+                                  c->stream) != hipSuccess) {
             return HWLM_ERROR_UNKNOWN;
+        }
         off.push_back(pos);
         len.push_back(lens[i]);
         st.push_back(0);
@@ -2129,29 +2254,17 @@ hwlm_error_t exec_pieces(vsa_ctx *c, const vsa_db *db, const u8 *hist, size_t hi
         pos += lens[i];
         seen += lens[i];
     }
+    if (staged && hipMemcpyAsync(c->ws.d_in + pre - hl0, c->ws.h_in + pre - hl0,
+                                 pos - (pre - hl0), hipMemcpyHostToDevice,
+                                 c->stream) != hipSuccess)
+        return HWLM_ERROR_UNKNOWN;
     uint64_t nm = 0;
     if (scan_blocks_impl(c, db, c->ws.d_in, off.data(), len.data(), st.data(),
                          (uint32_t)off.size(), SCAN_HOST_SORT_SMALL, &nm, hl.data()) != VSA_OK)
         return HWLM_ERROR_UNKNOWN;
-    std::vector<uint64_t> keys(nm);
-    std::vector<uint32_t> ids(nm);
-    if (nm) {
-        if (hipMemcpyAsync(keys.data(), c->ws.d_keys[c->cur], nm * 8, hipMemcpyDeviceToHost,
-                           c->stream) != hipSuccess ||
-            hipMemcpyAsync(ids.data(), c->ws.d_ids[c->cur], nm * 4, hipMemcpyDeviceToHost,
-                           c->stream) != hipSuccess ||
-            hipStreamSynchronize(c->stream) != hipSuccess)
-            return HWLM_ERROR_UNKNOWN;
-    }
-    if (c->host_sort && nm > 1) {
-        std::vector<std::pair<uint64_t, uint32_t>> kv(nm);
-        for (uint64_t i = 0; i < nm; i++) kv[i] = {keys[i], ids[i]};
-        std::sort(kv.begin(), kv.end());
-        for (uint64_t i = 0; i < nm; i++) {
-            keys[i] = kv[i].first;
-            ids[i] = kv[i].second;
-        }
-    }
+    std::vector<uint64_t> keys;
+    std::vector<uint32_t> ids;
+    if (fetch_records(c, nm, keys, ids) != VSA_OK) return HWLM_ERROR_UNKNOWN;
     hs_scratch *sc = (hs_scratch *)cbctx;
     std::vector<vsa::FloodEvent> ev;
     uint64_t k = 0;
@@ -2202,6 +2315,34 @@ int scan_records(vsa_ctx *c, const vsa_db *db, const u8 *d_data, const uint64_t 
         VSA_CHECK(hipStreamSynchronize(c->stream));
     }
     return VSA_OK;
+}
+
+int records_fetch_async(vsa_ctx *c, uint64_t n, uint64_t *h_keys, uint32_t *h_ids) {
+    if (!c->ev_rec) VSA_CHECK(hipEventCreateWithFlags(&c->ev_rec, hipEventDisableTiming));
+    if (n) {
+        VSA_CHECK(hipMemcpyAsync(h_keys, c->ws.d_keys[c->cur], n * 8, hipMemcpyDeviceToHost,
+                                 c->stream));
+        VSA_CHECK(hipMemcpyAsync(h_ids, c->ws.d_ids[c->cur], n * 4, hipMemcpyDeviceToHost,
+                                 c->stream));
+    }
+    VSA_CHECK(hipEventRecord(c->ev_rec, c->stream));
+    return VSA_OK;
+}
+
+int records_wait(vsa_ctx *c) {
+    if (c->ev_rec) VSA_CHECK(hipEventSynchronize(c->ev_rec));
+    return VSA_OK;
+}
+
+void *host_pinned_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, std::max<size_t>(bytes, 64), hipHostMallocDefault) != hipSuccess)
+        return nullptr;
+    return p;
+}
+
+void host_pinned_free(void *p) {
+    if (p) (void)hipHostFree(p);
 }
 
 /* The records of one call (ends relative to that call's buffer) through
@@ -2572,6 +2713,27 @@ const uint8_t *run_accel(const union AccelAux *accel, const uint8_t *c, const ui
     const uint8_t *rv = c + r;
     rv = std::max(c + accel->generic.offset, rv);
     return rv - accel->generic.offset;
+}
+
+int vsa_hwlm_register(const void *blob, int bare_type) {
+    if (!blob) return VSA_E_INVALID;
+    const uint8_t *p = (const uint8_t *)blob;
+    size_t size;
+    if (bare_type < 0) {
+        size = VSA_ROUNDUP_CL(sizeof(HWLM)) +
+               engine_size(p + VSA_ROUNDUP_CL(sizeof(HWLM)), p[0]);
+    } else {
+        if (bare_type != HWLM_ENGINE_NOOD && bare_type != HWLM_ENGINE_FDR) return VSA_E_INVALID;
+        size = engine_size(p, bare_type);
+    }
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_registered[blob] = size;
+    return VSA_OK;
+}
+
+int vsa_hwlm_unregister(const void *blob) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    return g_registered.erase(blob) ? VSA_OK : VSA_E_INVALID;
 }
 
 void vsa_set_scratch_layout(long fdr_conf_off, long fdr_conf_offset_off) {

@@ -77,6 +77,15 @@ int exec_pieces(vsa_ctx *c, const vsa_db *db, const u8 *hist, size_t hist_len,
 
 /* runtime.hip: one launch over device blocks (hlens NULL = block mode);
  * the sorted records to the host when keys != NULL, else only counted */
+/* pipelined corpus repeats (vsa_hs_corpus_scan_repeats): the last
+ * completed scan's n records copied into host buffers asynchronously on the
+ * scan stream (records_fetch_async, then records_wait), so the next scan can
+ * be queued behind the copy while the host replays; pinned host buffers */
+int records_fetch_async(vsa_ctx *c, uint64_t n, uint64_t *h_keys, uint32_t *h_ids);
+int records_wait(vsa_ctx *c);
+void *host_pinned_alloc(size_t bytes);
+void host_pinned_free(void *p);
+
 int scan_records(vsa_ctx *c, const vsa_db *db, const u8 *d_data, const uint64_t *offsets,
                  const uint64_t *lens, const uint64_t *hlens, uint32_t nblocks,
                  std::vector<uint64_t> *keys, std::vector<uint32_t> *ids, uint64_t *n,

@@ -271,6 +271,8 @@ _sig("vsa_hs_corpus_prepare", ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, c
      ctypes.POINTER(_vp))
 _sig("vsa_hs_corpus_scan", ctypes.c_int, _vp, _vp, _u64p, ctypes.c_uint)
 _sig("vsa_hs_corpus_scan_ex", ctypes.c_int, _vp, _vp, _vp, _u64p, ctypes.c_uint)
+_sig("vsa_hs_corpus_scan_repeats", ctypes.c_int, _vp, ctypes.c_uint32, _vp, _vp, _vp,
+     ctypes.c_uint)
 _sig("vsa_hs_corpus_free", ctypes.c_int, _vp)
 
 _M64 = (1 << 64) - 1
@@ -325,6 +327,18 @@ class Corpus:
         if digests:
             return rc, total.value, cnt, dg
         return rc, total.value, cnt
+
+    def scan_repeats(self, repeats, counts=False, threads=16, digests=False):
+        """vsa_hs_corpus_scan_repeats: `repeats` passes, pass k + 1 scanned
+        while pass k replays.  (rc, per-pass totals, last pass counts or
+        None, last pass digests or None)"""
+        tot = np.zeros(repeats, np.uint64)
+        cnt = np.zeros(self.n, np.uint64) if counts else None
+        dg = np.zeros(self.n, np.uint64) if digests else None
+        rc = lib.vsa_hs_corpus_scan_repeats(self.handle, repeats, tot.ctypes.data,
+                                            cnt.ctypes.data if cnt is not None else None,
+                                            dg.ctypes.data if dg is not None else None, threads)
+        return rc, tot, cnt, dg
 
     def close(self):
         if self.handle:

@@ -188,34 +188,53 @@ class PackedGather:
     waits on the scan context's stream); ``complete()``, if given, runs
     after the collectives are queued (bench.py: the rank's own scan is
     completed, which performs any output-overflow rescan, so a repeated
-    pack is final).  Device tensors use RCCL, CPU tensors gloo (tests)."""
+    pack is final).  Device tensors use RCCL, CPU tensors gloo (tests);
+    gloo with a device (the one-GPU rehearsal of bench.py's N > 1 path)
+    packs on the device and runs the collectives on host copies."""
 
     def __init__(self, dist, world, device=None, root=0):
         self.dist, self.world, self.device, self.root = dist, world, device, root
         self.rank = dist.get_rank()
+        self.stage = (device is not None and str(device).startswith("cuda") and
+                      dist.get_backend() == "gloo")
+        self.cdev = None if self.stage else device  # where the collectives run
         self.cap = 0
-        self.pk = self.hdr = self.recv = None
+        self.pk = self.pk_dev = self.hdr = self.recv = None
         self._grow(0)
 
     def _grow(self, m):
         import torch
         self.cap = cap = max(1024, m + m // 4)
         words = 1 + cap + (cap + 1) // 2
-        self.pk = torch.zeros(words, dtype=torch.int64, device=self.device)
-        self.hdr = torch.zeros(self.world, dtype=torch.int64, device=self.device)
-        self.recv = ([torch.zeros(words, dtype=torch.int64, device=self.device)
+        self.pk = torch.zeros(words, dtype=torch.int64, device=self.cdev)
+        self.pk_dev = (torch.zeros(words, dtype=torch.int64, device=self.device)
+                       if self.stage else self.pk)
+        self.hdr = torch.zeros(self.world, dtype=torch.int64, device=self.cdev)
+        self.recv = ([torch.zeros(words, dtype=torch.int64, device=self.cdev)
                       for _ in range(self.world)] if self.rank == self.root else None)
 
     def _once(self, pack, wait):
-        pack(self.pk, self.cap)
+        pack(self.pk_dev, self.cap)
         if wait is not None:
             wait()
+        if self.stage:
+            self.pk.copy_(self.pk_dev)
         self.dist.all_gather_into_tensor(self.hdr, self.pk[0:1])
         self.dist.gather(self.pk, self.recv, dst=self.root)
 
     def gather(self, pack, wait=None, complete=None):
         """every rank's record count (the records are on the root, merged())"""
+        self.start(pack, wait)
+        return self.finish(pack, wait, complete)
+
+    def start(self, pack, wait=None):
+        """queue the pack and both collectives (nothing is read on the host)"""
         self._once(pack, wait)
+
+    def finish(self, pack, wait=None, complete=None):
+        """after start(): complete(), read the gathered headers, repeat the
+        pack and collectives if some rank's records did not fit or were not
+        final; every rank's record count"""
         if complete is not None:
             complete()
         hdr = self.hdr.cpu().tolist()
