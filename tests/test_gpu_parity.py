@@ -528,3 +528,79 @@ def test_gpu_plan_memo(ctx):
         db.close()
     finally:
         ctx.free(d)
+
+
+def run_layout_scan(ctx, blob, bufs, misalign=0):
+    """bufs laid back to back (no gaps: hsbench corpora), one launch;
+    per-block [(end, id)]"""
+    offs, pos = [], misalign
+    for b in bufs:
+        offs.append(pos)
+        pos += len(b)
+    host = np.zeros(pos + 16, np.uint8)
+    for o, b in zip(offs, bufs):
+        host[o:o + len(b)] = np.frombuffer(bytes(b), np.uint8)
+    dbuf = ctx.malloc(len(host))
+    try:
+        ctx.h2d(dbuf, host)
+        db = vsa.Database(ctx, blob)
+        n = ctx.scan_blocks(db, dbuf, offs, [len(b) for b in bufs])
+        res = ctx.results(n)
+        db.close()
+    finally:
+        ctx.free(dbuf)
+    out = [[] for _ in bufs]
+    ends = res["key"] >> np.uint64(24)
+    bi = np.searchsorted(np.array(offs, np.uint64), ends, side="right") - 1
+    for e, i, b in zip(ends.tolist(), res["id"].tolist(), bi.tolist()):
+        out[b].append((e - offs[b], i))
+    return out
+
+
+@pytest.mark.parametrize("nlits", [1, 5, 30, 300, 3000])
+def test_gpu_back_to_back_runs(ctx, nlits):
+    """Back-to-back block-mode blocks >= 1 KiB packed into one segment are
+    scanned as one range (VSA_BLK_RUN, kernels.hip "runs"): every block's
+    records equal the oracle's hwlmExec of that block alone -- with literals
+    planted across every boundary (never reported), whole literals at block
+    starts and ends (reported), masks reaching before the literal -- at the
+    planner's segment size and at 128 KiB segments (runs of up to 128
+    blocks), and equal the per-block path (VSA_NO_RUNS)."""
+    import os
+    rng = random.Random(900 + nlits)
+    lo = 1 if nlits == 1 else (2 if nlits <= 30 else 4)
+    lits = rand_lits(rng, nlits, minlen=max(lo, 2) if nlits > 1 else 3, maxlen=8,
+                     msk_frac=0.15)
+    blob = vsa.hwlm_build(lits)
+    alpha = b"abcdefghABCDEFGH" if nlits <= 30 else bytes(range(0x61, 0x7b))
+    sizes = [1024, 1025, 1500, 2047, 2048, 3000, 4096, 9000, 16384, 40000]
+    bufs = [bytearray(rand_data(rng, rng.choice(sizes), alpha)) for _ in range(700)]
+    for k in range(len(bufs) - 1):
+        s = rng.choice(lits).s
+        if len(s) > 1:  # across the boundary k | k + 1
+            cut = rng.randint(1, len(s) - 1)
+            bufs[k][len(bufs[k]) - cut:] = s[:cut]
+            bufs[k + 1][:len(s) - cut] = s[cut:]
+        if rng.random() < 0.3:  # whole literal ending the block / starting the next
+            t = rng.choice(lits).s
+            bufs[k][len(bufs[k]) - len(t):] = t
+            u = rng.choice(lits).s
+            bufs[k + 1][:len(u)] = u
+    want = []
+    for b in bufs:
+        st, m = oracle.hwlm_exec(blob.ptr, bytes(b), cap=1 << 18)
+        assert st == 0
+        want.append(m)
+    assert sum(map(len, want)) > 100
+    for mis in (0, 3):
+        assert run_layout_scan(ctx, blob, bufs, mis) == want, mis
+    os.environ["VSA_SEG_KB"] = "128"
+    try:
+        assert run_layout_scan(ctx, blob, bufs, 5) == want
+    finally:
+        del os.environ["VSA_SEG_KB"]
+    os.environ["VSA_NO_RUNS"] = "1"
+    try:
+        assert run_layout_scan(ctx, blob, bufs) == want
+    finally:
+        del os.environ["VSA_NO_RUNS"]

@@ -1,6 +1,8 @@
 """Per-block overhead of the batch scan: 1 GiB cut into blocks of 2 KiB ..
 1 MiB, wall time of vsa_scan_blocks (tables built per call) and of
-vsa_scan_plan (tables built once) vs the kernel time (cfg-4 FDR set)."""
+vsa_scan_plan (tables built once) vs the kernel time (cfg-4 FDR set).
+The blocks are back to back, so packed segments scan as runs; run with
+VSA_NO_RUNS=1 for the per-block path."""
 import sys
 import time
 
@@ -18,6 +20,8 @@ total = 1 << 30
 data = bench.make_corpus(total, lits, seed=5, plant_every=64 << 10)
 d = ctx.malloc(total)
 ctx.h2d(d, data)
+for _ in range(40):  # clock settle (profiles/r03_ramp.jsonl)
+    ctx.scan_blocks(db, d, [0], [total])
 for chunk in [2 << 10, 4 << 10, 16 << 10, 64 << 10, 1 << 20, 256 << 20]:
     n = total // chunk
     offs = np.arange(n, dtype=np.uint64) * chunk

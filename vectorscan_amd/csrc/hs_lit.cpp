@@ -206,6 +206,7 @@ struct Run {
     std::vector<uint32_t> at_to; /* ids reported at last_to */
     std::map<uint32_t, uint64_t> som_log; /* id -> leftmost from at last_to */
     bool terminated = false;
+    std::vector<uint32_t> *touched = nullptr; /* corpus replay: ekeys set, to reset */
 };
 
 /* flushStoredSomMatches (src/som/som_runtime.c, report.h): the SOM reports
@@ -266,7 +267,10 @@ u64a on_fragment(size_t end, u32 frag, hs_scratch *sc) {
             if (std::find(r.at_to.begin(), r.at_to.end(), p.id) != r.at_to.end()) continue;
             r.at_to.push_back(p.id);
         }
-        if (p.ekey != NO_EKEY) r.st->exhausted[p.ekey] = 1;
+        if (p.ekey != NO_EKEY) {
+            r.st->exhausted[p.ekey] = 1;
+            if (r.touched) r.touched->push_back(p.ekey);
+        }
         const uint64_t from = p.som ? to - p.s.size() : 0;
         if (r.cb && r.cb(p.id, from, to, 0, r.ctx)) {
             r.terminated = true;
@@ -760,6 +764,7 @@ int vsa_hs_corpus_free(vsa_hs_corpus_t *c) {
 static int corpus_replay(vsa_hs_corpus *cp, uint64_t *keys, const uint32_t *ids, uint64_t nm,
                          uint64_t *counts, uint64_t *digests, uint64_t *total,
                          unsigned threads) {
+    const auto t_start = std::chrono::steady_clock::now();
     const vsa_hs_database *db = cp->db;
     vsa_db_t *ddb = device_db(cp->scratch, db);
     const uint32_t nblocks = (uint32_t)cp->offsets.size();
@@ -829,19 +834,35 @@ static int corpus_replay(vsa_hs_corpus *cp, uint64_t *keys, const uint32_t *ids,
         1, std::min<uint64_t>({threads ? threads : 1u, live.size(), 1 + live_recs / 2048}));
     std::vector<uint64_t> part(T, 0);
     std::vector<int> status(T, VSA_HS_SUCCESS);
+    static const bool timing = getenv("VSA_HOST_TIMING") != nullptr;
+    using clk = std::chrono::steady_clock;
+    const auto t_map = clk::now();
+    std::vector<double> busy(T, 0.0);
     auto work = [&](unsigned t) {
-        /* per-thread state, reused across units */
+        const auto w0 = clk::now();
+        /* per-thread state, reused across units: a unit resets only the
+         * exhaustion keys the previous one set */
         vsa_hs_stream st;
+        init_stream(&st, db);
+        std::vector<uint32_t> touched;
         std::vector<const uint8_t *> bufs;
         std::vector<size_t> bl_len;
         SeqDigest dg;
         uint64_t &cnt = dg.cnt;
         Run r{db, &st, digests ? digest_match : count_match, digests ? (void *)&dg : (void *)&cnt,
               nullptr, nullptr, {}, 0};
-        for (size_t i = t; i < live.size(); i += T) {
+        r.touched = &touched;
+        /* contiguous slices of the live units (neighbouring blocks share
+         * cache lines of the records, rb/re and the corpus image) */
+        const size_t u0 = live.size() * t / T, u1 = live.size() * (t + 1) / T;
+        for (size_t i = u0; i < u1; i++) {
             const uint32_t *bl = unit_blk + unit_off[live[i]];
             const size_t nbl = unit_off[live[i] + 1] - unit_off[live[i]];
-            init_stream(&st, db);
+            st.offset = 0;
+            st.hist.clear();
+            st.terminated = false;
+            for (uint32_t k : touched) st.exhausted[k] = 0;
+            touched.clear();
             cnt = 0;
             bufs.resize(nbl);
             bl_len.resize(nbl);
@@ -881,9 +902,23 @@ static int corpus_replay(vsa_hs_corpus *cp, uint64_t *keys, const uint32_t *ids,
             }
             part[t] += cnt;
         }
+        busy[t] = std::chrono::duration<double, std::milli>(clk::now() - w0).count();
     };
     if (T == 1) work(0);
     else replay_pool().run(T, work);
+    if (timing) {
+        double mx = 0, sum = 0;
+        for (double b : busy) {
+            mx = std::max(mx, b);
+            sum += b;
+        }
+        fprintf(stderr, "corpus_replay: %u threads, %zu live units, %llu records: map %.3f ms, "
+                "replay %.3f ms (thread busy max %.3f, mean %.3f ms)\n", T, live.size(),
+                (unsigned long long)live_recs,
+                std::chrono::duration<double, std::milli>(t_map - t_start).count(),
+                std::chrono::duration<double, std::milli>(clk::now() - t_map).count(), mx,
+                sum / T);
+    }
     for (unsigned t = 0; t < T; t++) {
         if (status[t] != VSA_HS_SUCCESS) return status[t];
         *total += part[t];

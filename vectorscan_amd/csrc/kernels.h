@@ -34,6 +34,13 @@ struct VsaBlock {
  * before `start` (getInitState fdr.c:129-142), Teddy / noodle read up to
  * nMasks - 1 / msk_len - 1 history bytes. */
 #define VSA_BLK_STREAM 1u
+/* Set on the first block of a packed segment whose blocks (2-128 of them)
+ * are back to back in memory, block mode (start 0, no history, no report_lo)
+ * and >= 1 KiB each: FDR / Teddy scan the segment as one range and the
+ * confirm places each end in its block (kernels.hip "runs"). */
+#define VSA_BLK_RUN 2u
+#define VSA_RUN_MAX 128u
+#define VSA_RUN_MIN_LEN 1024u
 
 /* A confirmed literal match.  `key` sorts into the reference callback order:
  * end (bits 63..24), bucket (23..20), LitInfo offset within its bucket's

@@ -273,7 +273,7 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
                                               u32 mis) {
     const u8 *fc[CONF_U], *li[CONF_U];
     u32 st[CONF_U], b[CONF_U];
-    u64 base[CONF_U];
+    u64 base[CONF_U], blen[CONF_U];
     int64_t hlen[CONF_U], e[CONF_U];
 #pragma unroll
     for (int i = 0; i < CONF_U; i++) {
@@ -282,11 +282,13 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
         fc[i] = P.conf_base + cl.off[b[i]];
         st[i] = 0;
         base[i] = 0;
+        blen[i] = ~0ULL;
         hlen[i] = 0;
         if (valid[i]) {
             const u32 c = conf_hash(q[i].key, cl.andmsk[b[i]], cl.mult[b[i]], cl.nbits[b[i]]);
             st[i] = *((const u32 *)(fc[i] + 32) + c);
             base[i] = P.blocks[blk].base;
+            blen[i] = P.blocks[blk].len;
             hlen[i] = (int64_t)P.blocks[blk].hlen;
         }
     }
@@ -296,6 +298,13 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
         live[i] = st[i] != 0;
         li[i] = fc[i] + st[i];
         e[i] = (int64_t)((q[i].meta >> 24) - mis - base[i]); /* block-relative end */
+        /* runs (VSA_BLK_RUN): an end past the entry's block is in the next,
+         * back-to-back block-mode block (>= 1 KiB: at most one boundary per
+         * chunk); outside runs every end lies inside its block */
+        if (e[i] >= (int64_t)blen[i]) {
+            base[i] += blen[i];
+            e[i] -= (int64_t)blen[i];
+        }
     }
     /* wave-uniform loop (every lane stays in, so the output slot reservation
      * below is one atomic per wave and step, not one per match: a single
@@ -392,6 +401,7 @@ struct SegCtx {
     int64_t start, len, zbase;
     int64_t rlo;      /* lowest reported end: max(start, block rlo) */
     int64_t qlo;      /* Teddy: lowest looked-up position (block-relative) */
+    int64_t run_nxt;  /* runs: aoff where block blk + 1 starts (else INT64_MAX) */
     bool stream;      /* streaming with history: no FDR start state */
 };
 
@@ -859,8 +869,11 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     /* bytes p0-8 .. p0+15 for the 8-byte confirm keys */
     u32 pv2 = lane_up1(d[2]);
     if (lane == 0) pv2 = (u32)in.pbytes;
-    /* one chunk entry per lane with candidates; the confirm wave expands it */
-    const u64 meta = (u64)p0 | ((u64)S.blk << ENT_BLK_SHIFT);
+    /* one chunk entry per lane with candidates; the confirm wave expands it.
+     * In a run the lane's block is the one holding p0 (a chunk across the
+     * boundary is moved on by the confirm, confirm_multi) */
+    const u32 lblk = S.blk + (p0 >= S.run_nxt ? 1u : 0u);
+    const u64 meta = (u64)p0 | ((u64)lblk << ENT_BLK_SHIFT);
     u32 w[4 * T::EW];
 #pragma unroll
     for (int i = 0; i < 4 * T::EW; i++) w[i] = 0;
@@ -1455,15 +1468,59 @@ vsa_lit_scan(VsaLitParams P) {
          * consecutive blocks (runtime.hip build_plan) */
         const u32 sbv = readfirstlane_u32(P.seg_blk[seg]);
         const u32 gcount = sbv >> 24;
-        const u32 nblk = gcount ? gcount : 1u;
+        /* a run (VSA_BLK_RUN, FDR / Teddy): the segment's back-to-back
+         * blocks are one range -- one prologue, one sweep, two checked
+         * iterations -- instead of that per block.  What crosses a block
+         * boundary is harmless: a literal inside a block has all its filter
+         * fields inside it (a field past the literal's length accepts any
+         * byte), so the filter stays a superset, and the confirm drops a
+         * literal starting before its block (e + 1 >= size) and keys on
+         * bytes of the literal only (fdr_confirm_runtime.h:43-102).  The FDR
+         * start state is applied to the run's first block only (it only
+         * removes candidates).  The run's block ends sit in two VGPRs (block
+         * lane, lane + 64, relative to the run's first byte); S.blk / S.run_nxt
+         * follow the sweep, and a pushed chunk names the block of its first
+         * byte. */
+        const u32 first = sbv & 0xffffffu;
+        bool run = false;
+        if constexpr (MODE != VSA_MODE_NOOD)
+            run = gcount > 1 && (P.blocks[first].flags & VSA_BLK_RUN);
+        u32 rend0 = 0xffffffffu, rend1 = 0xffffffffu;
+        const u32 nblk = run ? 1u : (gcount ? gcount : 1u);
         for (u32 gi = 0; gi < nblk; gi++) {
         lastb = gi + 1 == nblk;
-        const u32 blk = (sbv & 0xffffffu) + gi;
+        const u32 blk = first + gi;
         const VsaBlock B = P.blocks[blk];
         SegCtx S;
         S.blk = blk;
         S.blo = (int64_t)B.base + mis;
         S.bhi = S.blo + (int64_t)B.len;
+        S.run_nxt = INT64_MAX;
+        u32 rb = 0; /* runs: index of block S.blk in the run */
+        if (run) {
+            if (lane < gcount) {
+                const VsaBlock &bl = P.blocks[first + lane];
+                rend0 = (u32)(bl.base + bl.len - B.base);
+            }
+            if (lane + 64 < gcount) {
+                const VsaBlock &bl = P.blocks[first + 64 + lane];
+                rend1 = (u32)(bl.base + bl.len - B.base);
+            }
+            S.bhi = S.blo + (int64_t)(gcount > 64 ? readlane_u32(rend1, gcount - 65)
+                                                  : readlane_u32(rend0, gcount - 1));
+            S.run_nxt = S.blo + (int64_t)readlane_u32(rend0, 0);
+        }
+        /* runs: after the iteration at ib, move to the next block once the
+         * sweep has reached it (blocks >= 1 KiB: at most one per iteration) */
+        auto run_adv = [&](int64_t ib) {
+            if (run && ib + 1024 >= S.run_nxt) {
+                rb++;
+                S.blk++;
+                S.run_nxt = rb + 1 >= gcount ? INT64_MAX
+                          : S.blo + (int64_t)(rb < 64 ? readlane_u32(rend0, rb)
+                                                      : readlane_u32(rend1, rb - 64));
+            }
+        };
         S.vlo = S.blo - (int64_t)B.hist;
         S.stream = (B.flags & VSA_BLK_STREAM) != 0;
         S.qlo = 0;
@@ -1474,10 +1531,10 @@ vsa_lit_scan(VsaLitParams P) {
                 S.qlo = -min((int64_t)B.hlen, back);
         }
         S.start = (int64_t)B.start;
-        S.len = (int64_t)B.len;
+        S.len = S.bhi - S.blo;
         S.zbase = B.zbase;
         S.rlo = B.rlo > S.start ? B.rlo : S.start;
-        const int64_t s_lo = gcount ? B.org : B.org + (int64_t)(seg - B.seg_first) * SEG;
+        const int64_t s_lo = (gcount || run) ? B.org : B.org + (int64_t)(seg - B.seg_first) * SEG;
         const int64_t s_hi = (!gcount && s_lo + SEG < S.bhi) ? s_lo + SEG : S.bhi;
         const u32 niters = (u32)((s_hi - s_lo + 1023) >> 10);
         n_iter += niters;
@@ -1510,7 +1567,7 @@ vsa_lit_scan(VsaLitParams P) {
          * live through it and spills). */
         const bool pro1 = lane < (u32)(T::NL - 1);
         const int64_t pp = s_lo - (T::NL - 1) + (int64_t)lane;
-        const bool pro1_in = pro1 && pp - S.blo >= zlo && pp - S.blo < (int64_t)B.len;
+        const bool pro1_in = pro1 && pp - S.blo >= zlo && pp - S.blo < S.len;
         const u8 pb0 = pro1_in ? load_byte_masked(A, pp, S.vlo, S.bhi) : (u8)0;
         const u8 pb1 = (T::KEY16 && pro1_in) ? load_byte_masked(A, pp + 1, S.vlo, S.bhi) : (u8)0;
         const u32 pbb = lane < 8 ? load_byte_masked(A, s_lo - 8 + (int64_t)lane, S.vlo, S.bhi) : 0u;
@@ -1571,6 +1628,7 @@ vsa_lit_scan(VsaLitParams P) {
             }
             is = scan_iter<MODE, LDS_TABLE, true>(P, cl, L, S, mis, ib, cur, nxt0, is,
                                                  bucket_mask);
+            run_adv(ib);
         }
         if (nf > 0) {
             /* main sweep: LIT_DEPTH chunks in flight per wave.  ring[k] is
@@ -1596,6 +1654,7 @@ vsa_lit_scan(VsaLitParams P) {
                     const u32 nxt0 = (it + 1 < nf) ? nb : after;
                     is = scan_iter<MODE, LDS_TABLE, false>(P, cl, L, S, mis, ib, ring[k], nxt0,
                                                           is, bucket_mask);
+                    run_adv(ib);
                     const u32 itn = (it + LIT_DEPTH < nf) ? it + LIT_DEPTH : it;
                     ring[k] = load_wave_kib(sb, 1024u * itn);
                 }
@@ -1610,6 +1669,7 @@ vsa_lit_scan(VsaLitParams P) {
                     const u32 nxt0 = (it + 1 < nf) ? nb : after;
                     is = scan_iter<MODE, LDS_TABLE, false>(P, cl, L, S, mis, ib, ring[k], nxt0,
                                                           is, bucket_mask);
+                    run_adv(ib);
                 }
             }
         }
@@ -1624,6 +1684,7 @@ vsa_lit_scan(VsaLitParams P) {
             }
             is = scan_iter<MODE, LDS_TABLE, true>(P, cl, L, S, mis, ib, cur, nxt0, is,
                                                  bucket_mask);
+            run_adv(ib);
         }
         ncand_total = is.ncand;
         ring_tail_cache = is.tail_cache;

@@ -823,10 +823,25 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
     uint64_t seg = live.empty() ? (64u << 10) : pick_seg_bytes(live, waves);
     if (const char *e = getenv("VSA_SEG_KB")) seg = (uint64_t)std::max(1, atoi(e)) << 10;
     const bool group = !getenv("VSA_NO_GROUPS");
+    const bool no_runs = getenv("VSA_NO_RUNS") != nullptr;
     uint32_t g_first = 0, g_n = 0;
     int64_t g_span = 0;
+    /* a packed segment of back-to-back block-mode blocks >= 1 KiB is one
+     * range for the scan (VSA_BLK_RUN) */
+    auto runnable = [&]() {
+        if (no_runs || g_n < 2 || g_n > VSA_RUN_MAX) return false;
+        for (uint32_t k = g_first; k < g_first + g_n; k++) {
+            const VsaBlock &b = out[k];
+            if (b.start || b.hlen || b.rlo || b.len < VSA_RUN_MIN_LEN) return false;
+            if (k > g_first && b.base != out[k - 1].base + out[k - 1].len) return false;
+        }
+        return true;
+    };
     auto flush = [&]() {
-        if (g_n) pl.segblk.push_back(g_first | (g_n << SEG_GROUP_SHIFT));
+        if (g_n) {
+            if (runnable()) out[g_first].flags |= VSA_BLK_RUN;
+            pl.segblk.push_back(g_first | (g_n << SEG_GROUP_SHIFT));
+        }
         g_n = 0;
         g_span = 0;
     };
