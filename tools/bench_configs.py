@@ -175,6 +175,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--only", default="1,2,3,4s")
+    ap.add_argument("--cfg1-gib", type=int, default=1, help="cfg1 corpus size")
     args = ap.parse_args()
     import torch
     import vectorscan_amd as vsa
@@ -183,8 +184,9 @@ def main():
     if "1" in only:
         for nc in (False, True):
             lits = [vsa.HwlmLiteral(b"abcde", nc, 0)]
-            cfg_literal(ctx, torch, "cfg1 noodle 'abcde'%s 1 GiB" % (" nocase" if nc else ""),
-                        lits, 1 << 30, 4096, 1, args.steps, args.warmup)
+            cfg_literal(ctx, torch, "cfg1 noodle 'abcde'%s %d GiB" % (" nocase" if nc else "",
+                                                                       args.cfg1_gib),
+                        lits, args.cfg1_gib << 30, 4096, 1, args.steps, args.warmup)
     if "2" in only:
         cfg_class(ctx, torch, args.steps, args.warmup)
     if "4s" in only:

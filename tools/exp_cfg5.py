@@ -28,17 +28,21 @@ g = hsbench.GpuCorpus(exprs, ids, flags, blocks, hs.MODE_BLOCK)
 del blocks
 for _ in range(30):  # clock settle
     g.scan()
-for threads in (16, 8, 4):
+for threads in [int(t) for t in os.environ.get("EXP_THREADS", "16,8,4").split(",")]:
     t0 = time.perf_counter()
-    tots = []
+    tots, each = [], []
     for _ in range(reps):
+        t1 = time.perf_counter()
         tots.append(g.scan(threads=threads)[0])
+        each.append(time.perf_counter() - t1)
     one = (time.perf_counter() - t0) / reps
     t0 = time.perf_counter()
     pt = g.scan_repeats(reps, threads)
     pipe = (time.perf_counter() - t0) / reps
     print(json.dumps({"plant_every": plant, "shared_ids": shared, "threads": threads,
                       "repeats": reps, "one_ms_per_gib": round(one * 1e3, 3),
+                      "one_best_ms": round(min(each) * 1e3, 3),
+                      "one_median_ms": round(sorted(each)[len(each) // 2] * 1e3, 3),
                       "pipelined_ms_per_gib": round(pipe * 1e3, 3), "matches": tots[0],
                       "totals_equal": len(set(tots) | set(pt)) == 1}), flush=True)
 g.close()

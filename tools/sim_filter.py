@@ -79,6 +79,28 @@ def build_table(recs, key_offs, key_bits, ends):
     return T
 
 
+def conf_of(data, T, key_offs, key_bits, ends, stride, phase):
+    """per-end 8-bucket dead bits of one table design"""
+    n = len(data)
+    shifts = np.cumsum([0] + list(key_bits[:-1]))
+    pad = 16
+    buf = np.zeros(n + 2 * pad, dtype=np.int64)
+    buf[pad:pad + n] = data
+    pos = np.arange(n)
+    lk = pos[(pos % stride) == phase]
+    key = np.zeros(len(lk), dtype=np.int64)
+    for o, kb, sh in zip(key_offs, key_bits, shifts):
+        key |= (buf[lk + o + pad] & ((1 << kb) - 1)) << int(sh)
+    E = T[key]
+    conf = np.zeros(n + 16, dtype=np.uint64)
+    for fi, d in enumerate(ends):
+        f = (E >> np.uint64(8 * fi)) & np.uint64(0xFF)
+        e = lk + d
+        ok = (e >= 0) & (e < n)
+        conf[e[ok]] |= f[ok]
+    return conf[:n]
+
+
 def simulate(data, T, key_offs, key_bits, ends, stride, phase):
     n = len(data)
     shifts = np.cumsum([0] + list(key_bits[:-1]))
@@ -109,6 +131,11 @@ def simulate(data, T, key_offs, key_bits, ends, stride, phase):
 DESIGNS = {
     # current: stride 1, pair (p-1, p) 7+7 bits, ends p .. p+7
     "s1_pair77": dict(key_offs=(-1, 0), key_bits=(7, 7), ends=range(0, 8), stride=1),
+    "s1_pair76": dict(key_offs=(-1, 0), key_bits=(7, 6), ends=range(0, 8), stride=1),
+    "s1_pair67": dict(key_offs=(-1, 0), key_bits=(6, 7), ends=range(0, 8), stride=1),
+    "s1_skip77": dict(key_offs=(-2, 0), key_bits=(7, 7), ends=range(0, 8), stride=1),
+    "s1_skip76": dict(key_offs=(-2, 0), key_bits=(7, 6), ends=range(0, 8), stride=1),
+    "s1_gap377": dict(key_offs=(-3, 0), key_bits=(7, 7), ends=range(0, 8), stride=1),
     "s2_pair77": dict(key_offs=(-1, 0), key_bits=(7, 7), ends=range(0, 8), stride=2),
     "s2_tri554_back": dict(key_offs=(-2, -1, 0), key_bits=(5, 5, 4), ends=range(0, 8), stride=2),
     "s2_tri455_back": dict(key_offs=(-2, -1, 0), key_bits=(4, 5, 5), ends=range(0, 8), stride=2),
@@ -134,6 +161,21 @@ def main():
     data = bench.make_corpus(n, lits, seed=5, plant_every=64 << 10).astype(np.int64)
     print("records %d, engine %d, %d bytes" % (len(recs), blob.engine_id, n))
     for name in args.designs.split(","):
+        if "+" in name:
+            # two tables AND-ed: an end is a candidate only if both pass it
+            conf = np.zeros(n, dtype=np.uint64)
+            for part in name.split("+"):
+                d = DESIGNS[part]
+                T = build_table(recs, d["key_offs"], d["key_bits"], list(d["ends"]))
+                conf |= conf_of(data, T, d["key_offs"], d["key_bits"], list(d["ends"]),
+                                d["stride"], 0)
+            cand = (~conf) & np.uint64(0xFF)
+            cand[:16] = 0
+            bits = int(np.unpackbits(cand.astype(np.uint8)[:, None], axis=1).sum())
+            lanes = int((cand.reshape(-1, 16).max(axis=1) != 0).sum())
+            print("%-18s cand bits %9d (%.2e/B)  lanes %7s" % (name, bits, bits / n, lanes),
+                  flush=True)
+            continue
         d = DESIGNS[name]
         T = build_table(recs, d["key_offs"], d["key_bits"], list(d["ends"]))
         bits, ends, lanes = simulate(data, T, d["key_offs"], d["key_bits"], list(d["ends"]),

@@ -787,13 +787,19 @@ static int corpus_replay(vsa_hs_corpus *cp, uint64_t *keys, const uint32_t *ids,
     const uint32_t *bstamp = cp->bstamp.data();
     std::vector<uint32_t> live;
     uint64_t live_recs = 0;
-    {
-        const auto &so = cp->so, &se = cp->se;
-        uint64_t k = 0;
-        size_t at = 0; /* search start: the runs come in increasing order */
-        while (k < nm) {
+    const auto &so = cp->so, &se = cp->se;
+    /* the records of [k, k_end) -> blocks (each run with one gallop from the
+     * previous run's block plus a binary search); their units, in order,
+     * consecutive repeats dropped */
+    auto map_range = [&](uint64_t k, uint64_t k_end, std::vector<uint32_t> &units,
+                         uint64_t &recs) {
+        size_t at = (size_t)(std::upper_bound(so.begin(), so.end(),
+                                              k < k_end ? keys[k] >> KEY_END_SHIFT : 0) -
+                             so.begin());
+        at = at ? at - 1 : 0;
+        uint32_t last_u = ~0u;
+        while (k < k_end) {
             const uint64_t e = keys[k] >> KEY_END_SHIFT;
-            /* gallop from the previous run's block, then binary search */
             size_t lo = at, step = 1;
             while (lo + step < so.size() && so[lo + step] <= e) {
                 lo += step;
@@ -810,7 +816,7 @@ static int corpus_replay(vsa_hs_corpus *cp, uint64_t *keys, const uint32_t *ids,
             const uint32_t b = cp->order[oi - 1];
             const uint64_t o = so[oi - 1], hi = se[oi - 1];
             const uint64_t k0 = k;
-            while (k < nm && (keys[k] >> KEY_END_SHIFT) < hi) {
+            while (k < k_end && (keys[k] >> KEY_END_SHIFT) < hi) {
                 keys[k] -= o << KEY_END_SHIFT;
                 k++;
             }
@@ -818,11 +824,23 @@ static int corpus_replay(vsa_hs_corpus *cp, uint64_t *keys, const uint32_t *ids,
             re[b] = k;
             cp->bstamp[b] = gen;
             const uint32_t u = cp->blk_unit[b];
+            if (u != last_u) {
+                units.push_back(u);
+                last_u = u;
+            }
+            recs += k - k0;
+        }
+    };
+    /* one thread: splitting the map over the replay pool measured slower
+     * (pool hand-off and cache traffic outweigh ~10 ns per record) */
+    {
+        std::vector<uint32_t> units;
+        map_range(0, nm, units, live_recs);
+        for (uint32_t u : units) {
             if (cp->ustamp[u] != gen) {
                 cp->ustamp[u] = gen;
                 live.push_back(u);
             }
-            live_recs += k - k0;
         }
     }
     const uint32_t *unit_off = cp->unit_off.data(), *unit_blk = cp->unit_blk.data();

@@ -35,9 +35,11 @@ struct VsaBlock {
  * nMasks - 1 / msk_len - 1 history bytes. */
 #define VSA_BLK_STREAM 1u
 /* Set on the first block of a packed segment whose blocks (2-128 of them)
- * are back to back in memory, block mode (start 0, no history, no report_lo)
- * and >= 1 KiB each: FDR / Teddy scan the segment as one range and the
- * confirm places each end in its block (kernels.hip "runs"). */
+ * are back to back in memory, scanned from their first byte (start 0, no
+ * report_lo) and >= 1 KiB each: FDR / Teddy scan the segment as one range
+ * and the confirm places each end in its block (kernels.hip "runs").  A
+ * streaming block in a run reads its history from the bytes before it,
+ * which are its predecessor's in the layouts that make runs. */
 #define VSA_BLK_RUN 2u
 #define VSA_RUN_MAX 128u
 #define VSA_RUN_MIN_LEN 1024u

@@ -76,6 +76,15 @@ __device__ __forceinline__ u32 lane_up1(u32 v) {
 __device__ __forceinline__ u32 lane_down1(u32 v) {
     return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, true);
 }
+/* lane l gets lane l-1's v, lane 0 keeps old (wave_shr:1 with the
+ * out-of-range lane disabled): one v_mov_dpp */
+__device__ __forceinline__ u32 lane_up1_or_old(u32 old, u32 v) {
+    return (u32)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xf, 0xf, false);
+}
+/* lane l gets lane l-1's v, lane 0 lane 63's (wave_ror:1) */
+__device__ __forceinline__ u32 lane_ror1(u32 v) {
+    return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x13c, 0xf, 0xf, true);
+}
 /* v with lane `l` replaced by the wave-uniform s (v_writelane) */
 template <int L>
 __device__ __forceinline__ u32 writelane_u32(u32 v, u32 s) {
@@ -299,11 +308,13 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
         li[i] = fc[i] + st[i];
         e[i] = (int64_t)((q[i].meta >> 24) - mis - base[i]); /* block-relative end */
         /* runs (VSA_BLK_RUN): an end past the entry's block is in the next,
-         * back-to-back block-mode block (>= 1 KiB: at most one boundary per
-         * chunk); outside runs every end lies inside its block */
+         * back-to-back block (>= 1 KiB: at most one boundary per chunk);
+         * outside runs every end lies inside its block */
         if (e[i] >= (int64_t)blen[i]) {
+            const VsaBlock &nb = P.blocks[((q[i].meta >> 4) & 0xfffff) + 1];
             base[i] += blen[i];
             e[i] -= (int64_t)blen[i];
+            hlen[i] = (int64_t)nb.hlen;
         }
     }
     /* wave-uniform loop (every lane stays in, so the output slot reservation
@@ -389,6 +400,10 @@ __device__ __forceinline__ u32 lit_key(const u32 d[5], int j, u32 dmask) {
 struct IterState {
     u64 carry;  /* pending table contributions into the next chunk's first ends */
     u64 pbytes; /* the 8 bytes before the next chunk (lane 63's d[2..3]) */
+    /* FDR sweep: lane 0 holds the previous chunk's lane-63 d[3] / U[4] /
+     * U[5] (lane_ror1 of them); carry and pbytes' high half are refreshed
+     * from these only when the sweep ends (sweep_enter / sweep_leave) */
+    u32 p3, p4, p5;
     u32 ncand;  /* first-stage candidates so far (diagnostic, wave-uniform) */
     u32 tail_cache; /* last tail read from the confirm wave */
     u32 head;       /* entries this wave has pushed to its ring */
@@ -572,7 +587,7 @@ __device__ __forceinline__ void fdr_shift1(const u32 (&F)[6], u32 (&c)[4], u64 &
  * chunk, always looks up. */
 template <bool TWO>
 __device__ __forceinline__ void fdr_sweep_conf(const LitShared &L, const u32 (&d)[4], u32 pv3,
-                                               u64 carry, u32 (&U)[6]) {
+                                               u32 &p4, u32 &p5, u32 (&U)[6]) {
     u64 x[16];
     u32 ko[4], km[4], z[4];
 #pragma unroll
@@ -602,10 +617,26 @@ __device__ __forceinline__ void fdr_sweep_conf(const LitShared &L, const u32 (&d
      * lane 0 takes the previous chunk's carry in the same form. */
     fdr_acc_groups<0x5>(x, U);
     if (!TWO) fdr_acc_groups<0xA, true>(x, U);
-    const u64 cu = carry << 8; /* the carry (ends 0 .. 6 at bytes 0 .. 6), unshifted */
-    U[0] |= writelane_u32<0>(lane_up1(U[4]), (u32)cu);
-    U[1] |= writelane_u32<0>(lane_up1(U[5]), (u32)(cu >> 32));
-    if (!TWO) return;
+    /* The previous lane's U[4..5] (lane 0: the previous chunk's lane 63)
+     * land on this lane's U[0..1] once, after the last level (spill()).
+     * Level 2's lane masks are taken before it: a dword then counts as live
+     * whenever this lane's own slots leave it live, which keeps them
+     * conservative and saves a second cross-lane spill. */
+    auto spill = [&]() {
+        const u32 x4 = lane_ror1(U[4]), x5 = lane_ror1(U[5]);
+        U[0] |= lane_up1_or_old(p4, U[4]);
+        U[1] |= lane_up1_or_old(p5, U[5]);
+        p4 = x4;
+        p5 = x5;
+    };
+    if (!TWO) {
+        spill();
+        return;
+    }
+#ifdef VSA_SPILL_TIGHT /* experiment: spill before the masks too (tighter level 2) */
+    U[0] |= lane_up1_or_old(p4, U[4]);
+    U[1] |= lane_up1_or_old(p5, U[5]);
+#endif
     /* conf dwords with a live end after level 1 (lane masks; an absent
      * bucket's bit is set in every entry, derive_fdr_table).  The next
      * lane's U[0] / U[1] cover ends 15 .. 22 (its U[0] byte 0 = this lane's
@@ -639,10 +670,14 @@ __device__ __forceinline__ void fdr_sweep_conf(const LitShared &L, const u32 (&d
 #pragma unroll
     for (int i = 0; i < VSA_EXTRA_VALU; i++) asm volatile("v_or_b32 %0, %0, %0" : "+v"(U[i & 3]));
 #endif
-    /* spill again: the odd slots' part is new, the even slots' part is
-     * OR-ed twice (lane 0: the carry is in already) */
-    U[0] |= lane_up1(U[4]);
+#ifdef VSA_SPILL_TIGHT
+    U[0] |= lane_up1(U[4]); /* lane 0: its carry is in already */
     U[1] |= lane_up1(U[5]);
+    p4 = lane_ror1(U[4]);
+    p5 = lane_ror1(U[5]);
+#else
+    spill();
+#endif
 }
 
 /* Block-edge masks: position j (0..16) of a lane's chunk is end / byte
@@ -714,30 +749,43 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
      * is left out: a one-byte constraint on b[e] that field 1 (b[e - 1],
      * b[e]) implies (derive_fdr_table) — the filter stays a superset. */
     constexpr bool FDR_BACK = MODE == VSA_MODE_FDR && LDS_TABLE;
-    const u32 pv3 = writelane_u32<0>(lane_up1(d[3]), (u32)(in.pbytes >> 32));
+    constexpr bool SWEEP = FDR_BACK && !EDGE;
+    u32 pv3;
+    IterState out;
+    if constexpr (SWEEP) {
+        /* lane 0: the previous chunk's lane-63 d[3], rotated in last time */
+        pv3 = lane_up1_or_old(in.p3, d[3]);
+        out.p3 = lane_ror1(d[3]);
+    } else {
+        pv3 = writelane_u32<0>(lane_up1(d[3]), (u32)(in.pbytes >> 32));
+    }
     if constexpr (FDR_BACK) {
         if (EDGE) look_m = range_mask(rel32(S.zbase, q0) + 1, rel32(S.len, q0) + 1);
     }
 
-    constexpr bool SWEEP = FDR_BACK && !EDGE;
 #ifdef VSA_FDR_ONE_LEVEL /* experiment build: every lookup in every lane */
     constexpr bool TWO_LVL = false;
 #else
     constexpr bool TWO_LVL = true;
 #endif
     u32 c[T::CW];
-    IterState out;
     out.ncand = in.ncand;
     out.tail_cache = in.tail_cache;
     out.head = in.head;
-    out.pbytes = ((u64)readlane_u32(d[3], WAVE - 1) << 32) | readlane_u32(d[2], WAVE - 1);
+    if constexpr (SWEEP) {
+        out.pbytes = (in.pbytes & 0xffffffff00000000ULL) | readlane_u32(d[2], WAVE - 1);
+        out.carry = in.carry;
+    } else {
+        out.pbytes = ((u64)readlane_u32(d[3], WAVE - 1) << 32) | readlane_u32(d[2], WAVE - 1);
+    }
     if constexpr (SWEEP) {
         /* interior FDR iteration (fdr_sweep_conf): the candidate test runs on
          * the unshifted dwords (this lane's ends are U[0] bytes 1..3, U[1..3]
          * and U[4] byte 0); the shift to end order is done only for a push */
         u32 U[6];
-        fdr_sweep_conf<TWO_LVL>(L, {d[0], d[1], d[2], d[3]}, pv3, in.carry, U);
-        out.carry = (((u64)readlane_u32(U[5], WAVE - 1) << 32) | readlane_u32(U[4], WAVE - 1)) >> 8;
+        out.p4 = in.p4;
+        out.p5 = in.p5;
+        fdr_sweep_conf<TWO_LVL>(L, {d[0], d[1], d[2], d[3]}, pv3, out.p4, out.p5, U);
         const u32 nbm = ~bucket_mask;
         /* this lane's ends: U[0] bytes 1..3 and U[4] byte 0 (one v_bfi) */
         const u32 a123 = U[1] & U[2] & U[3];
@@ -1631,6 +1679,14 @@ vsa_lit_scan(VsaLitParams P) {
             run_adv(ib);
         }
         if (nf > 0) {
+            if constexpr (MODE == VSA_MODE_FDR && LDS_TABLE) {
+                /* sweep_enter: the carry and the previous chunk's last dword
+                 * move to lane 0 of p3..p5 (IterState) */
+                const u64 cu = is.carry << 8;
+                is.p3 = (u32)(is.pbytes >> 32);
+                is.p4 = (u32)cu;
+                is.p5 = (u32)(cu >> 32);
+            }
             /* main sweep: LIT_DEPTH chunks in flight per wave.  ring[k] is
              * consumed and then refilled in place (no register rotation), so
              * each step waits only for the load issued LIT_DEPTH-1 steps ago
@@ -1671,6 +1727,11 @@ vsa_lit_scan(VsaLitParams P) {
                                                           is, bucket_mask);
                     run_adv(ib);
                 }
+            }
+            if constexpr (MODE == VSA_MODE_FDR && LDS_TABLE) {
+                /* sweep_leave: back to the scalar carry / pbytes */
+                is.pbytes = ((u64)readlane_u32(is.p3, 0) << 32) | (u32)is.pbytes;
+                is.carry = (((u64)readlane_u32(is.p5, 0) << 32) | readlane_u32(is.p4, 0)) >> 8;
             }
         }
         prefetch_ticket();

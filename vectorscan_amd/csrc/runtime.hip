@@ -826,13 +826,15 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
     const bool no_runs = getenv("VSA_NO_RUNS") != nullptr;
     uint32_t g_first = 0, g_n = 0;
     int64_t g_span = 0;
-    /* a packed segment of back-to-back block-mode blocks >= 1 KiB is one
-     * range for the scan (VSA_BLK_RUN) */
+    /* a packed segment of back-to-back blocks >= 1 KiB scanned from their
+     * first byte is one range for the scan (VSA_BLK_RUN); a streaming write
+     * in it has its history right before it (the hs corpus and vectored
+     * layouts) */
     auto runnable = [&]() {
         if (no_runs || g_n < 2 || g_n > VSA_RUN_MAX) return false;
         for (uint32_t k = g_first; k < g_first + g_n; k++) {
             const VsaBlock &b = out[k];
-            if (b.start || b.hlen || b.rlo || b.len < VSA_RUN_MIN_LEN) return false;
+            if (b.start || b.rlo || b.len < VSA_RUN_MIN_LEN) return false;
             if (k > g_first && b.base != out[k - 1].base + out[k - 1].len) return false;
         }
         return true;
