@@ -194,6 +194,12 @@ int vsa_memcpy_h2d(vsa_ctx_t *ctx, void *dst, const void *src, size_t bytes);
 int vsa_memcpy_d2h(vsa_ctx_t *ctx, void *dst, const void *src, size_t bytes);
 int vsa_sync(vsa_ctx_t *ctx);
 
+/* Blocks per launch (scan_blocks / plans / hs corpora / hs_scan_vector
+ * pieces): the confirm records carry a 20-bit block index.  Larger batches
+ * are refused with VSA_E_INVALID (VSA_HS_INVALID at the hs level); split
+ * them into several calls. */
+#define VSA_MAX_BLOCKS (1u << 20)
+
 /* Scan nblocks device-resident blocks (each = one hwlmExec(start=starts[i],
  * groups=ALL)) in one launch.  offsets[i], lens[i] are relative to d_data;
  * starts may be NULL (all 0).  Matches are sorted on the device into the

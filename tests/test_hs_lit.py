@@ -415,3 +415,35 @@ def test_reference_literal_grid(case):
             assert rc == hs.SUCCESS
             assert (i, 0, len(exprs[i])) in seq, (mode, all_flags, num, i)
             assert seq == ohs.scan(odb, blob.ptr, text)
+
+
+@pytest.mark.gpu
+def test_hs_block_limit_is_invalid():
+    """one launch takes at most VSA_MAX_BLOCKS blocks (the records carry a
+    20-bit block index): a larger hs corpus or hs_scan_vector call is
+    refused with HS_INVALID, not a misleading NOMEM / UNKNOWN_ERROR"""
+    limit = 1 << 20
+    db = hs.compile_lit_multi([b"abcd"], [0], [1], hs.MODE_VECTORED)
+    scratch = hs.Scratch(db)
+    try:
+        one = b"abcd"
+        rc, _ = hs.scan_vector(db, [one] * (limit + 1), scratch)
+        assert rc == hs.INVALID
+        rc, out = hs.scan_vector(db, [one] * 4, scratch)
+        assert rc == hs.SUCCESS and len(out) == 4
+    finally:
+        scratch.close()
+        db.close()
+    bdb = hs.compile_lit_multi([b"abcd"], [0], [1], hs.MODE_BLOCK)
+    bs = hs.Scratch(bdb)
+    ctx = vsa.Context(0)
+    d = ctx.malloc(16)
+    try:
+        n = limit + 1
+        with pytest.raises(hs.HsError) as e:
+            hs.Corpus(bdb, bs, d, np.zeros(n, np.uint64), np.ones(n, np.uint64))
+        assert e.value.code == hs.INVALID
+    finally:
+        ctx.free(d)
+        bs.close()
+        bdb.close()

@@ -133,6 +133,9 @@ DESIGNS = {
     "s1_pair77": dict(key_offs=(-1, 0), key_bits=(7, 7), ends=range(0, 8), stride=1),
     "s1_pair76": dict(key_offs=(-1, 0), key_bits=(7, 6), ends=range(0, 8), stride=1),
     "s1_pair67": dict(key_offs=(-1, 0), key_bits=(6, 7), ends=range(0, 8), stride=1),
+    "s1_tri455": dict(key_offs=(-2, -1, 0), key_bits=(4, 5, 5), ends=range(0, 8), stride=1),
+    "s1_tri545": dict(key_offs=(-2, -1, 0), key_bits=(5, 4, 5), ends=range(0, 8), stride=1),
+    "s1_tri554": dict(key_offs=(-2, -1, 0), key_bits=(5, 5, 4), ends=range(0, 8), stride=1),
     "s1_skip77": dict(key_offs=(-2, 0), key_bits=(7, 7), ends=range(0, 8), stride=1),
     "s1_skip76": dict(key_offs=(-2, 0), key_bits=(7, 6), ends=range(0, 8), stride=1),
     "s1_gap377": dict(key_offs=(-3, 0), key_bits=(7, 7), ends=range(0, 8), stride=1),

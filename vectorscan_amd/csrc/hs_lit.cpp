@@ -623,6 +623,8 @@ int vsa_hs_scan_vector(const vsa_hs_database_t *db, const char *const *data,
     if (!scratch || !data || !length) return VSA_HS_INVALID;
     if (!valid_db(db)) return VSA_HS_INVALID;
     if (db->mode != VSA_HS_MODE_VECTORED) return VSA_HS_DB_MODE_ERROR;
+    /* one launch: at most VSA_MAX_BLOCKS pieces (vectorscan_amd.h) */
+    if (count > VSA_MAX_BLOCKS) return VSA_HS_INVALID;
     int rc = enter(db, scratch);
     if (rc != VSA_HS_SUCCESS) return rc;
     unsigned n = 0;
@@ -677,6 +679,9 @@ int vsa_hs_corpus_prepare(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch
                           vsa_hs_corpus_t **out) {
     if (!valid_db(db) || !offsets || !lens || !out || (nblocks && !d_data))
         return VSA_HS_INVALID;
+    /* one launch plan per corpus: at most VSA_MAX_BLOCKS chunks (the
+     * reference has no such limit; a larger corpus is prepared in parts) */
+    if (nblocks > VSA_MAX_BLOCKS) return VSA_HS_INVALID;
     if (db->max_len > SHORT_LIT && !h_data) return VSA_HS_INVALID;
     if (!scratch || scratch->magic != SCRATCH_MAGIC || !device_db(scratch, db))
         return VSA_HS_INVALID;

@@ -773,7 +773,7 @@ int finish_pending(vsa_ctx *c) {
 
 constexpr uint32_t SEG_GROUP_SHIFT = 24;
 constexpr uint32_t SEG_GROUP_MAX = 255;
-constexpr uint32_t PLAN_MAX_BLOCKS = 1u << 20; /* 20-bit block field of the keys */
+constexpr uint32_t PLAN_MAX_BLOCKS = VSA_MAX_BLOCKS; /* 20-bit block field of the keys */
 
 int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens,
                const uint64_t *starts, const uint64_t *hlens, const uint64_t *rlos,
