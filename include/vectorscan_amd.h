@@ -73,6 +73,24 @@ hwlm_error_t vsa_gpu_noodExec(const struct noodTable *n, const uint8_t *buf, siz
 int vsa_hwlm_register(const void *blob, int bare_type);
 int vsa_hwlm_unregister(const void *blob);
 
+/* Batching service for concurrent drop-in calls (many host threads, each
+ * scanning its blocks through hwlmExec: rose/block.c:259, hsbench -T).  A
+ * worker thread with its own GPU context takes the calls that arrive within
+ * window_us of each other (at most max_batch), stages their buffers in one
+ * DMA and scans them as the blocks of one launch; each caller then gets its
+ * records replayed through its own callback on its own thread, with
+ * hwlmExec's contract (same order, groups / NOREPEAT / squash / flood).
+ * vsa_batcher_hwlmExec blocks until the caller's matches are delivered.
+ * The accel pre-skip is not applied on this path (it only moves `start`).
+ * vsa_batcher_stats: launches so far and calls served by them. */
+typedef struct vsa_batcher vsa_batcher_t;
+int vsa_batcher_create(int device, uint32_t max_batch, uint32_t window_us, vsa_batcher_t **b);
+int vsa_batcher_destroy(vsa_batcher_t *b);
+int vsa_batcher_stats(vsa_batcher_t *b, uint64_t *batches, uint64_t *calls);
+hwlm_error_t vsa_batcher_hwlmExec(vsa_batcher_t *b, const struct HWLM *tab, const uint8_t *buf,
+                                  size_t len, size_t start, HWLMCallback cb,
+                                  struct hs_scratch *scratch, hwlm_group_t groups);
+
 /* Replaces hwlmExec, src/hwlm/hwlm.h:116 (impl. src/hwlm/hwlm.c:178).
  * Copies buf to the GPU, scans, replays confirmed matches through cb in the
  * reference order (end, bucket, confirm-chain order) applying groups /

@@ -22,3 +22,18 @@ def test_gpu_c_abi_harness():
     r = subprocess.run([HARNESS, "300"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert " 0 mismatches" in r.stdout, r.stdout
+
+
+def test_hwlm_registration_host_side():
+    """vsa_hwlm_register / unregister (host bookkeeping, no GPU): register
+    accepts an HWLM (-1) or a bare FDR / noodle engine type, unregister of a
+    blob that is not registered is an error"""
+    import bench
+    import vectorscan_amd as vsa
+    b = vsa.hwlm_build(bench.make_literals(50, seed=1))
+    vsa.hwlm_register(b)
+    vsa.hwlm_unregister(b)
+    with pytest.raises(Exception):
+        vsa.hwlm_unregister(b)
+    with pytest.raises(Exception):
+        vsa.hwlm_register(b, 7)  # not an engine type

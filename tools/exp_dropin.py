@@ -28,8 +28,6 @@ blob = vsa.hwlm_build(lits)
 eng = vsa.engine_blob(blob)
 data = bench.make_corpus(64 << 20, lits, seed=5, plant_every=64 << 10)
 lib = vsa.lib
-lib.vsa_hwlm_register.argtypes = [ctypes.c_void_p, ctypes.c_int]
-lib.vsa_hwlm_unregister.argtypes = [ctypes.c_void_p]
 count = ctypes.c_uint64(0)
 
 
@@ -61,9 +59,9 @@ for size in [1 << 10, 4 << 10, 16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 
 
     t_unreg = per_call(gpu, reps)
     n_gpu = count.value
-    lib.vsa_hwlm_register(blob.ptr, -1)
+    vsa.hwlm_register(blob)
     t_reg = per_call(gpu, reps)
-    lib.vsa_hwlm_unregister(blob.ptr)
+    vsa.hwlm_unregister(blob)
     creps = max(3, min(300, (16 << 20) // size))
     t_cpu = per_call(lambda: oracle.fdr_exec_simd(eng, buf), creps)
     st, m = oracle.fdr_exec_simd(eng, buf)

@@ -329,6 +329,64 @@ def hwlm_exec(blob, data, start=0, cb=None, groups=HWLM_ALL_GROUPS, scratch=None
     return rc if cb is not None else (rc, matches)
 
 
+_sig("vsa_hwlm_register", ctypes.c_int, ctypes.c_void_p, ctypes.c_int)
+_sig("vsa_hwlm_unregister", ctypes.c_int, ctypes.c_void_p)
+
+
+def hwlm_register(blob, bare_type=-1):
+    """vsa_hwlm_register: the drop-ins serve this (immutable) blob without
+    comparing it with their cached device copy on every call"""
+    _check(lib.vsa_hwlm_register(blob.ptr, bare_type))
+
+
+def hwlm_unregister(blob):
+    _check(lib.vsa_hwlm_unregister(blob.ptr))
+
+
+_sig("vsa_batcher_create", ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+     ctypes.POINTER(ctypes.c_void_p))
+_sig("vsa_batcher_destroy", ctypes.c_int, ctypes.c_void_p)
+_sig("vsa_batcher_stats", ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+     ctypes.POINTER(ctypes.c_uint64))
+_sig("vsa_batcher_hwlmExec", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+     ctypes.c_size_t, ctypes.c_size_t, HWLMCallback, ctypes.c_void_p, ctypes.c_uint64)
+
+
+class Batcher:
+    """vsa_batcher: concurrent hwlmExec calls from many threads share
+    launches (a worker with its own GPU context scans the calls queued
+    within ``window_us`` as one batch; each caller's callback runs on its
+    own thread)."""
+
+    def __init__(self, device=0, max_batch=256, window_us=20):
+        self.ptr = ctypes.c_void_p()
+        _check(lib.vsa_batcher_create(device, max_batch, window_us, ctypes.byref(self.ptr)))
+
+    def hwlm_exec(self, blob, data, start=0, cb=None, groups=HWLM_ALL_GROUPS, scratch=None):
+        """as hwlm_exec, through the batcher"""
+        keep, ptr, n = _as_buf(data)
+        ccb, matches = _runner(None, cb)
+        rc = lib.vsa_batcher_hwlmExec(self.ptr, blob.ptr, ptr, n, start, ccb, scratch, groups)
+        return rc if cb is not None else (rc, matches)
+
+    def stats(self):
+        """(launches, calls served)"""
+        b, c = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib.vsa_batcher_stats(self.ptr, ctypes.byref(b), ctypes.byref(c)))
+        return b.value, c.value
+
+    def close(self):
+        if self.ptr:
+            lib.vsa_batcher_destroy(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def fdr_exec(blob, data, start=0, cb=None, groups=HWLM_ALL_GROUPS, scratch=None):
     """fdrExec (fdr.h:58) on the FDR/Teddy engine inside an HWLM blob."""
     keep, ptr, n = _as_buf(data)

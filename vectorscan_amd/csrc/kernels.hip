@@ -1810,6 +1810,64 @@ __global__ void __launch_bounds__(256) vsa_bin_hist(const uint64_t *keys, const 
                                1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+/* the last of a grid's workgroups to get here (the others' global writes
+ * are visible to it afterwards); it resets `done` for the next launch */
+__device__ __forceinline__ bool last_workgroup(uint32_t *done) {
+    __shared__ bool last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+               gridDim.x - 1;
+    __syncthreads();
+    if (last) {
+        __threadfence();
+        if (threadIdx.x == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return last;
+}
+
+/* (1) + (2) in one launch: the histogram, then the last workgroup scans the
+ * counts (256 threads x 64 bins) */
+__global__ void __launch_bounds__(256) vsa_bin_hist_scan(const uint64_t *keys, uint64_t *ctr,
+                                                         uint64_t cap, uint32_t bin_shift,
+                                                         uint32_t *counts, uint32_t *cursor,
+                                                         uint32_t *done) {
+    const uint64_t n0 = ctr[0];
+    const uint64_t n = n0 > cap ? 0 : n0; /* an overflowed launch runs again */
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * 256)
+        __hip_atomic_fetch_add(&counts[(uint32_t)((keys[i] >> VSA_KEY_END_SHIFT) >> bin_shift)],
+                               1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!last_workgroup(done)) return;
+    __shared__ uint32_t part[256];
+    const uint32_t t = threadIdx.x;
+    constexpr uint32_t PER = VSA_SORT_BINS / 256;
+    uint32_t sum = 0, big = 0;
+    for (uint32_t k = 0; k < PER; k++) {
+        const uint32_t v = __hip_atomic_load(&counts[t * PER + k], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        sum += v;
+        big |= v > VSA_SORT_BIN_MAX;
+    }
+    if (big) ctr[VSA_CTR_BIN_OVERFLOW] = 1;
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 256; d <<= 1) {
+        const uint32_t x = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - sum;
+    for (uint32_t k = 0; k < PER; k++) {
+        const uint32_t v = __hip_atomic_load(&counts[t * PER + k], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        cursor[t * PER + k] = run;
+        run += v;
+    }
+}
+
 __global__ void __launch_bounds__(1024) vsa_bin_scan(const uint32_t *counts, uint32_t *cursor,
                                                     uint64_t *ctr) {
     __shared__ uint32_t part[1024];
@@ -1864,10 +1922,9 @@ __global__ void __launch_bounds__(256) vsa_bin_scatter(const uint64_t *keys, con
 }
 
 /* one wave per bin; after the scatter cursor[b] = the bin's end */
-__global__ void __launch_bounds__(256) vsa_bin_sort(const uint64_t *ctr, uint64_t cap,
-                                                    uint32_t *counts,
-                                                    const uint32_t *cursor, uint64_t *keys,
-                                                    uint32_t *ids) {
+__device__ __forceinline__ void bin_sort_wave(const uint64_t *ctr, uint64_t cap, uint32_t *counts,
+                                              const uint32_t *cursor, uint64_t *keys,
+                                              uint32_t *ids) {
     const uint32_t bin = blockIdx.x * 4 + threadIdx.x / WAVE;
     const u32 lane = lane_id();
     const uint32_t m = counts[bin];
@@ -1907,16 +1964,22 @@ __global__ void __launch_bounds__(256) vsa_bin_sort(const uint64_t *ctr, uint64_
     }
 }
 
+__global__ void __launch_bounds__(256) vsa_bin_sort(const uint64_t *ctr, uint64_t cap,
+                                                    uint32_t *counts,
+                                                    const uint32_t *cursor, uint64_t *keys,
+                                                    uint32_t *ids) {
+    bin_sort_wave(ctr, cap, counts, cursor, keys, ids);
+}
+
 /* The last launch of a binned scan: the scan's counters [0, 16) go to
  * host memory (fine-grained, h[1..16]) and then h[0] = seq with a
  * system-scope release, which the host polls instead of queueing a copy
  * and an event; then the scan's counters [0, nzero) are zeroed for the
  * next launch, which therefore needs no memset. */
-__global__ void __launch_bounds__(256) vsa_publish(unsigned long long *ctr,
-                                                   unsigned long long *h,
-                                                   unsigned long long seq, uint32_t nzero,
-                                                   const uint64_t *keys, const uint32_t *ids,
-                                                   uint32_t kmax) {
+__device__ __forceinline__ void publish_body(unsigned long long *ctr, unsigned long long *h,
+                                             unsigned long long seq, uint32_t nzero,
+                                             const uint64_t *keys, const uint32_t *ids,
+                                             uint32_t kmax) {
     const u32 t = threadIdx.x;
     unsigned long long v = 0;
     if (t < 16) v = ctr[t];
@@ -1945,6 +2008,28 @@ __global__ void __launch_bounds__(256) vsa_publish(unsigned long long *ctr,
         __threadfence_system();
         __hip_atomic_store(&h[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+__global__ void __launch_bounds__(256) vsa_publish(unsigned long long *ctr,
+                                                   unsigned long long *h,
+                                                   unsigned long long seq, uint32_t nzero,
+                                                   const uint64_t *keys, const uint32_t *ids,
+                                                   uint32_t kmax) {
+    publish_body(ctr, h, seq, nzero, keys, ids, kmax);
+}
+
+/* (4) + the publish in one launch: each wave sorts its bin, then the last
+ * workgroup publishes the counters (every sort wave has read them by then) */
+__global__ void __launch_bounds__(256) vsa_bin_sort_publish(unsigned long long *ctr, uint64_t cap,
+                                                            uint32_t *counts,
+                                                            const uint32_t *cursor,
+                                                            uint64_t *keys, uint32_t *ids,
+                                                            uint32_t *done, unsigned long long *h,
+                                                            unsigned long long seq,
+                                                            uint32_t nzero) {
+    bin_sort_wave((const uint64_t *)ctr, cap, counts, cursor, keys, ids);
+    if (!last_workgroup(done)) return;
+    publish_body(ctr, h, seq, nzero, nullptr, nullptr, 0u);
 }
 
 /* A binned scan's sorted records packed for a collective, on the device

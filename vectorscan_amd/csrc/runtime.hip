@@ -27,7 +27,10 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
+#include <thread>
 #include <vector>
 #include <chrono>
 #include <sched.h>
@@ -43,6 +46,13 @@ __global__ void vsa_class_scan(VsaClassParams P);
 __global__ void vsa_bin_hist(const uint64_t *keys, const uint64_t *ctr, uint64_t cap,
                              uint32_t bin_shift, uint32_t *counts);
 __global__ void vsa_bin_scan(const uint32_t *counts, uint32_t *cursor, uint64_t *ctr);
+__global__ void vsa_bin_hist_scan(const uint64_t *keys, uint64_t *ctr, uint64_t cap,
+                                  uint32_t bin_shift, uint32_t *counts, uint32_t *cursor,
+                                  uint32_t *done);
+__global__ void vsa_bin_sort_publish(unsigned long long *ctr, uint64_t cap, uint32_t *counts,
+                                     const uint32_t *cursor, uint64_t *keys, uint32_t *ids,
+                                     uint32_t *done, unsigned long long *h, unsigned long long seq,
+                                     uint32_t nzero);
 __global__ void vsa_bin_scatter(const uint64_t *keys, const uint32_t *ids, const uint64_t *ctr,
                                 uint64_t cap, uint32_t bin_shift, uint32_t *cursor,
                                 uint64_t *okeys, uint32_t *oids);
@@ -100,7 +110,8 @@ struct Workspace {
     void *d_tmp = nullptr;
     size_t tmp_bytes = 0;
     unsigned long long *d_counters = nullptr; /* layout above */
-    uint32_t *d_bins = nullptr; /* binned sort: counts[VSA_SORT_BINS], cursor[..] */
+    uint32_t *d_bins = nullptr; /* binned sort: counts[VSA_SORT_BINS], cursor[..],
+                                   then 2 done counters (last-workgroup launches) */
     unsigned long long *h_counters = nullptr; /* pinned mirror */
     /* fine-grained host memory the device publishes a binned scan's
      * counters into (vsa_publish): [0] = sequence, [1..16] = counters */
@@ -486,24 +497,45 @@ uint32_t bin_shift_for(int end_bits) {
     return end_bits > (int)VSA_SORT_BIN_BITS ? (uint32_t)end_bits - VSA_SORT_BIN_BITS : 0u;
 }
 
-/* the binned sort's three launches (kernels.hip): they read the record
- * count and the overflow flag from d_counters, so they may be queued before
- * the host has seen either (an overflowed launch leaves them idle) */
+/* the binned sort behind the scan (kernels.hip): histogram + scan (the
+ * last workgroup scans), scatter, then per-bin sorts + the publish (the last
+ * workgroup publishes): three launches.  They read the record count and the
+ * overflow flag from d_counters, so they are queued before the host has
+ * seen either (an overflowed launch leaves them idle).  VSA_SORT_SPLIT=1:
+ * the five separate launches of round 2 (A/B knob). */
 int queue_bin_sort(vsa_ctx *c) {
     Workspace &w = c->ws;
     uint32_t *counts = w.d_bins, *cursor = w.d_bins + VSA_SORT_BINS;
+    uint32_t *done = w.d_bins + 2 * VSA_SORT_BINS;
     const uint32_t shift = bin_shift_for(c->launch.end_bits);
-    hipLaunchKernelGGL(vsa_bin_hist, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, c->stream,
-                       w.d_keys[0], (const uint64_t *)w.d_counters, (uint64_t)w.out_cap, shift,
-                       counts);
-    hipLaunchKernelGGL(vsa_bin_scan, dim3(1), dim3(1024), 0, c->stream, counts, cursor,
-                       (uint64_t *)w.d_counters);
+    static const bool split = getenv("VSA_SORT_SPLIT") != nullptr;
+    if (split) {
+        hipLaunchKernelGGL(vsa_bin_hist, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, c->stream,
+                           w.d_keys[0], (const uint64_t *)w.d_counters, (uint64_t)w.out_cap,
+                           shift, counts);
+        hipLaunchKernelGGL(vsa_bin_scan, dim3(1), dim3(1024), 0, c->stream, counts, cursor,
+                           (uint64_t *)w.d_counters);
+    } else {
+        hipLaunchKernelGGL(vsa_bin_hist_scan, dim3((uint32_t)c->num_cus * 4), dim3(256), 0,
+                           c->stream, w.d_keys[0], (uint64_t *)w.d_counters,
+                           (uint64_t)w.out_cap, shift, counts, cursor, done);
+    }
     hipLaunchKernelGGL(vsa_bin_scatter, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, c->stream,
                        w.d_keys[0], w.d_ids[0], (const uint64_t *)w.d_counters,
                        (uint64_t)w.out_cap, shift, cursor, w.d_keys[1], w.d_ids[1]);
-    hipLaunchKernelGGL(vsa_bin_sort, dim3(VSA_SORT_BINS / 4), dim3(256), 0, c->stream,
-                       (const uint64_t *)w.d_counters, (uint64_t)w.out_cap, counts, cursor,
-                       w.d_keys[1], w.d_ids[1]);
+    if (split) {
+        hipLaunchKernelGGL(vsa_bin_sort, dim3(VSA_SORT_BINS / 4), dim3(256), 0, c->stream,
+                           (const uint64_t *)w.d_counters, (uint64_t)w.out_cap, counts, cursor,
+                           w.d_keys[1], w.d_ids[1]);
+        hipLaunchKernelGGL(vsa_publish, dim3(1), dim3(256), 0, c->stream, c->ws.d_counters,
+                           c->ws.d_pub, (unsigned long long)++c->pub_seq, 144u,
+                           (const uint64_t *)nullptr, (const uint32_t *)nullptr, 0u);
+    } else {
+        hipLaunchKernelGGL(vsa_bin_sort_publish, dim3(VSA_SORT_BINS / 4), dim3(256), 0,
+                           c->stream, c->ws.d_counters, (uint64_t)w.out_cap, counts, cursor,
+                           w.d_keys[1], w.d_ids[1], done + 1, c->ws.d_pub,
+                           (unsigned long long)++c->pub_seq, 144u);
+    }
     VSA_CHECK(hipGetLastError());
     return VSA_OK;
 }
@@ -550,15 +582,11 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
      * (finish_scan falls back to the library sort if a bin overflowed) */
     c->launch.dev_sort = c->launch.bins;
     if (!c->launch.dev_sort) return VSA_OK;
+    /* the sort zeroes every bin count; the publish hands the counters to
+     * the host and zeroes them */
     int r2 = queue_bin_sort(c);
     if (r2 != VSA_OK) return r2;
-    /* vsa_bin_sort zeroes every bin count; vsa_publish hands the counters
-     * to the host and zeroes them */
     c->bins_clean = true;
-    hipLaunchKernelGGL(vsa_publish, dim3(1), dim3(256), 0, c->stream, c->ws.d_counters,
-                       c->ws.d_pub, (unsigned long long)++c->pub_seq, 144u,
-                       (const uint64_t *)nullptr, (const uint32_t *)nullptr, 0u);
-    VSA_CHECK(hipGetLastError());
     c->launch.published = true;
     c->ctr_clean = true;
     return VSA_OK;
@@ -1443,7 +1471,9 @@ int vsa_ctx_create(int device, vsa_ctx_t **out) {
     VSA_CHECK(hipEventCreate(&c->ev1));
     VSA_CHECK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
     VSA_CHECK(hipMalloc(&c->ws.d_counters, N_COUNTERS * sizeof(unsigned long long)));
-    VSA_CHECK(hipMalloc(&c->ws.d_bins, 2 * VSA_SORT_BINS * sizeof(uint32_t)));
+    VSA_CHECK(hipMalloc(&c->ws.d_bins, (2 * VSA_SORT_BINS + 16) * sizeof(uint32_t)));
+    /* the done counters start at 0 and every launch leaves them at 0 */
+    VSA_CHECK(hipMemset(c->ws.d_bins + 2 * VSA_SORT_BINS, 0, 16 * sizeof(uint32_t)));
     VSA_CHECK(hipHostMalloc((void **)&c->ws.h_counters, N_COUNTERS * sizeof(unsigned long long),
                             hipHostMallocDefault));
     VSA_CHECK(hipHostMalloc((void **)&c->ws.h_pub, PUB_WORDS * sizeof(unsigned long long),
@@ -2224,6 +2254,204 @@ hwlm_error_t vsa_gpu_noodExec(const struct noodTable *n, const uint8_t *buf, siz
     return noodExec(n, buf, len, start, cb, scratch);
 }
 
+} // extern "C"
+
+/* ------------------------------------------------- batching service --- */
+
+/* Concurrent drop-in calls (many host threads scanning blocks, each through
+ * its Rose floating table: rose/block.c:259, hsbench -T) share launches: a
+ * worker thread with its own context takes the calls queued within a short
+ * window, stages all their buffers into pinned memory, sends them in one
+ * DMA, scans them as the blocks of ONE launch (vsa_scan_blocks, starts per
+ * block) and hands each caller its records (rebased to its buffer); the
+ * caller replays them through its own callback on its own thread, exactly as
+ * hwlmExec does (groups, NOREPEAT, squash, flood events).  A call pays one
+ * launch shared by the batch instead of one of its own.  The accel pre-skip
+ * is not applied on this path (it only moves `start` past positions where no
+ * literal can match). */
+struct vsa_batcher {
+    struct Req {
+        const void *tab;
+        const uint8_t *buf;
+        size_t len, start;
+        vsa_db *db = nullptr;
+        std::vector<uint64_t> keys;
+        std::vector<uint32_t> ids;
+        int rc = VSA_OK;
+        bool done = false;
+    };
+    int device = 0;
+    uint32_t max_batch = 256;
+    uint32_t window_us = 20;
+    size_t max_bytes = 64u << 20;
+    std::mutex m;
+    std::condition_variable cv_req, cv_done;
+    std::deque<Req *> q;
+    bool stop = false;
+    std::thread worker;
+    uint64_t batches = 0, calls = 0;
+
+    void run() {
+        vsa_ctx *c = nullptr;
+        if (vsa_ctx_create(device, &c) != VSA_OK) c = nullptr;
+        t_ctx = c; /* registry_get loads the tables on this context */
+        std::vector<Req *> batch;
+        std::vector<uint64_t> offs, lens, starts;
+        std::vector<uint64_t> keys;
+        std::vector<uint32_t> ids;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv_req.wait(lk, [&] { return stop || !q.empty(); });
+                if (stop && q.empty()) break;
+                /* a short window for more callers to join the launch */
+                if (q.size() < max_batch && window_us)
+                    cv_req.wait_for(lk, std::chrono::microseconds(window_us),
+                                    [&] { return stop || q.size() >= max_batch; });
+                batch.clear();
+                size_t bytes = 0;
+                while (!q.empty() && batch.size() < max_batch &&
+                       (batch.empty() || bytes + q.front()->len <= max_bytes)) {
+                    bytes += q.front()->len;
+                    batch.push_back(q.front());
+                    q.pop_front();
+                }
+            }
+            /* one launch per table in the batch */
+            std::stable_sort(batch.begin(), batch.end(),
+                             [](const Req *a, const Req *b) { return a->tab < b->tab; });
+            for (size_t i = 0; i < batch.size();) {
+                size_t j = i;
+                while (j < batch.size() && batch[j]->tab == batch[i]->tab) j++;
+                const int rc = c ? scan_group(c, batch.data() + i, j - i, offs, lens, starts,
+                                              keys, ids)
+                                 : VSA_E_DEVICE;
+                for (size_t k = i; k < j; k++)
+                    if (rc != VSA_OK) batch[k]->rc = rc;
+                i = j;
+            }
+            {
+                std::lock_guard<std::mutex> lk(m);
+                for (Req *r : batch) r->done = true;
+                batches++;
+                calls += batch.size();
+            }
+            cv_done.notify_all();
+        }
+        if (c) {
+            while (!t_registry.empty()) vsa_db_free(t_registry.begin()->second);
+            vsa_ctx_destroy(c);
+        }
+        t_ctx = nullptr;
+    }
+
+    static int scan_group(vsa_ctx *c, Req **rq, size_t n, std::vector<uint64_t> &offs,
+                          std::vector<uint64_t> &lens, std::vector<uint64_t> &starts,
+                          std::vector<uint64_t> &keys, std::vector<uint32_t> &ids) {
+        vsa_db *db = registry_get(rq[0]->tab, -1);
+        if (!db) return VSA_E_INVALID;
+        size_t total = 0;
+        offs.resize(n);
+        lens.resize(n);
+        starts.resize(n);
+        for (size_t k = 0; k < n; k++) {
+            offs[k] = total;
+            lens[k] = rq[k]->len;
+            starts[k] = rq[k]->start;
+            total += rq[k]->len;
+        }
+        int r;
+        if ((r = ensure_in(c, total + 16)) != VSA_OK) return r;
+        if ((r = ensure_hin(c, total)) != VSA_OK) return r;
+        for (size_t k = 0; k < n; k++) memcpy(c->ws.h_in + offs[k], rq[k]->buf, rq[k]->len);
+        c->res_host = nullptr;
+        VSA_CHECK(hipMemcpyAsync(c->ws.d_in, c->ws.h_in, total, hipMemcpyHostToDevice, c->stream));
+        uint64_t nm = 0;
+        if ((r = scan_blocks_impl(c, db, c->ws.d_in, offs.data(), lens.data(), starts.data(),
+                                  (uint32_t)n, 0, &nm)) != VSA_OK)
+            return r;
+        if ((r = fetch_records(c, nm, keys, ids)) != VSA_OK) return r;
+        /* the records are in end order: each caller's are one run */
+        uint64_t k0 = 0;
+        for (size_t k = 0; k < n; k++) {
+            const uint64_t hi = (offs[k] + lens[k]) << VSA_KEY_END_SHIFT;
+            uint64_t k1 = k0;
+            while (k1 < nm && keys[k1] < hi) k1++;
+            Req *q = rq[k];
+            q->db = db;
+            q->keys.resize(k1 - k0);
+            q->ids.assign(ids.begin() + (ptrdiff_t)k0, ids.begin() + (ptrdiff_t)k1);
+            const uint64_t base = offs[k] << VSA_KEY_END_SHIFT;
+            for (uint64_t i = k0; i < k1; i++) q->keys[i - k0] = keys[i] - base;
+            k0 = k1;
+        }
+        return VSA_OK;
+    }
+};
+
+extern "C" {
+
+int vsa_batcher_create(int device, uint32_t max_batch, uint32_t window_us, vsa_batcher_t **out) {
+    if (!out || !max_batch || max_batch > VSA_MAX_BLOCKS) return VSA_E_INVALID;
+    vsa_batcher *b = new (std::nothrow) vsa_batcher;
+    if (!b) return VSA_E_NOMEM;
+    b->device = device;
+    b->max_batch = max_batch;
+    b->window_us = window_us;
+    b->worker = std::thread([b] { b->run(); });
+    *out = b;
+    return VSA_OK;
+}
+
+int vsa_batcher_destroy(vsa_batcher_t *b) {
+    if (!b) return VSA_E_INVALID;
+    {
+        std::lock_guard<std::mutex> lk(b->m);
+        b->stop = true;
+    }
+    b->cv_req.notify_all();
+    b->worker.join();
+    delete b;
+    return VSA_OK;
+}
+
+int vsa_batcher_stats(vsa_batcher_t *b, uint64_t *batches, uint64_t *calls) {
+    if (!b) return VSA_E_INVALID;
+    std::lock_guard<std::mutex> lk(b->m);
+    if (batches) *batches = b->batches;
+    if (calls) *calls = b->calls;
+    return VSA_OK;
+}
+
+hwlm_error_t vsa_batcher_hwlmExec(vsa_batcher_t *b, const struct HWLM *tab, const uint8_t *buf,
+                                  size_t len, size_t start, HWLMCallback cb,
+                                  struct hs_scratch *scratch, hwlm_group_t groups) {
+    if (!b || !tab) return HWLM_ERROR_UNKNOWN;
+    if (!groups || start >= len) return HWLM_SUCCESS;
+    /* a buffer that would fill a batch on its own goes alone */
+    if (len > b->max_bytes / 4) return hwlmExec(tab, buf, len, start, cb, scratch, groups);
+    vsa_batcher::Req r;
+    r.tab = tab;
+    r.buf = buf;
+    r.len = len;
+    r.start = start;
+    {
+        std::unique_lock<std::mutex> lk(b->m);
+        if (b->stop) return HWLM_ERROR_UNKNOWN;
+        b->q.push_back(&r);
+        b->cv_req.notify_one();
+        b->cv_done.wait(lk, [&] { return r.done; });
+    }
+    if (r.rc != VSA_OK || !r.db) return HWLM_ERROR_UNKNOWN;
+    if (r.db->type == HWLM_ENGINE_NOOD)
+        return replay_nood(r.keys.data(), r.ids.data(), r.keys.size(), cb, scratch);
+    std::vector<vsa::FloodEvent> ev;
+    return replay_lit(r.db, r.keys.data(), r.keys.size(), cb, scratch, groups,
+                      floods_for(r.db, buf, len, start, ev));
+}
+
+} /* extern "C" */
+
 /* The writes of one logical stream (hs_scan: one block-mode write;
  * hs_scan_vector: all pieces) scanned in ONE launch: the history bytes and
  * the writes laid end to end in the context's input buffer, each write a
@@ -2231,8 +2459,6 @@ hwlm_error_t vsa_gpu_noodExec(const struct noodTable *n, const uint8_t *buf, siz
  * 8-byte HWLM literals); then each write's records replayed in order with
  * its own flood events and ends relative to it.  cbctx is an opaque
  * callback context (no Rose scratch: no INCLUDED_JUMP squash). */
-} // extern "C"
-
 namespace vsa {
 hwlm_error_t exec_pieces(vsa_ctx *c, const vsa_db *db, const u8 *hist, size_t hist_len,
                          const u8 *const *bufs, const size_t *lens, size_t n,
