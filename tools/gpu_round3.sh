@@ -8,7 +8,7 @@
 #   batcher  concurrent calls, plain vs batched (tools/exp_batcher.py)
 #   noodle   cfg 1 at 4 GiB (tools/bench_configs.py --cfg1-gib 4)
 #   ab       interleaved A/B of variant libraries (tools/gpu_abn.sh VARIANTS)
-#   sortab   bench with the fused / split (VSA_SORT_SPLIT) sort, pipelined or not
+#   sortab   bench with the split / fused (VSA_SORT_FUSED) sort, pipelined or not
 #   profile  rocprofv3 trace + PMC passes (tools/profile.sh r03)
 #   tools/gpu_round3.sh suite blocks cfg5 ...
 O=gpurun_out/r03
@@ -25,7 +25,7 @@ for step in "$@"; do
     ab) REPS=${REPS:-3} bash tools/gpu_abn.sh $VARIANTS || exit 1 ;;
     sortab)
       for v in fused split; do
-        e=""; [ $v = split ] && e="VSA_SORT_SPLIT=1"
+        e=""; [ $v = fused ] && e="VSA_SORT_FUSED=1"
         for m in pipe nopipe; do
           a=""; [ $m = nopipe ] && a="--no-pipeline"
           env $e timeout -k 10 300 python bench.py --no-cpu $a 2>$O/b.err | tail -1 > $O/sort_${v}_${m}.json || exit 1

@@ -497,18 +497,21 @@ uint32_t bin_shift_for(int end_bits) {
     return end_bits > (int)VSA_SORT_BIN_BITS ? (uint32_t)end_bits - VSA_SORT_BIN_BITS : 0u;
 }
 
-/* the binned sort behind the scan (kernels.hip): histogram + scan (the
- * last workgroup scans), scatter, then per-bin sorts + the publish (the last
- * workgroup publishes): three launches.  They read the record count and the
- * overflow flag from d_counters, so they are queued before the host has
- * seen either (an overflowed launch leaves them idle).  VSA_SORT_SPLIT=1:
- * the five separate launches of round 2 (A/B knob). */
+/* the binned sort behind the scan (kernels.hip): histogram, scan of the
+ * counts, scatter, per-bin sorts, publish: five short launches.  They read
+ * the record count and the overflow flag from d_counters, so they are
+ * queued before the host has seen either (an overflowed launch leaves them
+ * idle).  VSA_SORT_FUSED=1 (A/B knob): three launches, histogram + scan and
+ * sort + publish fused behind a last-workgroup ticket -- measured 107 us +
+ * 342 us against ~30 us for all five (profiles/r03_sort_fused_trace.csv):
+ * every workgroup's agent-scope acq_rel ticket on one address serializes
+ * (~85-100 ns each over 1,024 / 4,096 workgroups). */
 int queue_bin_sort(vsa_ctx *c) {
     Workspace &w = c->ws;
     uint32_t *counts = w.d_bins, *cursor = w.d_bins + VSA_SORT_BINS;
     uint32_t *done = w.d_bins + 2 * VSA_SORT_BINS;
     const uint32_t shift = bin_shift_for(c->launch.end_bits);
-    static const bool split = getenv("VSA_SORT_SPLIT") != nullptr;
+    static const bool split = getenv("VSA_SORT_FUSED") == nullptr;
     if (split) {
         hipLaunchKernelGGL(vsa_bin_hist, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, c->stream,
                            w.d_keys[0], (const uint64_t *)w.d_counters, (uint64_t)w.out_cap,
