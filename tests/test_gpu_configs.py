@@ -140,7 +140,10 @@ def test_gpu_large_literal_sets(ctx, nlits, monkeypatch):
     """Large FDR sets, where the confirm stage is the bound: the first launch
     (>= 16 MiB) measures the confirm-candidate rate and the next ones run
     with two confirm waves per workgroup; one launch also forces a single
-    confirm wave and one three (VSA_NCONF).  Every launch == the oracle."""
+    confirm wave and one three (VSA_NCONF).  From the second launch on the
+    scanning waves expand the candidates (scanner expansion, runtime.hip
+    use_xp); the last two launches force it off and on (VSA_XP).  Every
+    launch == the oracle."""
     lits = bench.make_literals(nlits, seed=12)
     blob = vsa.hwlm_build(lits)
     data = bench.make_corpus(24 << 20, lits, seed=5, plant_every=16 << 10)
@@ -151,14 +154,18 @@ def test_gpu_large_literal_sets(ctx, nlits, monkeypatch):
     db = vsa.Database(ctx, blob)
     try:
         ctx.h2d(d, data)
-        for nconf in (None, None, "1", "3"):
+        for nconf, xp in ((None, None), (None, None), ("1", None), ("3", None),
+                          ("2", "0"), ("2", "1")):
             if nconf:
                 monkeypatch.setenv("VSA_NCONF", nconf)
+            if xp:
+                monkeypatch.setenv("VSA_XP", xp)
             k = ctx.scan_blocks(db, d, [0], [n])
             res = ctx.results(k)
             got = list(zip((res["key"] >> np.uint64(24)).tolist(), res["id"].tolist()))
-            assert got == want, nconf
+            assert got == want, (nconf, xp)
     finally:
         monkeypatch.delenv("VSA_NCONF", raising=False)
+        monkeypatch.delenv("VSA_XP", raising=False)
         db.close()
         ctx.free(d)

@@ -604,3 +604,44 @@ def test_gpu_back_to_back_runs(ctx, nlits):
         assert run_layout_scan(ctx, blob, bufs) == want
     finally:
         del os.environ["VSA_NO_RUNS"]
+
+
+@pytest.mark.parametrize("nlits", [1, 30, 500, 3000])
+def test_gpu_scanner_expansion(ctx, nlits, monkeypatch):
+    """Scanner expansion (VSA_XP=1, kernels.hip xp_push: the scanning waves
+    expand candidate bits, apply the slot-bitmap prefilter and push confirm
+    entries; the runtime turns it on for large literal sets) forced on small
+    sets: per-block records equal the oracle's hwlmExec of each block, for
+    ragged blocks with starts and misalignment, back-to-back runs with
+    literals across every boundary, and one or two confirm waves."""
+    rng = random.Random(4200 + nlits)
+    lits = rand_lits(rng, nlits, minlen=1 if nlits == 1 else 2, maxlen=8, msk_frac=0.15)
+    blob = vsa.hwlm_build(lits)
+    sizes = [0, 1, 2, 7, 15, 16, 17, 100, 1023, 1024, 1025, 2047, 3000, 9000, 40000]
+    bufs = [rand_data(rng, rng.choice(sizes)) for _ in range(1500)]
+    starts = [rng.choice([0, 0, 0, 1, 5, 17]) if b else 0 for b in bufs]
+    starts = [s if s < max(1, len(b)) else 0 for s, b in zip(starts, bufs)]
+    want = []
+    for b, s in zip(bufs, starts):
+        if s >= len(b):
+            want.append([])
+            continue
+        st, m = oracle.hwlm_exec(blob.ptr, b, start=s, cap=1 << 16)
+        want.append(m)
+    monkeypatch.setenv("VSA_XP", "1")
+    for nconf in ("1", "2"):
+        monkeypatch.setenv("VSA_NCONF", nconf)
+        for mis in (0, 5):
+            assert batch_run(ctx, blob, bufs, starts=starts, misalign=mis) == want, (nconf, mis)
+    # back-to-back runs with literals across the boundaries
+    alpha = b"abcdefghABCDEFGH" if nlits <= 30 else bytes(range(0x61, 0x7b))
+    rb = [bytearray(rand_data(rng, rng.choice([1024, 1500, 2048, 4096, 16384]), alpha))
+          for _ in range(300)]
+    for k in range(len(rb) - 1):
+        s = rng.choice(lits).s
+        if len(s) > 1:
+            cut = rng.randint(1, len(s) - 1)
+            rb[k][len(rb[k]) - cut:] = s[:cut]
+            rb[k + 1][:len(s) - cut] = s[cut:]
+    want = [oracle.hwlm_exec(blob.ptr, bytes(b), cap=1 << 18)[1] for b in rb]
+    assert run_layout_scan(ctx, blob, rb, 3) == want

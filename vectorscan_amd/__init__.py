@@ -226,7 +226,8 @@ class Blob:
         _check(lib.vsa_hwlm_set_accel(self.ptr, a0, a1, accel1_groups))
 
     def __del__(self):
-        if getattr(self, "ptr", None) and getattr(self, "owned", True):
+        # lib is None once the interpreter is tearing the module down
+        if getattr(self, "ptr", None) and getattr(self, "owned", True) and lib is not None:
             lib.vsa_blob_free(self.ptr)
         self.ptr = None
 

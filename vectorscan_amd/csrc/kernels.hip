@@ -257,6 +257,7 @@ struct LitShared {
     u32 *head;       /* this ring's published head (written by this wave) */
     u32 lg;          /* log2 ring entries (>= 2) */
     u32 dbg;         /* VsaLitParams.dbg */
+    const u32 *slots; /* slot bitmaps (LDS; scanner expansion, XP) */
 };
 
 __device__ __forceinline__ u32 lds_ld32(const u32 *p) {
@@ -712,10 +713,62 @@ __device__ __forceinline__ u32 window4(const u32 (&s)[4], int o) {
     return __builtin_amdgcn_alignbyte(W(a + 1), W(a), b);
 }
 
+/* Scanner expansion (XP, large literal sets): the scanning wave expands its
+ * candidate bits itself -- each round every lane takes its lowest remaining
+ * (end, bucket) bit, cuts the 8-byte confirm key from the bytes it holds,
+ * and tests the bucket's LDS slot bitmap (litIndex[hash] == 0 rejects,
+ * fdr_confirm_runtime.h:43-60) -- and pushes only the survivors, as
+ * confirm-queue entries (QEnt), to its ring.  With thousands of literals per
+ * bucket the first stage passes ~1e-2 candidate bits per byte; one confirm
+ * wave expanding them one bit per lane per round was the bottleneck (20k
+ * literals: 97 M bits, ~20 of 64 lanes busy per round), where 14 scanning
+ * waves share the expansion and the confirm wave only confirms.
+ * c = candidate bits of ends 0..15 (byte i of c[w] = end 4 w + i, bit =
+ * bucket); meta = p0 | blk << ENT_BLK_SHIFT; W0..W2 = bytes p0 - 8 .. p0 + 15. */
+__device__ __forceinline__ void xp_push(const VsaLitParams &P, const ConfLds &cl,
+                                        const LitShared &L, IterState &st, u32 (&c)[4],
+                                        u64 meta, u32 pv2, u32 pv3, const u32 (&d)[5]) {
+    const u64 W0 = ((u64)pv3 << 32) | pv2, W1 = ((u64)d[1] << 32) | d[0],
+              W2 = ((u64)d[3] << 32) | d[2];
+    const u64 p0 = meta & ENT_P0_MASK;
+    const u64 blk4 = (meta >> ENT_BLK_SHIFT) << 4;
+    for (;;) {
+        u32 word = 0, bits = c[0];
+#pragma unroll
+        for (int k = 1; k < 4; k++) {
+            const bool take = bits == 0;
+            bits = take ? c[k] : bits;
+            word = take ? (u32)k : word;
+        }
+        const bool have = bits != 0;
+        if (!__any(have)) break;
+        const u32 bit = __ffs(bits) - 1;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (have && word == (u32)k) c[k] &= c[k] - 1;
+        const u32 jj = 4 * word + (bit >> 3), bb = bit & 7;
+        /* key = bytes [jj - 7, jj] = byte offset jj + 1 .. jj + 8 of W0:W1:W2 */
+        const u32 o = jj + 1;
+        u64 key;
+        if (o < 8) key = (W0 >> (8 * o)) | (W1 << (64 - 8 * o));
+        else if (o == 8) key = W1;
+        else if (o < 16) key = (W1 >> (8 * (o - 8))) | (W2 << (64 - 8 * (o - 8)));
+        else key = W2;
+        const PfRec pf = cl.pf[bb];
+        const bool chk = have && pf.slot_off != 0xffffffffu;
+        const u32 h = (u32)(((key & pf.andmsk) * P.pf_mult) >> pf.shift);
+        const u32 sw = chk ? lds_ld32(&L.slots[pf.slot_off + (h >> 5)]) : ~0u;
+        const bool push = have && ((sw >> (h & 31)) & 1u);
+        const u64 qm = ((p0 + jj) << 24) | blk4 | bb;
+        const u32 w[4] = {(u32)qm, (u32)(qm >> 32), (u32)key, (u32)(key >> 32)};
+        ring_push<1>(L, st, push, w);
+    }
+}
+
 /* One 1 KiB iteration at aoff `ib`: lane l owns bytes [ib + 16 l, +16).
  * d = the lane's 16 bytes, nxt0 = first byte of the following chunk (for
  * lane 63's last 2-byte key). */
-template <int MODE, bool LDS_TABLE, bool EDGE>
+template <int MODE, bool LDS_TABLE, bool EDGE, bool XP>
 __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfLds &cl,
                                               const LitShared &L, const SegCtx &S,
                                               u32 mis, int64_t ib, uint4 chunk,
@@ -922,6 +975,10 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
      * boundary is moved on by the confirm, confirm_multi) */
     const u32 lblk = S.blk + (p0 >= S.run_nxt ? 1u : 0u);
     const u64 meta = (u64)p0 | ((u64)lblk << ENT_BLK_SHIFT);
+    if constexpr (XP) {
+        xp_push(P, cl, L, out, c, meta, pv2, pv3, d);
+        return out;
+    }
     u32 w[4 * T::EW];
 #pragma unroll
     for (int i = 0; i < 4 * T::EW; i++) w[i] = 0;
@@ -1016,7 +1073,7 @@ __device__ __forceinline__ IterState nood_iter(const VsaLitParams &P, const LitS
     return out;
 }
 
-template <int MODE, bool LDS_TABLE, bool EDGE>
+template <int MODE, bool LDS_TABLE, bool EDGE, bool XP>
 __device__ __forceinline__ IterState scan_iter(const VsaLitParams &P, const ConfLds &cl,
                                                const LitShared &L, const SegCtx &S,
                                                u32 mis, int64_t ib, uint4 chunk,
@@ -1024,8 +1081,8 @@ __device__ __forceinline__ IterState scan_iter(const VsaLitParams &P, const Conf
     if constexpr (MODE == VSA_MODE_NOOD) {
         return nood_iter<EDGE>(P, L, S, ib, chunk, in);
     } else {
-        return lit_iter<MODE, LDS_TABLE, EDGE>(P, cl, L, S, mis, ib, chunk, nxt0, in,
-                                               bucket_mask);
+        return lit_iter<MODE, LDS_TABLE, EDGE, XP>(P, cl, L, S, mis, ib, chunk, nxt0, in,
+                                                   bucket_mask);
     }
 }
 
@@ -1087,14 +1144,14 @@ __device__ __forceinline__ uint4 load_wave_kib(const u8 *base, u32 off) {
 /* confirm queue entries of a confirm wave confirming CU per lane per batch:
  * >= CU * 64 + EXP_U * 64 - 1 (a round adds <= EXP_U * 64), a power of two */
 #define PQ_ENTRIES(CU) ((CU) == 4 ? 512 : 256)
-template <int MODE, int CONF_U>
+template <int MODE, int CONF_U, bool XP>
 __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLds &cl,
                                              const uint4 *rings, u32 lg, u32 *tails,
                                              const u32 *heads, const u32 *q_done, u32 mis,
                                              const u32 *slots, QEnt *pq, u32 cw, u32 nc,
                                              u64 *pcl) {
     typedef LitTraits<MODE> T;
-    constexpr int EW = T::EW;
+    constexpr int EW = XP ? 1 : T::EW; /* ring entry: chunk or QEnt (XP) */
     constexpr int CW = T::CW;
     constexpr u32 PQ_CAP = PQ_ENTRIES(CONF_U);
     static_assert(PQ_CAP >= CONF_U * 64 + EXP_U * 64 - 1, "confirm queue too small");
@@ -1191,6 +1248,25 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
             continue;
         }
         if (P.dbg & 128) continue; /* experiment: drop gathered entries */
+        if constexpr (XP) {
+            /* QEnt entries (scanner expansion): queue them and confirm */
+            const u64 pm = __ballot(valid);
+            if (valid) {
+                const u32 r = __builtin_amdgcn_mbcnt_hi((u32)(pm >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((u32)pm, 0));
+                QEnt *q = &pq[(pq_head + r) & (PQ_CAP - 1)];
+                q->meta = ((u64)e[1] << 32) | e[0];
+                q->key = ((u64)e[3] << 32) | e[2];
+            }
+            pq_head += filled;
+            /* < CONF_U * 64 queued before, <= 64 added */
+            if (pq_head - pq_tail >= (u32)WAVE * CONF_U) {
+                if (filled >= 16 && !(P.dbg & 1024)) __builtin_amdgcn_s_setprio(2);
+                else __builtin_amdgcn_s_setprio(0);
+                confirm_batch(WAVE * CONF_U);
+            }
+            continue;
+        }
         /* a backlog (many entries per gather): issue ahead of the scanners
          * on this SIMD (the youngest wave otherwise loses VALU arbitration
          * to all of them), as large literal sets need; a light load runs at
@@ -1340,10 +1416,12 @@ __device__ __forceinline__ void stage_lds(TV *dst, u32 n, u32 tid, F &&src) {
     }
 }
 
-template <int MODE, bool LDS_TABLE>
+template <int MODE, bool LDS_TABLE, bool XP>
 __global__ void __launch_bounds__(LIT_THREADS)
 vsa_lit_scan(VsaLitParams P) {
     typedef LitTraits<MODE> T;
+    /* uint4 words per ring entry: a chunk entry, or a QEnt (XP) */
+    constexpr int REW = XP ? 1 : T::EW;
     typedef typename T::S_t S_t;
     extern __shared__ __align__(16) u8 smem[];
     __shared__ ConfLds cl;
@@ -1383,7 +1461,7 @@ vsa_lit_scan(VsaLitParams P) {
     const u32 NC = P.nconf;
     const u32 NS = LIT_WAVES - NC;
     uint4 *rings = (uint4 *)(smem + ((tab_bytes + 15) & ~15u));
-    u32 *slots = (u32 *)(rings + (size_t)NS * P.qcap * T::EW);
+    u32 *slots = (u32 *)(rings + (size_t)NS * P.qcap * REW);
     QEnt *pqx = (QEnt *)(slots + ((P.slot_words + 3) & ~3u));
     stage_lds<4>(slots, P.slot_words, tid, [&](u32 i) { return P.slotmap[i]; });
     if (tid < 16) {
@@ -1421,10 +1499,10 @@ vsa_lit_scan(VsaLitParams P) {
         const u32 cw = wave - NS;
 #ifndef VSA_EXP_NO_CONFIRM /* experiment: VGPR use of the scanning path alone */
         if (NC == 1)
-            confirm_wave<MODE, 4>(P, cl, rings, 31 - __clz(P.qcap), q_tails, q_heads, &q_done,
+            confirm_wave<MODE, 4, XP>(P, cl, rings, 31 - __clz(P.qcap), q_tails, q_heads, &q_done,
                                   mis, slots, pqx, 0, 1, prof_lds);
         else
-            confirm_wave<MODE, 2>(P, cl, rings, 31 - __clz(P.qcap), q_tails, q_heads, &q_done,
+            confirm_wave<MODE, 2, XP>(P, cl, rings, 31 - __clz(P.qcap), q_tails, q_heads, &q_done,
                                   mis, slots, pqx + (size_t)cw * PQ_ENTRIES(2), cw, NC,
                                   prof_lds + 8 * cw);
 #endif
@@ -1451,7 +1529,8 @@ vsa_lit_scan(VsaLitParams P) {
     L.kf = P.dmask == 0x1fffu ? 0x003f003fu : 0x007f007fu;
     L.kshift2 = P.dmask == 0x1fffu ? 0x00020002u : 0x00010001u;
     L.tsel = TEDDY_TAB_LDS | ((lane & 31) << 3);
-    L.ring = rings + (size_t)wave * P.qcap * T::EW;
+    L.ring = rings + (size_t)wave * P.qcap * REW;
+    L.slots = slots;
     L.tail = &q_tails[wave];
     L.head = &q_heads[wave];
     L.lg = 31 - __clz(P.qcap);
@@ -1674,7 +1753,7 @@ vsa_lit_scan(VsaLitParams P) {
                 cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
                 nxt0 = load_byte_masked(A, ib + 1024, S.vlo, S.bhi);
             }
-            is = scan_iter<MODE, LDS_TABLE, true>(P, cl, L, S, mis, ib, cur, nxt0, is,
+            is = scan_iter<MODE, LDS_TABLE, true, XP>(P, cl, L, S, mis, ib, cur, nxt0, is,
                                                  bucket_mask);
             run_adv(ib);
         }
@@ -1708,7 +1787,7 @@ vsa_lit_scan(VsaLitParams P) {
                     const int64_t ib = fb + 1024 * (int64_t)it;
                     const u32 nb = readlane_u32(ring[(k + 1) % LIT_DEPTH].x, 0);
                     const u32 nxt0 = (it + 1 < nf) ? nb : after;
-                    is = scan_iter<MODE, LDS_TABLE, false>(P, cl, L, S, mis, ib, ring[k], nxt0,
+                    is = scan_iter<MODE, LDS_TABLE, false, XP>(P, cl, L, S, mis, ib, ring[k], nxt0,
                                                           is, bucket_mask);
                     run_adv(ib);
                     const u32 itn = (it + LIT_DEPTH < nf) ? it + LIT_DEPTH : it;
@@ -1723,7 +1802,7 @@ vsa_lit_scan(VsaLitParams P) {
                     const int64_t ib = fb + 1024 * (int64_t)it;
                     const u32 nb = readlane_u32(ring[(k + 1) % LIT_DEPTH].x, 0);
                     const u32 nxt0 = (it + 1 < nf) ? nb : after;
-                    is = scan_iter<MODE, LDS_TABLE, false>(P, cl, L, S, mis, ib, ring[k], nxt0,
+                    is = scan_iter<MODE, LDS_TABLE, false, XP>(P, cl, L, S, mis, ib, ring[k], nxt0,
                                                           is, bucket_mask);
                     run_adv(ib);
                 }
@@ -1743,7 +1822,7 @@ vsa_lit_scan(VsaLitParams P) {
                 cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
                 nxt0 = load_byte_masked(A, ib + 1024, S.vlo, S.bhi);
             }
-            is = scan_iter<MODE, LDS_TABLE, true>(P, cl, L, S, mis, ib, cur, nxt0, is,
+            is = scan_iter<MODE, LDS_TABLE, true, XP>(P, cl, L, S, mis, ib, cur, nxt0, is,
                                                  bucket_mask);
             run_adv(ib);
         }
@@ -1784,11 +1863,12 @@ vsa_lit_scan(VsaLitParams P) {
         atomicAdd(&P.counters[2], (unsigned long long)ncand_total);
 }
 
-template __global__ void vsa_lit_scan<VSA_MODE_FDR, true>(VsaLitParams);
-template __global__ void vsa_lit_scan<VSA_MODE_FDR, false>(VsaLitParams);
-template __global__ void vsa_lit_scan<VSA_MODE_TEDDY, true>(VsaLitParams);
-template __global__ void vsa_lit_scan<VSA_MODE_FAT, true>(VsaLitParams);
-template __global__ void vsa_lit_scan<VSA_MODE_NOOD, false>(VsaLitParams);
+template __global__ void vsa_lit_scan<VSA_MODE_FDR, true, false>(VsaLitParams);
+template __global__ void vsa_lit_scan<VSA_MODE_FDR, true, true>(VsaLitParams);
+template __global__ void vsa_lit_scan<VSA_MODE_FDR, false, false>(VsaLitParams);
+template __global__ void vsa_lit_scan<VSA_MODE_TEDDY, true, false>(VsaLitParams);
+template __global__ void vsa_lit_scan<VSA_MODE_FAT, true, false>(VsaLitParams);
+template __global__ void vsa_lit_scan<VSA_MODE_NOOD, false, false>(VsaLitParams);
 
 /* ====================================================== binned sort === */
 

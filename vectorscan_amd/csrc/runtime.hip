@@ -40,7 +40,7 @@
 #include "kernels.h"
 #include "vsa_internal.h"
 
-template <int MODE, bool LDS_TABLE>
+template <int MODE, bool LDS_TABLE, bool XP>
 __global__ void vsa_lit_scan(VsaLitParams P);
 __global__ void vsa_class_scan(VsaClassParams P);
 __global__ void vsa_bin_hist(const uint64_t *keys, const uint64_t *ctr, uint64_t cap,
@@ -178,6 +178,13 @@ struct vsa_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_done = nullptr; /* polled by wait_stream */
     hipEvent_t ev_rec = nullptr;  /* records_fetch_async's copies done */
+    /* side-stream sort (side_sort): the binned sort of this context's scan
+     * runs on its own stream, so the next scan queued on a shared stream
+     * overlaps it; ev_sorted = its last launch, joined (sort_join) before
+     * this context's next use of the scan stream */
+    hipStream_t sort_stream = nullptr;
+    hipEvent_t ev_sorted = nullptr;
+    bool sort_join = false;
     double last_kernel_ms = 0.0;
     uint32_t bin_skip = 0;   /* launches left without the binned sort */
     bool bins_clean = false; /* the bin counts are zero (no memset needed) */
@@ -263,9 +270,11 @@ struct vsa_db {
 static uint32_t nconf_for_rate(double rate) {
     /* measured (4 GiB, FDR): 5k literals (5e-5) best at 1; 10k (2.5e-4)
      * equal; 20k (5.7e-3) 9.4 -> 5.2 ms at 2; 50k (0.26) 124 -> 68 ms at 2.
-     * 3-4 waves leave too little LDS for rings of useful size beside a
-     * domain-14 table */
-    return rate > 1e-3 ? 2u : 1u;
+     * With scanner expansion (use_xp, on from 2 waves; 16-B ring entries):
+     * 20k 2.47 / 2.32 / 2.70 ms at 1 / 2 / 3 waves, 50k 62.9 / 34.1 / 30.6
+     * ms (profiles/r03_xp.jsonl; 4 fits no better than 3 beside a
+     * domain-14 table) */
+    return rate > 0.05 ? 3u : rate > 1e-3 ? 2u : 1u;
 }
 
 /* VECTORSIZE of the reference build emulated where results depend on it:
@@ -444,9 +453,9 @@ int bits_for(uint64_t v) {
     return b;
 }
 
-template <int MODE, bool LDS>
+template <int MODE, bool LDS, bool XP = false>
 int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds) {
-    auto fn = vsa_lit_scan<MODE, LDS>;
+    auto fn = vsa_lit_scan<MODE, LDS, XP>;
     VSA_CHECK(hipFuncSetAttribute((const void *)fn,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     uint64_t want = (P.nsegs + LIT_WAVES - 1) / LIT_WAVES;
@@ -485,6 +494,16 @@ uint32_t launch_nconf(const vsa_db *db, size_t tab, size_t ent, size_t budget) {
     return nc;
 }
 
+/* Scanner expansion (kernels.hip xp_push) for large literal sets: the
+ * scanning waves expand candidate bits and apply the slot-bitmap prefilter,
+ * the confirm waves only confirm.  On when the db's measured candidate rate
+ * asked for two confirm waves (> 1e-3 per byte, nconf_for_rate);
+ * VSA_XP=0 / 1 forces it off / on. */
+bool use_xp(const vsa_db *db) {
+    if (const char *e = getenv("VSA_XP")) return atoi(e) != 0;
+    return db->nconf.load(std::memory_order_relaxed) >= 2;
+}
+
 /* the binned sort (kernels.hip) replaces the library sort unless the
  * caller wants the records unsorted or VSA_LIB_SORT is set */
 bool use_bins(const vsa_ctx *c) {
@@ -506,36 +525,36 @@ uint32_t bin_shift_for(int end_bits) {
  * 342 us against ~30 us for all five (profiles/r03_sort_fused_trace.csv):
  * every workgroup's agent-scope acq_rel ticket on one address serializes
  * (~85-100 ns each over 1,024 / 4,096 workgroups). */
-int queue_bin_sort(vsa_ctx *c) {
+int queue_bin_sort(vsa_ctx *c, hipStream_t st) {
     Workspace &w = c->ws;
     uint32_t *counts = w.d_bins, *cursor = w.d_bins + VSA_SORT_BINS;
     uint32_t *done = w.d_bins + 2 * VSA_SORT_BINS;
     const uint32_t shift = bin_shift_for(c->launch.end_bits);
     static const bool split = getenv("VSA_SORT_FUSED") == nullptr;
     if (split) {
-        hipLaunchKernelGGL(vsa_bin_hist, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, c->stream,
+        hipLaunchKernelGGL(vsa_bin_hist, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, st,
                            w.d_keys[0], (const uint64_t *)w.d_counters, (uint64_t)w.out_cap,
                            shift, counts);
-        hipLaunchKernelGGL(vsa_bin_scan, dim3(1), dim3(1024), 0, c->stream, counts, cursor,
+        hipLaunchKernelGGL(vsa_bin_scan, dim3(1), dim3(1024), 0, st, counts, cursor,
                            (uint64_t *)w.d_counters);
     } else {
         hipLaunchKernelGGL(vsa_bin_hist_scan, dim3((uint32_t)c->num_cus * 4), dim3(256), 0,
-                           c->stream, w.d_keys[0], (uint64_t *)w.d_counters,
+                           st, w.d_keys[0], (uint64_t *)w.d_counters,
                            (uint64_t)w.out_cap, shift, counts, cursor, done);
     }
-    hipLaunchKernelGGL(vsa_bin_scatter, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, c->stream,
+    hipLaunchKernelGGL(vsa_bin_scatter, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, st,
                        w.d_keys[0], w.d_ids[0], (const uint64_t *)w.d_counters,
                        (uint64_t)w.out_cap, shift, cursor, w.d_keys[1], w.d_ids[1]);
     if (split) {
-        hipLaunchKernelGGL(vsa_bin_sort, dim3(VSA_SORT_BINS / 4), dim3(256), 0, c->stream,
+        hipLaunchKernelGGL(vsa_bin_sort, dim3(VSA_SORT_BINS / 4), dim3(256), 0, st,
                            (const uint64_t *)w.d_counters, (uint64_t)w.out_cap, counts, cursor,
                            w.d_keys[1], w.d_ids[1]);
-        hipLaunchKernelGGL(vsa_publish, dim3(1), dim3(256), 0, c->stream, c->ws.d_counters,
+        hipLaunchKernelGGL(vsa_publish, dim3(1), dim3(256), 0, st, c->ws.d_counters,
                            c->ws.d_pub, (unsigned long long)++c->pub_seq, 144u,
                            (const uint64_t *)nullptr, (const uint32_t *)nullptr, 0u);
     } else {
         hipLaunchKernelGGL(vsa_bin_sort_publish, dim3(VSA_SORT_BINS / 4), dim3(256), 0,
-                           c->stream, c->ws.d_counters, (uint64_t)w.out_cap, counts, cursor,
+                           st, c->ws.d_counters, (uint64_t)w.out_cap, counts, cursor,
                            w.d_keys[1], w.d_ids[1], done + 1, c->ws.d_pub,
                            (unsigned long long)++c->pub_seq, 144u);
     }
@@ -550,8 +569,32 @@ static unsigned long long *g_wave_log = nullptr;
 int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
                        uint64_t nsegs, uint32_t seg_bytes);
 
+/* the previous side-stream sort of this context before its next use of the
+ * scan stream (a no-op once the host has seen its publish) */
+int join_sort(vsa_ctx *c) {
+    if (c->sort_join) {
+        VSA_CHECK(hipStreamWaitEvent(c->stream, c->ev_sorted, 0));
+        c->sort_join = false;
+    }
+    return VSA_OK;
+}
+
+/* VSA_SIDE_SORT=1 (A/B knob, off by default): the binned sort goes to a
+ * side stream, so the next pipelined context's scan, queued behind this one
+ * on the shared stream, runs while this one's sort does.  Measured: no gain
+ * (cfg 4 step 1.019-1.075 ms against 1.005-1.014 ms on the same box; 512
+ * MiB rank step 0.187 either way): the sort's workgroups co-run with the
+ * scan's persistent ones and the scan kernel grows by what the step saves
+ * (profiles/r03_sidesort.jsonl). */
+bool side_sort(const vsa_ctx *c) {
+    static const char *e = getenv("VSA_SIDE_SORT");
+    (void)c;
+    return e && atoi(e) != 0;
+}
+
 int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
                 uint64_t nsegs, uint32_t seg_bytes) {
+    if (int r0 = join_sort(c)) return r0;
     if (!c->ctr_clean)
         VSA_CHECK(hipMemsetAsync(c->ws.d_counters, 0, 144 * sizeof(unsigned long long), c->stream));
     c->ctr_clean = false;
@@ -587,8 +630,21 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
     if (!c->launch.dev_sort) return VSA_OK;
     /* the sort zeroes every bin count; the publish hands the counters to
      * the host and zeroes them */
-    int r2 = queue_bin_sort(c);
+    hipStream_t st = c->stream;
+    if (side_sort(c)) {
+        if (!c->sort_stream) {
+            VSA_CHECK(hipStreamCreateWithFlags(&c->sort_stream, hipStreamNonBlocking));
+            VSA_CHECK(hipEventCreateWithFlags(&c->ev_sorted, hipEventDisableTiming));
+        }
+        VSA_CHECK(hipStreamWaitEvent(c->sort_stream, c->ev1, 0));
+        st = c->sort_stream;
+    }
+    int r2 = queue_bin_sort(c, st);
     if (r2 != VSA_OK) return r2;
+    if (st != c->stream) {
+        VSA_CHECK(hipEventRecord(c->ev_sorted, st));
+        c->sort_join = true;
+    }
     c->bins_clean = true;
     c->launch.published = true;
     c->ctr_clean = true;
@@ -669,9 +725,13 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     if (db->mode == VSA_MODE_FDR) {
         size_t tb = (size_t)db->table_entries * 8;
         if (tb <= 128 * 1024) {
-            P.nconf = launch_nconf(db, tb, 48, LDS_BUDGET);
-            size_t lds = plan_lds(tb, db->slot_words, 48, &P.qcap, LDS_BUDGET, P.nconf);
-            if (lds <= LDS_BUDGET) return launch_lit<VSA_MODE_FDR, true>(c, P, lds);
+            const bool xp = use_xp(db);
+            const size_t ent = xp ? 16 : 48; /* QEnt or chunk entries */
+            P.nconf = launch_nconf(db, tb, ent, LDS_BUDGET);
+            size_t lds = plan_lds(tb, db->slot_words, ent, &P.qcap, LDS_BUDGET, P.nconf);
+            if (lds <= LDS_BUDGET)
+                return xp ? launch_lit<VSA_MODE_FDR, true, true>(c, P, lds)
+                          : launch_lit<VSA_MODE_FDR, true>(c, P, lds);
         }
         P.nconf = launch_nconf(db, 0, 48, LDS_BUDGET);
         size_t lds = plan_lds(0, db->slot_words, 48, &P.qcap, LDS_BUDGET, P.nconf);
@@ -726,7 +786,7 @@ hipError_t wait_published(vsa_ctx *c, uint64_t seq) {
         if ((i & 15) == 15) {
             const auto dt = std::chrono::steady_clock::now() - t0;
             if (dt > std::chrono::milliseconds(50)) {
-                hipError_t e = hipStreamSynchronize(c->stream);
+                hipError_t e = hipStreamSynchronize(c->sort_join ? c->sort_stream : c->stream);
                 if (e != hipSuccess) return e;
                 if (h[0] != seq) return hipErrorUnknown;
                 break;
@@ -743,6 +803,7 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     if (c->launch.published) {
         VSA_CHECK(wait_published(c, c->pub_seq));
         for (int i = 0; i < 16; i++) w.h_counters[i] = w.h_pub[1 + i];
+        if (int r0 = join_sort(c)) return r0; /* later work on the scan stream follows the sort */
     } else {
         VSA_CHECK(hipMemcpyAsync(w.h_counters, w.d_counters, 16 * sizeof(unsigned long long),
                                  hipMemcpyDeviceToHost, c->stream));
@@ -1491,6 +1552,7 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (!c) return VSA_E_INVALID;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->sort_stream) (void)hipStreamSynchronize(c->sort_stream);
     /* plans outliving the context keep only their own device tables */
     for (vsa_plan *p : c->plans) p->ctx = nullptr;
     Workspace &w = c->ws;
@@ -1511,6 +1573,8 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->ev_rec) (void)hipEventDestroy(c->ev_rec);
+    if (c->ev_sorted) (void)hipEventDestroy(c->ev_sorted);
+    if (c->sort_stream) (void)hipStreamDestroy(c->sort_stream);
     if (t_ctx == c) t_ctx = nullptr;
     delete c; /* drops its hold on the stream */
     return VSA_OK;
@@ -1899,6 +1963,7 @@ int vsa_scan_pack(vsa_ctx_t *c, void *d_dst, uint64_t cap) {
     if (c->pending && c->launch.published && c->launch.dev_sort) {
         /* the async binned scan's sorted records (buffer 1) and the counters
          * vsa_publish keeps on the device: queued behind it, no wait */
+        if (int r0 = join_sort(c)) return r0;
         hipLaunchKernelGGL(vsa_pack, dim3(grid), dim3(256), 0, c->stream,
                            (const unsigned long long *)c->ws.d_counters + 144,
                            (uint64_t)c->ws.out_cap, (const uint64_t *)c->ws.d_keys[1],
