@@ -123,6 +123,11 @@ struct VsaLitParams {
     uint64_t *out_keys;
     uint32_t *out_ids;
     uint64_t out_cap;
+    uint32_t *bin_counts;        /* binned sort: records per bin of end >>
+                                    bin_shift, counted as they are emitted
+                                    (nullptr: no binned sort, or the separate
+                                    histogram launch) */
+    uint32_t bin_shift;
     unsigned long long *wave_log; /* diagnostic (dbg bit12): 8 u64 per scanning
                                      wave: start, end (100 MHz), segments,
                                      KiB iterations, workgroup, wave, XCC, HW_ID */

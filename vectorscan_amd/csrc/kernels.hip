@@ -363,6 +363,11 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
                                        ((u64)b[i] << VSA_KEY_BUCKET_SHIFT) | lidx;
                     P.out_ids[slot] = w1[i].z;
                 }
+                /* the binned sort's histogram (an overflowed launch's counts
+                 * are zeroed by its sort launch and never used) */
+                if (mt[i] && P.bin_counts)
+                    __hip_atomic_fetch_add(&P.bin_counts[(u32)((base[i] + (u64)e[i]) >> P.bin_shift)],
+                                           1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
 #pragma unroll
@@ -1295,6 +1300,9 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                         P.out_keys[slot] = (p0 + j - mis) << VSA_KEY_END_SHIFT;
                         P.out_ids[slot] = P.nood_id;
                     }
+                    if (P.bin_counts)
+                        __hip_atomic_fetch_add(&P.bin_counts[(u32)((p0 + j - mis) >> P.bin_shift)],
+                                               1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             continue;
@@ -1872,13 +1880,15 @@ template __global__ void vsa_lit_scan<VSA_MODE_NOOD, false, false>(VsaLitParams)
 
 /* ====================================================== binned sort === */
 
-/* Match records sorted in four short launches instead of a library sort's
- * dozen (runtime.hip finish_scan): bins = VSA_SORT_BINS ranges of end
- * positions; (1) a histogram of the records' bins (outside the scan kernel,
- * whose confirm loop then carries no per-record atomic), (2) exclusive scan
- * of the counts, (3) scatter into bin order, (4) one wave sorts each bin
- * (<= 64 records: a register bitonic sort on the full key).  Keys are unique (end,
- * bucket, LitInfo), so the result equals the full sort. */
+/* Match records sorted in three short launches instead of a library sort's
+ * dozen (runtime.hip queue_bin_sort): bins = VSA_SORT_BINS ranges of end
+ * positions; (1) the scan kernel counts each record into its bin as it
+ * emits it (one non-returning atomic per record: at cfg 4 that is cheaper
+ * than the separate histogram launch vsa_bin_hist, kept for A/B), (2)
+ * exclusive scan of the counts, (3) scatter into bin order, (4) one wave
+ * sorts each bin (<= 64 records: a register bitonic sort on the full key).
+ * Keys are unique (end, bucket, LitInfo), so the result equals the full
+ * sort. */
 __global__ void __launch_bounds__(256) vsa_bin_hist(const uint64_t *keys, const uint64_t *ctr,
                                                     uint64_t cap, uint32_t bin_shift,
                                                     uint32_t *counts) {
@@ -1890,92 +1900,48 @@ __global__ void __launch_bounds__(256) vsa_bin_hist(const uint64_t *keys, const 
                                1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-/* the last of a grid's workgroups to get here (the others' global writes
- * are visible to it afterwards); it resets `done` for the next launch */
-__device__ __forceinline__ bool last_workgroup(uint32_t *done) {
-    __shared__ bool last;
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-               gridDim.x - 1;
-    __syncthreads();
-    if (last) {
-        __threadfence();
-        if (threadIdx.x == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return last;
-}
-
-/* (1) + (2) in one launch: the histogram, then the last workgroup scans the
- * counts (256 threads x 64 bins) */
-__global__ void __launch_bounds__(256) vsa_bin_hist_scan(const uint64_t *keys, uint64_t *ctr,
-                                                         uint64_t cap, uint32_t bin_shift,
-                                                         uint32_t *counts, uint32_t *cursor,
-                                                         uint32_t *done) {
-    const uint64_t n0 = ctr[0];
-    const uint64_t n = n0 > cap ? 0 : n0; /* an overflowed launch runs again */
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * 256)
-        __hip_atomic_fetch_add(&counts[(uint32_t)((keys[i] >> VSA_KEY_END_SHIFT) >> bin_shift)],
-                               1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!last_workgroup(done)) return;
-    __shared__ uint32_t part[256];
-    const uint32_t t = threadIdx.x;
-    constexpr uint32_t PER = VSA_SORT_BINS / 256;
-    uint32_t sum = 0, big = 0;
-    for (uint32_t k = 0; k < PER; k++) {
-        const uint32_t v = __hip_atomic_load(&counts[t * PER + k], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-        sum += v;
-        big |= v > VSA_SORT_BIN_MAX;
-    }
-    if (big) ctr[VSA_CTR_BIN_OVERFLOW] = 1;
-    part[t] = sum;
-    __syncthreads();
-    for (uint32_t d = 1; d < 256; d <<= 1) {
-        const uint32_t x = t >= d ? part[t - d] : 0u;
-        __syncthreads();
-        part[t] += x;
-        __syncthreads();
-    }
-    uint32_t run = part[t] - sum;
-    for (uint32_t k = 0; k < PER; k++) {
-        const uint32_t v = __hip_atomic_load(&counts[t * PER + k], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-        cursor[t * PER + k] = run;
-        run += v;
-    }
-}
-
 __global__ void __launch_bounds__(1024) vsa_bin_scan(const uint32_t *counts, uint32_t *cursor,
                                                     uint64_t *ctr) {
-    __shared__ uint32_t part[1024];
-    const uint32_t t = threadIdx.x;
+    /* thread t owns bins [16 t, 16 t + 16) (four dwordx4 loads); a wave scan
+     * of the threads' sums, then one of the 16 waves' totals: two barriers */
+    __shared__ uint32_t wsum[16];
+    const uint32_t t = threadIdx.x, wv = t / WAVE;
     constexpr uint32_t PER = VSA_SORT_BINS / 1024;
-    uint32_t v[PER], sum = 0, big = 0;
+    static_assert(PER == 16, "four uint4 per thread");
+    uint4 v[4];
+    uint32_t sum = 0, big = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < PER; k++) {
-        v[k] = counts[t * PER + k];
-        sum += v[k];
-        big |= v[k] > VSA_SORT_BIN_MAX;
+    for (int k = 0; k < 4; k++) {
+        v[k] = ((const uint4 *)counts)[t * 4 + k];
+        sum += v[k].x + v[k].y + v[k].z + v[k].w;
+        big |= (v[k].x > VSA_SORT_BIN_MAX) | (v[k].y > VSA_SORT_BIN_MAX) |
+               (v[k].z > VSA_SORT_BIN_MAX) | (v[k].w > VSA_SORT_BIN_MAX);
     }
     /* a crowded bin: the scatter and sort stand down (bin_records) and the
      * host sorts with the library */
     if (big) ctr[VSA_CTR_BIN_OVERFLOW] = 1;
-    part[t] = sum;
+    u32 wtot;
+    const u32 ex = wave_excl_scan(sum, &wtot);
+    if (lane_id() == 0) wsum[wv] = wtot;
     __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
-        const uint32_t x = t >= d ? part[t - d] : 0u;
-        __syncthreads();
-        part[t] += x;
-        __syncthreads();
+    u32 base = 0;
+    if (wv == 0) {
+        u32 tot;
+        const u32 x = lane_id() < 16 ? wsum[lane_id()] : 0u;
+        const u32 e = wave_excl_scan(x, &tot);
+        if (lane_id() < 16) wsum[lane_id()] = e;
     }
-    uint32_t run = part[t] - sum; /* exclusive prefix of this thread's bins */
+    __syncthreads();
+    base = wsum[wv];
+    uint32_t run = base + ex; /* exclusive prefix of this thread's bins */
 #pragma unroll
-    for (uint32_t k = 0; k < PER; k++) {
-        cursor[t * PER + k] = run;
-        run += v[k];
+    for (int k = 0; k < 4; k++) {
+        uint4 o;
+        o.x = run; run += v[k].x;
+        o.y = run; run += v[k].y;
+        o.z = run; run += v[k].z;
+        o.w = run; run += v[k].w;
+        ((uint4 *)cursor)[t * 4 + k] = o;
     }
 }
 
@@ -2096,20 +2062,6 @@ __global__ void __launch_bounds__(256) vsa_publish(unsigned long long *ctr,
                                                    const uint64_t *keys, const uint32_t *ids,
                                                    uint32_t kmax) {
     publish_body(ctr, h, seq, nzero, keys, ids, kmax);
-}
-
-/* (4) + the publish in one launch: each wave sorts its bin, then the last
- * workgroup publishes the counters (every sort wave has read them by then) */
-__global__ void __launch_bounds__(256) vsa_bin_sort_publish(unsigned long long *ctr, uint64_t cap,
-                                                            uint32_t *counts,
-                                                            const uint32_t *cursor,
-                                                            uint64_t *keys, uint32_t *ids,
-                                                            uint32_t *done, unsigned long long *h,
-                                                            unsigned long long seq,
-                                                            uint32_t nzero) {
-    bin_sort_wave((const uint64_t *)ctr, cap, counts, cursor, keys, ids);
-    if (!last_workgroup(done)) return;
-    publish_body(ctr, h, seq, nzero, nullptr, nullptr, 0u);
 }
 
 /* A binned scan's sorted records packed for a collective, on the device

@@ -46,13 +46,6 @@ __global__ void vsa_class_scan(VsaClassParams P);
 __global__ void vsa_bin_hist(const uint64_t *keys, const uint64_t *ctr, uint64_t cap,
                              uint32_t bin_shift, uint32_t *counts);
 __global__ void vsa_bin_scan(const uint32_t *counts, uint32_t *cursor, uint64_t *ctr);
-__global__ void vsa_bin_hist_scan(const uint64_t *keys, uint64_t *ctr, uint64_t cap,
-                                  uint32_t bin_shift, uint32_t *counts, uint32_t *cursor,
-                                  uint32_t *done);
-__global__ void vsa_bin_sort_publish(unsigned long long *ctr, uint64_t cap, uint32_t *counts,
-                                     const uint32_t *cursor, uint64_t *keys, uint32_t *ids,
-                                     uint32_t *done, unsigned long long *h, unsigned long long seq,
-                                     uint32_t nzero);
 __global__ void vsa_bin_scatter(const uint64_t *keys, const uint32_t *ids, const uint64_t *ctr,
                                 uint64_t cap, uint32_t bin_shift, uint32_t *cursor,
                                 uint64_t *okeys, uint32_t *oids);
@@ -516,48 +509,43 @@ uint32_t bin_shift_for(int end_bits) {
     return end_bits > (int)VSA_SORT_BIN_BITS ? (uint32_t)end_bits - VSA_SORT_BIN_BITS : 0u;
 }
 
-/* the binned sort behind the scan (kernels.hip): histogram, scan of the
- * counts, scatter, per-bin sorts, publish: five short launches.  They read
- * the record count and the overflow flag from d_counters, so they are
- * queued before the host has seen either (an overflowed launch leaves them
- * idle).  VSA_SORT_FUSED=1 (A/B knob): three launches, histogram + scan and
- * sort + publish fused behind a last-workgroup ticket -- measured 107 us +
- * 342 us against ~30 us for all five (profiles/r03_sort_fused_trace.csv):
- * every workgroup's agent-scope acq_rel ticket on one address serializes
- * (~85-100 ns each over 1,024 / 4,096 workgroups). */
+/* the binned sort behind the scan (kernels.hip): the scan kernel counts
+ * its records into the bins as it emits them (VsaLitParams.bin_counts),
+ * then: scan of the counts, scatter, per-bin sorts, publish -- four short
+ * launches.  They read the record count and the overflow flag from
+ * d_counters, so they are queued before the host has seen either (an
+ * overflowed launch leaves them idle).
+ * VSA_SEP_HIST=1 (A/B knob): the histogram as its own launch over the
+ * records instead (round 2's five launches).
+ * Measured and dropped: histogram + scan and sort + publish fused behind a
+ * last-workgroup ticket (three launches) -- 107 us + 342 us against ~30 us
+ * for all five (profiles/r03_sort_fused_trace.csv): every workgroup's
+ * agent-scope release + acq_rel ticket serializes (~85-100 ns each over
+ * 1,024 / 4,096 workgroups; the XCDs' L2s are written back for it). */
+bool sep_hist() {
+    static const bool v = getenv("VSA_SEP_HIST") != nullptr;
+    return v;
+}
+
 int queue_bin_sort(vsa_ctx *c, hipStream_t st) {
     Workspace &w = c->ws;
     uint32_t *counts = w.d_bins, *cursor = w.d_bins + VSA_SORT_BINS;
-    uint32_t *done = w.d_bins + 2 * VSA_SORT_BINS;
     const uint32_t shift = bin_shift_for(c->launch.end_bits);
-    static const bool split = getenv("VSA_SORT_FUSED") == nullptr;
-    if (split) {
+    if (sep_hist())
         hipLaunchKernelGGL(vsa_bin_hist, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, st,
                            w.d_keys[0], (const uint64_t *)w.d_counters, (uint64_t)w.out_cap,
                            shift, counts);
-        hipLaunchKernelGGL(vsa_bin_scan, dim3(1), dim3(1024), 0, st, counts, cursor,
-                           (uint64_t *)w.d_counters);
-    } else {
-        hipLaunchKernelGGL(vsa_bin_hist_scan, dim3((uint32_t)c->num_cus * 4), dim3(256), 0,
-                           st, w.d_keys[0], (uint64_t *)w.d_counters,
-                           (uint64_t)w.out_cap, shift, counts, cursor, done);
-    }
+    hipLaunchKernelGGL(vsa_bin_scan, dim3(1), dim3(1024), 0, st, counts, cursor,
+                       (uint64_t *)w.d_counters);
     hipLaunchKernelGGL(vsa_bin_scatter, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, st,
                        w.d_keys[0], w.d_ids[0], (const uint64_t *)w.d_counters,
                        (uint64_t)w.out_cap, shift, cursor, w.d_keys[1], w.d_ids[1]);
-    if (split) {
-        hipLaunchKernelGGL(vsa_bin_sort, dim3(VSA_SORT_BINS / 4), dim3(256), 0, st,
-                           (const uint64_t *)w.d_counters, (uint64_t)w.out_cap, counts, cursor,
-                           w.d_keys[1], w.d_ids[1]);
-        hipLaunchKernelGGL(vsa_publish, dim3(1), dim3(256), 0, st, c->ws.d_counters,
-                           c->ws.d_pub, (unsigned long long)++c->pub_seq, 144u,
-                           (const uint64_t *)nullptr, (const uint32_t *)nullptr, 0u);
-    } else {
-        hipLaunchKernelGGL(vsa_bin_sort_publish, dim3(VSA_SORT_BINS / 4), dim3(256), 0,
-                           st, c->ws.d_counters, (uint64_t)w.out_cap, counts, cursor,
-                           w.d_keys[1], w.d_ids[1], done + 1, c->ws.d_pub,
-                           (unsigned long long)++c->pub_seq, 144u);
-    }
+    hipLaunchKernelGGL(vsa_bin_sort, dim3(VSA_SORT_BINS / 4), dim3(256), 0, st,
+                       (const uint64_t *)w.d_counters, (uint64_t)w.out_cap, counts, cursor,
+                       w.d_keys[1], w.d_ids[1]);
+    hipLaunchKernelGGL(vsa_publish, dim3(1), dim3(256), 0, st, c->ws.d_counters,
+                       c->ws.d_pub, (unsigned long long)++c->pub_seq, 144u,
+                       (const uint64_t *)nullptr, (const uint32_t *)nullptr, 0u);
     VSA_CHECK(hipGetLastError());
     return VSA_OK;
 }
@@ -674,6 +662,8 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         P.out_keys = w.d_keys[0];
         P.out_ids = w.d_ids[0];
         P.out_cap = w.out_cap;
+        P.bin_counts = c->launch.bins && !sep_hist() ? w.d_bins : nullptr;
+        P.bin_shift = bin_shift_for(c->launch.end_bits);
         P.counters = w.d_counters;
         P.wave_log = g_wave_log;
         {
@@ -711,6 +701,8 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.out_keys = w.d_keys[0];
     P.out_ids = w.d_ids[0];
     P.out_cap = w.out_cap;
+    P.bin_counts = c->launch.bins && !sep_hist() ? w.d_bins : nullptr;
+    P.bin_shift = bin_shift_for(c->launch.end_bits);
     P.counters = w.d_counters;
     P.wave_log = g_wave_log;
     {
@@ -1535,9 +1527,7 @@ int vsa_ctx_create(int device, vsa_ctx_t **out) {
     VSA_CHECK(hipEventCreate(&c->ev1));
     VSA_CHECK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
     VSA_CHECK(hipMalloc(&c->ws.d_counters, N_COUNTERS * sizeof(unsigned long long)));
-    VSA_CHECK(hipMalloc(&c->ws.d_bins, (2 * VSA_SORT_BINS + 16) * sizeof(uint32_t)));
-    /* the done counters start at 0 and every launch leaves them at 0 */
-    VSA_CHECK(hipMemset(c->ws.d_bins + 2 * VSA_SORT_BINS, 0, 16 * sizeof(uint32_t)));
+    VSA_CHECK(hipMalloc(&c->ws.d_bins, 2 * VSA_SORT_BINS * sizeof(uint32_t)));
     VSA_CHECK(hipHostMalloc((void **)&c->ws.h_counters, N_COUNTERS * sizeof(unsigned long long),
                             hipHostMallocDefault));
     VSA_CHECK(hipHostMalloc((void **)&c->ws.h_pub, PUB_WORDS * sizeof(unsigned long long),
