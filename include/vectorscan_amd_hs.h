@@ -31,6 +31,8 @@ extern "C" {
 #define VSA_HS_NOMEM (-2)
 #define VSA_HS_SCAN_TERMINATED (-3)
 #define VSA_HS_COMPILER_ERROR (-4)
+#define VSA_HS_DB_VERSION_ERROR (-5)
+#define VSA_HS_DB_PLATFORM_ERROR (-6)
 #define VSA_HS_DB_MODE_ERROR (-7)
 #define VSA_HS_SCRATCH_IN_USE (-10)
 #define VSA_HS_UNKNOWN_ERROR (-13)
@@ -166,6 +168,40 @@ static inline uint64_t vsa_hs_seq_digest_step(uint64_t h, unsigned id, unsigned 
     return x ^ (x >> 31);
 }
 int vsa_hs_corpus_free(vsa_hs_corpus_t *corpus);
+
+/* Streams, continued: hs_copy_stream / hs_reset_and_copy_stream
+ * (hs_runtime.h:291 / :324, runtime.c:713-779) and hs_stream_size
+ * (hs_common.h:183). */
+int vsa_hs_copy_stream(vsa_hs_stream_t **to_id, const vsa_hs_stream_t *from_id);
+int vsa_hs_reset_and_copy_stream(vsa_hs_stream_t *to_id, const vsa_hs_stream_t *from_id,
+                                 vsa_hs_scratch_t *scratch, vsa_hs_match_event_handler onEvent,
+                                 void *context);
+int vsa_hs_stream_size(const vsa_hs_database_t *db, size_t *stream_size);
+
+/* Scratch, continued: hs_clone_scratch / hs_scratch_size (hs_runtime.h:576
+ * / :593).  A clone has its own GPU context and database copies. */
+int vsa_hs_clone_scratch(const vsa_hs_scratch_t *src, vsa_hs_scratch_t **dest);
+int vsa_hs_scratch_size(const vsa_hs_scratch_t *scratch, size_t *scratch_size);
+
+/* hs_valid_platform / hs_version (hs_common.h:463 / :446) */
+int vsa_hs_valid_platform(void);
+const char *vsa_hs_version(void);
+
+/* Serialized databases in the reference's envelope (database.c:61-455):
+ * 32 header bytes (magic 0xdbdbdbdb, HS_VERSION_32BIT of 5.4.11, bytecode
+ * length, platform, CRC-32C), the bytecode, zero padding to 104 + length
+ * bytes.  The bytecode opens with the RoseEngine fields the reference reads
+ * without running it (pureLiteral, runtimeImpl = PURE_LITERAL, mode at
+ * byte 12), then this engine's pattern list, which deserializing compiles
+ * again.  A reference-serialized database (a full RoseEngine) is refused
+ * with VSA_HS_DB_PLATFORM_ERROR; hs_serialized_database_info reads either.
+ * `bytes` / `info` are malloc'ed (the reference's default allocator). */
+int vsa_hs_serialize_database(const vsa_hs_database_t *db, char **bytes, size_t *length);
+int vsa_hs_deserialize_database(const char *bytes, size_t length, vsa_hs_database_t **db);
+int vsa_hs_serialized_database_size(const char *bytes, size_t length, size_t *deserialized_size);
+int vsa_hs_database_size(const vsa_hs_database_t *db, size_t *database_size);
+int vsa_hs_serialized_database_info(const char *bytes, size_t length, char **info);
+int vsa_hs_database_info(const vsa_hs_database_t *db, char **info);
 
 /* Introspection for tests: the database's HWLM blob (fragment id = HWLM
  * literal id) and the number of literal fragments. */

@@ -91,6 +91,14 @@ struct vsa_hs_database {
     size_t max_len = 0;
     bool dedupe = false; /* some id belongs to more than one pattern */
     bool simple = false; /* one report per HWLM record (see vsa_hs_scan_corpus) */
+    /* the compile inputs, as given (the serialized form, which
+     * vsa_hs_deserialize_database compiles again) */
+    unsigned mode_full = 0;
+    struct Src {
+        std::string e;
+        unsigned flags, id;
+    };
+    std::vector<Src> src;
 };
 
 struct vsa_hs_scratch {
@@ -402,6 +410,7 @@ int vsa_hs_compile_lit_multi(const char *const *expressions, const unsigned *fla
     vsa_hs_database *out = new (std::nothrow) vsa_hs_database;
     if (!out) return fail("Unable to allocate memory.", -1);
     out->mode = kind;
+    out->mode_full = mode;
     out->serial = g_serial.fetch_add(1);
     std::map<uint32_t, std::pair<bool, unsigned>> ext; /* id -> (single, first index) */
     std::map<uint32_t, uint32_t> ekeys;
@@ -465,6 +474,7 @@ int vsa_hs_compile_lit_multi(const char *const *expressions, const unsigned *fla
             }
         }
         ext_count[id]++;
+        out->src.push_back({std::string(e, lens[i]), f, id});
         Pattern p;
         p.id = id;
         p.som = f & VSA_HS_FLAG_SOM_LEFTMOST;
@@ -1175,6 +1185,326 @@ int vsa_hs_reset_stream(vsa_hs_stream_t *id, unsigned int flags, vsa_hs_scratch_
     }
     init_stream(id, id->db);
     return VSA_HS_SUCCESS;
+}
+
+/* runtime.c:740-779: no EOD matches exist in a pure-literal database, so
+ * the reset reports nothing before the copy */
+int vsa_hs_reset_and_copy_stream(vsa_hs_stream_t *to_id, const vsa_hs_stream_t *from_id,
+                                 vsa_hs_scratch_t *scratch, vsa_hs_match_event_handler onEvent,
+                                 void *context) {
+    (void)context;
+    if (!from_id || from_id->magic != STREAM_MAGIC || !from_id->db) return VSA_HS_INVALID;
+    if (!to_id || to_id->magic != STREAM_MAGIC || to_id->db != from_id->db) return VSA_HS_INVALID;
+    if (to_id == from_id) return VSA_HS_INVALID;
+    if (onEvent) {
+        if (!scratch || scratch->magic != SCRATCH_MAGIC || !device_db(scratch, to_id->db))
+            return VSA_HS_INVALID;
+        if (scratch->in_use.load()) return VSA_HS_SCRATCH_IN_USE;
+    }
+    to_id->offset = from_id->offset;
+    to_id->hist = from_id->hist;
+    to_id->exhausted = from_id->exhausted;
+    to_id->terminated = from_id->terminated;
+    return VSA_HS_SUCCESS;
+}
+
+/* runtime.c:713-738 */
+int vsa_hs_copy_stream(vsa_hs_stream_t **to_id, const vsa_hs_stream_t *from_id) {
+    if (!to_id) return VSA_HS_INVALID;
+    *to_id = nullptr;
+    if (!from_id || from_id->magic != STREAM_MAGIC || !from_id->db) return VSA_HS_INVALID;
+    vsa_hs_stream *s = new (std::nothrow) vsa_hs_stream;
+    if (!s) return VSA_HS_NOMEM;
+    s->db = from_id->db;
+    s->offset = from_id->offset;
+    s->hist = from_id->hist;
+    s->exhausted = from_id->exhausted;
+    s->terminated = from_id->terminated;
+    *to_id = s;
+    return VSA_HS_SUCCESS;
+}
+
+/* hs_stream_size, hs_common.h:183: the bytes of one open stream's state */
+int vsa_hs_stream_size(const vsa_hs_database_t *db, size_t *stream_size) {
+    if (!stream_size || !valid_db(db)) return VSA_HS_INVALID;
+    if (db->mode != VSA_HS_MODE_STREAM) return VSA_HS_DB_MODE_ERROR;
+    *stream_size = sizeof(vsa_hs_stream) + db->max_len + HIST_MIN + db->n_ekeys;
+    return VSA_HS_SUCCESS;
+}
+
+/* scratch.c:373-423 (hs_clone_scratch): a new scratch, with its own GPU
+ * context, serving the same databases */
+int vsa_hs_clone_scratch(const vsa_hs_scratch_t *src, vsa_hs_scratch_t **dest) {
+    if (!dest || !src || src->magic != SCRATCH_MAGIC) return VSA_HS_INVALID;
+    *dest = nullptr;
+    vsa_hs_scratch *s = new (std::nothrow) vsa_hs_scratch;
+    if (!s) return VSA_HS_NOMEM;
+    const char *dev = getenv("VSA_DEVICE"); /* as vsa_hs_alloc_scratch */
+    if (vsa_ctx_create(dev ? atoi(dev) : 0, &s->ctx) != VSA_OK) {
+        delete s;
+        return VSA_HS_NOMEM;
+    }
+    for (const auto &e : src->dbs) {
+        const uint8_t *blob = nullptr;
+        size_t size = 0;
+        vsa_db_t *d = nullptr;
+        if (vsa::dbHostBlob(e.second, &blob, &size) != VSA_OK ||
+            vsa_db_load(s->ctx, blob, size, &d) != VSA_OK) {
+            vsa_hs_free_scratch(s);
+            return VSA_HS_NOMEM;
+        }
+        s->dbs.emplace_back(e.first, d);
+    }
+    *dest = s;
+    return VSA_HS_SUCCESS;
+}
+
+/* hs_scratch_size, hs_runtime.h:593: host bytes of the scratch and of the
+ * database copies it holds (their device copies mirror them) */
+int vsa_hs_scratch_size(const vsa_hs_scratch_t *scratch, size_t *scratch_size) {
+    if (!scratch_size || !scratch || scratch->magic != SCRATCH_MAGIC) return VSA_HS_INVALID;
+    size_t n = sizeof(vsa_hs_scratch);
+    for (const auto &e : scratch->dbs) {
+        const uint8_t *blob = nullptr;
+        size_t size = 0;
+        if (vsa::dbHostBlob(e.second, &blob, &size) == VSA_OK) n += size;
+    }
+    *scratch_size = n;
+    return VSA_HS_SUCCESS;
+}
+
+/* hs_valid_platform, hs_common.h:463: the GPU path needs no host ISA level */
+int vsa_hs_valid_platform(void) { return VSA_HS_SUCCESS; }
+
+/* hs_version, hs_common.h:446 (HS_VERSION_STRING: "major.minor.patch date") */
+const char *vsa_hs_version(void) { return "5.4.11 vectorscan_amd gfx950"; }
+
+/* ------------------------------------------------------ serialization --
+ * The reference's serialized database (database.c:61-110, db_decode_header
+ * :122-170): 32 header bytes -- magic 0xdbdbdbdb, version (HS_VERSION_32BIT
+ * of 5.4.11), bytecode length, platform (u64, unaligned at byte 12), CRC-32C
+ * of the bytecode, two reserved words -- then the bytecode, then zeroes up to
+ * sizeof(struct hs_database) (104) + length bytes in all.
+ *
+ * The bytecode starts with the fields of struct RoseEngine that the
+ * reference reads without running it (rose_internal.h:330-345): pureLiteral
+ * = 1, runtimeImpl = ROSE_RUNTIME_PURE_LITERAL, canExhaust, hasSom, mode at
+ * byte 12 (hs_serialized_database_info reads it there), historyRequired.
+ * The rest is this engine's own: tag "VSAL", a format version, the compile
+ * mode and the patterns as given (id, flags, length, bytes); deserializing
+ * compiles them again (deterministic: the same HWLM blob).  A database
+ * serialized by the reference holds a full RoseEngine instead and is refused
+ * with HS_DB_PLATFORM_ERROR; the envelope, version and CRC checks are the
+ * reference's. */
+} // extern "C"
+namespace {
+constexpr uint32_t HS_DB_MAGIC = 0xdbdbdbdbu;
+constexpr uint32_t HS_DB_VERSION = (5u << 24) | (4u << 16) | (11u << 8);
+constexpr size_t HS_DB_HEADER = 104; /* sizeof(struct hs_database), database.h:103-114 */
+constexpr size_t HS_DB_FIELDS = 32;  /* the header words database.c serializes */
+/* HS_PLATFORM_NOAVX2 | NOAVX512 | NOAVX512VBMI (database.h:55-57): no host
+ * SIMD level is assumed */
+constexpr uint64_t VSA_PLATFORM = (4ull << 13) | (8ull << 13) | (0x10ull << 13);
+constexpr uint32_t VSAL_TAG = 0x4c415356u; /* "VSAL" */
+constexpr uint32_t VSAL_FORMAT = 1;
+constexpr size_t VSAL_OFF = 64; /* our section, after the RoseEngine prefix */
+
+/* CRC-32C as Crc32c_ComputeBuf(0, ...) (crc32.c:528-601: reflected
+ * polynomial 0x82F63B78, no pre- or post-inversion) */
+uint32_t crc32c(const uint8_t *p, size_t n) {
+    static uint32_t T[256];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (uint32_t i = 0; i < 256; i++) {
+            uint32_t c = i;
+            for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+            T[i] = c;
+        }
+    });
+    uint32_t crc = 0;
+    while (n--) crc = T[(crc ^ *p++) & 0xff] ^ (crc >> 8);
+    return crc;
+}
+
+void put32(std::vector<uint8_t> &b, size_t off, uint32_t v) { memcpy(b.data() + off, &v, 4); }
+uint32_t get32(const uint8_t *p) {
+    uint32_t v;
+    memcpy(&v, p, 4);
+    return v;
+}
+
+std::vector<uint8_t> bytecode_of(const vsa_hs_database *db) {
+    size_t n = VSAL_OFF + 16;
+    for (const auto &x : db->src) n += 12 + x.e.size();
+    std::vector<uint8_t> b(n, 0);
+    bool exhaust = !db->pats.empty(), som = false;
+    for (const auto &pt : db->pats) {
+        exhaust &= pt.ekey != NO_EKEY;
+        som |= pt.som;
+    }
+    b[0] = 1;               /* pureLiteral */
+    b[4] = 1;               /* runtimeImpl: ROSE_RUNTIME_PURE_LITERAL */
+    b[6] = exhaust ? 1 : 0; /* canExhaust */
+    b[7] = som ? 1 : 0;     /* hasSom */
+    put32(b, 12, db->mode);
+    put32(b, 16, db->mode == VSA_HS_MODE_BLOCK ? 0u : (uint32_t)db->max_len);
+    put32(b, VSAL_OFF, VSAL_TAG);
+    put32(b, VSAL_OFF + 4, VSAL_FORMAT);
+    put32(b, VSAL_OFF + 8, db->mode_full);
+    put32(b, VSAL_OFF + 12, (uint32_t)db->src.size());
+    size_t o = VSAL_OFF + 16;
+    for (const auto &x : db->src) {
+        put32(b, o, x.id);
+        put32(b, o + 4, x.flags);
+        put32(b, o + 8, (uint32_t)x.e.size());
+        memcpy(b.data() + o + 12, x.e.data(), x.e.size());
+        o += 12 + x.e.size();
+    }
+    return b;
+}
+
+/* db_decode_header (database.c:122-170) + the platform check (:117-120) */
+int decode_header(const char *bytes, size_t length, uint32_t *version, uint64_t *platform,
+                  const uint8_t **code, uint32_t *code_len) {
+    if (!bytes || length < HS_DB_HEADER) return VSA_HS_INVALID;
+    const uint8_t *p = (const uint8_t *)bytes;
+    if (get32(p) != HS_DB_MAGIC) return VSA_HS_INVALID;
+    *version = get32(p + 4);
+    if (*version != HS_DB_VERSION) return VSA_HS_DB_VERSION_ERROR;
+    *code_len = get32(p + 8);
+    if (length != HS_DB_HEADER + *code_len) return VSA_HS_INVALID;
+    memcpy(platform, p + 12, 8);
+    *code = p + HS_DB_FIELDS;
+    return VSA_HS_SUCCESS;
+}
+} // namespace
+extern "C" {
+
+/* hs_serialize_database, hs_common.h:104 (database.c:61-110) */
+int vsa_hs_serialize_database(const vsa_hs_database_t *db, char **bytes, size_t *length) {
+    if (!db || !bytes || !length) return VSA_HS_INVALID;
+    if (!valid_db(db)) return VSA_HS_INVALID;
+    const std::vector<uint8_t> code = bytecode_of(db);
+    const size_t n = HS_DB_HEADER + code.size();
+    char *out = (char *)malloc(n);
+    if (!out) return VSA_HS_NOMEM;
+    memset(out, 0, n);
+    const uint32_t hdr[3] = {HS_DB_MAGIC, HS_DB_VERSION, (uint32_t)code.size()};
+    memcpy(out, hdr, 12);
+    memcpy(out + 12, &VSA_PLATFORM, 8);
+    const uint32_t crc = crc32c(code.data(), code.size());
+    memcpy(out + 20, &crc, 4); /* reserved0 / reserved1 stay 0 */
+    memcpy(out + HS_DB_FIELDS, code.data(), code.size());
+    *bytes = out;
+    *length = n;
+    return VSA_HS_SUCCESS;
+}
+
+/* hs_deserialize_database, hs_common.h:133 (database.c:246-296) */
+int vsa_hs_deserialize_database(const char *bytes, size_t length, vsa_hs_database_t **db) {
+    if (!bytes || !db) return VSA_HS_INVALID;
+    *db = nullptr;
+    uint32_t version, code_len;
+    uint64_t platform;
+    const uint8_t *code;
+    int r = decode_header(bytes, length, &version, &platform, &code, &code_len);
+    if (r != VSA_HS_SUCCESS) return r;
+    /* the order of database.c:246-296: platform, then CRC; then this
+     * engine's tag (a reference RoseEngine has none) */
+    if (platform != VSA_PLATFORM) return VSA_HS_DB_PLATFORM_ERROR;
+    uint32_t crc;
+    memcpy(&crc, bytes + 20, 4);
+    if (crc32c(code, code_len) != crc) return VSA_HS_INVALID;
+    if (code_len < VSAL_OFF + 16 || get32(code + VSAL_OFF) != VSAL_TAG ||
+        get32(code + VSAL_OFF + 4) != VSAL_FORMAT)
+        return VSA_HS_DB_PLATFORM_ERROR;
+    const unsigned mode = get32(code + VSAL_OFF + 8), n = get32(code + VSAL_OFF + 12);
+    std::vector<std::string> es;
+    std::vector<unsigned> fl, ids;
+    std::vector<size_t> lens;
+    size_t o = VSAL_OFF + 16;
+    for (unsigned i = 0; i < n; i++) {
+        if (o + 12 > code_len) return VSA_HS_INVALID;
+        ids.push_back(get32(code + o));
+        fl.push_back(get32(code + o + 4));
+        const uint32_t len = get32(code + o + 8);
+        if (o + 12 + len > code_len) return VSA_HS_INVALID;
+        es.emplace_back((const char *)code + o + 12, len);
+        lens.push_back(len);
+        o += 12 + len;
+    }
+    std::vector<const char *> ep;
+    for (const auto &e : es) ep.push_back(e.c_str());
+    vsa_hs_compile_error_t *err = nullptr;
+    r = vsa_hs_compile_lit_multi(ep.data(), fl.data(), ids.data(), lens.data(), n, mode, nullptr,
+                                 db, &err);
+    if (r != VSA_HS_SUCCESS) {
+        vsa_hs_free_compile_error(err);
+        return VSA_HS_INVALID;
+    }
+    return VSA_HS_SUCCESS;
+}
+
+/* hs_serialized_database_size, hs_common.h:226 (database.c:316-332) */
+int vsa_hs_serialized_database_size(const char *bytes, size_t length, size_t *deserialized_size) {
+    uint32_t version, code_len;
+    uint64_t platform;
+    const uint8_t *code;
+    int r = decode_header(bytes, length, &version, &platform, &code, &code_len);
+    if (r != VSA_HS_SUCCESS) return r;
+    if (!deserialized_size) return VSA_HS_INVALID;
+    *deserialized_size = HS_DB_HEADER + code_len;
+    return VSA_HS_SUCCESS;
+}
+
+/* hs_database_size, hs_common.h:199 (database.c:300-312): the size of the
+ * database in the reference's layout (header + bytecode) */
+int vsa_hs_database_size(const vsa_hs_database_t *db, size_t *database_size) {
+    if (!database_size) return VSA_HS_INVALID;
+    if (!valid_db(db)) return VSA_HS_INVALID;
+    *database_size = HS_DB_HEADER + bytecode_of(db).size();
+    return VSA_HS_SUCCESS;
+}
+
+} // extern "C"
+namespace {
+/* print_database_string (database.c:358-416) */
+int database_string(char **info, uint32_t version, uint64_t plat, uint32_t mode) {
+    const char *features = (plat & (0x10ull << 13))
+                               ? (plat & (8ull << 13)) ? (plat & (4ull << 13)) ? "" : "AVX2"
+                                                       : "AVX512"
+                               : "AVX512VBMI";
+    const char *m = mode == VSA_HS_MODE_STREAM ? "STREAM"
+                    : mode == VSA_HS_MODE_VECTORED ? "VECTORED" : "BLOCK";
+    char buf[256];
+    snprintf(buf, sizeof(buf), "Version: %u.%u.%u Features: %s Mode: %s", (version >> 24) & 0xff,
+             (version >> 16) & 0xff, (version >> 8) & 0xff, features, m);
+    *info = strdup(buf);
+    return *info ? VSA_HS_SUCCESS : VSA_HS_NOMEM;
+}
+} // namespace
+extern "C" {
+
+/* hs_serialized_database_info, hs_common.h:267 (database.c:419-436): the
+ * mode from the bytecode's RoseEngine.mode, whoever serialized it */
+int vsa_hs_serialized_database_info(const char *bytes, size_t length, char **info) {
+    if (!info) return VSA_HS_INVALID;
+    *info = nullptr;
+    uint32_t version, code_len;
+    uint64_t platform;
+    const uint8_t *code;
+    int r = decode_header(bytes, length, &version, &platform, &code, &code_len);
+    if (r != VSA_HS_SUCCESS) return r;
+    if (code_len < 16) return VSA_HS_INVALID;
+    return database_string(info, version, platform, get32(code + 12));
+}
+
+/* hs_database_info, hs_common.h:245 (database.c:438-455) */
+int vsa_hs_database_info(const vsa_hs_database_t *db, char **info) {
+    if (!info) return VSA_HS_INVALID;
+    *info = nullptr;
+    if (!valid_db(db)) return VSA_HS_INVALID;
+    return database_string(info, HS_DB_VERSION, VSA_PLATFORM, db->mode);
 }
 
 } // extern "C"

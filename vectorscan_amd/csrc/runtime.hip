@@ -2518,6 +2518,13 @@ hwlm_error_t vsa_batcher_hwlmExec(vsa_batcher_t *b, const struct HWLM *tab, cons
  * its own flood events and ends relative to it.  cbctx is an opaque
  * callback context (no Rose scratch: no INCLUDED_JUMP squash). */
 namespace vsa {
+/* the host copy of a loaded database's HWLM blob (vsa_internal.h) */
+int dbHostBlob(const struct vsa_db *db, const uint8_t **blob, size_t *size) {
+    if (!db || !blob || !size) return VSA_E_INVALID;
+    *blob = db->hblob;
+    *size = db->size;
+    return VSA_OK;
+}
 hwlm_error_t exec_pieces(vsa_ctx *c, const vsa_db *db, const u8 *hist, size_t hist_len,
                          const u8 *const *bufs, const size_t *lens, size_t n,
                          LitCallback cb, void *cbctx, void (*on_piece)(void *, size_t)) {

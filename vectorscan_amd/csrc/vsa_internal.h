@@ -103,6 +103,10 @@ bool shuftiDoubleMasks(const u8 onechar[32], const u8 *pairs, size_t npairs, u8 
                        u8 hi1[16], u8 lo2[16], u8 hi2[16]);
 void truffleMasks(const u8 cls[32], u8 m1[16], u8 m2[16]);
 
+/* the host copy of a loaded database's HWLM blob (hs_clone_scratch reloads
+ * it into another context) */
+int dbHostBlob(const struct vsa_db *db, const uint8_t **blob, size_t *size);
+
 } // namespace vsa
 
 #endif

@@ -18,6 +18,8 @@ INVALID = -1
 NOMEM = -2
 SCAN_TERMINATED = -3
 COMPILER_ERROR = -4
+DB_VERSION_ERROR = -5
+DB_PLATFORM_ERROR = -6
 DB_MODE_ERROR = -7
 SCRATCH_IN_USE = -10
 UNKNOWN_ERROR = -13
@@ -66,6 +68,33 @@ _sig("vsa_hs_scan_stream", ctypes.c_int, _vp, _vp, ctypes.c_uint, ctypes.c_uint,
      EventHandler, _vp)
 _sig("vsa_hs_close_stream", ctypes.c_int, _vp, _vp, EventHandler, _vp)
 _sig("vsa_hs_reset_stream", ctypes.c_int, _vp, ctypes.c_uint, _vp, EventHandler, _vp)
+_sig("vsa_hs_copy_stream", ctypes.c_int, ctypes.POINTER(_vp), _vp)
+_sig("vsa_hs_reset_and_copy_stream", ctypes.c_int, _vp, _vp, _vp, EventHandler, _vp)
+_sig("vsa_hs_stream_size", ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_size_t))
+_sig("vsa_hs_clone_scratch", ctypes.c_int, _vp, ctypes.POINTER(_vp))
+_sig("vsa_hs_scratch_size", ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_size_t))
+_sig("vsa_hs_valid_platform", ctypes.c_int)
+_sig("vsa_hs_version", ctypes.c_char_p)
+_sig("vsa_hs_serialize_database", ctypes.c_int, _vp, ctypes.POINTER(_vp),
+     ctypes.POINTER(ctypes.c_size_t))
+_sig("vsa_hs_deserialize_database", ctypes.c_int, _vp, ctypes.c_size_t, ctypes.POINTER(_vp))
+_sig("vsa_hs_serialized_database_size", ctypes.c_int, _vp, ctypes.c_size_t,
+     ctypes.POINTER(ctypes.c_size_t))
+_sig("vsa_hs_database_size", ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_size_t))
+_sig("vsa_hs_serialized_database_info", ctypes.c_int, _vp, ctypes.c_size_t, ctypes.POINTER(_vp))
+_sig("vsa_hs_database_info", ctypes.c_int, _vp, ctypes.POINTER(_vp))
+
+_libc = ctypes.CDLL(None)
+_libc.free.argtypes = [_vp]
+_libc.free.restype = None
+
+
+def _take_string(p):
+    """a malloc'ed C string from the library, freed"""
+    try:
+        return ctypes.string_at(p.value).decode()
+    finally:
+        _libc.free(p)
 
 
 class HsError(RuntimeError):
@@ -95,6 +124,42 @@ class Database:
     def hwlm_bytes(self):
         p, n, _ = self.hwlm()
         return ctypes.string_at(p, n)
+
+    def serialize(self):
+        """hs_serialize_database (hs_common.h:104): the reference's envelope
+        around this engine's bytecode."""
+        p, n = _vp(), ctypes.c_size_t()
+        rc = lib.vsa_hs_serialize_database(self.handle, ctypes.byref(p), ctypes.byref(n))
+        if rc:
+            raise HsError(rc)
+        try:
+            return ctypes.string_at(p.value, n.value)
+        finally:
+            _libc.free(p)
+
+    def size(self):
+        """hs_database_size (hs_common.h:199)"""
+        n = ctypes.c_size_t()
+        rc = lib.vsa_hs_database_size(self.handle, ctypes.byref(n))
+        if rc:
+            raise HsError(rc)
+        return n.value
+
+    def info(self):
+        """hs_database_info (hs_common.h:245): "Version: ... Mode: ..." """
+        p = _vp()
+        rc = lib.vsa_hs_database_info(self.handle, ctypes.byref(p))
+        if rc:
+            raise HsError(rc)
+        return _take_string(p)
+
+    def stream_size(self):
+        """hs_stream_size (hs_common.h:183)"""
+        n = ctypes.c_size_t()
+        rc = lib.vsa_hs_stream_size(self.handle, ctypes.byref(n))
+        if rc:
+            raise HsError(rc)
+        return n.value
 
     def close(self):
         if self.handle:
@@ -131,6 +196,48 @@ def compile_lit_multi(expressions, flags=None, ids=None, mode=MODE_BLOCK):
     return Database(db.value, mode)
 
 
+def deserialize(data):
+    """hs_deserialize_database (hs_common.h:133).  Raises HsError with the
+    reference's codes (INVALID, DB_VERSION_ERROR, DB_PLATFORM_ERROR)."""
+    buf = ctypes.create_string_buffer(bytes(data), max(1, len(data)))
+    h = _vp()
+    rc = lib.vsa_hs_deserialize_database(buf, len(data), ctypes.byref(h))
+    if rc:
+        raise HsError(rc)
+    mode = int.from_bytes(bytes(data[32 + 12:32 + 16]), "little")
+    return Database(h.value, mode)
+
+
+def serialized_size(data):
+    """hs_serialized_database_size (hs_common.h:226)"""
+    buf = ctypes.create_string_buffer(bytes(data), max(1, len(data)))
+    n = ctypes.c_size_t()
+    rc = lib.vsa_hs_serialized_database_size(buf, len(data), ctypes.byref(n))
+    if rc:
+        raise HsError(rc)
+    return n.value
+
+
+def serialized_info(data):
+    """hs_serialized_database_info (hs_common.h:267)"""
+    buf = ctypes.create_string_buffer(bytes(data), max(1, len(data)))
+    p = _vp()
+    rc = lib.vsa_hs_serialized_database_info(buf, len(data), ctypes.byref(p))
+    if rc:
+        raise HsError(rc)
+    return _take_string(p)
+
+
+def valid_platform():
+    """hs_valid_platform (hs_common.h:463)"""
+    return lib.vsa_hs_valid_platform()
+
+
+def version():
+    """hs_version (hs_common.h:446)"""
+    return lib.vsa_hs_version().decode()
+
+
 def compile_lit(expression, flags=0, mode=MODE_BLOCK):
     """hs_compile_lit (hs_compile.h:608): id 0."""
     return compile_lit_multi([expression], [flags], [0], mode)
@@ -149,6 +256,25 @@ class Scratch:
         if rc:
             raise HsError(rc)
         self.handle = h.value
+
+    def clone(self):
+        """hs_clone_scratch (hs_runtime.h:576): a scratch with its own GPU
+        context serving the same databases"""
+        h = _vp()
+        rc = lib.vsa_hs_clone_scratch(self.handle, ctypes.byref(h))
+        if rc:
+            raise HsError(rc)
+        s = Scratch.__new__(Scratch)
+        s.handle = h.value
+        return s
+
+    def size(self):
+        """hs_scratch_size (hs_runtime.h:593)"""
+        n = ctypes.c_size_t()
+        rc = lib.vsa_hs_scratch_size(self.handle, ctypes.byref(n))
+        if rc:
+            raise HsError(rc)
+        return n.value
 
     def close(self):
         if self.handle:
@@ -223,6 +349,25 @@ class Stream:
                                     scratch.handle if scratch else None,
                                     _handler(on_event, out), None)
         return rc, out
+
+    def copy(self):
+        """hs_copy_stream (hs_runtime.h:291)"""
+        h = _vp()
+        rc = lib.vsa_hs_copy_stream(ctypes.byref(h), self.handle)
+        if rc:
+            raise HsError(rc)
+        s = Stream.__new__(Stream)
+        s.handle = h.value
+        s._keep = []
+        return s
+
+    def reset_and_copy(self, src, scratch=None, on_event=None):
+        """hs_reset_and_copy_stream (hs_runtime.h:324): this stream becomes a
+        copy of src (both open on the same database)"""
+        out = []
+        h = _handler(on_event, out) if on_event else EventHandler()
+        return lib.vsa_hs_reset_and_copy_stream(self.handle, src.handle,
+                                                scratch.handle if scratch else None, h, None)
 
     def reset(self, scratch=None, on_event=None, flags=0):
         out = []
