@@ -167,6 +167,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=4)
     ap.add_argument("--lits", type=int, default=5000)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline timing")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the end-to-end (matches delivered to the host) line")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one scan context: each step completed before the next is queued")
@@ -358,6 +360,12 @@ def run(args):
             keys = st["keys"].cpu().numpy().view(np.uint64)
             ids = st["ids"].cpu().numpy().astype(np.uint64)
     kavg = float(np.mean(kms))
+    e2e = None
+    if world == 1 and not args.no_e2e:
+        try:
+            e2e = end_to_end(lits, data.data_ptr(), bl, nblocks, total, nm, args.steps)
+        except Exception as e:  # a side measurement never voids the bench line
+            e2e = {"error": repr(e)}
     del data
     torch.cuda.empty_cache()
 
@@ -440,6 +448,7 @@ def run(args):
                          "scope": "rank 0 scan kernel (%d input bytes)" % local_bytes},
             "cpu_baseline": cpu,
             "pipeline": nslot,
+            "end_to_end": e2e,
             "settle": {"launches": settle_n, "s": round(t_settle, 3),
                        "why": "GPU clock ramp after idle (profiles/r03_ramp.jsonl): untimed "
                               "scans until the kernel time is stable, before the warmup"},
@@ -453,6 +462,43 @@ def run(args):
     db.close()
     for c in ctxs:
         c.close()
+
+
+def end_to_end(lits, d_data, bl, nblocks, total, hwlm_records, reps):
+    """hsbench block mode end to end (tools/hsbench/main.cpp:487-511), beside
+    `value` (which stops at the sorted records in HBM): the same literals as
+    a pure-literal hs database (id = literal index, nocase -> CASELESS), the
+    same bytes as `nblocks` hs_scan blocks, every match delivered to the host
+    through the report program and counted; `reps` passes pipelined
+    (vsa_hs_corpus_scan_repeats: pass k + 1 scans on the GPU while the host
+    replays pass k), after 3 untimed passes."""
+    from vectorscan_amd import hs
+    db = hs.compile_lit_multi([l.s for l in lits],
+                              [hs.FLAG_CASELESS if l.nocase else 0 for l in lits],
+                              [l.id for l in lits], hs.MODE_BLOCK)
+    scratch = hs.Scratch(db)
+    offs = [b * bl for b in range(nblocks)]
+    lens = [min(total, (b + 1) * bl) - b * bl for b in range(nblocks)]
+    corpus = hs.Corpus(db, scratch, d_data, offs, lens)
+    try:
+        rc, _, _, _ = corpus.scan_repeats(3)
+        if rc:
+            return {"error": rc}
+        t0 = time.perf_counter()
+        rc, tot, _, _ = corpus.scan_repeats(reps)
+        el = time.perf_counter() - t0
+        if rc:
+            return {"error": rc}
+        return {"value": round(total * reps / el / 1e9, 3), "unit": "GB/s",
+                "ms_per_pass": round(el / reps * 1e3, 4), "passes": reps,
+                "matches_per_pass": int(tot[-1]), "hwlm_records": int(hwlm_records),
+                "what": "hs_scan of each block with every match delivered to the host "
+                        "(pure-literal hs database of the same literals; pipelined passes, "
+                        "16 replay threads)"}
+    finally:
+        corpus.close()
+        scratch.close()
+        db.close()
 
 
 def blob_domain(blob):
