@@ -383,6 +383,12 @@ int64_t vsa_verm_find(int mode, uint8_t c1, uint8_t c2, uint8_t m1, uint8_t m2,
  * 256 entries, 4 x 16).  Returns entries written or a VSA_E_* code. */
 int vsa_derive_first_stage(const void *hwlm, size_t size, uint64_t *table, uint32_t cap,
                            uint32_t *key_bits, uint32_t *field_bits);
+/* Host-only: the 4-field FDR first stage the engine scans with by default
+ * (2^bits u32 entries, bits 14 / 15: field f (byte f) = the buckets dead at
+ * end p + f; key = (b[p-1] & 0x7f) | (b[p] & 0x7f) << 7 | (b[p-2] & 1) << 14
+ * at 15 bits).  Returns entries written or a VSA_E_* code. */
+int vsa_derive_fdr4_table(const void *hwlm, size_t size, uint32_t bits, uint32_t *table,
+                          uint32_t cap);
 
 /* Optional: hs_scratch field offsets for INCLUDED_JUMP squash replay
  * (offsetof(struct hs_scratch, fdr_conf / fdr_conf_offset)); the defaults

@@ -492,6 +492,50 @@ def test_derived_first_stage_no_false_negatives(nlits, hint, minlen):
         assert len(cand) < 0.05 * len(data), len(cand)
 
 
+def _fdr4_candidates(table, bits, data):
+    """numpy restatement of the FDR4 first stage (kernels.hip fdr4_conf):
+    key of position p from b[p-2] (bit 0, 15-bit keys), b[p-1], b[p] (7 bits
+    each), field f of T[key] on end p + f; bytes before the buffer are 0."""
+    b = np.frombuffer(bytes(data), np.uint8).astype(np.uint64)
+    n = len(b)
+    p1 = np.concatenate([np.zeros(1, np.uint64), b[:-1]])
+    p2 = np.concatenate([np.zeros(2, np.uint64), b[:-2]])
+    key = (p1 & np.uint64(0x7F)) | ((b & np.uint64(0x7F)) << np.uint64(7))
+    if bits == 15:
+        key |= (p2 & np.uint64(1)) << np.uint64(14)
+    x = table[key.astype(np.int64)].astype(np.uint64)
+    conf = np.zeros(n, np.uint64)
+    for f in range(4):
+        conf[f:] |= (x[:n - f] >> np.uint64(8 * f)) & np.uint64(0xFF)
+    return np.nonzero((~conf) & np.uint64(0xFF))[0]
+
+
+@pytest.mark.parametrize("bits", [14, 15])
+@pytest.mark.parametrize("nlits,minlen", [(2000, 1), (2000, 4), (300, 2), (5000, 4)])
+def test_fdr4_first_stage_no_false_negatives(nlits, minlen, bits):
+    """The 4-field FDR first stage (derive_fdr4_table, the default scan
+    table) passes every end the reference's confirm accepts, and (literals
+    of 4+ bytes) stays at least as selective as the 8-field pair table."""
+    import bench
+    rng = random.Random(700 + nlits + minlen)
+    lits = [vsa.HwlmLiteral(bytes(rng.randint(0x20, 0x7E)
+                                  for _ in range(rng.randint(minlen, 8))),
+                            rng.random() < 0.1, i) for i in range(nlits)]
+    blob = build_or_none(lits, 0)
+    if blob is None:
+        pytest.skip("FDR not buildable for this set")
+    table = vsa.derive_fdr4_table(blob, bits)
+    data = bench.make_corpus(1 << 20, lits, seed=nlits + bits, plant_every=512)
+    st, m = oracle.fdr_exec(vsa.engine_blob(blob), data, cap=1 << 20)
+    assert st == 0 and len(m) > 1000
+    cand = set(_fdr4_candidates(table, bits, data).tolist())
+    missing = [e for e, _ in m if e not in cand]
+    assert not missing, missing[:10]
+    if minlen >= 4 and bits == 15:
+        t8, kb, fb = vsa.derive_first_stage(blob)
+        assert len(cand) <= len(set(_first_stage_candidates(t8, kb, fb, data).tolist()))
+
+
 # ------------------------------------------------- SIMD CPU baseline ---
 
 @pytest.mark.parametrize("hint", [0, -1])

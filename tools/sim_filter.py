@@ -146,6 +146,23 @@ DESIGNS = {
     "s2_tri455_ctr": dict(key_offs=(-1, 0, 1), key_bits=(4, 5, 5), ends=range(-1, 7), stride=2),
     "s2_tri545_ctr": dict(key_offs=(-1, 0, 1), key_bits=(5, 4, 5), ends=range(-1, 7), stride=2),
     "s2_tri664_ctr13": dict(key_offs=(-1, 0, 1), key_bits=(5, 5, 3), ends=range(-1, 7), stride=2),
+    # 4-field (u32) entries with trigram keys: 2^15 x 4 B = 128 KiB
+    "s1_tri555_f4": dict(key_offs=(-2, -1, 0), key_bits=(5, 5, 5), ends=range(0, 4), stride=1),
+    "s1_tri465_f4": dict(key_offs=(-2, -1, 0), key_bits=(4, 6, 5), ends=range(0, 4), stride=1),
+    "s1_tri564_f4": dict(key_offs=(-2, -1, 0), key_bits=(5, 6, 4), ends=range(0, 4), stride=1),
+    "s1_tri456_f4": dict(key_offs=(-2, -1, 0), key_bits=(4, 5, 6), ends=range(0, 4), stride=1),
+    "s1_pair78_f4": dict(key_offs=(-1, 0), key_bits=(7, 8), ends=range(0, 4), stride=1),
+    "s1_tri177_f4": dict(key_offs=(-2, -1, 0), key_bits=(1, 7, 7), ends=range(0, 4), stride=1),
+    "s1_tri276_f4": dict(key_offs=(-2, -1, 0), key_bits=(2, 7, 6), ends=range(0, 4), stride=1),
+    "s1_tri366_f4": dict(key_offs=(-2, -1, 0), key_bits=(3, 6, 6), ends=range(0, 4), stride=1),
+    "s1_tri375_f4": dict(key_offs=(-2, -1, 0), key_bits=(3, 7, 5), ends=range(0, 4), stride=1),
+    "s1_tri555_f5": dict(key_offs=(-2, -1, 0), key_bits=(5, 5, 5), ends=range(0, 5), stride=1),
+    # level 1 alone (even positions) of the two-level sweeps
+    "s2_tri555_f4": dict(key_offs=(-2, -1, 0), key_bits=(5, 5, 5), ends=range(0, 4), stride=2),
+    "s2_tri465_f4": dict(key_offs=(-2, -1, 0), key_bits=(4, 6, 5), ends=range(0, 4), stride=2),
+    "s2_tri177_f4": dict(key_offs=(-2, -1, 0), key_bits=(1, 7, 7), ends=range(0, 4), stride=2),
+    "s2_tri276_f4": dict(key_offs=(-2, -1, 0), key_bits=(2, 7, 6), ends=range(0, 4), stride=2),
+    "s1_tri177_f3": dict(key_offs=(-2, -1, 0), key_bits=(1, 7, 7), ends=range(0, 3), stride=1),
 }
 
 

@@ -293,6 +293,21 @@ def derive_first_stage(blob):
     return out[:n], kb.value, fb.value
 
 
+_sig("vsa_derive_fdr4_table", ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
+     ctypes.c_void_p, ctypes.c_uint32)
+
+
+def derive_fdr4_table(blob, bits=15):
+    """the 4-field FDR first stage (u32 array of 2^bits entries) the engine
+    scans with (host only; see vsa_derive_fdr4_table)"""
+    cap = 1 << bits
+    out = np.zeros(cap, np.uint32)
+    n = lib.vsa_derive_fdr4_table(blob.ptr, blob.size, bits, out.ctypes.data, cap)
+    if n < 0:
+        raise BuildError("vsa_derive_fdr4_table failed with %d" % n)
+    return out[:n]
+
+
 def engine_blob(blob):
     """Pointer to the engine inside an HWLM blob (HWLM_C_DATA, hwlm_internal.h:56)."""
     return blob.ptr + HWLM_HEADER

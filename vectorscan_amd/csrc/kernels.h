@@ -69,11 +69,24 @@ static inline uint32_t vsa_fdr_key(uint32_t b0, uint32_t b1, uint32_t dmask) {
     return (b0 & 0x7fu) | ((b1 << 7) & dmask & ~0x7fu);
 }
 
+/* Key of the 4-field derived FDR first stage (VSA_MODE_FDR4, runtime.hip
+ * derive_fdr4_table) at position p, from the bytes b2 = b[p-2], b1 =
+ * b[p-1], b0 = b[p]: the low 7 bits of b1 and of b0 and, at 15 bits, bit 0
+ * of b2 on top.  The kernels build it two keys per dword: bit 0 of b[p-2]
+ * is funnel-shifted into bit 7 of b[p]'s (masked) byte, then fdr_key2. */
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+static inline uint32_t vsa_fdr4_key(uint32_t b2, uint32_t b1, uint32_t b0, uint32_t bits) {
+    return (b1 & 0x7fu) | ((b0 & 0x7fu) << 7) | (bits >= 15 ? (b2 & 1u) << 14 : 0u);
+}
+
 enum VsaLitMode {
     VSA_MODE_FDR = 0,   /* 8 lanes x 8 buckets, 2-byte key & domainMask */
     VSA_MODE_TEDDY = 1, /* 4 lanes x 8 buckets, 1-byte key */
     VSA_MODE_FAT = 2,   /* 4 lanes x 16 buckets, 1-byte key */
     VSA_MODE_NOOD = 3,  /* noodle: masked compare of the <= 8 bytes ending at e */
+    VSA_MODE_FDR4 = 4,  /* FDR engines, 4 fields x 8 buckets (u32), 3-byte key */
 };
 
 /* binned sort of the match records: bins by the end's top bits, each bin

@@ -202,6 +202,18 @@ struct LitTraits<VSA_MODE_FAT> {
     static constexpr bool KEY16 = false;
     typedef u64 S_t;
 };
+/* FDR engines, 4-field first stage (runtime.hip derive_fdr4_table): u32
+ * entries, 4 ends x 8 buckets, keyed by 15 bits of the 3 bytes ending at
+ * the position (vsa_fdr4_key) */
+template <>
+struct LitTraits<VSA_MODE_FDR4> {
+    static constexpr int LB = 8;
+    static constexpr int NL = 4;
+    static constexpr int CW = 4;
+    static constexpr int EW = 3;
+    static constexpr bool KEY16 = false;
+    typedef u32 S_t;
+};
 
 /* per-bucket confirm parameters staged in LDS (FDRConfirm, fdr_confirm.h:78) */
 struct PfRec {
@@ -384,6 +396,9 @@ __device__ __forceinline__ u64 lit_lookup(const void *tab, u32 key, u32 lane) {
     if constexpr (MODE == VSA_MODE_FDR) {
         (void)lane;
         return ((const u64 *)tab)[key];
+    } else if constexpr (MODE == VSA_MODE_FDR4) {
+        (void)lane;
+        return ((const u32 *)tab)[key];
     } else {
         return ((const u64 *)tab)[(key << 5) | (lane & 31)];
     }
@@ -576,6 +591,114 @@ __device__ __forceinline__ void fdr_shift1(const u32 (&F)[6], u32 (&c)[4], u64 &
 #pragma unroll
     for (int w = 0; w < 4; w++) c[w] = __builtin_amdgcn_alignbyte(F[w + 1], F[w], 1);
     s = ((u64)(F[5] >> 8) << 32) | __builtin_amdgcn_alignbyte(F[5], F[4], 1);
+}
+
+/* ---- FDR4: the 4-field first stage (VSA_MODE_FDR4) ----
+ * Lane l looks up positions 0 .. 15 of its chunk; the key of position p is
+ * vsa_fdr4_key(b[p-2], b[p-1], b[p]) (bytes -2, -1: the previous lane's, or
+ * chunk's, last ones) and field f (byte f) of the entry applies to end p + f.
+ * U[0..3] = the conf bytes of ends 0 .. 15, U[4] bytes 0..2 = ends 16..18,
+ * which are the next lane's ends 0..2 (spilled once per iteration).
+ *
+ * Keys, two per dword (fdr_key2 on 16-bit halves): the even positions (4w,
+ * 4w + 2) from t = bytes 4w-1 .. 4w+2, the odd ones (4w + 1, 4w + 3) from
+ * bytes 4w .. 4w+3; bit 0 of each key's b[p-2] goes into bit 7 of b[p]'s
+ * masked byte (bits 15 / 31 of the dword) by a funnel shift (v_alignbit) and
+ * one v_bfi, so fdr_key2 lands it at key bit 14 (15-bit keys only: a
+ * database whose slot bitmaps leave no room for the 128 KiB table scans
+ * with the 8-field table, runtime.hip). */
+__device__ __forceinline__ void fdr4_keys(const u32 (&z)[4], u32 zp, u32 (&ke)[4],
+                                          u32 (&ko)[4]) {
+    const u32 kf = 0x007f007fu, ks = 0x00010001u;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const u32 zq = w ? z[w - 1] : zp;
+        const u32 t = __builtin_amdgcn_alignbyte(z[w], zq, 3);
+        /* bit 15 = b(4w-2), bit 31 = b(4w) (even); b(4w-1), b(4w+1) (odd) */
+        u32 te, to;
+        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(te) : "s"(0x80008000u),
+            "v"(__builtin_amdgcn_alignbit(z[w], zq, 1)), "v"(t));
+        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(to) : "s"(0x80008000u),
+            "v"(__builtin_amdgcn_alignbit(z[w], zq, 9)), "v"(z[w]));
+        ke[w] = fdr_key2(te, kf, ks);
+        ko[w] = fdr_key2(to, kf, ks);
+    }
+}
+/* LDS byte address of a u32 entry: base + 4 * (16-bit half H of w) */
+template <int H>
+__device__ __forceinline__ u32 tab_addr16x4(u32 w, u32 base) {
+    u32 r;
+    if constexpr (H == 0)
+        asm("v_mad_u32_u16 %0, %1, 4, %2" : "=v"(r) : "v"(w), "s"(base));
+    else
+        asm("v_mad_u32_u16 %0, %1, 4, %2 op_sel:[1,0,0,0]" : "=v"(r) : "v"(w), "s"(base));
+    return r;
+}
+__device__ __forceinline__ u32 lds_ld32a(u32 addr) {
+    return *(const __attribute__((address_space(3))) u32 *)(uintptr_t)addr;
+}
+/* OR-into-place: field f of x[p] onto end p + f.  EVEN: x[0, 2, .., 14]
+ * (the first writes of U); ODD: x[1, 3, .., 15] OR-ed on top. */
+__device__ __forceinline__ void fdr4_acc_even(const u32 (&x)[16], u32 (&U)[5]) {
+    U[0] = x[0] | (x[2] << 16);
+#pragma unroll
+    for (int k = 1; k < 4; k++) U[k] = x[4 * k] | __builtin_amdgcn_alignbyte(x[4 * k + 2], x[4 * k - 2], 2);
+    U[4] = x[14] >> 16;
+}
+__device__ __forceinline__ void fdr4_acc_odd(const u32 (&x)[16], u32 (&U)[5]) {
+    U[0] = or3(U[0], x[1] << 8, x[3] << 24);
+#pragma unroll
+    for (int k = 1; k < 4; k++)
+        U[k] = or3(U[k], __builtin_amdgcn_alignbyte(x[4 * k + 1], x[4 * k - 3], 3),
+                   __builtin_amdgcn_alignbyte(x[4 * k + 3], x[4 * k - 1], 1));
+    U[4] = or3(U[4], x[13] >> 24, x[15] >> 8);
+}
+/* One chunk's conf bytes (before the previous lane's spill into U[0]).
+ * Sweep (LOOKM == false): two levels -- the even positions for every lane,
+ * then the odd ones with their real keys only in lanes where a conf dword
+ * they reach is still live (else key 0: an LDS broadcast; its entry is
+ * OR-ed only into ends already dead, so the result is the one-level
+ * filter's).  Edge iterations (LOOKM): one level, position p looked up
+ * only where bit p of look_m is set. */
+template <bool LOOKM>
+__device__ __forceinline__ void fdr4_conf(const LitShared &L, const u32 (&d)[4], u32 pv3,
+                                          u32 look_m, u32 (&U)[5]) {
+    u32 z[4], ke[4], ko[4], x[16];
+#pragma unroll
+    for (int w = 0; w < 4; w++) z[w] = d[w] & 0x7f7f7f7fu;
+    fdr4_keys(z, pv3 & 0x7f7f7f7fu, ke, ko);
+    auto ld = [&](int p, u32 a) {
+        if (LOOKM) x[p] = ((look_m >> p) & 1u) ? lds_ld32a(a) : 0u;
+        else x[p] = lds_ld32a(a);
+    };
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        ld(4 * w, tab_addr16x4<0>(ke[w], L.tab_lds));
+        ld(4 * w + 2, tab_addr16x4<1>(ke[w], L.tab_lds));
+    }
+    if (LOOKM) {
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            ld(4 * w + 1, tab_addr16x4<0>(ko[w], L.tab_lds));
+            ld(4 * w + 3, tab_addr16x4<1>(ko[w], L.tab_lds));
+        }
+        fdr4_acc_even(x, U);
+        fdr4_acc_odd(x, U);
+        return;
+    }
+    fdr4_acc_even(x, U);
+    /* odd key dword w (positions 4w + 1, 4w + 3) reaches ends 4w + 1 ..
+     * 4w + 6: conf dwords w and w + 1 */
+    u64 m[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) m[k] = __ballot(U[k] != 0xffffffffu);
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const u32 k = __builtin_amdgcn_inverse_ballot_w64(m[w] | m[w + 1]) ? ko[w] : 0u;
+        x[4 * w + 1] = lds_ld32a(tab_addr16x4<0>(k, L.tab_lds));
+        x[4 * w + 3] = lds_ld32a(tab_addr16x4<1>(k, L.tab_lds));
+    }
+    fdr4_acc_odd(x, U);
 }
 
 /* FDR sweep (LDS table, interior iteration): the 16 lookups in two levels.
@@ -796,7 +919,9 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
 #pragma unroll
         for (int w = 0; w < 4; w++) d[w] &= nib_to_bytes(bm >> (4 * w));
         if (!((bm >> 16) & 1u)) d[4] = 0;
-        look_m = range_mask(rel32(MODE == VSA_MODE_FDR ? S.zbase : S.qlo, q0), r_len);
+        look_m = range_mask(rel32((MODE == VSA_MODE_FDR || MODE == VSA_MODE_FDR4) ? S.zbase
+                                                                                 : S.qlo, q0),
+                            r_len);
     }
 
     /* FDR (LDS table): the lane looks up positions -1 .. 14, keyed by the
@@ -808,9 +933,12 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
      * b[e]) implies (derive_fdr_table) — the filter stays a superset. */
     constexpr bool FDR_BACK = MODE == VSA_MODE_FDR && LDS_TABLE;
     constexpr bool SWEEP = FDR_BACK && !EDGE;
+    constexpr bool F4 = MODE == VSA_MODE_FDR4;
+    /* sweep state in lane-rotated registers (p3 / p4 / p5) */
+    constexpr bool PSTATE = (FDR_BACK || F4) && !EDGE;
     u32 pv3;
     IterState out;
-    if constexpr (SWEEP) {
+    if constexpr (PSTATE) {
         /* lane 0: the previous chunk's lane-63 d[3], rotated in last time */
         pv3 = lane_up1_or_old(in.p3, d[3]);
         out.p3 = lane_ror1(d[3]);
@@ -830,13 +958,32 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     out.ncand = in.ncand;
     out.tail_cache = in.tail_cache;
     out.head = in.head;
-    if constexpr (SWEEP) {
+    if constexpr (PSTATE) {
         out.pbytes = (in.pbytes & 0xffffffff00000000ULL) | readlane_u32(d[2], WAVE - 1);
         out.carry = in.carry;
     } else {
         out.pbytes = ((u64)readlane_u32(d[3], WAVE - 1) << 32) | readlane_u32(d[2], WAVE - 1);
     }
-    if constexpr (SWEEP) {
+    if constexpr (F4) {
+        /* FDR4 (fdr4_conf): ends 0..15 in U[0..3] in end order; U[4] = the
+         * next lane's ends 0..2 (lane 63: the next chunk's) */
+        u32 U[5];
+        fdr4_conf<EDGE>(L, {d[0], d[1], d[2], d[3]}, pv3, look_m, U);
+        if constexpr (EDGE) {
+            const u32 s_in = writelane_u32<0>(lane_up1(U[4]), (u32)in.carry);
+            out.carry = readlane_u32(U[4], WAVE - 1);
+            U[0] |= s_in;
+        } else {
+            /* lane 0: the previous chunk's lane-63 U[4], rotated in last time */
+            U[0] |= lane_up1_or_old(in.p4, U[4]);
+            out.p4 = lane_ror1(U[4]);
+            out.p5 = in.p5;
+            const u32 nbm = ~bucket_mask;
+            if (!__any(((U[0] & U[1] & U[2] & U[3]) | nbm) != 0xffffffffu)) return out;
+        }
+#pragma unroll
+        for (int w = 0; w < 4; w++) c[w] = U[w];
+    } else if constexpr (SWEEP) {
         /* interior FDR iteration (fdr_sweep_conf): the candidate test runs on
          * the unshifted dwords (this lane's ends are U[0] bytes 1..3, U[1..3]
          * and U[4] byte 0); the shift to end order is done only for a push */
@@ -921,7 +1068,7 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     if constexpr (sizeof(S_t) == 8) c[1] |= (u32)(s_in >> 32);
     } /* one-level lookups */
     if (EDGE) {
-        if constexpr (MODE == VSA_MODE_FDR) if (!S.stream) {
+        if constexpr (MODE == VSA_MODE_FDR || MODE == VSA_MODE_FDR4) if (!S.stream) {
             /* start state: byte i applies to end start + i (the short zone
              * shifts fdr->start by 16 - (len - start) against a scan from
              * len - 16, fdr.c:372-440 and :712-720, landing on start too):
@@ -1444,9 +1591,9 @@ vsa_lit_scan(VsaLitParams P) {
     /* ---- stage tables into LDS ---- */
     u32 tab_bytes = 0;
     const void *tab;
-    if constexpr (MODE == VSA_MODE_FDR) {
+    if constexpr (MODE == VSA_MODE_FDR || MODE == VSA_MODE_FDR4) {
         if (LDS_TABLE) {
-            tab_bytes = P.table_entries * 8;
+            tab_bytes = P.table_entries * (MODE == VSA_MODE_FDR4 ? 4 : 8);
             const uint4 *src = (const uint4 *)P.table;
             stage_lds<8>((uint4 *)smem, tab_bytes / 16, tid, [&](u32 i) { return src[i]; });
             tab = smem;
@@ -1673,7 +1820,7 @@ vsa_lit_scan(VsaLitParams P) {
         const int64_t s_hi = (!gcount && s_lo + SEG < S.bhi) ? s_lo + SEG : S.bhi;
         const u32 niters = (u32)((s_hi - s_lo + 1023) >> 10);
         n_iter += niters;
-        const int64_t zlo = (MODE == VSA_MODE_FDR) ? B.zbase : S.qlo;
+        const int64_t zlo = (MODE == VSA_MODE_FDR || MODE == VSA_MODE_FDR4) ? B.zbase : S.qlo;
 
         /* iterations [f0, f1) are interior ("fast"): no byte of the 1 KiB
          * chunk or its successor byte lies outside the block, and the FDR
@@ -1731,6 +1878,9 @@ vsa_lit_scan(VsaLitParams P) {
             if (pro1_in) {
                 u32 key;
                 if constexpr (T::KEY16) key = vsa_fdr_key(pb0, pb1, P.dmask);
+                else if constexpr (MODE == VSA_MODE_FDR4)
+                    key = vsa_fdr4_key(load_byte_masked(A, pp - 2, S.vlo, S.bhi),
+                                       load_byte_masked(A, pp - 1, S.vlo, S.bhi), pb0, 15u);
                 else key = pb0;
                 x = (S_t)lit_lookup<MODE, LDS_TABLE>(tab, key, lane);
                 x >>= T::LB * (s_lo - pp);
@@ -1773,6 +1923,12 @@ vsa_lit_scan(VsaLitParams P) {
                 is.p3 = (u32)(is.pbytes >> 32);
                 is.p4 = (u32)cu;
                 is.p5 = (u32)(cu >> 32);
+            }
+            if constexpr (MODE == VSA_MODE_FDR4) {
+                /* the carry (ends 0..2 of the chunk) is U[4]'s form */
+                is.p3 = (u32)(is.pbytes >> 32);
+                is.p4 = (u32)is.carry;
+                is.p5 = 0;
             }
             /* main sweep: LIT_DEPTH chunks in flight per wave.  ring[k] is
              * consumed and then refilled in place (no register rotation), so
@@ -1819,6 +1975,10 @@ vsa_lit_scan(VsaLitParams P) {
                 /* sweep_leave: back to the scalar carry / pbytes */
                 is.pbytes = ((u64)readlane_u32(is.p3, 0) << 32) | (u32)is.pbytes;
                 is.carry = (((u64)readlane_u32(is.p5, 0) << 32) | readlane_u32(is.p4, 0)) >> 8;
+            }
+            if constexpr (MODE == VSA_MODE_FDR4) {
+                is.pbytes = ((u64)readlane_u32(is.p3, 0) << 32) | (u32)is.pbytes;
+                is.carry = readlane_u32(is.p4, 0);
             }
         }
         prefetch_ticket();
@@ -1873,6 +2033,8 @@ vsa_lit_scan(VsaLitParams P) {
 
 template __global__ void vsa_lit_scan<VSA_MODE_FDR, true, false>(VsaLitParams);
 template __global__ void vsa_lit_scan<VSA_MODE_FDR, true, true>(VsaLitParams);
+template __global__ void vsa_lit_scan<VSA_MODE_FDR4, true, false>(VsaLitParams);
+template __global__ void vsa_lit_scan<VSA_MODE_FDR4, true, true>(VsaLitParams);
 template __global__ void vsa_lit_scan<VSA_MODE_FDR, false, false>(VsaLitParams);
 template __global__ void vsa_lit_scan<VSA_MODE_TEDDY, true, false>(VsaLitParams);
 template __global__ void vsa_lit_scan<VSA_MODE_FAT, true, false>(VsaLitParams);

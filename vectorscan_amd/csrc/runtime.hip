@@ -237,6 +237,7 @@ struct vsa_db {
     int type = 0;                /* HWLM_ENGINE_NOOD / FDR */
     uint32_t engine_id = 0;
     int mode = 0;                /* VsaLitMode */
+    bool fdr4 = false;           /* FDR engine scanned with the 4-field first stage */
     uint32_t table_entries = 0;
     uint32_t dmask = 0;
     uint64_t state_lo = 0, state_hi = 0;
@@ -714,6 +715,16 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     memcpy(P.slot_off, db->slot_off, sizeof(P.slot_off));
     memcpy(P.slot_bits, db->slot_bits, sizeof(P.slot_bits));
     P.pf_mult = db->pf_mult;
+    if (db->mode == VSA_MODE_FDR && db->fdr4) {
+        const size_t tb = (size_t)db->table_entries * 4;
+        const bool xp = use_xp(db);
+        const size_t ent = xp ? 16 : 48; /* QEnt or chunk entries */
+        P.nconf = launch_nconf(db, tb, ent, LDS_BUDGET);
+        size_t lds = plan_lds(tb, db->slot_words, ent, &P.qcap, LDS_BUDGET, P.nconf);
+        if (lds > LDS_BUDGET) return VSA_E_INVALID;
+        return xp ? launch_lit<VSA_MODE_FDR4, true, true>(c, P, lds)
+                  : launch_lit<VSA_MODE_FDR4, true>(c, P, lds);
+    }
     if (db->mode == VSA_MODE_FDR) {
         size_t tb = (size_t)db->table_entries * 8;
         if (tb <= 128 * 1024) {
@@ -1656,6 +1667,81 @@ static void derive_fdr_table(const uint8_t *eng, const uint32_t conf_off[8], uin
     }
 }
 
+/* The 4-field FDR first stage (VSA_MODE_FDR4), derived like
+ * derive_fdr_table: bit (f * 8 + b) of T[key] is 0 when some literal of
+ * bucket b is consistent with the three bytes ending f bytes before its end
+ * (back offsets f + 2, f + 1, f; bytes before the literal are don't-cares,
+ * msk 0), keyed by vsa_fdr4_key (kernels.h: 7 + 7 bits of the last two and,
+ * at 15 bits, bit 0 of the first).  u32 entries, 4 fields.  On the cfg-4
+ * set it passes half the candidate bits of the 8-field pair table (1.7e-4
+ * against 3.3e-4 per byte, tools/sim_filter.py s1_tri177_f4) from the same
+ * 128 KiB, and its even positions alone leave 4.0 % of ends live against
+ * 6.9 % (the two-level sweep's level 1). */
+static void derive_fdr4_table(const uint8_t *eng, const uint32_t conf_off[8], uint32_t bits,
+                              std::vector<uint32_t> &T) {
+    const uint32_t n = 1u << bits;
+    T.assign(n, ~0u);
+    uint32_t always = 0;
+    const uint8_t *confBase = eng + ((const uint32_t *)eng)[4];
+    auto proj = [](uint8_t m, uint8_t v, uint32_t keep) {
+        /* the distinct (x & keep) over bytes x with (x & m) == v */
+        std::vector<uint32_t> out;
+        bool seen[256] = {false};
+        for (uint32_t x = 0; x < 256; x++)
+            if ((x & m) == v && !seen[x & keep]) {
+                seen[x & keep] = true;
+                out.push_back(x & keep);
+            }
+        return out;
+    };
+    for (uint32_t b = 0; b < 8; b++) {
+        if (!conf_off[b]) continue;
+        const uint8_t *fc = confBase + conf_off[b];
+        const FDRConfirm *cf = (const FDRConfirm *)fc;
+        const uint32_t *li = (const uint32_t *)(fc + sizeof(FDRConfirm));
+        std::vector<uint32_t> offs;
+        for (uint32_t h = 0; h < (1u << cf->nBits); h++) {
+            uint32_t o = li[h];
+            if (!o) continue;
+            for (;;) {
+                offs.push_back(o);
+                const LitInfo *L = (const LitInfo *)(fc + o);
+                if (!L->next) break;
+                o += sizeof(LitInfo);
+            }
+        }
+        std::sort(offs.begin(), offs.end());
+        offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
+        for (uint32_t o : offs) {
+            const LitInfo *L = (const LitInfo *)(fc + o);
+            auto mv = [&](uint32_t back, uint8_t *m, uint8_t *v) {
+                /* the byte `back` before the end: byte 7 - back of the window */
+                *m = (uint8_t)(L->msk >> (8 * (7 - back)));
+                *v = (uint8_t)(L->v >> (8 * (7 - back))) & *m;
+            };
+            for (uint32_t f = 0; f < 4; f++) {
+                const uint32_t bit = 1u << (f * 8 + b);
+                uint8_t m0, v0, m1, v1, m2, v2;
+                mv(f, &m0, &v0);
+                mv(f + 1, &m1, &v1);
+                mv(f + 2, &m2, &v2);
+                const auto c0 = proj(m0, v0, 0x7f), c1 = proj(m1, v1, 0x7f);
+                const auto c2 = proj(m2, v2, bits >= 15 ? 1u : 0u);
+                if (c0.size() * c1.size() * c2.size() >= n) {
+                    always |= bit;
+                    continue;
+                }
+                for (uint32_t x2 : c2)
+                    for (uint32_t x1 : c1)
+                        for (uint32_t x0 : c0) T[vsa_fdr4_key(x2, x1, x0, bits)] &= ~bit;
+            }
+        }
+    }
+    if (always) {
+        for (auto &t : T) t &= ~always;
+    }
+}
+
 /* Teddy / Fat Teddy first stage, rebuilt at load like FDR's: bit (k * lb +
  * b) of W[c] is 0 when some literal of bucket b has byte c (under its
  * mask) k bytes before its end (LitInfo v / msk, fdr_confirm.h:57-65), for
@@ -1807,7 +1893,21 @@ int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
     VSA_CHECK(hipSetDevice(c->device));
     VSA_CHECK(hipMalloc(&db->d_blob, size));
     VSA_CHECK(hipMemcpy(db->d_blob, db->hblob, size, hipMemcpyHostToDevice));
-    if (db->mode == VSA_MODE_FDR) {
+    uint32_t qc4 = 0;
+    if (db->mode == VSA_MODE_FDR && !getenv("VSA_FDR8") &&
+        plan_lds((size_t)4 << 15, db->slot_words, 48, &qc4) <= LDS_BUDGET) {
+        /* the 4-field first stage (derive_fdr4_table, 15-bit keys) when the
+         * 128 KiB table fits in LDS beside the rings and slot bitmaps; else,
+         * or with VSA_FDR8=1 (A/B), the 8-field pair table below */
+        const uint32_t bits = 15;
+        std::vector<uint32_t> T;
+        derive_fdr4_table(eng, db->conf_off, bits, T);
+        db->fdr4 = true;
+        db->table_entries = 1u << bits;
+        db->dmask = (1u << bits) - 1;
+        VSA_CHECK(hipMalloc(&db->d_table, T.size() * 4));
+        VSA_CHECK(hipMemcpy(db->d_table, T.data(), T.size() * 4, hipMemcpyHostToDevice));
+    } else if (db->mode == VSA_MODE_FDR) {
         /* derived stride-1 first stage: domain 14 when it fits in LDS beside
          * the rings and slot bitmaps, else 13 (see derive_fdr_table) */
         uint32_t qc = 0;
@@ -1880,6 +1980,27 @@ int vsa_derive_first_stage(const void *hwlm, size_t size, uint64_t *table, uint3
     }
     const uint32_t n = (uint32_t)std::min<size_t>(cap, T.size());
     memcpy(table, T.data(), n * sizeof(uint64_t));
+    return (int)n;
+}
+
+/* Host-only: the 4-field first stage (derive_fdr4_table) of an FDR blob at
+ * `bits` (14 or 15) key bits, for tests and tools.  Returns the entries
+ * written (<= cap) or a VSA_E_* code. */
+int vsa_derive_fdr4_table(const void *hwlm, size_t size, uint32_t bits, uint32_t *table,
+                          uint32_t cap) {
+    if (!hwlm || !table || size < VSA_ROUNDUP_CL(sizeof(HWLM)) || bits < 14 || bits > 15)
+        return VSA_E_INVALID;
+    const HWLM *h = (const HWLM *)hwlm;
+    if (h->type != HWLM_ENGINE_FDR) return VSA_E_INVALID;
+    const uint8_t *eng = (const uint8_t *)hwlm + VSA_ROUNDUP_CL(sizeof(HWLM));
+    if (((const uint32_t *)eng)[0] != VSA_ENGINE_FDR) return VSA_E_INVALID;
+    const uint32_t *confBase = (const uint32_t *)(eng + ((const uint32_t *)eng)[4]);
+    uint32_t conf_off[8];
+    for (int b = 0; b < 8; b++) conf_off[b] = confBase[b];
+    std::vector<uint32_t> T;
+    derive_fdr4_table(eng, conf_off, bits, T);
+    const uint32_t n = (uint32_t)std::min<size_t>(cap, T.size());
+    memcpy(table, T.data(), n * sizeof(uint32_t));
     return (int)n;
 }
 
