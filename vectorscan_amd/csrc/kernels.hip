@@ -600,7 +600,7 @@ __device__ __forceinline__ void fdr_shift1(const u32 (&F)[6], u32 (&c)[4], u64 &
  * U[0..3] = the conf bytes of ends 0 .. 15, U[4] bytes 0..2 = ends 16..18,
  * which are the next lane's ends 0..2 (spilled once per iteration).
  *
- * Keys, two per dword (fdr_key2 on 16-bit halves): the even positions (4w,
+ * Keys, two per dword (fdr_key2 on 16-bit halves, raw bytes): the even positions (4w,
  * 4w + 2) from t = bytes 4w-1 .. 4w+2, the odd ones (4w + 1, 4w + 3) from
  * bytes 4w .. 4w+3; bit 0 of each key's b[p-2] goes into bit 7 of b[p]'s
  * masked byte (bits 15 / 31 of the dword) by a funnel shift (v_alignbit) and
@@ -663,10 +663,10 @@ __device__ __forceinline__ void fdr4_acc_odd(const u32 (&x)[16], u32 (&U)[5]) {
 template <bool LOOKM>
 __device__ __forceinline__ void fdr4_conf(const LitShared &L, const u32 (&d)[4], u32 pv3,
                                           u32 look_m, u32 (&U)[5]) {
-    u32 z[4], ke[4], ko[4], x[16];
-#pragma unroll
-    for (int w = 0; w < 4; w++) z[w] = d[w] & 0x7f7f7f7fu;
-    fdr4_keys(z, pv3 & 0x7f7f7f7fu, ke, ko);
+    /* no 7-bit masking: fdr_key2 keeps 7 bits of each pair's first byte,
+     * and the injected bit replaces bit 7 of its second byte */
+    u32 ke[4], ko[4], x[16];
+    fdr4_keys(d, pv3, ke, ko);
     auto ld = [&](int p, u32 a) {
         if (LOOKM) x[p] = ((look_m >> p) & 1u) ? lds_ld32a(a) : 0u;
         else x[p] = lds_ld32a(a);
@@ -688,7 +688,11 @@ __device__ __forceinline__ void fdr4_conf(const LitShared &L, const u32 (&d)[4],
     }
     fdr4_acc_even(x, U);
     /* odd key dword w (positions 4w + 1, 4w + 3) reaches ends 4w + 1 ..
-     * 4w + 6: conf dwords w and w + 1 */
+     * 4w + 6: gated on conf dwords w and w + 1 (lanes with one live end
+     * among 4w .. 4w + 7; 28 % of them on cfg-4 text).  One gate per slot
+     * (exact 4 ends: 15 % real lookups) measured slower -- 0.985 against
+     * 0.919 ms: its 20 more VALU per iteration cost more than the LDS
+     * conflicts it saves (profiles/r03_fdr4_gate_ab.txt). */
     u64 m[5];
 #pragma unroll
     for (int k = 0; k < 5; k++) m[k] = __ballot(U[k] != 0xffffffffu);
