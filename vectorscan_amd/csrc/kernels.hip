@@ -1798,13 +1798,18 @@ vsa_lit_scan(VsaLitParams P) {
         }
         /* runs: after the iteration at ib, move to the next block once the
          * sweep has reached it (blocks >= 1 KiB: at most one per iteration) */
+        /* the next block start as a 32-bit offset from the run's first byte
+         * (a run spans one segment), so the per-iteration test is a scalar
+         * compare, not a 64-bit vector one */
+        int32_t rn32 = run ? (int32_t)readlane_u32(rend0, 0) : INT32_MAX;
         auto run_adv = [&](int64_t ib) {
-            if (run && ib + 1024 >= S.run_nxt) {
+            if ((int32_t)(ib - S.blo) + 1024 >= rn32) {
                 rb++;
                 S.blk++;
-                S.run_nxt = rb + 1 >= gcount ? INT64_MAX
-                          : S.blo + (int64_t)(rb < 64 ? readlane_u32(rend0, rb)
-                                                      : readlane_u32(rend1, rb - 64));
+                const bool last = rb + 1 >= gcount;
+                const u32 nx = rb < 64 ? readlane_u32(rend0, rb) : readlane_u32(rend1, rb - 64);
+                S.run_nxt = last ? INT64_MAX : S.blo + (int64_t)nx;
+                rn32 = last ? INT32_MAX : (int32_t)nx;
             }
         };
         S.vlo = S.blo - (int64_t)B.hist;
