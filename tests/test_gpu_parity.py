@@ -645,3 +645,36 @@ def test_gpu_scanner_expansion(ctx, nlits, monkeypatch):
             rb[k + 1][:len(s) - cut] = s[cut:]
     want = [oracle.hwlm_exec(blob.ptr, bytes(b), cap=1 << 18)[1] for b in rb]
     assert run_layout_scan(ctx, blob, rb, 3) == want
+
+
+def test_gpu_plan_free_after_async_overflow():
+    """a plan freed while its asynchronous scan is still pending
+    -- a scan that overflows the output (its rescan reads the plan's tables)
+    -- is completed before the tables go (vsa_plan_free), and the scan's
+    count still reads back right; a plan outliving its context frees only
+    its own tables."""
+    ctx = vsa.Context(0)
+    lits = [vsa.HwlmLiteral(b"ab", False, 1), vsa.HwlmLiteral(b"bab", False, 2)]
+    blob = vsa.hwlm_build(lits)
+    n = 1 << 20
+    host = np.frombuffer(b"ab" * (n // 2), np.uint8)
+    want = n // 2 + (n // 2 - 1)  # every "ab", every "bab"
+    d = ctx.malloc(n + 64)
+    db = vsa.Database(ctx, blob)
+    try:
+        ctx.h2d(d, host)
+        for _ in range(2):
+            plan = ctx.plan(d, [0], [n])
+            ctx.scan_plan(db, plan, asynchronous=True)  # > 65,536 records: overflows
+            plan.close()                                  # completes the scan first
+            assert ctx.scan_wait() == want
+        plan = ctx.plan(d, [0], [n])
+        assert ctx.scan_plan(db, plan) == want
+        db.close()
+        ctx.free(d)
+        d = None
+        ctx.close()      # the plan outlives its context
+        plan.close()
+    finally:
+        if d is not None:
+            ctx.free(d)

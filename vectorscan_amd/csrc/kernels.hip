@@ -676,7 +676,12 @@ __device__ __forceinline__ void fdr4_conf(const LitShared &L, const u32 (&d)[4],
         ld(4 * w, tab_addr16x4<0>(ke[w], L.tab_lds));
         ld(4 * w + 2, tab_addr16x4<1>(ke[w], L.tab_lds));
     }
-    if (LOOKM) {
+#ifdef VSA_FDR4_ONE_LEVEL /* A/B: every lookup in every lane */
+    constexpr bool ONE = true;
+#else
+    constexpr bool ONE = LOOKM;
+#endif
+    if (ONE) {
 #pragma unroll
         for (int w = 0; w < 4; w++) {
             ld(4 * w + 1, tab_addr16x4<0>(ko[w], L.tab_lds));
