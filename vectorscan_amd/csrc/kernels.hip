@@ -1596,6 +1596,8 @@ vsa_lit_scan(VsaLitParams P) {
     /* provably wave-uniform: the confirm wave's s_setprio is a scalar
      * instruction that an EXEC-masked branch would run in every wave */
     const u32 wave = readfirstlane_u32(tid / WAVE);
+    /* diagnostic (dbg & 8192, wave log): the kernel's entry, before staging */
+    const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
 
     /* ---- stage tables into LDS ---- */
     u32 tab_bytes = 0;
@@ -1670,6 +1672,12 @@ vsa_lit_scan(VsaLitParams P) {
                                   mis, slots, pqx + (size_t)cw * PQ_ENTRIES(2), cw, NC,
                                   prof_lds + 8 * cw);
 #endif
+        if ((P.dbg & 8192) && P.wave_log && lane < 8) {
+            /* diagnostic: a confirm wave's entry and end */
+            const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+            P.wave_log[((size_t)blockIdx.x * LIT_WAVES + wave) * 8 + lane] =
+                lane == 0 ? t_entry : lane == 1 ? t_end : lane == 2 ? 1ull : 0ull;
+        }
         return;
     }
 
@@ -2021,7 +2029,7 @@ vsa_lit_scan(VsaLitParams P) {
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         const unsigned long long v[8] = {t_start, t_end, n_seg, n_iter, blockIdx.x, wave,
-                                         xcc, hwid};
+                                         xcc, (P.dbg & 8192) ? t_entry : hwid};
         unsigned long long x = 0;
 #pragma unroll
         for (int k = 0; k < 8; k++) x = (u32)k == lane ? v[k] : x;

@@ -416,7 +416,10 @@ uint64_t pick_seg_bytes(const std::vector<int64_t> &spans, uint64_t waves) {
                                  5-8 % faster for Teddy / noodle at 1 GiB */
     if (const char *e = getenv("VSA_SEG_MAX_KIB"))
         seg = (uint64_t)std::max(4, std::min(4096, atoi(e))) << 10;
-    while (seg > (4u << 10) && count(seg) < 2 * waves) seg >>= 1;
+    /* 1 KiB segments for inputs up to 64 KiB (the drop-ins: one short
+     * segment per scanning wave), else at least 4 KiB */
+    const uint64_t min_seg = total <= (64u << 10) ? (1u << 10) : (4u << 10);
+    while (seg > min_seg && count(seg) < 2 * waves) seg >>= 1;
     const uint64_t k = (count(seg) + waves - 1) / waves; /* rounds per wave */
     if (k >= 2) {
         uint64_t bal = (total + k * waves - 1) / (k * waves);
@@ -450,12 +453,28 @@ int bits_for(uint64_t v) {
 template <int MODE, bool LDS, bool XP = false>
 int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds) {
     auto fn = vsa_lit_scan<MODE, LDS, XP>;
-    VSA_CHECK(hipFuncSetAttribute((const void *)fn,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    uint64_t want = (P.nsegs + LIT_WAVES - 1) / LIT_WAVES;
+    /* the dynamic-LDS limit is raised once per device and kernel (the call
+     * costs a few us, a drop-in scan ~25 us) */
+    static std::atomic<int> lds_set[64];
+    std::atomic<int> &ls = lds_set[c->device & 63];
+    if (ls.load(std::memory_order_relaxed) < (int)lds) {
+        VSA_CHECK(hipFuncSetAttribute((const void *)fn,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        int cur = ls.load(std::memory_order_relaxed);
+        while (cur < (int)lds && !ls.compare_exchange_weak(cur, (int)lds)) {
+        }
+    }
+    const uint64_t ns = LIT_WAVES - P.nconf; /* scanning waves per workgroup */
+    uint64_t want = (P.nsegs + ns - 1) / ns;
     uint64_t cap = (uint64_t)c->num_cus; /* persistent: one 16-wave WG per CU */
     uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(LIT_THREADS), lds, c->stream, P);
+    /* at most one segment per scanning wave (small scans, the drop-ins):
+     * static assignment.  Dynamic tickets would cost every wave a walk over
+     * the drained regions, one returning atomic each (~5.5 us measured on a
+     * 1 KiB drop-in, profiles/r03_dropin_waves.txt) */
+    VsaLitParams Q = P;
+    if (Q.dynamic && Q.nsegs <= (uint64_t)grid * ns) Q.dynamic = 0;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(LIT_THREADS), lds, c->stream, Q);
     VSA_CHECK(hipGetLastError());
     return VSA_OK;
 }
