@@ -414,6 +414,24 @@ uint64_t pick_seg_bytes(const std::vector<int64_t> &spans, uint64_t waves) {
     for (int64_t sp : spans) total += (uint64_t)sp;
     uint64_t seg = 128 << 10; /* 64-256 KiB measured equal for FDR, 128 KiB
                                  5-8 % faster for Teddy / noodle at 1 GiB */
+    /* 16-192 KiB per scanning wave (the 2-8-GPU stripes of the 4 GiB corpus
+     * are 512 MiB-2 GiB, 136-546 KiB a wave): ~1.4 segments per wave.  A CU's waves scan at rates set by their age
+     * (issue priority, 1.82 down to 0.69 KiB/us), so its 8 oldest waves take
+     * two segments and the rest one; the balanced >= 2 rounds below pays
+     * more segment starts and ends on a young wave's last segment.  At 512
+     * MiB: 96 KiB segments 0.149 ms against 0.159 for 46 KiB (3 rounds);
+     * 64 / 128 / 192 / 256 MiB: -8 / -16 / -21 / -14 %; from 768 MiB up the
+     * rules tie (profiles/r03_seg_stripes.txt).  VSA_SEG_ROUNDS_OLD=1: the
+     * old rule. */
+    static const bool old_rule = getenv("VSA_SEG_ROUNDS_OLD") != nullptr;
+    if (!old_rule && !getenv("VSA_SEG_MAX_KIB") && ns <= 64 && total >= 16 * 1024 * waves &&
+        total <= 192 * 1024 * waves) {
+        uint64_t s = (uint64_t)((double)total / (1.42 * (double)waves));
+        s = (s + 1023) & ~(uint64_t)1023;
+        bool large = true; /* every block spans several such segments */
+        for (int64_t sp : spans) large = large && (uint64_t)sp >= 4 * s;
+        if (large) return s;
+    }
     if (const char *e = getenv("VSA_SEG_MAX_KIB"))
         seg = (uint64_t)std::max(4, std::min(4096, atoi(e))) << 10;
     /* 1 KiB segments for inputs up to 64 KiB (the drop-ins: one short
