@@ -22,10 +22,12 @@ union over ranks is exactly the single-GPU match set (strong scaling: total
 work fixed).  The timed region is bracketed by barrier + synchronize and the
 max over ranks is reported.
 
-Parity (every run): rank 0 checks the TIMED step's gathered match set, per
+Parity (every run): rank 0 checks the TIMED step's gathered records, per
 block, against the oracle (oracle/oracle.c, the scalar restatement) over all
-4 GiB: match count and an order-free (sum, xor) digest of the (end, id) pairs
-(`parity_bytes` = bytes checked), plus sortedness of the merged keys.
+4 GiB, order-exact: the block's (end, id) sequence as sorted on the device
+equals the oracle's callback sequence element for element (`parity_bytes` =
+bytes checked).  The end_to_end line's delivered (id, from, to) sequences are
+checked per block against oracle/hs_lit.py (digest + count).
 
 Extra JSON fields: roofline (rank 0's scan kernel from hipEvents vs the 8 TB/s
 MI355X peak; PMC traffic from profiles/), cpu_baseline (the SSE2 port of
@@ -128,19 +130,6 @@ def make_corpus_device(torch, lo, hi, total, lits, seed, plant_every, device, pl
     sel = (idx >= lo) & (idx < hi)
     if sel.any():
         out[torch.from_numpy(idx[sel] - lo).to(device)] = torch.from_numpy(val[sel]).to(device)
-    return out
-
-
-def block_digests(ends, ids, block_len, nblocks):
-    """per-block (count, sum, xor) digests of global (end, id) records"""
-    import oracle
-    ends = np.asarray(ends, np.uint64)
-    ids = np.asarray(ids, np.uint64)
-    blk = (ends // np.uint64(block_len)).astype(np.int64)
-    out = []
-    for b in range(nblocks):
-        sel = blk == b
-        out.append(oracle.digest_of(ends[sel] - np.uint64(b * block_len), ids[sel]))
     return out
 
 
@@ -379,30 +368,76 @@ def run(args):
         eng = vsa.engine_blob(blob)
         parity, parity_bytes, cpu = None, 0, None
         if not args.no_parity:
+            # order-exact: the timed step's (end, id) sequence of every block,
+            # in the order the device sort put it (end, bucket, LitInfo chain =
+            # the reference's callback order, fdr.c:299-333), equal element
+            # for element to the oracle's callback sequence of that block
             ends = keys >> np.uint64(24)
-            sorted_ok = bool(np.all(keys[1:] >= keys[:-1])) if len(keys) > 1 else True
-            got = block_digests(ends, ids, bl, nblocks)
-            want, t_cpu, cpu_ok = [], 0.0, True
+            blk = ends // np.uint64(bl)
+            bad, t_cpu, cpu_ok = [], 0.0, True
+            n_want = 0
+            e2e_chk = e2e is not None and "_digests" in e2e
+            if e2e_chk:
+                # the end-to-end line's delivered sequences vs oracle/hs_lit.py:
+                # the same patterns compiled by the restatement, their HWLM
+                # blob from the product builder (byte-identical to the hs
+                # database's, tests/test_hs_lit.py), its records through the
+                # restated report program, per block
+                import oracle.hs_lit as ohl
+                from vectorscan_amd import hs
+                odb = ohl.compile_lit_multi([l.s for l in lits],
+                                            [ohl.CASELESS if l.nocase else 0 for l in lits],
+                                            [l.id for l in lits])
+                oblob = vsa.hwlm_build([vsa.HwlmLiteral(t, nc, f, noruns=nr)
+                                        for t, nc, f, nr in odb.hwlm_literals()])
+                oeng = vsa.engine_blob(oblob)
+                e2e_bad = []
             for b in range(nblocks):
                 lo, hi = b * bl, min(total, (b + 1) * bl)
                 host = make_corpus_device(torch, lo, hi, total, lits, 5, plant_every, dev,
                                           pplan).cpu().numpy()
-                want.append(oracle.digest_mt(eng, host, threads))
+                if e2e_chk:
+                    he, hi_ = oracle.records_mt(oeng, host, threads, nood=oblob.is_noodle)
+                    seq = ohl.scan_records(odb, host, zip(he.tolist(), hi_.tolist()))
+                    if (hs.seq_digest(seq) != e2e["_digests"][b] or
+                            len(seq) != e2e["_counts"][b]):
+                        e2e_bad.append(b)
+                oe, oi = oracle.records_mt(eng, host, threads)
+                n_want += len(oe)
+                sel = blk == np.uint64(b)
+                ge, gi = ends[sel] - np.uint64(lo), ids[sel]
+                # the block's records are one contiguous run of the sequence
+                run = np.flatnonzero(sel)
+                contiguous = len(run) == 0 or run[-1] - run[0] + 1 == len(run)
+                if not (contiguous and len(ge) == len(oe) and np.array_equal(ge, oe) and
+                        np.array_equal(gi.astype(np.uint32), oi)):
+                    bad.append(b)
                 if with_cpu:
                     # CPU baseline: the SSE2 port of fdr.c's main loop
                     # (get_conf_stride_1 :145-213 + confirm), same bytes,
-                    # same host threads; its result must match as well
+                    # same host threads; its match set must equal the oracle's
                     tc = time.perf_counter()
                     d = oracle.digest_mt(eng, host, threads, simd=True)
                     t_cpu += time.perf_counter() - tc
-                    cpu_ok = cpu_ok and d == want[-1]
+                    cpu_ok = cpu_ok and d == oracle.digest_of(oe, oi)
                 parity_bytes += hi - lo
                 del host
-            parity = (sorted_ok and got == want and sum(w[0] for w in want) == nm and
+            parity = (not bad and n_want == nm and len(keys) == nm and
                       all(c == nm for c in counts))
             if not parity:
-                print("bench: PARITY FAILURE got %s want %s sorted %s" % (got, want, sorted_ok),
-                      file=sys.stderr, flush=True)
+                print("bench: PARITY FAILURE in blocks %s (records %d, oracle %d)" %
+                      (bad, nm, n_want), file=sys.stderr, flush=True)
+            if e2e_chk:
+                e2e["parity"] = not e2e_bad
+                e2e["parity_kind"] = ("order-exact: per-block digest of the delivered "
+                                      "(id, from, to) callback sequence and its count vs "
+                                      "oracle/hs_lit.py over all %d bytes" % parity_bytes)
+                if e2e_bad:
+                    print("bench: END-TO-END PARITY FAILURE in blocks %s" % e2e_bad,
+                          file=sys.stderr, flush=True)
+        if e2e is not None:
+            e2e.pop("_digests", None)
+            e2e.pop("_counts", None)
             if with_cpu:
                 cpu = {"value": round(parity_bytes / t_cpu / 1e9, 4), "unit": "GB/s",
                        "cores": threads, "kind": "port", "match_set_equal": cpu_ok,
@@ -442,6 +477,8 @@ def run(args):
             "confirm_candidates": ncand,
             "parity": parity,
             "parity_bytes": parity_bytes,
+            "parity_kind": "order-exact: every block's (end, id) sequence equal element for "
+                           "element to the oracle's callback sequence",
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "kernel_ms": round(kavg, 4),
@@ -472,7 +509,12 @@ def end_to_end(lits, d_data, bl, nblocks, total, hwlm_records, reps):
     through the report program and counted; `reps` passes pipelined
     (vsa_hs_corpus_scan_repeats: pass k + 1 scans on the GPU while the host
     replays pass k), after 60 untimed passes (compiling the database idles
-    the GPU long enough for its clock to drop: the same settle as `value`)."""
+    the GPU long enough for its clock to drop: the same settle as `value`).
+    Every pass replays every record through the report program into a
+    callback (the per-block sequence digests ask for it; without them a
+    one-record-one-match database only counts on the GPU); the last pass's
+    per-block digests of the delivered (id, from, to) sequences are returned
+    under "_digests" for the parity check against oracle/hs_lit.py."""
     from vectorscan_amd import hs
     db = hs.compile_lit_multi([l.s for l in lits],
                               [hs.FLAG_CASELESS if l.nocase else 0 for l in lits],
@@ -483,20 +525,21 @@ def end_to_end(lits, d_data, bl, nblocks, total, hwlm_records, reps):
     corpus = hs.Corpus(db, scratch, d_data, offs, lens)
     try:
         for _ in range(2):
-            rc, _, _, _ = corpus.scan_repeats(30)
+            rc, _, _, _ = corpus.scan_repeats(30, digests=True)
             if rc:
                 return {"error": rc}
         t0 = time.perf_counter()
-        rc, tot, _, _ = corpus.scan_repeats(reps)
+        rc, tot, cnt, dg = corpus.scan_repeats(reps, counts=True, digests=True)
         el = time.perf_counter() - t0
         if rc:
             return {"error": rc}
         return {"value": round(total * reps / el / 1e9, 3), "unit": "GB/s",
                 "ms_per_pass": round(el / reps * 1e3, 4), "passes": reps,
                 "matches_per_pass": int(tot[-1]), "hwlm_records": int(hwlm_records),
-                "what": "hs_scan of each block with every match delivered to the host "
-                        "(pure-literal hs database of the same literals; pipelined passes, "
-                        "16 replay threads)"}
+                "what": "hs_scan of each block with every match delivered to a host callback "
+                        "through the report program (pure-literal hs database of the same "
+                        "literals; pipelined passes, replay threads per block)",
+                "_digests": [int(x) for x in dg], "_counts": [int(x) for x in cnt]}
     finally:
         corpus.close()
         scratch.close()

@@ -311,6 +311,28 @@ def digest_mt(engine_ptr, data, nthreads, nood=False, simd=False):
     return int(n), int(out[0]), int(out[1])
 
 
+_sig("orc_records_mt", ctypes.c_long, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+     ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+
+
+def records_mt(engine_ptr, data, nthreads, nood=False, cap=1 << 24):
+    """(ends, ids) of the block scan in the reference's callback order
+    (oracle.c orc_records_mt: `nthreads` stripes with a 7-byte halo,
+    concatenated in stripe order).  Raises if more than `cap` records."""
+    buf = np.ascontiguousarray(data, dtype=np.uint8)
+    for _ in range(2):
+        ends = np.zeros(cap, np.uint64)
+        ids = np.zeros(cap, np.uint32)
+        n = _lib.orc_records_mt(engine_ptr, int(nood), buf.ctypes.data, len(buf), int(nthreads),
+                                ends.ctypes.data, ids.ctypes.data, cap)
+        if n < 0:
+            raise RuntimeError("orc_records_mt failed")
+        if n <= cap:
+            return ends[:n], ids[:n]
+        cap = n
+    raise RuntimeError("orc_records_mt: record count changed between runs")
+
+
 def mix64(x):
     """splitmix64 finalizer over a uint64 numpy array (oracle.c orc_mix64)."""
     with np.errstate(over="ignore"):

@@ -188,19 +188,29 @@ class _Run:
                 return False
         return True
 
-    def write(self, blob_ptr, data, out, stop_after=None):
-        """One write (pureLiteralStreamExec; offset 0 = block mode)."""
-        data_b = bytes(data) if not hasattr(data, "tobytes") else data.tobytes()
+    def write(self, blob_ptr, data, out, stop_after=None, recs=None):
+        """One write (pureLiteralStreamExec; offset 0 = block mode).  recs:
+        the write's HWLM records [(end, fragment)] in callback order when the
+        caller has them already (oracle.records_mt over a large block)."""
         off = self.length
         tail = self.buf[max(0, len(self.buf) - self.keep):]
         self.buf_off = off - len(tail)
-        self.buf = tail + data_b
-        self.length += len(data_b)
-        if not data_b:
-            return
-        if off == 0:
-            _, recs = oracle.hwlm_exec(blob_ptr, data, cap=4096)
+        if recs is not None and self.keep <= SHORT:
+            # given records and no pattern past the 8-byte tail: the report
+            # program reads no bytes, so a large block is not copied
+            n = len(data)
+            self.buf = b""
+            self.buf_off = off + n
         else:
+            data_b = bytes(data) if not hasattr(data, "tobytes") else data.tobytes()
+            n = len(data_b)
+            self.buf = tail + data_b
+        self.length += n
+        if not n:
+            return
+        if recs is None and off == 0:
+            _, recs = oracle.hwlm_exec(blob_ptr, data, cap=4096)
+        elif recs is None:
             hl = min(off, self.db.history_required)
             hist = tail[len(tail) - hl:]
             _, recs = oracle.hwlm_exec_stream(blob_ptr, hist, data, cap=4096)
@@ -223,6 +233,16 @@ def scan(db, blob_ptr, data, stop_after=None):
     if db.min_width > len(data):
         return out
     _Run(db).write(blob_ptr, data, out, stop_after)
+    return out
+
+
+def scan_records(db, data, recs):
+    """hs_scan of one block whose HWLM records (end, fragment) the caller
+    computed (oracle.records_mt): the report program over them."""
+    out = []
+    if db.min_width > len(data):
+        return out
+    _Run(db).write(None, data, out, None, recs)
     return out
 
 

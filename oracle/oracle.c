@@ -110,6 +110,23 @@ static inline u64a orc_mix64(u64a x) {
 }
 
 static u64a emit(cbctx *c, u64a end, u32 id) {
+    if (c->digest == 2) {
+        /* record mode (orc_records_mt): every end >= drop_below, in callback
+         * order, into a growing array */
+        if (end >= c->drop_below) {
+            if (c->n == c->cap) {
+                const size_t nc = c->cap ? 2 * c->cap : 4096;
+                orc_match *o = (orc_match *)realloc(c->out, nc * sizeof(orc_match));
+                if (!o) return 0; /* terminate: the caller sees the short count */
+                c->out = o;
+                c->cap = nc;
+            }
+            c->out[c->n].end = c->base + end;
+            c->out[c->n].id = id;
+            c->n++;
+        }
+        return c->ret_groups;
+    }
     if (c->digest) {
         if (end >= c->drop_below) {
             const u64a m = orc_mix64(((c->base + end) << 32) ^ id);
@@ -1133,6 +1150,42 @@ long orc_digest_mt2(const void *eng, int nood, int simd, const u8 *buf, size_t l
         if (n >= 0) n += (long)jobs[t].cb.n;
         out[0] += jobs[t].cb.dsum;
         out[1] ^= jobs[t].cb.dxor;
+    }
+    return n;
+}
+
+/* The same striped scan, keeping every record: (end, id) in the reference's
+ * callback order (fdr.c:299-333 per stripe; stripes are contiguous ranges of
+ * ends, so their concatenation in stripe order is the single call's order).
+ * Writes min(total, cap) records to ends / ids and returns the total (-1 on
+ * a failed stripe or allocation).  bench.py's order-exact parity check. */
+long orc_records_mt(const void *eng, int nood, const u8 *buf, size_t len, int nthreads,
+                    u64a *ends, u32 *ids, size_t cap) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    if ((size_t)nthreads > len / 64 + 1) nthreads = (int)(len / 64 + 1);
+    orc_mt_job jobs[256];
+    pthread_t th[256];
+    const size_t s = len / (size_t)nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        const size_t lo = (size_t)t * s, hi = t == nthreads - 1 ? len : lo + s;
+        const size_t blo = lo >= 7 ? lo - 7 : 0;
+        cbctx cb = {NULL, 0, 0, -1, ~0ULL, 2, lo - blo, blo, 0, 0};
+        jobs[t] = (orc_mt_job){eng, nood, 0, buf + blo, hi - blo, cb, 0};
+        if (pthread_create(&th[t], NULL, orc_mt_run, &jobs[t]) != 0) return -1;
+    }
+    long n = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        if (jobs[t].status != 0) n = -1;
+        for (size_t i = 0; n >= 0 && i < jobs[t].cb.n; i++) {
+            if ((size_t)n < cap) {
+                ends[n] = jobs[t].cb.out[i].end;
+                ids[n] = jobs[t].cb.out[i].id;
+            }
+            n++;
+        }
+        free(jobs[t].cb.out);
     }
     return n;
 }

@@ -223,6 +223,42 @@ def test_digest_matches_oracle_list():
         assert oracle.digest_mt(vsa.engine_blob(blob), data, t) == want
 
 
+def test_records_mt_is_the_callback_sequence():
+    """oracle.records_mt (bench.py's order-exact full-corpus check) == the
+    single-call oracle's callback sequence element for element, for any
+    thread count, and a small cap still reports the total"""
+    blob, data = _corpus_case(3, 300000, 300000)
+    _, m = oracle.fdr_exec(vsa.engine_blob(blob), data, cap=1 << 20)
+    assert len(m) > 100
+    for t in (1, 2, 7, 16):
+        e, i = oracle.records_mt(vsa.engine_blob(blob), data, t)
+        assert list(zip(e.tolist(), i.tolist())) == m
+    e, i = oracle.records_mt(vsa.engine_blob(blob), data, 3, cap=10)
+    assert list(zip(e.tolist(), i.tolist())) == m
+
+
+def test_hs_scan_records_equals_scan():
+    """oracle.hs_lit.scan_records over records_mt's records == hs_lit.scan
+    (bench.py's end-to-end check), for short-only and long-literal sets"""
+    import bench
+    from oracle import hs_lit as ohl
+    data = bench.make_corpus(200000, bench.make_literals(50, seed=4), seed=6, plant_every=512)
+    for maxlen in (8, 16):
+        ex, fl, ids = bench.make_mixed_set(300, seed=5, maxlen=maxlen)
+        # plant some of the set's own patterns
+        d = data.copy()
+        for k, p in enumerate(range(100, 190000, 997)):
+            s = ex[k % len(ex)]
+            d[p:p + len(s)] = np.frombuffer(s, np.uint8)
+        odb = ohl.compile_lit_multi(ex, fl, ids)
+        blob = vsa.hwlm_build([vsa.HwlmLiteral(t, nc, f, noruns=nr)
+                               for t, nc, f, nr in odb.hwlm_literals()])
+        want = ohl.scan(odb, blob.ptr, d)
+        e, i = oracle.records_mt(vsa.engine_blob(blob), d, 5, nood=blob.is_noodle)
+        got = ohl.scan_records(odb, d, zip(e.tolist(), i.tolist()))
+        assert len(want) > 50 and got == want
+
+
 def _packed_worker(rank, world, port, q):
     import torch
     os.environ["MASTER_ADDR"] = "127.0.0.1"

@@ -633,8 +633,6 @@ int vsa_hs_scan_vector(const vsa_hs_database_t *db, const char *const *data,
     if (!scratch || !data || !length) return VSA_HS_INVALID;
     if (!valid_db(db)) return VSA_HS_INVALID;
     if (db->mode != VSA_HS_MODE_VECTORED) return VSA_HS_DB_MODE_ERROR;
-    /* one launch: at most VSA_MAX_BLOCKS pieces (vectorscan_amd.h) */
-    if (count > VSA_MAX_BLOCKS) return VSA_HS_INVALID;
     int rc = enter(db, scratch);
     if (rc != VSA_HS_SUCCESS) return rc;
     unsigned n = 0;
@@ -642,8 +640,17 @@ int vsa_hs_scan_vector(const vsa_hs_database_t *db, const char *const *data,
     std::vector<size_t> lens(length, length + n);
     vsa_hs_stream st;
     init_stream(&st, db);
-    rc = scan_writes(&st, scratch, (const uint8_t *const *)data, lens.data(), n, onEvent,
-                     context);
+    /* one launch holds at most VSA_MAX_BLOCKS non-empty pieces (empty ones
+     * are not launched): a longer vector is scanned as consecutive launches
+     * of the same stream, its state (offset, history, exhaustion) carried
+     * across, which is what the reference's per-piece stream writes do */
+    const uint8_t *const *bufs = (const uint8_t *const *)data;
+    for (unsigned i0 = 0; i0 < n && rc == VSA_HS_SUCCESS;) {
+        unsigned i1 = i0, live = 0;
+        while (i1 < n && (live < VSA_MAX_BLOCKS || !lens[i1])) live += lens[i1++] != 0;
+        rc = scan_writes(&st, scratch, bufs + i0, lens.data() + i0, i1 - i0, onEvent, context);
+        i0 = i1;
+    }
     leave(scratch);
     if (rc != VSA_HS_SUCCESS) return rc;
     return n < count ? VSA_HS_INVALID : VSA_HS_SUCCESS;
@@ -1239,8 +1246,8 @@ int vsa_hs_clone_scratch(const vsa_hs_scratch_t *src, vsa_hs_scratch_t **dest) {
     *dest = nullptr;
     vsa_hs_scratch *s = new (std::nothrow) vsa_hs_scratch;
     if (!s) return VSA_HS_NOMEM;
-    const char *dev = getenv("VSA_DEVICE"); /* as vsa_hs_alloc_scratch */
-    if (vsa_ctx_create(dev ? atoi(dev) : 0, &s->ctx) != VSA_OK) {
+    /* the source's GPU, whatever VSA_DEVICE says now */
+    if (!src->ctx || vsa_ctx_create(vsa::ctxDevice(src->ctx), &s->ctx) != VSA_OK) {
         delete s;
         return VSA_HS_NOMEM;
     }

@@ -250,12 +250,13 @@ struct vsa_db {
     uint8_t slot_bits[16] = {0}; /* prefilter hash bits per bucket (<= nBits) */
     uint64_t pf_mult = 0;
     bool flood_live = false;     /* some FDRFlood record can fire (idCount < max) */
-    /* confirm waves per workgroup, set once from the confirm-candidate rate
-     * of the first representative launch (>= 16 MiB) of the db on any
-     * context; atomic, as dbs are shared by contexts and threads.  It feeds
-     * the segment sizes, so a db's launch plans change at most once. */
+    /* confirm waves per workgroup: the largest count the confirm-candidate
+     * rate of any representative launch (>= 16 MiB) of the db asked for, on
+     * any context (a sparse first launch, e.g. a warm-up, does not pin a
+     * dense db to one wave); atomic, as dbs are shared by contexts and
+     * threads.  It only grows (1 -> 2 -> 3) and feeds the segment sizes, so
+     * a db's launch plans change at most twice. */
     mutable std::atomic<uint32_t> nconf{1};
-    mutable std::atomic<bool> nconf_set{false};
 };
 
 /* confirm waves for a measured confirm-candidate rate (candidates per
@@ -853,10 +854,12 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     c->last_cand = w.h_counters[2];
     /* adapt the db's confirm-wave count to the measured candidate rate
      * (over a representative launch; not under diagnostic flags) */
-    if (c->launch.db && c->launch.bytes >= (16u << 20) && !getenv("VSA_DEBUG_FLAGS") &&
-        !c->launch.db->nconf_set.exchange(true))
-        c->launch.db->nconf.store(
-            nconf_for_rate((double)c->last_cand / (double)c->launch.bytes));
+    if (c->launch.db && c->launch.bytes >= (16u << 20) && !getenv("VSA_DEBUG_FLAGS")) {
+        const uint32_t want = nconf_for_rate((double)c->last_cand / (double)c->launch.bytes);
+        uint32_t cur = c->launch.db->nconf.load(std::memory_order_relaxed);
+        while (want > cur && !c->launch.db->nconf.compare_exchange_weak(cur, want)) {
+        }
+    }
     if (getenv("VSA_DEBUG_FLAGS") && w.h_counters[3]) {
         fprintf(stderr, "vsa: %llu queued confirm keys differ from HBM\n",
                 (unsigned long long)w.h_counters[3]);
@@ -2504,6 +2507,10 @@ struct vsa_batcher {
     std::condition_variable cv_req, cv_done;
     std::deque<Req *> q;
     bool stop = false;
+    /* callers inside vsa_batcher_hwlmExec that still hold m or will re-lock
+     * it (counted under m); destroy waits for zero before freeing m / cv */
+    uint32_t inflight = 0;
+    std::condition_variable cv_idle;
     std::thread worker;
     uint64_t batches = 0, calls = 0;
 
@@ -2627,6 +2634,12 @@ int vsa_batcher_destroy(vsa_batcher_t *b) {
     }
     b->cv_req.notify_all();
     b->worker.join();
+    {
+        /* the worker finished every queued call before exiting; wait for
+         * their callers to leave the mutex (a woken caller re-locks it) */
+        std::unique_lock<std::mutex> lk(b->m);
+        b->cv_idle.wait(lk, [&] { return b->inflight == 0; });
+    }
     delete b;
     return VSA_OK;
 }
@@ -2652,11 +2665,16 @@ hwlm_error_t vsa_batcher_hwlmExec(vsa_batcher_t *b, const struct HWLM *tab, cons
     r.len = len;
     r.start = start;
     {
+        /* destroy may run concurrently: a call that finds it stopping is
+         * refused; one already queued is served (the worker drains the
+         * queue before it exits) and is counted until it has left m */
         std::unique_lock<std::mutex> lk(b->m);
         if (b->stop) return HWLM_ERROR_UNKNOWN;
+        b->inflight++;
         b->q.push_back(&r);
         b->cv_req.notify_one();
         b->cv_done.wait(lk, [&] { return r.done; });
+        if (--b->inflight == 0 && b->stop) b->cv_idle.notify_all();
     }
     if (r.rc != VSA_OK || !r.db) return HWLM_ERROR_UNKNOWN;
     if (r.db->type == HWLM_ENGINE_NOOD)
@@ -2677,6 +2695,7 @@ hwlm_error_t vsa_batcher_hwlmExec(vsa_batcher_t *b, const struct HWLM *tab, cons
  * callback context (no Rose scratch: no INCLUDED_JUMP squash). */
 namespace vsa {
 /* the host copy of a loaded database's HWLM blob (vsa_internal.h) */
+int ctxDevice(const struct vsa_ctx *c) { return c ? c->device : 0; }
 int dbHostBlob(const struct vsa_db *db, const uint8_t **blob, size_t *size) {
     if (!db || !blob || !size) return VSA_E_INVALID;
     *blob = db->hblob;

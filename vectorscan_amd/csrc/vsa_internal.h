@@ -106,6 +106,9 @@ void truffleMasks(const u8 cls[32], u8 m1[16], u8 m2[16]);
 /* the host copy of a loaded database's HWLM blob (hs_clone_scratch reloads
  * it into another context) */
 int dbHostBlob(const struct vsa_db *db, const uint8_t **blob, size_t *size);
+/* the GPU a context was created on (hs_clone_scratch builds the clone's
+ * context on the source's device) */
+int ctxDevice(const struct vsa_ctx *c);
 
 } // namespace vsa
 

@@ -247,6 +247,11 @@ class PackedGather:
             counts = [h & ~NOT_READY for h in hdr]
             if any(h & NOT_READY for h in hdr):
                 raise RuntimeError("PackedGather: records still not final after the rescan")
+            if max(counts) > self.cap:
+                # a count that grew after complete() would make merged()
+                # slice past the keys region: fail rather than return junk
+                raise RuntimeError("PackedGather: %d records exceed the regrown capacity %d"
+                                   % (max(counts), self.cap))
         return counts
 
     def merged(self, counts):
