@@ -8,7 +8,9 @@ HARNESS := tests/c/abi_harness
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
             -Wno-unused-parameter -Iinclude
 
-all: $(LIB) $(ORACLE) $(HARNESS)
+DROPIN := tools/dropin_threads
+
+all: $(LIB) $(ORACLE) $(HARNESS) $(DROPIN)
 
 $(CSRC)/compile.o: $(CSRC)/compile.cpp $(CSRC)/hs_layout.h $(CSRC)/vsa_internal.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -41,7 +43,14 @@ $(HARNESS): tests/c/abi_harness.c include/vectorscan_amd.h $(LIB) $(ORACLE)
 	    -Loracle/_build -loracle -Wl,-rpath,'$$ORIGIN/../../vectorscan_amd' \
 	    -Wl,-rpath,'$$ORIGIN/../../oracle/_build'
 
+# measurement tool: small drop-in calls from POSIX threads (GPU, batcher,
+# the oracle's SSE2 port as the CPU comparator)
+$(DROPIN): tools/dropin_threads.c include/vectorscan_amd.h $(LIB) $(ORACLE)
+	gcc -O2 -std=gnu11 -Wall -Iinclude $< -o $@ -Lvectorscan_amd -lvectorscan_amd \
+	    -Loracle/_build -loracle -pthread -Wl,-rpath,'$$ORIGIN/../vectorscan_amd' \
+	    -Wl,-rpath,'$$ORIGIN/../oracle/_build'
+
 clean:
-	rm -f $(CSRC)/*.o $(LIB) $(ORACLE) $(HARNESS)
+	rm -f $(CSRC)/*.o $(LIB) $(ORACLE) $(HARNESS) $(DROPIN)
 
 .PHONY: all clean

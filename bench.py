@@ -31,8 +31,9 @@ checked per block against oracle/hs_lit.py (digest + count).
 
 Extra JSON fields: roofline (rank 0's scan kernel from hipEvents vs the 8 TB/s
 MI355X peak; PMC traffic from profiles/), cpu_baseline (the SSE2 port of
-the reference FDR main loop over the same 4 GiB on the host's 16-thread
-share, its match set checked too).
+the reference FDR main loop over the same 4 GiB, one pinned thread per
+physical core the process may use, capped by the cgroup CPU quota, its match
+set checked too).
 """
 import argparse
 import json
@@ -364,7 +365,12 @@ def run(args):
     with_cpu = not args.no_cpu and world == 1
     if rank == 0:
         import oracle
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        # one pinned thread per physical core the process may use, no more
+        # than the cgroup quota lets run at once (the GPU box: 16 CPUs of
+        # quota over 256 visible; tools/exp_cpu_threads.py sweeps the count)
+        pins, quota, visible, phys = host_cpu_share()
+        threads = args.cpu_threads or max(1, min(len(pins), int(quota) if quota else len(pins)))
+        oracle.set_pin(pins)
         eng = vsa.engine_blob(blob)
         parity, parity_bytes, cpu = None, 0, None
         if not args.no_parity:
@@ -441,6 +447,8 @@ def run(args):
             if with_cpu:
                 cpu = {"value": round(parity_bytes / t_cpu / 1e9, 4), "unit": "GB/s",
                        "cores": threads, "kind": "port", "match_set_equal": cpu_ok,
+                       "pinned": "one thread per physical core", "physical_cores": phys,
+                       "cpus_visible": visible, "cpu_quota": quota,
                        "sample": "the whole %d-byte corpus, 4 x 1 GiB blocks: oracle/oracle.c "
                                  "SSE2 port of the reference FDR main loop (fdr.c:145-333, "
                                  "m128 state, flood checks) on the reference bytecode's own "
@@ -550,6 +558,33 @@ def blob_domain(blob):
     """FDR.domain of the blob's engine (fdr_internal.h:69-85, byte 25)"""
     import ctypes
     return ctypes.string_at(blob.ptr + 192 + 25, 1)[0]
+
+
+def host_cpu_share():
+    """The host CPUs this process may use (the CPU baseline runs
+    one pinned thread per physical core): the affinity set, one CPU per
+    physical core (/sys topology: lowest-numbered sibling), and the cgroup
+    CPU quota (cpu.max), which caps how many of them can run at once.
+    Returns (pin list, quota CPUs or None, visible CPUs, physical cores)."""
+    allowed = sorted(os.sched_getaffinity(0))
+    cores = {}
+    for c in allowed:
+        try:
+            base = "/sys/devices/system/cpu/cpu%d/topology/" % c
+            key = (open(base + "physical_package_id").read().strip(),
+                   open(base + "core_id").read().strip())
+        except OSError:
+            key = ("?", str(c))
+        cores.setdefault(key, c)
+    pins = sorted(cores.values())
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    return pins, quota, os.cpu_count() or len(allowed), len(pins)
 
 
 def _cpu_model():

@@ -306,6 +306,12 @@ int vsa_class_scan(vsa_ctx_t *ctx, const uint8_t cls[32], const uint8_t *cls2,
                    const uint8_t *d_data, uint64_t len, uint64_t *d_bitmap,
                    uint64_t *first, uint64_t *last, uint64_t *count,
                    uint32_t flags);
+/* The same over a shufti (kind 0: lo, hi) or truffle (kind 1: m1, m2) mask
+ * pair, the bytecode shuftiExec / truffleExec take (shufti.h:46,
+ * truffle.h:45): the class is the set of bytes the masks accept. */
+int vsa_class_scan_masks(vsa_ctx_t *ctx, int kind, const uint8_t a[16], const uint8_t b[16],
+                         const uint8_t *d_data, uint64_t len, uint64_t *d_bitmap,
+                         uint64_t *first, uint64_t *last, uint64_t *count);
 
 /* ------------------------------------------------------------------ *
  * Part 3 — HWLM bytecode builder (reference layout; see compile.cpp)

@@ -311,6 +311,35 @@ def digest_mt(engine_ptr, data, nthreads, nood=False, simd=False):
     return int(n), int(out[0]), int(out[1])
 
 
+_sig("orc_shufti_bitmap", ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+     ctypes.c_size_t, ctypes.c_void_p)
+_sig("orc_truffle_bitmap", ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+     ctypes.c_size_t, ctypes.c_void_p)
+
+
+def class_bitmap_of_masks(kind, a, b, data):
+    """(bitmap as uint64 words, member count) of every position's shufti
+    (kind "shufti": lo, hi) or truffle ("truffle": m1, m2) verdict, from the
+    masks (oracle.c orc_shufti_bitmap / orc_truffle_bitmap)."""
+    buf = np.ascontiguousarray(data, dtype=np.uint8)
+    bits = np.zeros((len(buf) + 63) // 64, np.uint64)
+    ma = ctypes.create_string_buffer(bytes(a), 16)
+    mb = ctypes.create_string_buffer(bytes(b), 16)
+    fn = _lib.orc_shufti_bitmap if kind == "shufti" else _lib.orc_truffle_bitmap
+    n = fn(ma, mb, buf.ctypes.data, len(buf), bits.ctypes.data)
+    return bits, int(n)
+
+
+_sig("orc_set_pin", None, ctypes.c_void_p, ctypes.c_int)
+
+
+def set_pin(cpus):
+    """pin the multi-threaded harness's thread t to cpus[t % len(cpus)]
+    (empty: no pinning)"""
+    arr = (ctypes.c_int * max(1, len(cpus)))(*cpus)
+    _lib.orc_set_pin(arr, len(cpus))
+
+
 _sig("orc_records_mt", ctypes.c_long, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
      ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 

@@ -28,6 +28,7 @@
  * blobs the tests build carry idCount == FDR_FLOOD_MAX_IDS for every char,
  * under which the reference's floodDetect never changes the scan.
  */
+#define _GNU_SOURCE 1 /* pthread_setaffinity_np (the harness pinning) */
 #include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -232,6 +233,36 @@ long orc_shufti_double(const u8 *lo1, const u8 *hi1, const u8 *lo2, const u8 *hi
 static inline int truffle_member(const u8 *m1, const u8 *m2, u8 c) {
     const u8 *m = (c & 0x80) ? m2 : m1;
     return (m[c & 0xf] >> ((c >> 4) & 7)) & 1;
+}
+
+/* Every position's verdict as a bitmap (bit i & 63 of word i >> 6), from
+ * the masks (the cfg-2 full-buffer check): shufti_simd.hpp:63-76 /
+ * x86/shufti.hpp blockSingleMask (lo[c & 15] & hi[c >> 4] != 0 per byte)
+ * and truffle_simd.hpp:56-61 / x86/truffle.hpp blockSingleMask
+ * (truffle_member above).  Returns the member count. */
+long orc_shufti_bitmap(const u8 *lo, const u8 *hi, const u8 *buf, size_t len, u64a *bits) {
+    long n = 0;
+    memset(bits, 0, ((len + 63) / 64) * sizeof(u64a));
+    for (size_t i = 0; i < len; i++) {
+        const u8 c = buf[i];
+        if (lo[c & 0xf] & hi[c >> 4]) {
+            bits[i >> 6] |= 1ULL << (i & 63);
+            n++;
+        }
+    }
+    return n;
+}
+
+long orc_truffle_bitmap(const u8 *m1, const u8 *m2, const u8 *buf, size_t len, u64a *bits) {
+    long n = 0;
+    memset(bits, 0, ((len + 63) / 64) * sizeof(u64a));
+    for (size_t i = 0; i < len; i++) {
+        if (truffle_member(m1, m2, buf[i])) {
+            bits[i >> 6] |= 1ULL << (i & 63);
+            n++;
+        }
+    }
+    return n;
 }
 
 long orc_truffle(const u8 *m1, const u8 *m2, const u8 *buf, size_t len) {
@@ -1100,6 +1131,7 @@ u64a orc_fdr_candidates(const void *eng, const u8 *buf, size_t len) {
  * which is sequential host state: the digests cover the confirmed set).
  * Output: the match count and the (sum, xor) digest of the (end, id) set. */
 #include <pthread.h>
+#include <sched.h>
 
 typedef struct {
     const void *eng;
@@ -1108,10 +1140,27 @@ typedef struct {
     size_t len;
     cbctx cb;
     int status;
+    int t; /* thread index (pinning) */
 } orc_mt_job;
+
+/* optional pinning of the harness threads (bench.py's cpu_baseline: one
+ * thread per physical core): thread t runs on g_pin[t % g_npin] */
+static int g_pin[1024], g_npin = 0;
+void orc_set_pin(const int *cpus, int n) {
+    g_npin = n < 0 ? 0 : (n > 1024 ? 1024 : n);
+    for (int i = 0; i < g_npin; i++) g_pin[i] = cpus[i];
+}
+static void orc_pin_self(int t) {
+    if (!g_npin) return;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(g_pin[t % g_npin], &set);
+    pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
 
 static void *orc_mt_run(void *p) {
     orc_mt_job *j = (orc_mt_job *)p;
+    orc_pin_self(j->t);
     if (j->nood) j->status = nood_run((const struct o_nood *)j->eng, j->buf, j->len, 0, &j->cb);
     else j->status = fdr_dispatch_s(j->eng, j->buf, j->len, 0, ~0ULL, &j->cb, j->simd);
     return NULL;
@@ -1139,7 +1188,7 @@ long orc_digest_mt2(const void *eng, int nood, int simd, const u8 *buf, size_t l
         const size_t lo = (size_t)t * s, hi = t == nthreads - 1 ? len : lo + s;
         const size_t blo = lo >= 7 ? lo - 7 : 0;
         cbctx cb = {NULL, 0, 0, -1, ~0ULL, 1, lo - blo, blo, 0, 0};
-        jobs[t] = (orc_mt_job){eng, nood, simd, buf + blo, hi - blo, cb, 0};
+        jobs[t] = (orc_mt_job){eng, nood, simd, buf + blo, hi - blo, cb, 0, t};
         if (pthread_create(&th[t], NULL, orc_mt_run, &jobs[t]) != 0) return -1;
     }
     long n = 0;
@@ -1171,7 +1220,7 @@ long orc_records_mt(const void *eng, int nood, const u8 *buf, size_t len, int nt
         const size_t lo = (size_t)t * s, hi = t == nthreads - 1 ? len : lo + s;
         const size_t blo = lo >= 7 ? lo - 7 : 0;
         cbctx cb = {NULL, 0, 0, -1, ~0ULL, 2, lo - blo, blo, 0, 0};
-        jobs[t] = (orc_mt_job){eng, nood, 0, buf + blo, hi - blo, cb, 0};
+        jobs[t] = (orc_mt_job){eng, nood, 0, buf + blo, hi - blo, cb, 0, t};
         if (pthread_create(&th[t], NULL, orc_mt_run, &jobs[t]) != 0) return -1;
     }
     long n = 0;

@@ -563,3 +563,30 @@ def test_simd_fdr_equals_scalar_oracle(hint):
                 a = oracle.fdr_exec(vsa.engine_blob(blob), data, start=start, cap=1 << 18)
                 b = oracle.fdr_exec_simd(vsa.engine_blob(blob), data, start=start, cap=1 << 18)
                 assert a == b, (trial, ln, start)
+
+
+@pytest.mark.parametrize("kind", ["shufti", "truffle"])
+def test_class_bitmap_of_masks(kind):
+    """oracle.class_bitmap_of_masks (the cfg-2 full-buffer check) agrees with
+    the oracle's own first / last scans over the same masks and with
+    membership of the class the masks were built from."""
+    rng = np.random.default_rng(7)
+    for nchars in (0, 1, 8, 60, 200):
+        chars = bytes(rng.choice(256, nchars, replace=False).astype(np.uint8))
+        data = rng.integers(0, 256, 20000 + nchars, dtype=np.uint8)
+        if kind == "shufti":
+            m = vsa.shufti_build_masks(chars) if chars else (bytes(16), bytes(16))
+            if m is None:
+                continue
+            first, last = oracle.shufti(*m, data), oracle.shufti(*m, data, reverse=True)
+        else:
+            m = vsa.truffle_build_masks(chars)
+            first, last = oracle.truffle(*m, data), oracle.truffle(*m, data, reverse=True)
+        bits, n = oracle.class_bitmap_of_masks(kind, m[0], m[1], data)
+        member = np.isin(data, np.frombuffer(chars, np.uint8))
+        assert np.array_equal(bits.view(np.uint8)[:(len(data) + 7) // 8],
+                              np.packbits(member, bitorder="little"))
+        idx = np.flatnonzero(member)
+        assert n == len(idx)
+        assert first == (idx[0] if len(idx) else len(data))
+        assert last == (idx[-1] if len(idx) else -1)

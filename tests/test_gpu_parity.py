@@ -232,26 +232,33 @@ def test_gpu_fdr_5k_64mib(ctx):
     assert len(m) >= (64 << 20) // (64 << 10)
 
 
-def test_gpu_class_scan_256mib(ctx):
-    """cfg-2: 256 MiB uniform bytes, class A; bitmap == numpy membership."""
+@pytest.mark.parametrize("kind", ["shufti", "truffle"])
+def test_gpu_class_scan_256mib(ctx, kind):
+    """cfg-2: 256 MiB uniform bytes, class A, driven by the shufti / truffle
+    masks (vsa_class_scan_masks: the class the bytecode accepts, derived as
+    the drop-ins do): bitmap, count, first and last == the oracle's per-byte
+    mask test over the whole buffer (orc_shufti_bitmap / orc_truffle_bitmap),
+    and that equals numpy membership of the class's characters."""
     rng = np.random.default_rng(2)
     n = 256 << 20
     data = rng.integers(0, 256, n, dtype=np.uint8)
     chars = [0x01, 0x7F, 0x80, 0xFE, ord("<"), ord(">"), ord('"'), ord("'")]
-    cls = vsa.class_bitmap(chars)
+    a, b = (vsa.shufti_build_masks(bytes(chars)) if kind == "shufti"
+            else vsa.truffle_build_masks(bytes(chars)))
     dbuf = ctx.malloc(n)
     dbm = ctx.malloc(n // 8)
     try:
         ctx.h2d(dbuf, data)
-        f, l, cnt = ctx.class_scan(cls, dbuf, n, d_bitmap=dbm)
-        bm = np.zeros(n // 8, np.uint8)
+        f, l, cnt = ctx.class_scan_masks(kind, a, b, dbuf, n, d_bitmap=dbm)
+        bm = np.zeros(n // 64, np.uint64)
         ctx.d2h(bm, dbm)
     finally:
         ctx.free(dbuf)
         ctx.free(dbm)
+    want, want_n = oracle.class_bitmap_of_masks(kind, a, b, data)
+    assert np.array_equal(bm, want) and cnt == want_n
     member = np.isin(data, np.array(chars, np.uint8))
-    exp = np.packbits(member, bitorder="little")
-    assert np.array_equal(bm, exp)
+    assert np.array_equal(bm.view(np.uint8), np.packbits(member, bitorder="little"))
     idx = np.nonzero(member)[0]
     assert cnt == len(idx) and f == idx[0] and l == idx[-1] + 1
 

@@ -420,15 +420,25 @@ def test_reference_literal_grid(case):
 @pytest.mark.gpu
 def test_hs_block_limit_is_invalid():
     """one launch takes at most VSA_MAX_BLOCKS blocks (the records carry a
-    20-bit block index): a larger hs corpus or hs_scan_vector call is
-    refused with HS_INVALID, not a misleading NOMEM / UNKNOWN_ERROR"""
+    20-bit block index): an hs_scan_vector call with more non-empty pieces
+    is scanned as consecutive launches of one stream (the reference has no
+    such limit), empty pieces do not count, and a larger prepared hs corpus
+    is refused with HS_INVALID, not a misleading NOMEM / UNKNOWN_ERROR"""
     limit = 1 << 20
     db = hs.compile_lit_multi([b"abcd"], [0], [1], hs.MODE_VECTORED)
     scratch = hs.Scratch(db)
     try:
         one = b"abcd"
-        rc, _ = hs.scan_vector(db, [one] * (limit + 1), scratch)
-        assert rc == hs.INVALID
+        rc, out = hs.scan_vector(db, [one] * (limit + 1), scratch)
+        assert rc == hs.SUCCESS and len(out) == limit + 1
+        assert out[0] == (1, 0, 4) and out[-1] == (1, 0, 4 * (limit + 1))
+        assert all(out[k][2] == 4 * (k + 1) for k in range(0, limit + 1, 4099))
+        rc, out = hs.scan_vector(db, [b""] * (limit + 5) + [one], scratch)
+        assert rc == hs.SUCCESS and out == [(1, 0, 4)]
+        # a match across the launch boundary: "ab" ends the first launch's
+        # last piece, "cd" starts the next launch
+        rc, out = hs.scan_vector(db, [b"xxxx"] * (limit - 1) + [b"xxab", b"cdxx"], scratch)
+        assert rc == hs.SUCCESS and out == [(1, 0, 4 * limit + 2)]
         rc, out = hs.scan_vector(db, [one] * 4, scratch)
         assert rc == hs.SUCCESS and len(out) == 4
     finally:

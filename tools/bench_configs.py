@@ -130,6 +130,13 @@ def cfg_stream(ctx, torch, steps, warmup, chunk):
 
 
 def cfg_class(ctx, torch, steps, warmup):
+    """cfg 2: the shufti / truffle bytecode (the masks shufticompile /
+    trufflecompile build) scanned over 256 MiB through vsa_class_scan_masks,
+    which derives the class from the masks as the drop-ins do; parity = the
+    whole bitmap, count, first and last against the oracle's per-byte mask
+    test (orc_shufti_bitmap / orc_truffle_bitmap), plus membership of the
+    intended characters (the masks accept exactly the class)"""
+    import oracle
     import vectorscan_amd as vsa
     n = 256 << 20
     g = torch.Generator(device="cuda")
@@ -143,30 +150,25 @@ def cfg_class(ctx, torch, steps, warmup):
     for name, chars, kind in (("cfg2 shufti class A (8 chars)", classA, "shufti"),
                               ("cfg2 truffle class B (100 bytes)", classB, "truffle"),
                               ("cfg2 shufti no-match", b"", "shufti")):
-        if kind == "shufti" and chars:
-            lo, hi = vsa.shufti_build_masks(chars)
-            cls = vsa.class_bitmap(chars)
-        elif kind == "shufti":
-            cls = np.zeros(32, np.uint8)
+        if kind == "shufti":
+            a, b = vsa.shufti_build_masks(chars) if chars else (bytes(16), bytes(16))
         else:
-            m1, m2 = vsa.truffle_build_masks(chars)
-            cls = vsa.class_bitmap(chars)
+            a, b = vsa.truffle_build_masks(chars)
         res = [None]
 
         def step():
-            res[0] = ctx.class_scan(cls, data.data_ptr(), n, bitmap.data_ptr())
+            res[0] = ctx.class_scan_masks(kind, a, b, data.data_ptr(), n, bitmap.data_ptr())
 
         kms, wall = timed(step, steps, warmup, ctx)
         f, l, c = res[0]
+        want_bm, want_n = oracle.class_bitmap_of_masks(kind, a, b, host)
+        got_bm = bitmap.cpu().numpy().view(np.uint64)[:len(want_bm)]
         member = np.zeros(256, bool)
         member[list(chars)] = True
-        hits = member[host]
-        idx = np.flatnonzero(hits)
-        want_bm = np.packbits(hits, bitorder="little").view(np.int64)
-        ok = (c == len(idx) and f == (idx[0] if len(idx) else n) and
-              l == (idx[-1] + 1 if len(idx) else 0) and
-              np.array_equal(bitmap.cpu().numpy()[:len(want_bm)], want_bm))
-        line(name, n, kms, wall, n // 8, bool(ok), {"hits": int(c)})
+        idx = np.flatnonzero(member[host])
+        ok = (c == want_n == len(idx) and f == (idx[0] if len(idx) else n) and
+              l == (idx[-1] + 1 if len(idx) else 0) and np.array_equal(got_bm, want_bm))
+        line(name, n, kms, wall, n // 8, bool(ok), {"hits": int(c), "masks": kind})
     del data, bitmap
 
 

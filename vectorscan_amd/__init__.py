@@ -163,6 +163,8 @@ _sig("vsa_scan_kernel_ms", ctypes.c_double, ctypes.c_void_p)
 _sig("vsa_class_scan", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, _u64p,
      _u64p, _u64p, ctypes.c_uint32)
+_sig("vsa_class_scan_masks", ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, _u64p, _u64p, _u64p)
 _sig("vsa_version", ctypes.c_char_p)
 _sig("vsa_set_scratch_layout", None, ctypes.c_long, ctypes.c_long)
 _sig("vsa_get_scratch_layout", None, ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_long))
@@ -772,6 +774,17 @@ class Context:
                                   None if c2 is None else c2.ctypes.data, d_data,
                                   length, d_bitmap, ctypes.byref(f), ctypes.byref(l),
                                   ctypes.byref(c), 0))
+        return f.value, l.value, c.value
+
+    def class_scan_masks(self, kind, a, b, d_data, length, d_bitmap=None):
+        """vsa_class_scan_masks: the shufti (kind "shufti": lo, hi) or truffle
+        ("truffle": m1, m2) masks over a device buffer -> (first, last, count)"""
+        ma = ctypes.create_string_buffer(bytes(a), 16)
+        mb = ctypes.create_string_buffer(bytes(b), 16)
+        f, l, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib.vsa_class_scan_masks(self.ptr, 0 if kind == "shufti" else 1, ma, mb, d_data,
+                                        length, d_bitmap, ctypes.byref(f), ctypes.byref(l),
+                                        ctypes.byref(c)))
         return f.value, l.value, c.value
 
     def close(self):

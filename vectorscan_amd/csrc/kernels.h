@@ -141,6 +141,13 @@ struct VsaLitParams {
                                     (nullptr: no binned sort, or the separate
                                     histogram launch) */
     uint32_t bin_shift;
+    uint32_t *bin_slots;         /* staged binned sort (vsa_bin_finish): the
+                                    output slot of record s of bin b goes to
+                                    [b * VSA_SORT_BIN_MAX + s] (s from the
+                                    returning count atomic; a bin past
+                                    VSA_SORT_BIN_MAX sets
+                                    counters[VSA_CTR_BIN_OVERFLOW]); nullptr:
+                                    the count-only histogram */
     unsigned long long *wave_log; /* diagnostic (dbg bit12): 8 u64 per scanning
                                      wave: start, end (100 MHz), segments,
                                      KiB iterations, workgroup, wave, XCC, HW_ID */

@@ -363,6 +363,19 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
             tot += (u32)__popcll(pm);
         }
         if (tot) {
+            /* staged binned sort: every match's bin slot (returning atomics,
+             * issued with the output reservation: one round trip for both) */
+            u32 bslot[CONF_U], bix[CONF_U];
+            if (P.bin_slots) {
+#pragma unroll
+                for (int i = 0; i < CONF_U; i++) {
+                    bix[i] = (u32)((base[i] + (u64)e[i]) >> P.bin_shift);
+                    if (mt[i])
+                        bslot[i] = __hip_atomic_fetch_add(&P.bin_counts[bix[i]], 1u,
+                                                          __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
             unsigned long long s0 = 0;
             if (lane_id() == 0) s0 = atomicAdd(&P.counters[0], (unsigned long long)tot);
             const u64 sb = ((u64)readlane_u32((u32)(s0 >> 32), 0) << 32) | readlane_u32((u32)s0, 0);
@@ -375,11 +388,19 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
                                        ((u64)b[i] << VSA_KEY_BUCKET_SHIFT) | lidx;
                     P.out_ids[slot] = w1[i].z;
                 }
-                /* the binned sort's histogram (an overflowed launch's counts
-                 * are zeroed by its sort launch and never used) */
-                if (mt[i] && P.bin_counts)
+                if (mt[i] && P.bin_slots) {
+                    /* the record's output slot, staged in its bin (an
+                     * overflowed output or bin leaves the sort to the host) */
+                    if (bslot[i] < VSA_SORT_BIN_MAX)
+                        P.bin_slots[bix[i] * VSA_SORT_BIN_MAX + bslot[i]] = (u32)slot;
+                    else
+                        P.counters[VSA_CTR_BIN_OVERFLOW] = 1;
+                } else if (mt[i] && P.bin_counts) {
+                    /* the count-only histogram (an overflowed launch's counts
+                     * are zeroed by its sort launch and never used) */
                     __hip_atomic_fetch_add(&P.bin_counts[(u32)((base[i] + (u64)e[i]) >> P.bin_shift)],
                                            1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
         }
 #pragma unroll
@@ -1452,13 +1473,28 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                 consumed += n;
                 for (; hits; hits &= hits - 1, slot++) {
                     const u32 j = __ffs(hits) - 1;
+                    const u64 key = (p0 + j - mis) << VSA_KEY_END_SHIFT;
                     if (slot < P.out_cap) {
-                        P.out_keys[slot] = (p0 + j - mis) << VSA_KEY_END_SHIFT;
+                        P.out_keys[slot] = key;
                         P.out_ids[slot] = P.nood_id;
                     }
-                    if (P.bin_counts)
-                        __hip_atomic_fetch_add(&P.bin_counts[(u32)((p0 + j - mis) >> P.bin_shift)],
-                                               1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (P.bin_counts) {
+                        const u32 bin = (u32)((p0 + j - mis) >> P.bin_shift);
+                        if (P.bin_slots) {
+                            /* staged binned sort (vsa_bin_finish) */
+                            const u32 s = __hip_atomic_fetch_add(&P.bin_counts[bin], 1u,
+                                                                 __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT);
+                            if (s < VSA_SORT_BIN_MAX) {
+                                P.bin_slots[(size_t)bin * VSA_SORT_BIN_MAX + s] = (u32)slot;
+                            } else {
+                                P.counters[VSA_CTR_BIN_OVERFLOW] = 1;
+                            }
+                        } else {
+                            __hip_atomic_fetch_add(&P.bin_counts[bin], 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    }
                 }
             }
             continue;
@@ -2246,6 +2282,128 @@ __global__ void __launch_bounds__(256) vsa_publish(unsigned long long *ctr,
                                                    const uint64_t *keys, const uint32_t *ids,
                                                    uint32_t kmax) {
     publish_body(ctr, h, seq, nzero, keys, ids, kmax);
+}
+
+/* Staged binned sort, the one launch behind a scan (runtime.hip
+ * queue_bin_sort): the scan wrote every record's output slot into its bin's
+ * staging slots (bin_slots, VSA_SORT_BIN_MAX per bin) as it counted it, so
+ * no scatter pass is needed: the records are gathered through them.  Workgroup w owns bins [64 w, 64 w + 64): it
+ * sums the counts of every earlier bin itself (<= 64 KiB of L2 reads; no
+ * hand-off between workgroups, which on this chip costs an agent-scope
+ * release per workgroup), scans its own 64 counts, and each of its 16 waves
+ * sorts 4 bins in registers -- one bitonic network of S = the next power of
+ * two >= the largest of the 4 counts, 64 / S bins per pass -- and writes
+ * them to their sorted positions.  It also zeroes the same bins of the other
+ * count buffer (the next launch counts there: the buffers alternate, since
+ * this launch still reads its own), and workgroup 0 publishes the counters
+ * to the host (publish_body) at its start: the count and the overflow flags
+ * are final when the scan ends, and everything that reads the sorted records
+ * is queued on the stream behind this launch.  A bin past VSA_SORT_BIN_MAX
+ * (flagged by the scan) or an output past out_cap leaves the output to the
+ * host's library sort / rescan, which read the scan's unsorted records. */
+#define FIN_BINS 64 /* bins per workgroup (1024 threads, 16 waves x 4) */
+__global__ void __launch_bounds__(1024) vsa_bin_finish(const uint32_t *counts, uint32_t *counts_next,
+                                                     const uint32_t *slots, const uint64_t *ikeys,
+                                                     const uint32_t *iids, uint64_t *okeys,
+                                                     uint32_t *oids,
+                                                     uint64_t out_cap, unsigned long long *ctr,
+                                                     unsigned long long *h,
+                                                     unsigned long long seq) {
+    __shared__ u32 red[16], cnt[FIN_BINS], off[FIN_BINS];
+    const u32 t = threadIdx.x, wv = t / WAVE, lane = lane_id();
+    const u32 b0 = blockIdx.x * FIN_BINS;
+    /* the records of every bin before b0 */
+    u32 s = 0;
+    for (u32 i = t; i < b0 / 4; i += 1024) {
+        const uint4 v = ((const uint4 *)counts)[i];
+        s += v.x + v.y + v.z + v.w;
+    }
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) s += shfl_xor_u32(s, dd);
+    if (lane == 0) red[wv] = s;
+    if (t < FIN_BINS) {
+        cnt[t] = counts[b0 + t];
+        counts_next[b0 + t] = 0;
+    }
+    __syncthreads();
+    if (wv == 0) {
+        u32 base = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) base += red[k];
+        u32 tot;
+        const u32 e = wave_excl_scan(cnt[lane], &tot);
+        off[lane] = base + e;
+    }
+    if (blockIdx.x == 0) publish_body(ctr, h, seq, 144u, nullptr, nullptr, 0u);
+    __syncthreads();
+    /* this wave's 4 bins */
+    const u32 lb = wv * 4;
+    u32 m[4], mmax = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        m[j] = cnt[lb + j];
+        mmax = m[j] > mmax ? m[j] : mmax;
+    }
+    if (mmax == 0 || mmax > VSA_SORT_BIN_MAX) return; /* empty, or left to the library sort */
+    u32 S = 2;
+    while (S < mmax) S <<= 1;
+    const u32 per = WAVE / S; /* bins per pass (1..32; >= 4 covers all 4 in one) */
+    const u32 j_l = lane / S, r = lane % S;
+    u64 k[4];
+    u32 id[4], jb[4];
+    bool ok[4];
+    /* every pass's loads issued together: the staged output slots, then
+     * the records they point at (a slot past out_cap: the output overflowed,
+     * the host rescans) */
+    u32 at[4];
+#pragma unroll
+    for (u32 p = 0; p < 4; p++) {
+        const u32 j = p * per + j_l;
+        jb[p] = j;
+        const u32 mj = j == 0 ? m[0] : j == 1 ? m[1] : j == 2 ? m[2] : j == 3 ? m[3] : 0u;
+        ok[p] = p * per < 4 && r < mj;
+        at[p] = ~0u;
+        if (ok[p]) at[p] = slots[(size_t)(b0 + lb + j) * VSA_SORT_BIN_MAX + r];
+    }
+#pragma unroll
+    for (u32 p = 0; p < 4; p++) {
+        k[p] = ~0ULL;
+        id[p] = 0;
+        if (ok[p] && at[p] < out_cap) {
+            k[p] = ikeys[at[p]];
+            id[p] = iids[at[p]];
+        }
+    }
+#pragma unroll
+    for (u32 p = 0; p < 4; p++) {
+        if (p * per >= 4) break; /* wave-uniform */
+        u64 kk = k[p];
+        u32 ii = id[p];
+        for (u32 size = 2; size <= S; size <<= 1) {
+            for (u32 jj = size >> 1; jj > 0; jj >>= 1) {
+                const u32 plo = shfl_xor_u32((u32)kk, (int)jj);
+                const u32 phi = shfl_xor_u32((u32)(kk >> 32), (int)jj);
+                const u32 pid = shfl_xor_u32(ii, (int)jj);
+                const u64 pk = ((u64)phi << 32) | plo;
+                /* ascending within each S-lane segment: the last merge is
+                 * ascending everywhere, earlier ones alternate */
+                const bool up = size == S || (lane & size) == 0;
+                const bool lower = (lane & jj) == 0;
+                const bool take = (lower == up) ? (pk < kk) : (pk > kk);
+                if (take) {
+                    kk = pk;
+                    ii = pid;
+                }
+            }
+        }
+        if (ok[p]) {
+            const u64 o = (u64)off[lb + jb[p]] + r;
+            if (o < out_cap) {
+                okeys[o] = kk;
+                oids[o] = ii;
+            }
+        }
+    }
 }
 
 /* A binned scan's sorted records packed for a collective, on the device

@@ -51,6 +51,11 @@ __global__ void vsa_bin_scatter(const uint64_t *keys, const uint32_t *ids, const
                                 uint64_t *okeys, uint32_t *oids);
 __global__ void vsa_bin_sort(const uint64_t *ctr, uint64_t cap, uint32_t *counts,
                              const uint32_t *cursor, uint64_t *keys, uint32_t *ids);
+__global__ void vsa_bin_finish(const uint32_t *counts, uint32_t *counts_next,
+                               const uint32_t *slots, const uint64_t *ikeys, const uint32_t *iids,
+                               uint64_t *okeys, uint32_t *oids, uint64_t out_cap,
+                               unsigned long long *ctr,
+                               unsigned long long *h, unsigned long long seq);
 __global__ void vsa_class_scan_lut(VsaClassParams P, uint64_t span);
 __global__ void vsa_publish(unsigned long long *ctr, unsigned long long *h, unsigned long long seq,
                             uint32_t nzero, const uint64_t *keys, const uint32_t *ids,
@@ -103,8 +108,12 @@ struct Workspace {
     void *d_tmp = nullptr;
     size_t tmp_bytes = 0;
     unsigned long long *d_counters = nullptr; /* layout above */
-    uint32_t *d_bins = nullptr; /* binned sort: counts[VSA_SORT_BINS], cursor[..],
-                                   then 2 done counters (last-workgroup launches) */
+    uint32_t *d_bins = nullptr; /* binned sort: two count buffers of
+                                   VSA_SORT_BINS, used in turn (staged sort,
+                                   vsa_bin_finish) or counts + cursor (the
+                                   scatter chain, VSA_OLD_SORT) */
+    /* staged output slots of the binned sort: VSA_SORT_BIN_MAX per bin */
+    uint32_t *d_bslots = nullptr;
     unsigned long long *h_counters = nullptr; /* pinned mirror */
     /* fine-grained host memory the device publishes a binned scan's
      * counters into (vsa_publish): [0] = sequence, [1..16] = counters */
@@ -180,7 +189,8 @@ struct vsa_ctx {
     bool sort_join = false;
     double last_kernel_ms = 0.0;
     uint32_t bin_skip = 0;   /* launches left without the binned sort */
-    bool bins_clean = false; /* the bin counts are zero (no memset needed) */
+    bool bins_clean[2] = {false, false}; /* bin count buffer b is zero (no memset) */
+    uint32_t bin_par = 0;                /* the count buffer the next binned scan uses */
     /* host bytes already in ws.d_in (set only inside one drop-in call, so the
      * accel pre-skip and the literal scan share one upload) */
     const uint8_t *res_host = nullptr;
@@ -566,8 +576,32 @@ bool sep_hist() {
     return v;
 }
 
+/* VSA_OLD_SORT=1 (A/B knob): the round-3 chain behind a binned scan --
+ * count-only histogram in the scan, then vsa_bin_scan, vsa_bin_scatter,
+ * vsa_bin_sort and vsa_publish (four launches) -- instead of the staged
+ * sort (records staged per bin by the scan, one vsa_bin_finish launch) */
+bool old_sort() {
+    static const bool v = getenv("VSA_OLD_SORT") != nullptr || sep_hist();
+    return v;
+}
+
+uint32_t *bin_counts_of(vsa_ctx *c, uint32_t par) {
+    return c->ws.d_bins + (old_sort() ? 0u : par * VSA_SORT_BINS);
+}
+
 int queue_bin_sort(vsa_ctx *c, hipStream_t st) {
     Workspace &w = c->ws;
+    if (!old_sort()) {
+        const uint32_t par = c->bin_par;
+        hipLaunchKernelGGL(vsa_bin_finish, dim3(VSA_SORT_BINS / 64), dim3(1024), 0, st,
+                           bin_counts_of(c, par), bin_counts_of(c, par ^ 1u), w.d_bslots,
+                           w.d_keys[0], w.d_ids[0], w.d_keys[1], w.d_ids[1], (uint64_t)w.out_cap,
+                           c->ws.d_counters, c->ws.d_pub, (unsigned long long)++c->pub_seq);
+        VSA_CHECK(hipGetLastError());
+        c->bins_clean[par ^ 1u] = true;
+        c->bin_par = par ^ 1u;
+        return VSA_OK;
+    }
     uint32_t *counts = w.d_bins, *cursor = w.d_bins + VSA_SORT_BINS;
     const uint32_t shift = bin_shift_for(c->launch.end_bits);
     if (sep_hist())
@@ -629,9 +663,14 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
     /* not for the drop-in calls, whose few records the host sorts (a
      * larger result takes the library sort) */
     c->launch.bins = use_bins(c) && !(c->launch.flags & SCAN_HOST_SORT_SMALL);
-    if (c->launch.bins && !c->bins_clean)
-        VSA_CHECK(hipMemsetAsync(c->ws.d_bins, 0, VSA_SORT_BINS * sizeof(uint32_t), c->stream));
-    c->bins_clean = false;
+    if (c->launch.bins && !old_sort() && !c->ws.d_bslots)
+        VSA_CHECK(hipMalloc(&c->ws.d_bslots,
+                            (size_t)VSA_SORT_BINS * VSA_SORT_BIN_MAX * sizeof(uint32_t)));
+    const uint32_t par = old_sort() ? 0u : c->bin_par;
+    if (c->launch.bins && !c->bins_clean[par])
+        VSA_CHECK(hipMemsetAsync(bin_counts_of(c, par), 0, VSA_SORT_BINS * sizeof(uint32_t),
+                                 c->stream));
+    c->bins_clean[par] = false;
     /* drop-in calls (a few records, sorted by the host) skip the kernel
      * timing and get their counters and records published (no copies) */
     const bool small = (c->launch.flags & SCAN_HOST_SORT_SMALL) != 0;
@@ -672,7 +711,7 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
         VSA_CHECK(hipEventRecord(c->ev_sorted, st));
         c->sort_join = true;
     }
-    c->bins_clean = true;
+    if (old_sort()) c->bins_clean[0] = true; /* vsa_bin_sort zeroed the counts */
     c->launch.published = true;
     c->ctr_clean = true;
     return VSA_OK;
@@ -701,8 +740,9 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         P.out_keys = w.d_keys[0];
         P.out_ids = w.d_ids[0];
         P.out_cap = w.out_cap;
-        P.bin_counts = c->launch.bins && !sep_hist() ? w.d_bins : nullptr;
+        P.bin_counts = c->launch.bins && !sep_hist() ? bin_counts_of(c, c->bin_par) : nullptr;
         P.bin_shift = bin_shift_for(c->launch.end_bits);
+        P.bin_slots = c->launch.bins && !old_sort() ? w.d_bslots : nullptr;
         P.counters = w.d_counters;
         P.wave_log = g_wave_log;
         {
@@ -740,8 +780,9 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.out_keys = w.d_keys[0];
     P.out_ids = w.d_ids[0];
     P.out_cap = w.out_cap;
-    P.bin_counts = c->launch.bins && !sep_hist() ? w.d_bins : nullptr;
+    P.bin_counts = c->launch.bins && !sep_hist() ? bin_counts_of(c, c->bin_par) : nullptr;
     P.bin_shift = bin_shift_for(c->launch.end_bits);
+    P.bin_slots = c->launch.bins && !old_sort() ? w.d_bslots : nullptr;
     P.counters = w.d_counters;
     P.wave_log = g_wave_log;
     {
@@ -1605,6 +1646,7 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (w.d_in) (void)hipFree(w.d_in);
     if (w.d_counters) (void)hipFree(w.d_counters);
     if (w.d_bins) (void)hipFree(w.d_bins);
+    if (w.d_bslots) (void)hipFree(w.d_bslots);
     if (w.h_counters) (void)hipHostFree(w.h_counters);
     if (w.h_pub) (void)hipHostFree(w.h_pub);
     if (w.h_in) (void)hipHostFree(w.h_in);
@@ -2184,6 +2226,21 @@ int vsa_scan_debug_counters(vsa_ctx_t *c, uint64_t out[16]) {
 }
 
 double vsa_scan_kernel_ms(vsa_ctx_t *c) { return c ? c->last_kernel_ms : 0.0; }
+
+/* The shufti / truffle bytecode (masks, shufticompile.cpp:54 /
+ * trufflecompile.cpp:60) over a device buffer: the class the masks accept,
+ * as the drop-ins derive it (cls_from_shufti / cls_from_truffle), through
+ * vsa_class_scan.  kind 0: shufti (a = lo, b = hi); 1: truffle (a = m1,
+ * b = m2). */
+int vsa_class_scan_masks(vsa_ctx_t *c, int kind, const uint8_t a[16], const uint8_t b[16],
+                         const uint8_t *d_data, uint64_t len, uint64_t *d_bitmap,
+                         uint64_t *first, uint64_t *last, uint64_t *count) {
+    if (!a || !b || (kind != 0 && kind != 1)) return VSA_E_INVALID;
+    uint8_t cls[32];
+    if (kind == 0) cls_from_shufti(a, b, cls);
+    else cls_from_truffle(a, b, cls);
+    return vsa_class_scan(c, cls, nullptr, d_data, len, d_bitmap, first, last, count, 0);
+}
 
 int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
                    const uint8_t *d_data, uint64_t len, uint64_t *d_bitmap, uint64_t *first,
