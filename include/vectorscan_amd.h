@@ -256,6 +256,13 @@ int vsa_scan_blocks_stream(vsa_ctx_t *ctx, const vsa_db_t *db, const uint8_t *d_
  * be NULL).  At most 2^20 blocks per batch.  A plan belongs to its context
  * and must outlive the scans that use it. */
 typedef struct vsa_plan vsa_plan_t;
+/* Host-only: the schedule (segment descriptors, per-workgroup list bounds)
+ * the planner makes for a batch on num_cus CUs with ns scanning waves each,
+ * for tests and tools; returns the word count. */
+int vsa_plan_describe(const uint8_t *d_data, const uint64_t *offsets, const uint64_t *lens,
+                      const uint64_t *starts, const uint64_t *hlens, const uint64_t *report_lo,
+                      uint32_t nblocks, uint32_t num_cus, uint32_t ns, uint32_t *words,
+                      uint64_t cap, uint64_t *nsegs, uint32_t *grid);
 int vsa_plan_create(vsa_ctx_t *ctx, const uint8_t *d_data, const uint64_t *offsets,
                     const uint64_t *lens, const uint64_t *starts, const uint64_t *hlens,
                     const uint64_t *report_lo, uint32_t nblocks, vsa_plan_t **plan);

@@ -1,0 +1,139 @@
+"""CPU tests of the scan schedule (runtime.hip build_plan, through the
+host-only vsa_plan_describe): whatever the block layout, the segments cover
+every live block's span exactly once, in order, and the per-workgroup lists
+(kernels.hip dynamic 2: one list per workgroup, no global tickets) give
+every workgroup an equal share of the bytes -- stealing balances waves only
+inside a workgroup, so a workgroup with more bytes than its share would set
+the kernel's end."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+import vectorscan_amd as vsa
+
+lib = vsa.lib
+lib.vsa_plan_describe.restype = ctypes.c_int
+lib.vsa_plan_describe.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5 + [
+    ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64,
+    ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]
+
+
+def describe(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000):
+    o = np.ascontiguousarray(offs, np.uint64)
+    ln = np.ascontiguousarray(lens, np.uint64)
+    st = None if starts is None else np.ascontiguousarray(starts, np.uint64)
+    n = ctypes.c_uint64()
+    g = ctypes.c_uint32()
+    w = lib.vsa_plan_describe(base, o.ctypes.data, ln.ctypes.data,
+                              None if st is None else st.ctypes.data, None, None, len(o),
+                              num_cus, ns, None, 0, ctypes.byref(n), ctypes.byref(g))
+    assert w >= 0
+    words = np.zeros(w, np.uint32)
+    lib.vsa_plan_describe(base, o.ctypes.data, ln.ctypes.data,
+                          None if st is None else st.ctypes.data, None, None, len(o), num_cus,
+                          ns, words.ctypes.data, w, ctypes.byref(n), ctypes.byref(g))
+    nseg, grid = n.value, g.value
+    desc = words[:4 * nseg].reshape(-1, 4)
+    bounds = words[4 * nseg:] if grid else None
+    return desc, bounds, grid
+
+
+def spans(offs, lens, starts, base):
+    """each block's scanned span from its 1 KiB-aligned origin (build_plan)"""
+    mis = base & 15
+    out = []
+    for o, ln, st in zip(offs, lens, starts):
+        blo = o + mis
+        org = (blo + max(0, st - 16)) & ~1023
+        out.append(blo + ln - org if st < ln else -1)
+    return out
+
+
+def check(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000):
+    starts = list(starts) if starts is not None else [0] * len(offs)
+    desc, bounds, grid = describe(offs, lens, starts, num_cus, ns, base)
+    sp = spans(offs, lens, starts, base)
+    covered = {}
+    seg_bytes = []
+    for k, (info, off_kib, len_kib, _) in enumerate(desc.tolist()):
+        first, cnt = info & 0xffffff, info >> 24
+        if cnt:
+            for b in range(first, first + cnt):
+                assert sp[b] >= 0 and b not in covered, (k, b)
+                covered[b] = "group"
+            seg_bytes.append(sum(sp[b] for b in range(first, first + cnt)))
+        else:
+            b = first
+            end = covered.get(b, 0)
+            assert end != "group"
+            # parts of a block come in order, back to back, 1 KiB aligned
+            assert off_kib * 1024 == end, (k, b, off_kib, end)
+            assert len_kib > 0
+            covered[b] = min(sp[b], off_kib * 1024 + len_kib * 1024)
+            seg_bytes.append(covered[b] - end)
+    for b, s in enumerate(sp):
+        if s < 0:
+            assert b not in covered
+        else:
+            assert covered.get(b) in ("group", s), (b, covered.get(b), s)
+    T = sum(s for s in sp if s >= 0)
+    if grid:
+        assert 1 <= grid <= num_cus and len(bounds) == grid + 1
+        assert bounds[0] == 0 and bounds[-1] == len(desc)
+        assert np.all(np.diff(bounds.astype(np.int64)) >= 0)
+        per = [sum(seg_bytes[bounds[g]:bounds[g + 1]]) for g in range(grid)]
+        return desc, bounds, grid, per, T, seg_bytes
+    return desc, None, 0, None, T, seg_bytes
+
+
+@pytest.mark.parametrize("mib,nblk", [(4096, 4), (512, 4), (512, 1), (64, 3), (1, 1)])
+def test_plan_large_blocks_equal_shares(mib, nblk):
+    total = mib << 20
+    bl = total // nblk
+    desc, bounds, grid, per, T, _ = check([i * bl for i in range(nblk)], [bl] * nblk)
+    assert grid == min(256, -(-T // (15 * 4096)))
+    share = T / grid
+    # every share to the KiB, plus at most one sliver (< the 4 KiB minimum)
+    assert max(per) - share <= 1024 * nblk + 4096 + 1024, (max(per), share)
+    assert share - min(per) <= 1024 * nblk + 4096 + 1024, (min(per), share)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_plan_random_layouts(seed):
+    rng = random.Random(seed)
+    offs, lens, starts = [], [], []
+    pos = 0
+    for _ in range(rng.choice([5, 50, 400, 3000])):
+        kind = rng.random()
+        ln = (rng.randint(0, 600) if kind < 0.3 else rng.randint(1000, 40000) if kind < 0.8
+              else rng.randint(1 << 20, 8 << 20))
+        gap = rng.choice([0, 0, 0, rng.randint(1, 5000)])
+        pos += gap
+        offs.append(pos)
+        lens.append(ln)
+        starts.append(rng.choice([0, 0, 0, rng.randint(0, ln)]) if ln else 0)
+        pos += ln
+    desc, bounds, grid, per, T, seg_bytes = check(offs, lens, starts, base=0x10000 +
+                                                  rng.randint(0, 15))
+    if grid:
+        share = T / grid
+        # a workgroup's bytes exceed its share by at most one packed group or
+        # one sliver
+        assert max(per) - share <= max(seg_bytes) + 4096
+
+
+def test_plan_back_to_back_small_blocks_pack_into_runs():
+    n = 65536
+    desc, bounds, grid, per, T, seg_bytes = check([i * 16384 for i in range(n)], [16384] * n)
+    groups = [d for d in desc.tolist() if d[0] >> 24]
+    assert groups, "16 KiB blocks must be packed"
+    assert grid == 256
+    assert max(per) - T / grid <= max(seg_bytes) + 4096
+
+
+def test_plan_drop_in_sizes_use_few_workgroups():
+    for ln in (1, 100, 1024, 5000, 65536):
+        desc, bounds, grid, per, T, _ = check([0], [ln])
+        assert grid == max(1, min(256, -(-T // (15 * 1024))))

@@ -7,7 +7,7 @@
  *   batcher  vsa_batcher_hwlmExec (concurrent calls share one launch)
  *   cpu      the oracle's SSE2 port of the reference FDR loop (oracle.c
  *            orc_fdr_exec_simd, the CPU baseline engine), one call per call
- * for T in 1..32 and buffers of 1-256 KiB; each cell runs `secs` seconds.
+ * for T in 1..32 and buffers of 1 KiB-4 MiB; each cell runs `secs` seconds.
  * Database: 5,000 random printable literals of 4-8 bytes (2 % nocase, the
  * cfg-4 shape); corpus: 64 MiB printable with one planted literal per
  * 64 KiB.  One JSON line per (mode, threads, bytes): calls/s, GB/s, mean /
@@ -202,7 +202,7 @@ int main(int argc, char **argv) {
         fprintf(stderr, "batcher failed\n");
         return 1;
     }
-    static const size_t sizes[] = {1 << 10, 4 << 10, 16 << 10, 64 << 10, 256 << 10};
+    static const size_t sizes[] = {1 << 10, 4 << 10, 16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20};
     static const int tcount[] = {1, 2, 4, 8, 16, 32};
     /* warm every path (contexts, device tables, clocks) */
     for (int m = 0; m < 3; m++) cell(m, 4, 4096, 0.2);

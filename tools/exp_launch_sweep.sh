@@ -8,7 +8,10 @@ SIZES=${SIZES:-32,512,4096}
 mkdir -p gpurun_out/$TAG
 OUT=gpurun_out/$TAG/sweep.jsonl
 : > $OUT
-for v in "" "VSA_STATIC_SEGS=1" "VSA_SEG_KB=16" "VSA_SEG_KB=32" "VSA_SEG_KB=64" "VSA_SEG_KB=256" "VSA_REGIONS=1" "VSA_STATIC_SEGS=1 VSA_SEG_KB=16"; do
+VARIANTS=${VARIANTS:-"default VSA_SCHED_OLD=1 VSA_STATIC_SEGS=1 VSA_SEG_KB=16 VSA_SEG_KB=32 VSA_SEG_KB=64 VSA_SEG_KB=256 VSA_REGIONS=1"}
+for v in $VARIANTS; do
+    [ "$v" = default ] && v=""
+    v=${v//,/ }
     echo "variant: ${v:-default}" >&2
     env $v timeout -k 10 200 python -u tools/exp_launch.py --sizes $SIZES --extra "" --launches 5 \
         | sed "s/^{/{\"variant\": \"${v:-default}\", /" >> $OUT || exit 1

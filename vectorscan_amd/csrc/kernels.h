@@ -100,12 +100,21 @@ struct VsaLitParams {
     const uint8_t *data;
     const VsaBlock *blocks;
     uint32_t nblocks;
-    uint32_t seg_bytes;     /* segment size (multiple of 1 KiB) */
-    uint32_t dynamic;       /* 1: segments by atomic ticket per region */
+    uint32_t seg_bytes;     /* nominal segment size (multiple of 1 KiB) */
+    uint32_t dynamic;       /* 0: static (wave g takes g, g + G, ..); 1:
+                               atomic ticket per region; 2: per-workgroup
+                               segment lists (wg_seg) handed out in LDS */
     uint32_t nregions;      /* ticket regions (counters[16 + 16 r], one
                                128-B line each), <= 8 */
     uint64_t nsegs;
-    const uint32_t *seg_blk;  /* block of each segment */
+    const uint32_t *seg_desc; /* 4 words per segment: first block | count <<
+                                 24, offset and length in KiB from the block
+                                 origin (a part of one block), 0 */
+    const uint32_t *wg_seg;   /* dynamic 2: workgroup b's segments are
+                                 [wg_seg[b], wg_seg[b + 1]) */
+    uint32_t steal;           /* dynamic 2: a wave out of segments steals sweep
+                                 groups inside its workgroup when some wave
+                                 has at least `steal` unclaimed (0: off) */
     const uint64_t *table;  /* FDR domain table / Teddy combined byte table */
     uint32_t table_entries;
     uint32_t dmask;

@@ -1625,7 +1625,11 @@ vsa_lit_scan(VsaLitParams P) {
     typedef typename T::S_t S_t;
     extern __shared__ __align__(16) u8 smem[];
     __shared__ ConfLds cl;
-    __shared__ u32 q_tails[16], q_heads[16], q_done;
+    __shared__ u32 q_tails[16], q_heads[16], q_done, wg_ctr;
+    /* work stealing (dynamic 2): per scanning wave, the sweep groups of its
+     * current segment it has not claimed yet: seg << 40 | end << 20 | cur
+     * (groups of LIT_DEPTH iterations; cur = the next group to claim) */
+    __shared__ unsigned long long rng[16];
     __shared__ u64 prof_lds[8 * MAX_CONF_WAVES]; /* confirm-wave profile (dbg & 64) */
     const u32 tid = threadIdx.x;
     const u32 lane = lane_id();
@@ -1691,8 +1695,12 @@ vsa_lit_scan(VsaLitParams P) {
     if (tid < 16) {
         q_tails[tid] = 0;
         q_heads[tid] = 0;
+        rng[tid] = 0;
     }
-    if (tid == 0) q_done = 0;
+    if (tid == 0) {
+        q_done = 0;
+        wg_ctr = 0;
+    }
     if (tid < 8 * MAX_CONF_WAVES) prof_lds[tid] = 0;
     __syncthreads();
 
@@ -1749,7 +1757,6 @@ vsa_lit_scan(VsaLitParams P) {
     if ((P.dbg & 2048) && lane == 0) /* diagnostic: first scanning-wave start */
         atomicMax(&P.counters[8], ~t_start);
     const u8 *A = P.data - mis;
-    const int64_t SEG = (int64_t)P.seg_bytes;
     u32 ncand_total = 0;
     u32 ring_tail_cache = 0, ring_head = 0;
 
@@ -1762,22 +1769,44 @@ vsa_lit_scan(VsaLitParams P) {
      * One ticket address per region keeps the atomics from serializing the
      * grid (a single-address ticket capped streaming at ~4.4 TB/s,
      * tools/probe_stream.hip).  P.dynamic == 0: plain static assignment
-     * (wave g takes g, g + G, ...). */
+     * (wave g takes g, g + G, ...).
+     * P.dynamic == 2 (the default): workgroup b owns the host-built list
+     * [wg_seg[b], wg_seg[b + 1]) -- an equal share of the bytes, cut into
+     * segments that shrink toward the end of the list (runtime.hip
+     * plan_wg_lists) -- and its scanning waves take the next one from an
+     * LDS counter: no global atomics at all (dynamic tickets measured 50
+     * us of contention at 32 MiB and ~0.15 us of CU time per segment at 4
+     * GiB, profiles/r04c_launch_sweep.jsonl), and the CU's waves, whose
+     * issue rates differ ~3x by age, still balance among themselves down
+     * to the last, small segments. */
     const u64 G = (u64)gridDim.x * NS;
-    const u32 nreg = P.dynamic ? P.nregions : 1u;
+    const u32 sched = P.dynamic;
+    const u32 nreg = sched == 1 ? P.nregions : 1u;
     u32 reg_i = 0; /* regions tried so far */
     u32 reg = blockIdx.x % nreg;
     auto region_lo = [&](u32 r) { return P.nsegs * r / nreg; };
+    u32 wg_lo = 0, wg_hi = 0;
+    if (sched == 2) {
+        wg_lo = readfirstlane_u32(P.wg_seg[blockIdx.x]);
+        wg_hi = readfirstlane_u32(P.wg_seg[blockIdx.x + 1]);
+    }
     /* the next ticket is taken (lane 0, returning atomic) during the last
      * group of the current segment's sweep, so its latency hides behind
      * that group without one wave holding a whole segment ahead */
     auto take = [&]() -> unsigned long long {
         unsigned long long t = 0;
-        if (lane == 0) t = atomicAdd(&P.counters[16 + 16 * reg], 1ULL);
+        if (sched == 2) {
+            if (lane == 0)
+                t = __hip_atomic_fetch_add(&wg_ctr, 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (lane == 0) {
+            t = atomicAdd(&P.counters[16 + 16 * reg], 1ULL);
+        }
         return t;
     };
     auto resolve = [&](unsigned long long t0) -> u64 {
         u64 t = ((u64)readlane_u32((u32)(t0 >> 32), 0) << 32) | readlane_u32((u32)t0, 0);
+        if (sched == 2) return wg_lo + t < wg_hi ? wg_lo + t : P.nsegs;
         for (;;) {
             const u64 sg = region_lo(reg) + t;
             if (sg < region_lo(reg + 1)) return sg;
@@ -1787,21 +1816,77 @@ vsa_lit_scan(VsaLitParams P) {
             t = ((u64)readlane_u32((u32)(t1 >> 32), 0) << 32) | readlane_u32((u32)t1, 0);
         }
     };
-    u64 seg = P.dynamic ? resolve(take()) : (u64)blockIdx.x * NS + wave;
-    while (seg < P.nsegs) {
+    /* Work stealing inside the workgroup (dynamic 2, P.steal): a wave whose
+     * list is exhausted takes the back half of the unclaimed sweep groups of
+     * the scanning wave with the most left (one LDS compare-and-swap on the
+     * victim's rng word; the victim claims each next group with an LDS
+     * atomic add one group ahead, so a group is never both's).  The thief
+     * scans [mid, end) as a range of the same segment: its own prologue at
+     * the range start, and the segment's last checked iterations when its
+     * range reaches the segment end.  Only parts of one block (not packed
+     * groups or runs) are stolen. */
+    const bool steal_on = sched == 2 && P.steal != 0;
+    auto steal = [&](u64 &sg, u32 &gs, u32 &ge) -> bool {
+        for (int tries = 0; tries < 64; tries++) {
+            unsigned long long w = 0;
+            if (lane < NS) w = rng[lane];
+            const u32 c = (u32)w & 0xfffffu, e = (u32)(w >> 20) & 0xfffffu;
+            u32 best = e > c ? e - c : 0u;
+            const u32 mine = best;
+#pragma unroll
+            for (int dd = 32; dd >= 1; dd >>= 1) {
+                const u32 o = shfl_xor_u32(best, dd);
+                best = o > best ? o : best;
+            }
+            best = readfirstlane_u32(best);
+            if (best < P.steal) return false;
+            const u64 mk = __ballot(mine == best);
+            const u32 v = (u32)__ffsll((long long)mk) - 1;
+            const unsigned long long wv =
+                ((unsigned long long)readlane_u32((u32)(w >> 32), (int)v) << 32) |
+                readlane_u32((u32)w, (int)v);
+            const u32 vc = (u32)wv & 0xfffffu, ve = (u32)(wv >> 20) & 0xfffffu;
+            const u32 mid = vc + (ve - vc + 1) / 2;
+            const unsigned long long nw = (wv & ~(0xfffffULL << 20)) | ((unsigned long long)mid << 20);
+            unsigned long long old = wv;
+            if (lane == 0)
+                __hip_atomic_compare_exchange_strong(&rng[v], &old, nw, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            old = ((unsigned long long)readlane_u32((u32)(old >> 32), 0) << 32) |
+                  readlane_u32((u32)old, 0);
+            if (old == wv) {
+                sg = wv >> 40;
+                gs = mid;
+                ge = ve;
+                return true;
+            }
+        }
+        return false;
+    };
+    u64 seg = sched ? resolve(take()) : (u64)blockIdx.x * NS + wave;
+    u32 st_gs = 0, st_ge = 0; /* a stolen range: sweep groups [st_gs, st_ge) */
+    for (;;) {
+        bool stolen = false;
+        if (seg >= P.nsegs) {
+            if (!steal_on || !steal(seg, st_gs, st_ge)) break;
+            stolen = true;
+        }
         unsigned long long t_next = 0;
         bool have_next = false;
         bool lastb = true;
         auto prefetch_ticket = [&]() {
-            if (P.dynamic && !have_next && lastb) {
+            if (sched && !have_next && lastb) {
                 t_next = take();
                 have_next = true;
             }
         };
-        /* the segment's blocks: host-built segment -> block map, first block
-         * | count << 24; count 0 = a part of one block, else `count` whole
-         * consecutive blocks (runtime.hip build_plan) */
-        const u32 sbv = readfirstlane_u32(P.seg_blk[seg]);
+        /* the segment's descriptor (runtime.hip build_plan): its blocks,
+         * first block | count << 24 (count 0: a part of one block, else
+         * `count` whole consecutive blocks), and for a part its offset and
+         * length in KiB from the block's origin */
+        const uint4 dsc = ((const uint4 *)P.seg_desc)[seg];
+        const u32 sbv = readfirstlane_u32(dsc.x);
+        const u32 d_off = readfirstlane_u32(dsc.y), d_len = readfirstlane_u32(dsc.z);
         const u32 gcount = sbv >> 24;
         /* a run (VSA_BLK_RUN, FDR / Teddy): the segment's back-to-back
          * blocks are one range -- one prologue, one sweep, two checked
@@ -1874,8 +1959,9 @@ vsa_lit_scan(VsaLitParams P) {
         S.len = S.bhi - S.blo;
         S.zbase = B.zbase;
         S.rlo = B.rlo > S.start ? B.rlo : S.start;
-        const int64_t s_lo = (gcount || run) ? B.org : B.org + (int64_t)(seg - B.seg_first) * SEG;
-        const int64_t s_hi = (!gcount && s_lo + SEG < S.bhi) ? s_lo + SEG : S.bhi;
+        const int64_t s_lo = (gcount || run) ? B.org : B.org + ((int64_t)d_off << 10);
+        const int64_t s_hi =
+            (!gcount && s_lo + ((int64_t)d_len << 10) < S.bhi) ? s_lo + ((int64_t)d_len << 10) : S.bhi;
         const u32 niters = (u32)((s_hi - s_lo + 1023) >> 10);
         n_iter += niters;
         const int64_t zlo = (MODE == VSA_MODE_FDR || MODE == VSA_MODE_FDR4) ? B.zbase : S.qlo;
@@ -1905,16 +1991,41 @@ vsa_lit_scan(VsaLitParams P) {
          * one per step (hsbench corpora).  The sweep's chunks follow the
          * first checked iteration (issuing them earlier keeps 16 more VGPRs
          * live through it and spills). */
+        const u32 ng = nf / LIT_DEPTH;
+        /* a stolen range starts at sweep group st_gs: its prologue is there,
+         * and the owner's first checked iterations are not its own */
+        const u32 gs = stolen ? st_gs : 0u;
+        const u32 it0 = gs * LIT_DEPTH;
+        const int64_t pro_lo = stolen ? fb + 1024 * (int64_t)it0 : s_lo;
         const bool pro1 = lane < (u32)(T::NL - 1);
-        const int64_t pp = s_lo - (T::NL - 1) + (int64_t)lane;
+        const int64_t pp = pro_lo - (T::NL - 1) + (int64_t)lane;
         const bool pro1_in = pro1 && pp - S.blo >= zlo && pp - S.blo < S.len;
         const u8 pb0 = pro1_in ? load_byte_masked(A, pp, S.vlo, S.bhi) : (u8)0;
         const u8 pb1 = (T::KEY16 && pro1_in) ? load_byte_masked(A, pp + 1, S.vlo, S.bhi) : (u8)0;
-        const u32 pbb = lane < 8 ? load_byte_masked(A, s_lo - 8 + (int64_t)lane, S.vlo, S.bhi) : 0u;
+        /* FDR4 keys also need the two bytes before each position: issued
+         * with the others (one memory round trip for the whole prologue) */
+        const bool F4P = MODE == VSA_MODE_FDR4;
+        const u8 pm2 = (F4P && pro1_in) ? load_byte_masked(A, pp - 2, S.vlo, S.bhi) : (u8)0;
+        const u8 pm1 = (F4P && pro1_in) ? load_byte_masked(A, pp - 1, S.vlo, S.bhi) : (u8)0;
+        const u32 pbb = lane < 8 ? load_byte_masked(A, pro_lo - 8 + (int64_t)lane, S.vlo, S.bhi) : 0u;
+        /* a range that starts with the sweep (a segment inside a block, the
+         * common case of large blocks): its first LIT_DEPTH chunks go out
+         * with the prologue bytes, so a segment start waits for one memory
+         * round trip, not two (prologue, then the sweep's first chunk) */
+        const bool early = (f0 == 0 || stolen) && nf > 0;
+        const u8 *sb = uniform_ptr(A + fb);
+        if (early) {
+#pragma unroll
+            for (int k = 0; k < LIT_DEPTH; k++)
+                ring[k] = load_wave_kib(sb, it0 + (u32)k < nf ? 1024u * (it0 + k) : 1024u * it0);
+            after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.vlo, S.bhi);
+        }
         u32 nxt_f = 0, nxt_t = 0;
-        ring[0] = make_uint4(0, 0, 0, 0);
-        ring[1] = make_uint4(0, 0, 0, 0);
-        if (f0 > 0) {
+        if (!early) {
+            ring[0] = make_uint4(0, 0, 0, 0);
+            ring[1] = make_uint4(0, 0, 0, 0);
+        }
+        if (f0 > 0 && !stolen) {
             ring[0] = load_chunk(A, s_lo + 16 * (int64_t)lane, S.bhi);
             nxt_f = load_byte_masked(A, s_lo + 1024, S.vlo, S.bhi);
         }
@@ -1937,11 +2048,10 @@ vsa_lit_scan(VsaLitParams P) {
                 u32 key;
                 if constexpr (T::KEY16) key = vsa_fdr_key(pb0, pb1, P.dmask);
                 else if constexpr (MODE == VSA_MODE_FDR4)
-                    key = vsa_fdr4_key(load_byte_masked(A, pp - 2, S.vlo, S.bhi),
-                                       load_byte_masked(A, pp - 1, S.vlo, S.bhi), pb0, 15u);
+                    key = vsa_fdr4_key(pm2, pm1, pb0, 15u);
                 else key = pb0;
                 x = (S_t)lit_lookup<MODE, LDS_TABLE>(tab, key, lane);
-                x >>= T::LB * (s_lo - pp);
+                x >>= T::LB * (pro_lo - pp);
             }
             u64 xv = (u64)x;
 #pragma unroll
@@ -1961,7 +2071,7 @@ vsa_lit_scan(VsaLitParams P) {
             }
             is.pbytes = ((u64)shfl_u32((u32)(pb >> 32), 0) << 32) | shfl_u32((u32)pb, 0);
         }
-        for (u32 it = 0; it < f0; it++) {
+        for (u32 it = 0; it < (stolen ? 0u : f0); it++) {
             const int64_t ib = s_lo + 1024 * (int64_t)it;
             uint4 cur = ring[0];
             u32 nxt0 = nxt_f;
@@ -1973,6 +2083,7 @@ vsa_lit_scan(VsaLitParams P) {
                                                  bucket_mask);
             run_adv(ib);
         }
+        bool tail_mine = true; /* a stolen-from range leaves its tail to the thief */
         if (nf > 0) {
             if constexpr (MODE == VSA_MODE_FDR && LDS_TABLE) {
                 /* sweep_enter: the carry and the previous chunk's last dword
@@ -1994,15 +2105,26 @@ vsa_lit_scan(VsaLitParams P) {
              * (the next chunk's first byte).  Every load is unconditional (an
              * out-of-range prefetch re-reads the current chunk) so the wait
              * counters stay exact. */
-            /* segment base in SGPRs, 32-bit offsets (segments <= 64 KiB) */
-            const u8 *sb = uniform_ptr(A + fb);
+            /* segment base in SGPRs, 32-bit offsets */
+            if (!early) {
 #pragma unroll
-            for (int k = 0; k < LIT_DEPTH; k++)
-                ring[k] = load_wave_kib(sb, (u32)k < nf ? 1024u * k : 0u);
-            after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.vlo, S.bhi);
-            const u32 ng = nf / LIT_DEPTH;
-            for (u32 g = 0; g < ng; g++) {
-                if (g + 1 == ng) prefetch_ticket();
+                for (int k = 0; k < LIT_DEPTH; k++)
+                    ring[k] = load_wave_kib(sb, (u32)k < nf ? 1024u * k : 0u);
+                after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.vlo, S.bhi);
+            }
+            /* the groups this wave scans: all (or the stolen [gs, ge));
+             * with stealing on, each next group is claimed one group ahead
+             * and a thief may lower the end meanwhile */
+            u32 g_end = stolen ? st_ge : ng;
+            const bool stealable = steal_on && gcount == 0 && !run && g_end > gs + 1;
+            if (stealable && lane == 0)
+                rng[wave] = (seg << 40) | ((unsigned long long)g_end << 20) | (gs + 1);
+            for (u32 g = gs; g < g_end; g++) {
+                unsigned long long clm = 0;
+                if (stealable && lane == 0)
+                    clm = __hip_atomic_fetch_add(&rng[wave], 1ULL, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (g + 1 == g_end) prefetch_ticket();
 #pragma unroll
                 for (int k = 0; k < LIT_DEPTH; k++) {
                     const u32 it = g * LIT_DEPTH + k;
@@ -2015,8 +2137,20 @@ vsa_lit_scan(VsaLitParams P) {
                     const u32 itn = (it + LIT_DEPTH < nf) ? it + LIT_DEPTH : it;
                     ring[k] = load_wave_kib(sb, 1024u * itn);
                 }
+                if (stealable) {
+                    /* group g + 1 is this wave's only if a thief left it */
+                    const u32 oe = (readlane_u32((u32)clm, 0) >> 20) |
+                                   ((readlane_u32((u32)(clm >> 32), 0) & 0xffu) << 12);
+                    if (g + 1 >= oe) {
+                        g_end = g + 1;
+                        prefetch_ticket();
+                    }
+                }
             }
-            const u32 rem = nf - ng * LIT_DEPTH;
+            /* the segment's remaining iterations go to whoever scanned its
+             * last group */
+            tail_mine = g_end == ng;
+            const u32 rem = tail_mine ? nf - ng * LIT_DEPTH : 0u;
 #pragma unroll
             for (int k = 0; k < LIT_DEPTH - 1; k++) {
                 if ((u32)k < rem) {
@@ -2040,7 +2174,7 @@ vsa_lit_scan(VsaLitParams P) {
             }
         }
         prefetch_ticket();
-        for (u32 it = f1; it < niters; it++) {
+        for (u32 it = f1; tail_mine && it < niters; it++) {
             const int64_t ib = s_lo + 1024 * (int64_t)it;
             uint4 cur = ring[1];
             u32 nxt0 = nxt_t;
@@ -2057,7 +2191,8 @@ vsa_lit_scan(VsaLitParams P) {
         ring_head = is.head;
         } /* blocks of the segment */
         n_seg++;
-        seg = P.dynamic ? resolve(t_next) : seg + G;
+        /* after a stolen range the list is known to be exhausted */
+        seg = stolen ? P.nsegs : sched ? resolve(t_next) : seg + G;
     }
     if ((P.dbg & 4096) && P.wave_log && lane < 8) {
         u32 xcc, hwid;

@@ -136,7 +136,11 @@ struct Workspace {
  * count << 24 (count 0: part of one block). */
 struct BatchPlan {
     std::vector<VsaBlock> blocks;
+    /* 4 words per segment (kernels.h seg_desc), then for per-workgroup
+     * lists (grid != 0) grid + 1 list bounds */
     std::vector<uint32_t> segblk;
+    uint64_t nsegs = 0;
+    uint32_t grid = 0; /* workgroups of a per-workgroup-list plan, else 0 */
     uint32_t seg_bytes = 0;
     int end_bits = 0;
     uint64_t bytes = 0; /* scanned bytes (len - start summed) */
@@ -166,6 +170,7 @@ struct vsa_ctx {
         uint32_t nb = 0;
         uint64_t segs = 0;
         uint32_t seg_bytes = 0;
+        uint32_t grid = 0; /* per-workgroup lists: the plan's workgroups */
         int end_bits = 0;
         uint32_t flags = 0;
         bool bins = false;     /* the scan counts records into the sort bins */
@@ -226,6 +231,7 @@ struct vsa_plan {
     uint32_t nb = 0;
     uint64_t segs = 0;
     uint32_t seg_bytes = 0;
+    uint32_t grid = 0;
     int end_bits = 0;
     uint64_t bytes = 0;
     VsaBlock *d_blocks = nullptr;
@@ -400,6 +406,31 @@ uint64_t count_range(const std::vector<int64_t> &spans, size_t first, size_t n, 
     return cnt + (gn ? 1 : 0);
 }
 
+int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
+/* The scan's schedule: per-workgroup segment lists handed out in LDS
+ * (build_plan, kernels.hip dynamic 2), unless one of the A/B knobs of the
+ * region-ticket scheduler asks for it (VSA_SCHED_OLD, VSA_STATIC_SEGS,
+ * VSA_SEG_KB, VSA_REGIONS, VSA_SEG_MAX_KIB) */
+bool sched_wg_lists() {
+    static const bool v = !getenv("VSA_SCHED_OLD") && !getenv("VSA_STATIC_SEGS") &&
+                          !getenv("VSA_SEG_KB") && !getenv("VSA_REGIONS") &&
+                          !getenv("VSA_SEG_MAX_KIB");
+    return v;
+}
+
+/* work stealing inside a workgroup (kernels.hip, dynamic 2): a wave out of
+ * segments steals when another has at least this many sweep groups (4 KiB)
+ * unclaimed; VSA_STEAL=0 turns it off (the plan then cuts large blocks into
+ * shrinking segments instead) */
+uint32_t steal_min() {
+    static const uint32_t v = (uint32_t)std::max(0, env_int("VSA_STEAL", 4));
+    return v;
+}
+
 uint64_t pick_seg_bytes(const std::vector<int64_t> &spans, uint64_t waves) {
     /* segments of a candidate size, blocks of at most half a segment packed
      * whole (up to 255 per segment) as build_plan does.  Past 64 Ki blocks
@@ -497,12 +528,13 @@ int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds) {
     uint64_t want = (P.nsegs + ns - 1) / ns;
     uint64_t cap = (uint64_t)c->num_cus; /* persistent: one 16-wave WG per CU */
     uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
+    if (P.dynamic == 2) grid = c->launch.grid; /* one workgroup per list */
     /* at most one segment per scanning wave (small scans, the drop-ins):
      * static assignment.  Dynamic tickets would cost every wave a walk over
      * the drained regions, one returning atomic each (~5.5 us measured on a
      * 1 KiB drop-in, profiles/r03_dropin_waves.txt) */
     VsaLitParams Q = P;
-    if (Q.dynamic && Q.nsegs <= (uint64_t)grid * ns) Q.dynamic = 0;
+    if (Q.dynamic == 1 && Q.nsegs <= (uint64_t)grid * ns) Q.dynamic = 0;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(LIT_THREADS), lds, c->stream, Q);
     VSA_CHECK(hipGetLastError());
     return VSA_OK;
@@ -725,10 +757,12 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         memset(&P, 0, sizeof(P));
         P.data = d_data;
         P.blocks = c->launch.d_blocks;
-        P.seg_blk = c->launch.d_segblk;
+        P.seg_desc = c->launch.d_segblk;
+        P.wg_seg = c->launch.grid ? c->launch.d_segblk + 4 * nsegs : nullptr;
         P.nblocks = nb;
         P.seg_bytes = seg_bytes;
-    P.dynamic = getenv("VSA_STATIC_SEGS") ? 0u : 1u;
+    P.dynamic = c->launch.grid ? 2u : getenv("VSA_STATIC_SEGS") ? 0u : 1u;
+    P.steal = P.dynamic == 2 ? steal_min() : 0u;
     P.nregions = 8;
     if (const char *e = getenv("VSA_REGIONS")) P.nregions = (uint32_t)std::min(8, std::max(1, atoi(e)));
         P.nsegs = nsegs;
@@ -758,10 +792,12 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     memset(&P, 0, sizeof(P));
     P.data = d_data;
     P.blocks = c->launch.d_blocks;
-    P.seg_blk = c->launch.d_segblk;
+    P.seg_desc = c->launch.d_segblk;
+        P.wg_seg = c->launch.grid ? c->launch.d_segblk + 4 * nsegs : nullptr;
     P.nblocks = nb;
     P.seg_bytes = seg_bytes;
-    P.dynamic = getenv("VSA_STATIC_SEGS") ? 0u : 1u;
+    P.dynamic = c->launch.grid ? 2u : getenv("VSA_STATIC_SEGS") ? 0u : 1u;
+    P.steal = P.dynamic == 2 ? steal_min() : 0u;
     P.nregions = 8;
     if (const char *e = getenv("VSA_REGIONS")) P.nregions = (uint32_t)std::min(8, std::max(1, atoi(e)));
     P.nsegs = nsegs;
@@ -953,7 +989,8 @@ constexpr uint32_t PLAN_MAX_BLOCKS = VSA_MAX_BLOCKS; /* 20-bit block field of th
 
 int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens,
                const uint64_t *starts, const uint64_t *hlens, const uint64_t *rlos,
-               uint32_t nb, uint64_t waves, BatchPlan &pl, VsaBlock *out = nullptr) {
+               uint32_t nb, uint64_t waves, BatchPlan &pl, VsaBlock *out = nullptr,
+               uint64_t ns = LIT_WAVES - 1) {
     if (nb > PLAN_MAX_BLOCKS) return VSA_E_INVALID;
     /* the block table goes to `out` (a pinned mirror) or pl.blocks */
     if (!out) {
@@ -996,12 +1033,23 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
             pl.bytes += (uint64_t)(len - st);
         }
     }
+    const bool wgl = sched_wg_lists();
     uint64_t seg = live.empty() ? (64u << 10) : pick_seg_bytes(live, waves);
     if (const char *e = getenv("VSA_SEG_KB")) seg = (uint64_t)std::max(1, atoi(e)) << 10;
     const bool group = !getenv("VSA_NO_GROUPS");
     const bool no_runs = getenv("VSA_NO_RUNS") != nullptr;
     uint32_t g_first = 0, g_n = 0;
     int64_t g_span = 0;
+    pl.nsegs = 0;
+    pl.grid = 0;
+    /* one 16-byte descriptor per segment (kernels.h VsaLitParams.seg_desc) */
+    auto push_desc = [&](uint32_t info, uint64_t off, uint64_t len) {
+        pl.segblk.push_back(info);
+        pl.segblk.push_back((uint32_t)(off >> 10));
+        pl.segblk.push_back((uint32_t)((len + 1023) >> 10));
+        pl.segblk.push_back(0u);
+        pl.nsegs++;
+    };
     /* a packed segment of back-to-back blocks >= 1 KiB scanned from their
      * first byte is one range for the scan (VSA_BLK_RUN); a streaming write
      * in it has its history right before it (the hs corpus and vectored
@@ -1018,31 +1066,114 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
     auto flush = [&]() {
         if (g_n) {
             if (runnable()) out[g_first].flags |= VSA_BLK_RUN;
-            pl.segblk.push_back(g_first | (g_n << SEG_GROUP_SHIFT));
+            push_desc(g_first | (g_n << SEG_GROUP_SHIFT), 0, 0);
         }
         g_n = 0;
         g_span = 0;
     };
-    for (uint32_t i = 0; i < nb; i++) {
-        const int64_t sp = spans[i];
-        if (sp < 0) {
+    if (!wgl) {
+        /* fixed-size segments for the region tickets / static assignment */
+        for (uint32_t i = 0; i < nb; i++) {
+            const int64_t sp = spans[i];
+            if (sp < 0) {
+                flush();
+                continue;
+            }
+            if (group && 2 * sp <= (int64_t)seg) {
+                if (g_n && (g_span + sp > (int64_t)seg || g_n == SEG_GROUP_MAX)) flush();
+                if (!g_n) g_first = i;
+                out[i].seg_first = pl.nsegs;
+                g_n++;
+                g_span += sp;
+                continue;
+            }
             flush();
-            continue;
-        }
-        if (group && 2 * sp <= (int64_t)seg) {
-            if (g_n && (g_span + sp > (int64_t)seg || g_n == SEG_GROUP_MAX)) flush();
-            if (!g_n) g_first = i;
-            out[i].seg_first = pl.segblk.size();
-            g_n++;
-            g_span += sp;
-            continue;
+            out[i].seg_first = pl.nsegs;
+            for (int64_t off = 0; off < sp; off += (int64_t)seg) push_desc(i, (uint64_t)off, seg);
         }
         flush();
-        out[i].seg_first = pl.segblk.size();
-        const uint64_t k = (uint64_t)((sp + (int64_t)seg - 1) / (int64_t)seg);
-        for (uint64_t j = 0; j < k; j++) pl.segblk.push_back(i);
+    } else {
+        /* Per-workgroup lists (kernels.hip, dynamic 2): the live bytes are
+         * split into G equal shares, one per workgroup, in block order; each
+         * share is cut into segments of clamp(r / (K x ns), min, max), r =
+         * the bytes of the share still uncut, so they shrink geometrically
+         * toward the share's end (guided self-scheduling): the CU's waves,
+         * whose rates differ ~3x by issue age, take the big ones first and
+         * finish on small ones together.  Blocks shorter than half the
+         * current size are packed whole as before. */
+        uint64_t T = 0;
+        for (int64_t sp : live) T += (uint64_t)sp;
+        static const uint64_t K = std::max(1, env_int("VSA_WG_K", 2));
+        static const uint64_t smax = (uint64_t)std::max(1, env_int("VSA_WG_MAX_KIB", 256)) << 10;
+        static const uint64_t smin0 = (uint64_t)std::max(1, env_int("VSA_WG_MIN_KIB", 4)) << 10;
+        const uint64_t smin = T <= (64u << 10) ? 1024u : smin0;
+        const uint64_t gmax = std::max<uint64_t>(1, waves / ns);
+        const uint64_t G = std::max<uint64_t>(1, std::min(gmax, (T + ns * smin - 1) / (ns * smin)));
+        std::vector<uint32_t> wg_first(G + 1, 0);
+        uint64_t g = 0, acc = 0;
+        auto cum = [&](uint64_t k) { return (uint64_t)((unsigned __int128)T * (k + 1) / G); };
+        auto advance = [&]() {
+            while (g + 1 < G && acc >= cum(g)) wg_first[++g] = (uint32_t)pl.nsegs;
+        };
+        static const uint64_t bmax = (uint64_t)std::max(4, env_int("VSA_WG_BIG_MAX_KIB", 16384)) << 10;
+        const uint64_t big = std::min(bmax, std::max(smin, ((T / G / ns) + 1023) & ~(uint64_t)1023));
+        auto size_now = [&]() -> uint64_t {
+            const uint64_t c = cum(g);
+            const uint64_t r = c > acc ? c - acc : 0;
+            uint64_t v = (r / (K * ns) + 1023) & ~(uint64_t)1023;
+            return std::min(smax, std::max(smin, v));
+        };
+        for (uint32_t i = 0; i < nb; i++) {
+            const int64_t sp = spans[i];
+            if (sp < 0) {
+                flush();
+                continue;
+            }
+            uint64_t sz = size_now();
+            if (group && 2 * (uint64_t)sp <= sz) {
+                if (g_n && (g_span + sp > (int64_t)sz || g_n == SEG_GROUP_MAX)) {
+                    flush();
+                    advance();
+                }
+                if (!g_n) g_first = i;
+                out[i].seg_first = pl.nsegs;
+                g_n++;
+                g_span += sp;
+                acc += (uint64_t)sp;
+                if (acc >= cum(g)) { /* the share ends here */
+                    flush();
+                    advance();
+                }
+                continue;
+            }
+            flush();
+            advance();
+            out[i].seg_first = pl.nsegs;
+            for (uint64_t off = 0; off < (uint64_t)sp;) {
+                /* with stealing, a part of a large block is one wave's share
+                 * of its workgroup's bytes: the waves balance by stealing
+                 * sweep groups, so no segment needs to be small (fewer
+                 * segment starts); without it, the guided size */
+                sz = steal_min() ? big : size_now();
+                /* a piece ends at its share's end: every workgroup gets its
+                 * share to the KiB (stealing balances inside a workgroup
+                 * only) */
+                const uint64_t cg = cum(g);
+                if (cg > acc) sz = std::min(sz, (cg - acc + 1023) & ~(uint64_t)1023);
+                uint64_t piece = std::min<uint64_t>(sz, (uint64_t)sp - off);
+                /* no sliver shorter than the minimum after this piece */
+                if ((uint64_t)sp - off - piece < smin) piece = (uint64_t)sp - off;
+                push_desc(i, off, piece);
+                off += piece;
+                acc += piece;
+                advance();
+            }
+        }
+        flush();
+        for (uint64_t k = g + 1; k <= G; k++) wg_first[k] = (uint32_t)pl.nsegs;
+        pl.grid = (uint32_t)G;
+        pl.segblk.insert(pl.segblk.end(), wg_first.begin(), wg_first.end());
     }
-    flush();
     pl.seg_bytes = (uint32_t)seg;
     pl.end_bits = bits_for(span);
     return VSA_OK;
@@ -1064,7 +1195,7 @@ int upload_plan(vsa_ctx *c, const BatchPlan &pl, VsaBlock *d_blocks, uint32_t *d
 /* launch a planned batch whose tables are on the device */
 int launch_planned(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, const VsaBlock *d_blocks,
                    const uint32_t *d_segblk, uint32_t nb, uint64_t segs, uint32_t seg_bytes,
-                   int end_bits, uint64_t bytes, uint32_t flags, uint64_t *n_out) {
+                   uint32_t grid, int end_bits, uint64_t bytes, uint32_t flags, uint64_t *n_out) {
     int r;
     if ((r = ensure_out(c, 1)) != VSA_OK) return r;
     if (segs == 0) {
@@ -1080,6 +1211,7 @@ int launch_planned(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, const Vs
     c->launch.nb = nb;
     c->launch.segs = segs;
     c->launch.seg_bytes = seg_bytes;
+    c->launch.grid = grid;
     c->launch.end_bits = end_bits;
     c->launch.bytes = bytes;
     c->launch.flags = flags;
@@ -1120,7 +1252,7 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         M.valid = false;
         if ((r = ensure_tables(c, nb, 0)) != VSA_OK) return r;
         if ((r = build_plan(d_data, offs, lens, starts, hlens, rlos, nb, waves, pl,
-                            w.h_blocks)) != VSA_OK)
+                            w.h_blocks, LIT_WAVES - db->nconf.load())) != VSA_OK)
             return r;
         T1 = std::chrono::steady_clock::now();
         if ((r = ensure_tables(c, nb, pl.segblk.size(), true)) != VSA_OK) return r;
@@ -1139,13 +1271,13 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         }
         M.valid = true;
     }
-    int rr = launch_planned(c, db, d_data, c->ws.d_blocks, c->ws.d_segblk, nb, pl.segblk.size(),
-                          pl.seg_bytes, pl.end_bits, pl.bytes, flags, n_out);
+    int rr = launch_planned(c, db, d_data, c->ws.d_blocks, c->ws.d_segblk, nb, pl.nsegs,
+                          pl.seg_bytes, pl.grid, pl.end_bits, pl.bytes, flags, n_out);
     auto T3 = std::chrono::steady_clock::now();
     /* diagnostic: host-side cost of a per-call plan (tools/exp_host.py) */
     static const bool timing = getenv("VSA_HOST_TIMING") != nullptr;
     if (timing)
-        fprintf(stderr, "host: nb %u segs %zu build %.3f memcpy %.3f launch+wait %.3f ms (kernel %.3f)\n", nb, pl.segblk.size(),
+        fprintf(stderr, "host: nb %u segs %llu build %.3f memcpy %.3f launch+wait %.3f ms (kernel %.3f)\n", nb, (unsigned long long)pl.nsegs,
                 std::chrono::duration<double, std::milli>(T1 - T0).count(),
                 std::chrono::duration<double, std::milli>(T2 - T1).count(),
                 std::chrono::duration<double, std::milli>(T3 - T2).count(), c->last_kernel_ms);
@@ -2918,6 +3050,29 @@ int vsa_scan_blocks_stream(vsa_ctx_t *c, const vsa_db_t *db, const uint8_t *d_da
 }
 
 
+/* Host-only view of the schedule build_plan makes for a batch (no GPU
+ * needed; tests/test_plan.py checks its invariants): the segment
+ * descriptors (4 words each) and, for per-workgroup lists, the grid + 1
+ * list bounds after them.  `words` receives up to cap words; returns the
+ * word count (or a negative error), *nsegs / *grid the segment count and
+ * the workgroups (0: region tickets).  waves / ns as a launch on num_cus
+ * CUs with ns scanning waves each would use; d_data only sets the
+ * alignment. */
+int vsa_plan_describe(const uint8_t *d_data, const uint64_t *offsets, const uint64_t *lens,
+                      const uint64_t *starts, const uint64_t *hlens, const uint64_t *report_lo,
+                      uint32_t nblocks, uint32_t num_cus, uint32_t ns, uint32_t *words,
+                      uint64_t cap, uint64_t *nsegs, uint32_t *grid) {
+    if (!offsets || !lens || !nblocks || !ns || !num_cus) return VSA_E_INVALID;
+    BatchPlan pl;
+    int r = build_plan(d_data, offsets, lens, starts, hlens, report_lo, nblocks,
+                       (uint64_t)num_cus * ns, pl, nullptr, ns);
+    if (r != VSA_OK) return r;
+    if (words) memcpy(words, pl.segblk.data(), std::min<uint64_t>(cap, pl.segblk.size()) * 4);
+    if (nsegs) *nsegs = pl.nsegs;
+    if (grid) *grid = pl.grid;
+    return (int)pl.segblk.size();
+}
+
 int vsa_plan_create(vsa_ctx_t *c, const uint8_t *d_data, const uint64_t *offsets,
                     const uint64_t *lens, const uint64_t *starts, const uint64_t *hlens,
                     const uint64_t *report_lo, uint32_t nblocks, vsa_plan_t **out) {
@@ -2932,8 +3087,9 @@ int vsa_plan_create(vsa_ctx_t *c, const uint8_t *d_data, const uint64_t *offsets
     c->plans.push_back(p);
     p->d_data = d_data;
     p->nb = nblocks;
-    p->segs = pl.segblk.size();
+    p->segs = pl.nsegs;
     p->seg_bytes = pl.seg_bytes;
+    p->grid = pl.grid;
     p->end_bits = pl.end_bits;
     p->bytes = pl.bytes;
     if (hipSetDevice(c->device) != hipSuccess ||
@@ -2975,7 +3131,7 @@ int vsa_scan_plan(vsa_ctx_t *c, const vsa_db_t *db, const vsa_plan_t *p, uint32_
     if (int r0 = finish_pending(c)) return r0;
     uint64_t dummy;
     return launch_planned(c, db, p->d_data, p->d_blocks, p->d_segblk, p->nb, p->segs,
-                          p->seg_bytes, p->end_bits, p->bytes, flags,
+                          p->seg_bytes, p->grid, p->end_bits, p->bytes, flags,
                           n_matches ? n_matches : &dummy);
 }
 
