@@ -365,11 +365,17 @@ def run(args):
     with_cpu = not args.no_cpu and world == 1
     if rank == 0:
         import oracle
-        # one pinned thread per physical core the process may use, no more
-        # than the cgroup quota lets run at once (the GPU box: 16 CPUs of
-        # quota over 256 visible; tools/exp_cpu_threads.py sweeps the count)
+        # one pinned thread per physical core the process may use
+        # (all physical host cores), capped by the cgroup CPU
+        # quota: the GPU box shows 128 physical cores but grants 16 CPUs, and
+        # past the quota the threads are throttled -- short best-of-3 runs
+        # burst above it (profiles/r04e_cpu_threads.jsonl: 16 / 128 threads
+        # 21 / 66 GB/s on 1 GiB), but over the whole 4 GiB corpus 128 threads
+        # gave 12.7 GB/s against 25-30 GB/s for 16 (profiles/r04f_bench.json,
+        # r04d_bench.json)
         pins, quota, visible, phys = host_cpu_share()
-        threads = args.cpu_threads or max(1, min(len(pins), int(quota) if quota else len(pins)))
+        cap = len(pins) if quota is None else max(1, min(len(pins), int(quota + 0.5)))
+        threads = args.cpu_threads or cap
         oracle.set_pin(pins)
         eng = vsa.engine_blob(blob)
         parity, parity_bytes, cpu = None, 0, None
@@ -447,7 +453,8 @@ def run(args):
             if with_cpu:
                 cpu = {"value": round(parity_bytes / t_cpu / 1e9, 4), "unit": "GB/s",
                        "cores": threads, "kind": "port", "match_set_equal": cpu_ok,
-                       "pinned": "one thread per physical core", "physical_cores": phys,
+                       "pinned": "one thread per physical core, as many as the cgroup CPU quota "
+                                 "grants", "physical_cores": phys,
                        "cpus_visible": visible, "cpu_quota": quota,
                        "sample": "the whole %d-byte corpus, 4 x 1 GiB blocks: oracle/oracle.c "
                                  "SSE2 port of the reference FDR main loop (fdr.c:145-333, "

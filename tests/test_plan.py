@@ -1,10 +1,11 @@
 """CPU tests of the scan schedule (runtime.hip build_plan, through the
 host-only vsa_plan_describe): whatever the block layout, the segments cover
-every live block's span exactly once, in order, and the per-workgroup lists
-(kernels.hip dynamic 2: one list per workgroup, no global tickets) give
-every workgroup an equal share of the bytes -- stealing balances waves only
-inside a workgroup, so a workgroup with more bytes than its share would set
-the kernel's end."""
+every live block's span exactly once, in order; the per-workgroup lists
+(kernels.hip dynamic 2: one list per workgroup, handed out in LDS) give
+every workgroup an equal share of the static bytes -- stealing balances
+waves only inside a workgroup -- and the rest (VSA_POOL_PM, 12.5 % by
+default) is a pool of small segments after the lists, shared by all
+workgroups, which balances the XCDs."""
 import ctypes
 import random
 
@@ -81,10 +82,16 @@ def check(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000):
     T = sum(s for s in sp if s >= 0)
     if grid:
         assert 1 <= grid <= num_cus and len(bounds) == grid + 1
-        assert bounds[0] == 0 and bounds[-1] == len(desc)
+        assert bounds[0] == 0 and bounds[-1] <= len(desc)
         assert np.all(np.diff(bounds.astype(np.int64)) >= 0)
         per = [sum(seg_bytes[bounds[g]:bounds[g + 1]]) for g in range(grid)]
-        return desc, bounds, grid, per, T, seg_bytes
+        pool = seg_bytes[bounds[-1]:]
+        if grid >= 16:
+            # the pool: 12.5 % of the bytes (to a segment), small segments
+            assert abs(sum(pool) - T * 125 // 1000) <= max(seg_bytes) + 4096
+        else:
+            assert not pool
+        return desc, bounds, grid, per, sum(per), seg_bytes
     return desc, None, 0, None, T, seg_bytes
 
 
@@ -92,8 +99,9 @@ def check(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000):
 def test_plan_large_blocks_equal_shares(mib, nblk):
     total = mib << 20
     bl = total // nblk
-    desc, bounds, grid, per, T, _ = check([i * bl for i in range(nblk)], [bl] * nblk)
-    assert grid == min(256, -(-T // (15 * 4096)))
+    desc, bounds, grid, per, T, segb = check([i * bl for i in range(nblk)], [bl] * nblk)
+    assert grid == min(256, -(-total // (15 * 4096)))
+    assert all(b <= 128 << 10 for b in segb[bounds[-1]:])
     share = T / grid
     # every share to the KiB, plus at most one sliver (< the 4 KiB minimum)
     assert max(per) - share <= 1024 * nblk + 4096 + 1024, (max(per), share)
@@ -137,3 +145,4 @@ def test_plan_drop_in_sizes_use_few_workgroups():
     for ln in (1, 100, 1024, 5000, 65536):
         desc, bounds, grid, per, T, _ = check([0], [ln])
         assert grid == max(1, min(256, -(-T // (15 * 1024))))
+        assert bounds[-1] == len(desc)  # no pool for a few workgroups

@@ -5,7 +5,7 @@ import ctypes
 import os
 import sys
 
-os.environ["VSA_DEBUG_FLAGS"] = str(4096 | int(os.environ.get("EXTRA_DBG", "0")))
+os.environ["VSA_DEBUG_FLAGS"] = str(4096 | 16384 | int(os.environ.get("EXTRA_DBG", "0")))
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -16,7 +16,7 @@ dev = torch.device("cuda", 0)
 ctx = vsa.Context(0)
 lits = bench.make_literals(5000, seed=12)
 db = vsa.Database(ctx, vsa.hwlm_build(lits))
-total = 4 << 30
+total = int(float(os.environ.get("GIB", "4")) * (1 << 30))
 bl = total // 4
 data = bench.make_corpus_device(torch, 0, total, total, lits, 5, 64 << 10, dev)
 log = torch.zeros(1024 * 16 * 8, dtype=torch.int64, device=dev)
@@ -27,8 +27,12 @@ offs = [i * bl for i in range(4)]
 for i in range(22):
     log.zero_()
     ctx.scan_blocks(db, data.data_ptr(), offs, [bl] * 4)
-L = log.view(-1, 8).cpu().numpy().astype(np.int64)
+LA = log.cpu().numpy().astype(np.int64)
+L = LA[:65536].reshape(-1, 8)
+nev = int(LA[65535])
+EV = LA[65536:65536 + 4 * min(nev, 16000)].reshape(-1, 4)
 L = L[L[:, 0] != 0]
+L = L[L[:, 1] != 0] if len(L) else L
 t0 = L[:, 0].min()
 st, en = (L[:, 0] - t0) / 100.0, (L[:, 1] - t0) / 100.0
 it = L[:, 3]
@@ -55,7 +59,41 @@ for w, e in zip(wg.tolist(), en.tolist()):
 we = np.array(sorted(wg_end.values()))
 print("workgroup done us: min %.1f p10 %.1f p50 %.1f p90 %.1f max %.1f" %
       (we.min(), *np.percentile(we, [10, 50, 90]), we.max()))
+# per workgroup: bytes scanned and the rate over its busy span
+wk, wkib = {}, {}
+for w, k, s0, e0 in zip(wg.tolist(), it.tolist(), st.tolist(), en.tolist()):
+    wkib[w] = wkib.get(w, 0) + k
+wr = np.array([wkib[w] / max(wg_end[w], 1e-3) for w in sorted(wg_end)])
+print("workgroup KiB: min %d p50 %d max %d; KiB/us (share / done): min %.2f p10 %.2f p50 %.2f p90 %.2f max %.2f" %
+      (min(wkib.values()), np.median(list(wkib.values())), max(wkib.values()),
+       wr.min(), *np.percentile(wr, [10, 50, 90]), wr.max()))
+wxcc = {}
+for w, x in zip(wg.tolist(), xcc.tolist()):
+    wxcc[w] = x
+for x in sorted(set(wxcc.values())):
+    ends = [wg_end[w] for w in wg_end if wxcc[w] == x]
+    print("xcc %d workgroups done us: min %.1f p50 %.1f max %.1f" % (x, min(ends), np.median(ends), max(ends)))
 order = np.argsort(-en)[:12]
 print("latest waves: end, start, segs, KiB, wg, wave, xcc, rate")
 for k in order:
     print("  %.1f %.1f %d %d %d %d %d %.3f" % (en[k], st[k], L[k, 2], it[k], L[k, 4], L[k, 5], xcc[k], rate[k]))
+
+# pool takes: when each workgroup took its pool segments
+if len(EV):
+    et = (EV[:, 0] - t0) / 100.0
+    print("pool takes %d: first %.1f p10 %.1f p50 %.1f p90 %.1f last %.1f us" %
+          (len(EV), et.min(), *np.percentile(et, [10, 50, 90]), et.max()))
+    pw = {}
+    for w, t in zip(EV[:, 1].tolist(), et.tolist()):
+        pw.setdefault(w, []).append(t)
+    firsts = np.array([min(v) for v in pw.values()])
+    print("workgroups taking pool: %d; first take p10 %.1f p50 %.1f p90 %.1f; takes per wg p50 %d max %d" %
+          (len(pw), *np.percentile(firsts, [10, 50, 90]), np.median([len(v) for v in pw.values()]),
+           max(len(v) for v in pw.values())))
+    late = sorted(wg_end, key=lambda w: -wg_end[w])[:6]
+    early = sorted(wg_end, key=lambda w: wg_end[w])[:6]
+    for tag, ws in (("latest", late), ("earliest", early)):
+        for w in ws:
+            v = sorted(pw.get(w, []))
+            print("  %s wg %d done %.1f KiB %d pool takes %d at %s" %
+                  (tag, w, wg_end[w], wkib[w], len(v), " ".join("%.0f" % x for x in v[:12])))

@@ -1630,6 +1630,7 @@ vsa_lit_scan(VsaLitParams P) {
      * current segment it has not claimed yet: seg << 40 | end << 20 | cur
      * (groups of LIT_DEPTH iterations; cur = the next group to claim) */
     __shared__ unsigned long long rng[16];
+    __shared__ u32 pool_drained; /* pool regions this workgroup found empty */
     __shared__ u64 prof_lds[8 * MAX_CONF_WAVES]; /* confirm-wave profile (dbg & 64) */
     const u32 tid = threadIdx.x;
     const u32 lane = lane_id();
@@ -1700,6 +1701,7 @@ vsa_lit_scan(VsaLitParams P) {
     if (tid == 0) {
         q_done = 0;
         wg_ctr = 0;
+        pool_drained = 0;
     }
     if (tid < 8 * MAX_CONF_WAVES) prof_lds[tid] = 0;
     __syncthreads();
@@ -1771,49 +1773,50 @@ vsa_lit_scan(VsaLitParams P) {
      * tools/probe_stream.hip).  P.dynamic == 0: plain static assignment
      * (wave g takes g, g + G, ...).
      * P.dynamic == 2 (the default): workgroup b owns the host-built list
-     * [wg_seg[b], wg_seg[b + 1]) -- an equal share of the bytes, cut into
-     * segments that shrink toward the end of the list (runtime.hip
-     * plan_wg_lists) -- and its scanning waves take the next one from an
+     * [wg_seg[b], wg_seg[b + 1]) -- an equal share of the bytes (runtime.hip
+     * build_plan) -- and its scanning waves take the next segment from an
      * LDS counter: no global atomics at all (dynamic tickets measured 50
      * us of contention at 32 MiB and ~0.15 us of CU time per segment at 4
-     * GiB, profiles/r04c_launch_sweep.jsonl), and the CU's waves, whose
-     * issue rates differ ~3x by age, still balance among themselves down
-     * to the last, small segments. */
+     * GiB, profiles/r04c_launch_sweep.jsonl).  The CU's waves, whose issue
+     * rates differ ~3x by age, balance by stealing sweep groups from each
+     * other (below), so a large block is cut into one segment per wave;
+     * without stealing (VSA_STEAL=0) the list's segments shrink toward its
+     * end instead (guided sizes). */
     const u64 G = (u64)gridDim.x * NS;
     const u32 sched = P.dynamic;
     const u32 nreg = sched == 1 ? P.nregions : 1u;
     u32 reg_i = 0; /* regions tried so far */
     u32 reg = blockIdx.x % nreg;
     auto region_lo = [&](u32 r) { return P.nsegs * r / nreg; };
-    u32 wg_lo = 0, wg_hi = 0;
-    if (sched == 2) {
-        wg_lo = readfirstlane_u32(P.wg_seg[blockIdx.x]);
-        wg_hi = readfirstlane_u32(P.wg_seg[blockIdx.x + 1]);
-    }
     /* the next ticket is taken (lane 0, returning atomic) during the last
      * group of the current segment's sweep, so its latency hides behind
      * that group without one wave holding a whole segment ahead */
-    auto take = [&]() -> unsigned long long {
-        unsigned long long t = 0;
+    auto take = [&]() -> u32 {
+        u32 t = 0;
         if (sched == 2) {
             if (lane == 0)
                 t = __hip_atomic_fetch_add(&wg_ctr, 1u, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_WORKGROUP);
         } else if (lane == 0) {
-            t = atomicAdd(&P.counters[16 + 16 * reg], 1ULL);
+            t = (u32)atomicAdd(&P.counters[16 + 16 * reg], 1ULL);
         }
         return t;
     };
-    auto resolve = [&](unsigned long long t0) -> u64 {
-        u64 t = ((u64)readlane_u32((u32)(t0 >> 32), 0) << 32) | readlane_u32((u32)t0, 0);
-        if (sched == 2) return wg_lo + t < wg_hi ? wg_lo + t : P.nsegs;
+    auto resolve = [&](u32 t0) -> u32 {
+        u32 t = readlane_u32(t0, 0);
+        if (sched == 2) {
+            /* reloaded per segment (scalar loads) rather than held: the
+             * sweep needs the SGPRs */
+            const u32 wg_lo = readfirstlane_u32(P.wg_seg[blockIdx.x]);
+            const u32 wg_hi = readfirstlane_u32(P.wg_seg[blockIdx.x + 1]);
+            return wg_lo + t < wg_hi ? wg_lo + t : (u32)P.nsegs;
+        }
         for (;;) {
             const u64 sg = region_lo(reg) + t;
-            if (sg < region_lo(reg + 1)) return sg;
-            if (++reg_i == nreg) return P.nsegs; /* every region drained */
+            if (sg < region_lo(reg + 1)) return (u32)sg;
+            if (++reg_i == nreg) return (u32)P.nsegs; /* every region drained */
             reg = (reg + 1) % nreg;
-            const unsigned long long t1 = take();
-            t = ((u64)readlane_u32((u32)(t1 >> 32), 0) << 32) | readlane_u32((u32)t1, 0);
+            t = readlane_u32(take(), 0);
         }
     };
     /* Work stealing inside the workgroup (dynamic 2, P.steal): a wave whose
@@ -1826,7 +1829,7 @@ vsa_lit_scan(VsaLitParams P) {
      * range reaches the segment end.  Only parts of one block (not packed
      * groups or runs) are stolen. */
     const bool steal_on = sched == 2 && P.steal != 0;
-    auto steal = [&](u64 &sg, u32 &gs, u32 &ge) -> bool {
+    auto steal = [&](u32 &sg, u32 &gs, u32 &ge) -> bool {
         for (int tries = 0; tries < 64; tries++) {
             unsigned long long w = 0;
             if (lane < NS) w = rng[lane];
@@ -1855,7 +1858,7 @@ vsa_lit_scan(VsaLitParams P) {
             old = ((unsigned long long)readlane_u32((u32)(old >> 32), 0) << 32) |
                   readlane_u32((u32)old, 0);
             if (old == wv) {
-                sg = wv >> 40;
+                sg = (u32)(wv >> 40);
                 gs = mid;
                 ge = ve;
                 return true;
@@ -1863,15 +1866,58 @@ vsa_lit_scan(VsaLitParams P) {
         }
         return false;
     };
-    u64 seg = sched ? resolve(take()) : (u64)blockIdx.x * NS + wave;
+    /* The shared pool (dynamic 2): segments [wg_seg[G], nsegs) in 8
+     * regions of tickets (counters[16 + 16 r]), this workgroup's XCD region
+     * first; a region found empty is remembered in LDS, so a workgroup walks
+     * the drained regions once, not once per wave. */
+    auto pool_take = [&]() -> u32 {
+        const u32 pool_lo = readfirstlane_u32(P.wg_seg[gridDim.x]);
+        const u32 npool = (u32)P.nsegs - pool_lo;
+        u32 r = blockIdx.x & 7u;
+        for (int i = 0; npool && i < 8; i++, r = (r + 1) & 7u) {
+            if ((lds_ld32(&pool_drained) >> r) & 1u) continue;
+            unsigned long long t0 = 0;
+            if (lane == 0) t0 = atomicAdd(&P.counters[16 + 16 * r], 1ULL);
+            const u64 t = ((u64)readlane_u32((u32)(t0 >> 32), 0) << 32) | readlane_u32((u32)t0, 0);
+            const u64 lo = pool_lo + (u64)npool * r / 8, hi = pool_lo + (u64)npool * (r + 1) / 8;
+            if (lo + t < hi) {
+                if ((P.dbg & 16384) && P.wave_log && lane == 0) {
+                    /* diagnostic: pool take events (time, workgroup, wave,
+                     * segment) after the per-wave records */
+                    unsigned long long *ev = (unsigned long long *)P.wave_log + 65536;
+                    const unsigned long long k = atomicAdd(&ev[-1], 1ULL);
+                    if (k < 16000) {
+                        ev[4 * k] = __builtin_amdgcn_s_memrealtime();
+                        ev[4 * k + 1] = blockIdx.x;
+                        ev[4 * k + 2] = wave;
+                        ev[4 * k + 3] = lo + t;
+                    }
+                }
+                return (u32)(lo + t);
+            }
+            if (lane == 0)
+                __hip_atomic_fetch_or(&pool_drained, 1u << r, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        return (u32)P.nsegs;
+    };
+    /* segment indices are 32-bit (the plan's descriptors; the kernel's
+     * SGPRs are scarce) */
+    u32 seg = sched ? resolve(take()) : blockIdx.x * NS + wave;
     u32 st_gs = 0, st_ge = 0; /* a stolen range: sweep groups [st_gs, st_ge) */
+    bool from_list = true;     /* seg came from the workgroup's list */
     for (;;) {
         bool stolen = false;
         if (seg >= P.nsegs) {
-            if (!steal_on || !steal(seg, st_gs, st_ge)) break;
-            stolen = true;
+            /* out of list work: help the workgroup's waves, then the pool,
+             * then (the pool empty) the workgroup again */
+            from_list = false;
+            if (steal_on && steal(seg, st_gs, st_ge)) stolen = true;
+            else if (sched == 2 && (seg = pool_take()) < P.nsegs) stolen = false;
+            else if (steal_on && steal(seg, st_gs, st_ge)) stolen = true;
+            else break;
         }
-        unsigned long long t_next = 0;
+        u32 t_next = 0;
         bool have_next = false;
         bool lastb = true;
         auto prefetch_ticket = [&]() {
@@ -1963,7 +2009,6 @@ vsa_lit_scan(VsaLitParams P) {
         const int64_t s_hi =
             (!gcount && s_lo + ((int64_t)d_len << 10) < S.bhi) ? s_lo + ((int64_t)d_len << 10) : S.bhi;
         const u32 niters = (u32)((s_hi - s_lo + 1023) >> 10);
-        n_iter += niters;
         const int64_t zlo = (MODE == VSA_MODE_FDR || MODE == VSA_MODE_FDR4) ? B.zbase : S.qlo;
 
         /* iterations [f0, f1) are interior ("fast"): no byte of the 1 KiB
@@ -2084,6 +2129,7 @@ vsa_lit_scan(VsaLitParams P) {
             run_adv(ib);
         }
         bool tail_mine = true; /* a stolen-from range leaves its tail to the thief */
+        u32 swept = 0;         /* sweep iterations scanned (diagnostic) */
         if (nf > 0) {
             if constexpr (MODE == VSA_MODE_FDR && LDS_TABLE) {
                 /* sweep_enter: the carry and the previous chunk's last dword
@@ -2118,7 +2164,7 @@ vsa_lit_scan(VsaLitParams P) {
             u32 g_end = stolen ? st_ge : ng;
             const bool stealable = steal_on && gcount == 0 && !run && g_end > gs + 1;
             if (stealable && lane == 0)
-                rng[wave] = (seg << 40) | ((unsigned long long)g_end << 20) | (gs + 1);
+                rng[wave] = ((unsigned long long)seg << 40) | ((unsigned long long)g_end << 20) | (gs + 1);
             for (u32 g = gs; g < g_end; g++) {
                 unsigned long long clm = 0;
                 if (stealable && lane == 0)
@@ -2151,6 +2197,7 @@ vsa_lit_scan(VsaLitParams P) {
              * last group */
             tail_mine = g_end == ng;
             const u32 rem = tail_mine ? nf - ng * LIT_DEPTH : 0u;
+            swept = (g_end - gs) * LIT_DEPTH + rem;
 #pragma unroll
             for (int k = 0; k < LIT_DEPTH - 1; k++) {
                 if ((u32)k < rem) {
@@ -2186,13 +2233,15 @@ vsa_lit_scan(VsaLitParams P) {
                                                  bucket_mask);
             run_adv(ib);
         }
+        n_iter += (stolen ? 0u : f0) + swept + (tail_mine ? niters - f1 : 0u);
         ncand_total = is.ncand;
         ring_tail_cache = is.tail_cache;
         ring_head = is.head;
         } /* blocks of the segment */
         n_seg++;
-        /* after a stolen range the list is known to be exhausted */
-        seg = stolen ? P.nsegs : sched ? resolve(t_next) : seg + G;
+        /* after a stolen range or a pool segment, the list is known to be
+         * exhausted */
+        seg = (stolen || !from_list) ? (u32)P.nsegs : sched ? resolve(t_next) : seg + (u32)G;
     }
     if ((P.dbg & 4096) && P.wave_log && lane < 8) {
         u32 xcc, hwid;
@@ -2411,6 +2460,27 @@ __device__ __forceinline__ void publish_body(unsigned long long *ctr, unsigned l
     }
 }
 
+/* publish_body for one wave (no workgroup barrier): wave 0 of
+ * vsa_bin_finish's first workgroup publishes while its other waves sort */
+__device__ __forceinline__ void publish_wave(unsigned long long *ctr, unsigned long long *h,
+                                             unsigned long long seq, uint32_t nzero) {
+    const u32 l = lane_id();
+    const unsigned long long v = l < 16 ? ctr[l] : 0ULL;
+    /* every read above before any zeroing below (one wave: program order
+     * and a wait for the loads) */
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (l < 16) {
+        h[1 + l] = v;
+        ctr[nzero + l] = v; /* kept on the device too (vsa_pack) */
+    }
+    for (u32 i = l; i < nzero; i += WAVE) ctr[i] = 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (l == 0) {
+        __threadfence_system();
+        __hip_atomic_store(&h[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 __global__ void __launch_bounds__(256) vsa_publish(unsigned long long *ctr,
                                                    unsigned long long *h,
                                                    unsigned long long seq, uint32_t nzero,
@@ -2469,8 +2539,8 @@ __global__ void __launch_bounds__(1024) vsa_bin_finish(const uint32_t *counts, u
         const u32 e = wave_excl_scan(cnt[lane], &tot);
         off[lane] = base + e;
     }
-    if (blockIdx.x == 0) publish_body(ctr, h, seq, 144u, nullptr, nullptr, 0u);
     __syncthreads();
+    if (blockIdx.x == 0 && wv == 0) publish_wave(ctr, h, seq, 144u);
     /* this wave's 4 bins */
     const u32 lb = wv * 4;
     u32 m[4], mmax = 0;
@@ -2736,26 +2806,37 @@ typedef const __attribute__((address_space(3))) u8 lds_cu8_t;
 __device__ __forceinline__ u32 lds_ld8(u32 addr) { return *(lds_cu8_t *)(uintptr_t)addr; }
 
 #define CLS_DEPTH 4
-__global__ void __launch_bounds__(1024) vsa_class_scan_lut(VsaClassParams P, u64 span) {
+/* One 1024-thread workgroup per CU; workgroup b owns bytes [b wspan, (b + 1)
+ * wspan) (wspan a multiple of 4 KiB) and its 16 waves take 4 KiB groups of
+ * them from an LDS counter, the next group claimed one group ahead: no carry
+ * crosses a chunk here, so any wave can take any group, and waves whose issue
+ * rates differ by age (up to ~3x) finish together instead of a young wave's
+ * static span setting the end. */
+__global__ void __launch_bounds__(1024) vsa_class_scan_lut(VsaClassParams P, u64 wspan) {
     __shared__ __align__(16) u8 T[65536];
     __shared__ u8 mem[256];
+    __shared__ u32 gctr;
     const u32 tid = threadIdx.x;
     const u32 lane = lane_id();
     const u32 wave = readfirstlane_u32(tid / WAVE);
-    const u64 g = (u64)blockIdx.x * 16 + wave;
-    const u64 lo = g * span;
-    const u64 hi = min(lo + span, (u64)P.len);
+    const u64 lo = (u64)blockIdx.x * wspan;
+    const u64 hi = min(lo + wspan, (u64)P.len);
+    /* iterations (1 KiB) of the range, the full ones, and its groups */
     const u32 nit = lo < hi ? (u32)((hi - lo + 1023) >> 10) : 0u;
-    /* full iterations: the whole 1 KiB lies inside [0, len) */
     const u32 nfull = lo < hi ? (u32)min((u64)nit, ((u64)P.len - lo) >> 10) : 0u;
+    const u32 ngr = (nit + CLS_DEPTH - 1) / CLS_DEPTH;
     const u8 *sb = uniform_ptr(P.data + (lo < hi ? lo : 0));
-    /* the first ring loads go out before the table is built (plain loads
-     * stay in flight across the barriers) */
+    auto chunk_off = [&](u32 it, u32 fallback) { return 1024u * (it < nfull ? it : fallback); };
+    /* the first group (= wave) goes out before the table is built (plain
+     * loads stay in flight across the barriers); the second is wave + 16 */
+    u32 g = wave, gn = wave + 16;
     uint4 ring[CLS_DEPTH];
 #pragma unroll
     for (int k = 0; k < CLS_DEPTH; k++)
-        ring[k] = nfull ? load_wave_kib(sb, (u32)k < nfull ? 1024u * k : 0u) : make_uint4(0, 0, 0, 0);
+        ring[k] = g < ngr && nfull ? load_wave_kib(sb, chunk_off(g * CLS_DEPTH + k, 0))
+                                   : make_uint4(0, 0, 0, 0);
     if (tid < 256) mem[tid] = (u8)((P.cls[tid >> 5] >> (tid & 31)) & 1u);
+    if (tid == 0) gctr = 32;
     __syncthreads();
     {
         /* dword i holds T[4i .. 4i+3]: low bytes 4i & 0xff .., high byte i >> 6 */
@@ -2767,52 +2848,53 @@ __global__ void __launch_bounds__(1024) vsa_class_scan_lut(VsaClassParams P, u64
     __syncthreads();
     const u32 base = readfirstlane_u32((u32)(uintptr_t)(lds_cu8_t *)T);
     unsigned long long first = ~0ULL, last = 0, cnt = 0;
-    if (lo < hi) {
-        auto classify = [&](u32 it, const uint4 v, u32 valid_bytes) {
-            const u32 dw[4] = {v.x, v.y, v.z, v.w};
-            u32 bits = 0;
+    auto classify = [&](u32 it, const uint4 v, u32 valid_bytes) {
+        const u32 dw[4] = {v.x, v.y, v.z, v.w};
+        u32 bits = 0;
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const u32 r0 = lds_ld8(lut_addr16<0>(dw[k], base));
-                const u32 r1 = lds_ld8(lut_addr16<1>(dw[k], base));
-                bits |= (r0 | (r1 << 2)) << (4 * k);
-            }
-            if (valid_bytes < 16) bits &= (1u << valid_bytes) - 1u;
-            const u64 p0 = lo + 1024 * (u64)it + 16 * lane;
-            if (P.bitmap) ((uint16_t *)P.bitmap)[p0 >> 4] = (uint16_t)bits;
-            if (bits) {
-                const u64 f = p0 + (u64)(__ffs(bits) - 1);
-                const u64 l = p0 + (u64)(31 - __clz(bits)) + 1;
-                first = f < first ? f : first;
-                last = l > last ? l : last;
-                cnt += __popc(bits);
-            }
-        };
-        u32 it = 0;
-        for (; it + CLS_DEPTH <= nfull; it += CLS_DEPTH) {
+        for (int k = 0; k < 4; k++) {
+            const u32 r0 = lds_ld8(lut_addr16<0>(dw[k], base));
+            const u32 r1 = lds_ld8(lut_addr16<1>(dw[k], base));
+            bits |= (r0 | (r1 << 2)) << (4 * k);
+        }
+        if (valid_bytes < 16) bits &= (1u << valid_bytes) - 1u;
+        const u64 p0 = lo + 1024 * (u64)it + 16 * lane;
+        if (P.bitmap) ((uint16_t *)P.bitmap)[p0 >> 4] = (uint16_t)bits;
+        if (bits) {
+            const u64 f = p0 + (u64)(__ffs(bits) - 1);
+            const u64 l = p0 + (u64)(31 - __clz(bits)) + 1;
+            first = f < first ? f : first;
+            last = l > last ? l : last;
+            cnt += __popc(bits);
+        }
+    };
+    while (g < ngr) {
+        u32 gnn = 0;
+        if (lane == 0)
+            gnn = __hip_atomic_fetch_add(&gctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
-            for (int k = 0; k < CLS_DEPTH; k++) {
-                const uint4 v = ring[k];
-                const u32 itn = it + k + CLS_DEPTH;
-                ring[k] = load_wave_kib(sb, 1024u * (itn < nfull ? itn : it + k));
-                classify(it + k, v, 16);
+        for (int k = 0; k < CLS_DEPTH; k++) {
+            const u32 it = g * CLS_DEPTH + k;
+            const uint4 v = ring[k];
+            /* the next group's chunk k (past the range: this chunk again) */
+            const u32 itn = gn < ngr ? gn * CLS_DEPTH + k : it;
+            if (nfull) ring[k] = load_wave_kib(sb, chunk_off(itn, it < nfull ? it : 0));
+            if (it < nfull) {
+                classify(it, v, 16);
+            } else if (it < nit) {
+                /* the ragged last iteration (buffer end): bytes past len read as 0 */
+                const u64 p0 = lo + 1024 * (u64)it + 16 * lane;
+                u32 d[4] = {0, 0, 0, 0};
+                u32 nv = 0;
+                if (p0 < hi) {
+                    nv = (u32)min((u64)16, hi - p0);
+                    for (u32 b = 0; b < nv; b++) d[b >> 2] |= (u32)P.data[p0 + b] << (8 * (b & 3));
+                }
+                if (p0 < hi) classify(it, make_uint4(d[0], d[1], d[2], d[3]), nv);
             }
         }
-#pragma unroll
-        for (int k = 0; k < CLS_DEPTH - 1; k++)
-            if (it + k < nfull) classify(it + k, ring[k], 16);
-        it = nfull;
-        /* the ragged last iteration (buffer end): bytes past len read as 0 */
-        for (; it < nit; it++) {
-            const u64 p0 = lo + 1024 * (u64)it + 16 * lane;
-            u32 d[4] = {0, 0, 0, 0};
-            u32 nv = 0;
-            if (p0 < hi) {
-                nv = (u32)min((u64)16, hi - p0);
-                for (u32 b = 0; b < nv; b++) d[b >> 2] |= (u32)P.data[p0 + b] << (8 * (b & 3));
-            }
-            if (p0 < hi) classify(it, make_uint4(d[0], d[1], d[2], d[3]), nv);
-        }
+        g = gn;
+        gn = readfirstlane_u32(gnn);
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {

@@ -1093,31 +1093,49 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
         }
         flush();
     } else {
-        /* Per-workgroup lists (kernels.hip, dynamic 2): the live bytes are
-         * split into G equal shares, one per workgroup, in block order; each
-         * share is cut into segments of clamp(r / (K x ns), min, max), r =
-         * the bytes of the share still uncut, so they shrink geometrically
-         * toward the share's end (guided self-scheduling): the CU's waves,
-         * whose rates differ ~3x by issue age, take the big ones first and
-         * finish on small ones together.  Blocks shorter than half the
-         * current size are packed whole as before. */
+        /* Per-workgroup lists (kernels.hip, dynamic 2).  The first
+         * (1 - VSA_POOL_PM / 1000) of the live bytes, in block order, are
+         * split into G equal shares, one list per workgroup; the rest is a
+         * shared pool of small segments (region tickets, like the round-3
+         * scheduler) that workgroups take from once their own list and
+         * their waves' stealing run dry.  The pool is what balances the
+         * XCDs: on some boxes one XCD runs ~10 % slower than another
+         * (profiles/r04e_waves_4g.txt: workgroups of XCD 7 done at 954 us,
+         * XCD 2 at 859 us, with equal shares).  With stealing, a large block
+         * is cut into one segment per wave of the share; without it
+         * (VSA_STEAL=0) into segments of clamp(r / (K x ns), min, max), r =
+         * the bytes of the share still uncut (guided sizes).  Blocks shorter
+         * than half the current size are packed whole as before. */
         uint64_t T = 0;
         for (int64_t sp : live) T += (uint64_t)sp;
         static const uint64_t K = std::max(1, env_int("VSA_WG_K", 2));
         static const uint64_t smax = (uint64_t)std::max(1, env_int("VSA_WG_MAX_KIB", 256)) << 10;
         static const uint64_t smin0 = (uint64_t)std::max(1, env_int("VSA_WG_MIN_KIB", 4)) << 10;
+        static const uint64_t pool_pm = (uint64_t)std::min(900, std::max(0, env_int("VSA_POOL_PM", 125)));
         const uint64_t smin = T <= (64u << 10) ? 1024u : smin0;
         const uint64_t gmax = std::max<uint64_t>(1, waves / ns);
         const uint64_t G = std::max<uint64_t>(1, std::min(gmax, (T + ns * smin - 1) / (ns * smin)));
+        /* the pool: only for a grid wide enough to be unbalanced */
+        const bool pool_on = G >= 16 && pool_pm > 0;
+        const uint64_t Tst = pool_on ? T - T * pool_pm / 1000 : T;
+        const uint64_t ps = std::min<uint64_t>(
+            128u << 10, std::max<uint64_t>(16u << 10, (((T - Tst) / (8 * G)) + 1023) & ~(uint64_t)1023));
         std::vector<uint32_t> wg_first(G + 1, 0);
         uint64_t g = 0, acc = 0;
-        auto cum = [&](uint64_t k) { return (uint64_t)((unsigned __int128)T * (k + 1) / G); };
+        bool in_pool = false;
+        uint64_t pool_lo = 0;
+        auto cum = [&](uint64_t k) { return (uint64_t)((unsigned __int128)Tst * (k + 1) / G); };
         auto advance = [&]() {
             while (g + 1 < G && acc >= cum(g)) wg_first[++g] = (uint32_t)pl.nsegs;
+            if (pool_on && !in_pool && acc >= Tst) {
+                in_pool = true;
+                pool_lo = pl.nsegs;
+            }
         };
         static const uint64_t bmax = (uint64_t)std::max(4, env_int("VSA_WG_BIG_MAX_KIB", 16384)) << 10;
-        const uint64_t big = std::min(bmax, std::max(smin, ((T / G / ns) + 1023) & ~(uint64_t)1023));
+        const uint64_t big = std::min(bmax, std::max(smin, ((Tst / G / ns) + 1023) & ~(uint64_t)1023));
         auto size_now = [&]() -> uint64_t {
+            if (in_pool) return ps;
             const uint64_t c = cum(g);
             const uint64_t r = c > acc ? c - acc : 0;
             uint64_t v = (r / (K * ns) + 1023) & ~(uint64_t)1023;
@@ -1140,7 +1158,7 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
                 g_n++;
                 g_span += sp;
                 acc += (uint64_t)sp;
-                if (acc >= cum(g)) { /* the share ends here */
+                if (!in_pool && acc >= cum(g)) { /* the share ends here */
                     flush();
                     advance();
                 }
@@ -1153,13 +1171,13 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
                 /* with stealing, a part of a large block is one wave's share
                  * of its workgroup's bytes: the waves balance by stealing
                  * sweep groups, so no segment needs to be small (fewer
-                 * segment starts); without it, the guided size */
-                sz = steal_min() ? big : size_now();
+                 * segment starts); without it, the guided size; in the pool,
+                 * the pool's size */
+                sz = in_pool ? ps : steal_min() ? big : size_now();
                 /* a piece ends at its share's end: every workgroup gets its
-                 * share to the KiB (stealing balances inside a workgroup
-                 * only) */
+                 * share to the KiB */
                 const uint64_t cg = cum(g);
-                if (cg > acc) sz = std::min(sz, (cg - acc + 1023) & ~(uint64_t)1023);
+                if (!in_pool && cg > acc) sz = std::min(sz, (cg - acc + 1023) & ~(uint64_t)1023);
                 uint64_t piece = std::min<uint64_t>(sz, (uint64_t)sp - off);
                 /* no sliver shorter than the minimum after this piece */
                 if ((uint64_t)sp - off - piece < smin) piece = (uint64_t)sp - off;
@@ -1170,7 +1188,9 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
             }
         }
         flush();
-        for (uint64_t k = g + 1; k <= G; k++) wg_first[k] = (uint32_t)pl.nsegs;
+        if (!in_pool) pool_lo = pl.nsegs;
+        for (uint64_t k = g + 1; k <= G; k++) wg_first[k] = (uint32_t)pool_lo;
+        wg_first[G] = (uint32_t)pool_lo; /* the pool: segments [wg_first[G], nsegs) */
         pl.grid = (uint32_t)G;
         pl.segblk.insert(pl.segblk.end(), wg_first.begin(), wg_first.end());
     }
@@ -2412,11 +2432,12 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
     VSA_CHECK(hipEventRecord(c->ev0, c->stream));
     if (!cls2 && len >= ((uint64_t)8 << 20) && !getenv("VSA_CLASS_SIMPLE")) {
         /* large buffers: pair-LUT kernel, one 1024-thread workgroup per CU,
-         * a contiguous 1 KiB-aligned span per wave */
-        const uint64_t waves = (uint64_t)c->num_cus * 16;
-        const uint64_t span = ((len + waves - 1) / waves + 1023) & ~(uint64_t)1023;
-        hipLaunchKernelGGL(vsa_class_scan_lut, dim3(c->num_cus), dim3(1024), 0, c->stream, P,
-                           span);
+         * an equal 4 KiB-aligned share per workgroup, taken by its waves in
+         * 4 KiB groups (kernels.hip vsa_class_scan_lut) */
+        const uint64_t G = (uint64_t)c->num_cus;
+        const uint64_t wspan = ((len + G - 1) / G + 4095) & ~(uint64_t)4095;
+        const uint32_t grid = (uint32_t)((len + wspan - 1) / wspan);
+        hipLaunchKernelGGL(vsa_class_scan_lut, dim3(grid), dim3(1024), 0, c->stream, P, wspan);
     } else {
         uint64_t chunks = (len + 15) / 16;
         uint64_t want = (chunks + 255) / 256;
