@@ -258,11 +258,14 @@ int vsa_scan_blocks_stream(vsa_ctx_t *ctx, const vsa_db_t *db, const uint8_t *d_
 typedef struct vsa_plan vsa_plan_t;
 /* Host-only: the schedule (segment descriptors, per-workgroup list bounds)
  * the planner makes for a batch on num_cus CUs with ns scanning waves each,
- * for tests and tools; returns the word count. */
+ * for tests and tools; returns the word count.  wg_weights (NULL: equal)
+ * weights workgroup b's static share, as the schedule feedback does (one
+ * float per workgroup, at least num_cus of them). */
 int vsa_plan_describe(const uint8_t *d_data, const uint64_t *offsets, const uint64_t *lens,
                       const uint64_t *starts, const uint64_t *hlens, const uint64_t *report_lo,
                       uint32_t nblocks, uint32_t num_cus, uint32_t ns, uint32_t *words,
-                      uint64_t cap, uint64_t *nsegs, uint32_t *grid);
+                      uint64_t cap, uint64_t *nsegs, uint32_t *grid,
+                      const float *wg_weights);
 int vsa_plan_create(vsa_ctx_t *ctx, const uint8_t *d_data, const uint64_t *offsets,
                     const uint64_t *lens, const uint64_t *starts, const uint64_t *hlens,
                     const uint64_t *report_lo, uint32_t nblocks, vsa_plan_t **plan);
@@ -402,6 +405,21 @@ int vsa_derive_first_stage(const void *hwlm, size_t size, uint64_t *table, uint3
  * at 15 bits).  Returns entries written or a VSA_E_* code. */
 int vsa_derive_fdr4_table(const void *hwlm, size_t size, uint32_t bits, uint32_t *table,
                           uint32_t cap);
+
+/* Host-only (tests / tools): the 15-bit 4-field table of one split pass --
+ * par 0 / 1: the literals whose last byte can have bit 0 == par, the table
+ * a large set's pass over the ends with that end-byte bit uses; -1: the
+ * one-pass table -- and in *text_rate (may be NULL) the candidate bits per
+ * text byte estimated from it (the rule that turns the split passes on past
+ * 0.015).  table may be NULL (rate only).  Returns the entries written or a
+ * VSA_E_* code.  No reference counterpart: the split is this engine's
+ * schedule for sets the reference scans with one FDR pass (fdr.c:776-796). */
+int vsa_derive_fdr4_pass(const void *hwlm, size_t size, int par, uint32_t *table, uint32_t cap,
+                         double *text_rate);
+
+/* 1 when the database scans in split passes (vsa_derive_fdr4_pass), 0 if
+ * not, or a VSA_E_* code. */
+int vsa_db_split(const vsa_db_t *db);
 
 /* Optional: hs_scratch field offsets for INCLUDED_JUMP squash replay
  * (offsetof(struct hs_scratch, fdr_conf / fdr_conf_offset)); the defaults

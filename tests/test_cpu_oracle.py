@@ -536,6 +536,55 @@ def test_fdr4_first_stage_no_false_negatives(nlits, minlen, bits):
         assert len(cand) <= len(set(_first_stage_candidates(t8, kb, fb, data).tolist()))
 
 
+@pytest.mark.parametrize("nlits,minlen,msk", [(2000, 1, 0.0), (3000, 4, 0.0), (800, 2, 0.3)])
+def test_fdr4_split_passes_no_false_negatives(nlits, minlen, msk):
+    """Split passes (runtime.hip, large sets): pass `par` keeps the ends
+    whose byte has bit 0 == par and scans them with the table of the
+    literals whose last byte can have that bit (vsa_derive_fdr4_pass).
+    Every end the reference's confirm accepts is a candidate of exactly the
+    pass its byte belongs to, and each pass table is at least as selective
+    on its ends as the one-pass table."""
+    import bench
+    rng = random.Random(910 + nlits + minlen)
+    lits = (rand_lits(rng, nlits, minlen=minlen, maxlen=8, msk_frac=msk) if msk else
+            [vsa.HwlmLiteral(bytes(rng.randint(0x20, 0x7E) for _ in range(rng.randint(minlen, 8))),
+                             rng.random() < 0.1, i) for i in range(nlits)])
+    blob = build_or_none(lits, 0)
+    if blob is None or blob.is_noodle or blob.engine_id != 0:
+        pytest.skip("FDR not buildable for this set")
+    data = (bench.make_corpus(1 << 20, lits, seed=nlits, plant_every=512) if not msk else
+            np.frombuffer(rand_data(rng, 1 << 20, alphabet=bytes(range(0x61, 0x6b))), np.uint8))
+    st, m = oracle.fdr_exec(vsa.engine_blob(blob), data, cap=1 << 21)
+    assert st == 0 and len(m) > 100
+    full, _ = vsa.derive_fdr4_pass(blob, -1)
+    assert np.array_equal(full, vsa.derive_fdr4_table(blob, 15))
+    b = np.frombuffer(bytes(data), np.uint8)
+    ends = np.array(sorted({e for e, _ in m}), np.int64)
+    one = set(_fdr4_candidates(full, 15, data).tolist())
+    for par in (0, 1):
+        t, _ = vsa.derive_fdr4_pass(blob, par)
+        c = _fdr4_candidates(t, 15, data)
+        c = c[(b[c] & 1) == par]
+        mine = ends[(b[ends] & 1) == par]
+        assert set(mine.tolist()) <= set(c.tolist()), par
+        assert set(c.tolist()) <= one
+
+
+def test_fdr4_split_rule():
+    """The split rule (runtime.hip split_passes: estimated text rate of the
+    one-pass table > 0.015, the measured crossover): one pass for the
+    20k-literal cfg-4 set, split passes for 30k and 50k, whose pass tables
+    estimate well under the one-pass rate."""
+    import bench
+    r20 = vsa.derive_fdr4_pass(vsa.hwlm_build(bench.make_literals(20000, seed=12)), -1)[1]
+    b50 = vsa.hwlm_build(bench.make_literals(50000, seed=12))
+    r30 = vsa.derive_fdr4_pass(vsa.hwlm_build(bench.make_literals(30000, seed=12)), -1)[1]
+    r50 = vsa.derive_fdr4_pass(b50, -1)[1]
+    p0, p1 = (vsa.derive_fdr4_pass(b50, p)[1] for p in (0, 1))
+    assert r20 < 0.015 < r30 < r50
+    assert (p0 + p1) / 2 < r50 / 3
+
+
 # ------------------------------------------------- SIMD CPU baseline ---
 
 @pytest.mark.parametrize("hint", [0, -1])

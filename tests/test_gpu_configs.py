@@ -142,7 +142,9 @@ def test_gpu_large_literal_sets(ctx, nlits, monkeypatch):
     with two confirm waves per workgroup; one launch also forces a single
     confirm wave and one three (VSA_NCONF).  From the second launch on the
     scanning waves expand the candidates (scanner expansion, runtime.hip
-    use_xp); the last two launches force it off and on (VSA_XP).  Every
+    use_xp); the last two launches force it off and on (VSA_XP).  The
+    database is loaded with the split passes at their default (on for 50k,
+    runtime.hip split_passes) and forced off and on (VSA_SPLIT).  Every
     launch == the oracle."""
     lits = bench.make_literals(nlits, seed=12)
     blob = vsa.hwlm_build(lits)
@@ -151,21 +153,29 @@ def test_gpu_large_literal_sets(ctx, nlits, monkeypatch):
     assert st == 0 and len(want) >= len(data) // (16 << 10)
     n = len(data)
     d = ctx.malloc(n + 64)
-    db = vsa.Database(ctx, blob)
     try:
         ctx.h2d(d, data)
-        for nconf, xp in ((None, None), (None, None), ("1", None), ("3", None),
-                          ("2", "0"), ("2", "1")):
-            if nconf:
-                monkeypatch.setenv("VSA_NCONF", nconf)
-            if xp:
-                monkeypatch.setenv("VSA_XP", xp)
-            k = ctx.scan_blocks(db, d, [0], [n])
-            res = ctx.results(k)
-            got = list(zip((res["key"] >> np.uint64(24)).tolist(), res["id"].tolist()))
-            assert got == want, (nconf, xp)
+        for split in (None, "0", "1"):
+            if split:
+                monkeypatch.setenv("VSA_SPLIT", split)
+            db = vsa.Database(ctx, blob)
+            try:
+                runs = (((None, None), (None, None), ("1", None), ("3", None), ("2", "0"),
+                         ("2", "1")) if split is None else ((None, None), ("2", "1")))
+                for nconf, xp in runs:
+                    if nconf:
+                        monkeypatch.setenv("VSA_NCONF", nconf)
+                    if xp:
+                        monkeypatch.setenv("VSA_XP", xp)
+                    k = ctx.scan_blocks(db, d, [0], [n])
+                    res = ctx.results(k)
+                    got = list(zip((res["key"] >> np.uint64(24)).tolist(),
+                                   res["id"].tolist()))
+                    assert got == want, (split, nconf, xp)
+            finally:
+                monkeypatch.delenv("VSA_NCONF", raising=False)
+                monkeypatch.delenv("VSA_XP", raising=False)
+                db.close()
     finally:
-        monkeypatch.delenv("VSA_NCONF", raising=False)
-        monkeypatch.delenv("VSA_XP", raising=False)
-        db.close()
+        monkeypatch.delenv("VSA_SPLIT", raising=False)
         ctx.free(d)

@@ -654,6 +654,51 @@ def test_gpu_scanner_expansion(ctx, nlits, monkeypatch):
     assert run_layout_scan(ctx, blob, rb, 3) == want
 
 
+@pytest.mark.parametrize("nlits", [1, 30, 500, 3000])
+def test_gpu_split_passes(ctx, nlits, monkeypatch):
+    """Split passes (VSA_SPLIT=1; runtime.hip turns them on for large
+    literal sets): one launch per bit 0 of the end byte, each with the
+    first-stage table of the literals whose last byte has that bit (both
+    for a last byte whose mask leaves bit 0 free), into one output.  Forced
+    on small sets with masked literals: per-block records equal the
+    oracle's hwlmExec of each block, for ragged blocks with starts and
+    misalignment, with scanner expansion off and on, and back-to-back runs
+    with literals across every boundary."""
+    rng = random.Random(5300 + nlits)
+    lits = rand_lits(rng, nlits, minlen=1 if nlits == 1 else 2, maxlen=8, msk_frac=0.3)
+    blob = vsa.hwlm_build(lits, engine_hint=0, allow_noodle=False)
+    if blob.engine_id != 0:
+        pytest.skip("split passes are an FDR schedule (engine %d)" % blob.engine_id)
+    sizes = [0, 1, 2, 7, 15, 16, 17, 100, 1023, 1024, 1025, 2047, 3000, 9000, 40000]
+    bufs = [rand_data(rng, rng.choice(sizes)) for _ in range(1200)]
+    starts = [rng.choice([0, 0, 0, 1, 5, 17]) if b else 0 for b in bufs]
+    starts = [s if s < max(1, len(b)) else 0 for s, b in zip(starts, bufs)]
+    want = []
+    for b, s in zip(bufs, starts):
+        if s >= len(b):
+            want.append([])
+            continue
+        st, m = oracle.hwlm_exec(blob.ptr, b, start=s, cap=1 << 16)
+        want.append(m)
+    monkeypatch.setenv("VSA_SPLIT", "1")
+    for xp in ("0", "1"):
+        monkeypatch.setenv("VSA_XP", xp)
+        for mis in (0, 5):
+            assert batch_run(ctx, blob, bufs, starts=starts, misalign=mis) == want, (xp, mis)
+    monkeypatch.delenv("VSA_XP")
+    alpha = b"abcdefghABCDEFGH" if nlits <= 30 else bytes(range(0x61, 0x7b))
+    rb = [bytearray(rand_data(rng, rng.choice([1024, 1500, 2048, 4096, 16384]), alpha))
+          for _ in range(300)]
+    for k in range(len(rb) - 1):
+        s = rng.choice(lits).s
+        if len(s) > 1:
+            cut = rng.randint(1, len(s) - 1)
+            rb[k][len(rb[k]) - cut:] = s[:cut]
+            rb[k + 1][:len(s) - cut] = s[cut:]
+    want = [oracle.hwlm_exec(blob.ptr, bytes(b), cap=1 << 18)[1] for b in rb]
+    assert run_layout_scan(ctx, blob, rb, 3) == want
+
+
 def test_gpu_plan_free_after_async_overflow():
     """a plan freed while its asynchronous scan is still pending
     -- a scan that overflows the output (its rescan reads the plan's tables)

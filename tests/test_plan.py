@@ -3,9 +3,9 @@ host-only vsa_plan_describe): whatever the block layout, the segments cover
 every live block's span exactly once, in order; the per-workgroup lists
 (kernels.hip dynamic 2: one list per workgroup, handed out in LDS) give
 every workgroup an equal share of the static bytes -- stealing balances
-waves only inside a workgroup -- and the rest (VSA_POOL_PM, 12.5 % by
-default) is a pool of small segments after the lists, shared by all
-workgroups, which balances the XCDs."""
+waves only inside a workgroup -- and the rest (VSA_POOL_PM per mille, off
+by default, 125 in the pool tests) is a pool of small segments after the
+lists, shared by all workgroups."""
 import ctypes
 import random
 
@@ -18,10 +18,12 @@ lib = vsa.lib
 lib.vsa_plan_describe.restype = ctypes.c_int
 lib.vsa_plan_describe.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5 + [
     ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64,
-    ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]
+    ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32), ctypes.c_void_p]
 
 
-def describe(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000):
+def describe(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000, weights=None):
+    wv = None if weights is None else np.ascontiguousarray(weights, np.float32)
+    wp = None if wv is None else wv.ctypes.data
     o = np.ascontiguousarray(offs, np.uint64)
     ln = np.ascontiguousarray(lens, np.uint64)
     st = None if starts is None else np.ascontiguousarray(starts, np.uint64)
@@ -29,12 +31,12 @@ def describe(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000):
     g = ctypes.c_uint32()
     w = lib.vsa_plan_describe(base, o.ctypes.data, ln.ctypes.data,
                               None if st is None else st.ctypes.data, None, None, len(o),
-                              num_cus, ns, None, 0, ctypes.byref(n), ctypes.byref(g))
+                              num_cus, ns, None, 0, ctypes.byref(n), ctypes.byref(g), wp)
     assert w >= 0
     words = np.zeros(w, np.uint32)
     lib.vsa_plan_describe(base, o.ctypes.data, ln.ctypes.data,
                           None if st is None else st.ctypes.data, None, None, len(o), num_cus,
-                          ns, words.ctypes.data, w, ctypes.byref(n), ctypes.byref(g))
+                          ns, words.ctypes.data, w, ctypes.byref(n), ctypes.byref(g), wp)
     nseg, grid = n.value, g.value
     desc = words[:4 * nseg].reshape(-1, 4)
     bounds = words[4 * nseg:] if grid else None
@@ -52,9 +54,20 @@ def spans(offs, lens, starts, base):
     return out
 
 
-def check(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000):
+POOL_PM = [0]
+
+
+@pytest.fixture(params=[0, 125], ids=["no_pool", "pool125"])
+def pool(request, monkeypatch):
+    monkeypatch.setenv("VSA_POOL_PM", str(request.param))
+    POOL_PM[0] = request.param
+    yield request.param
+    POOL_PM[0] = 0
+
+
+def check(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000, weights=None):
     starts = list(starts) if starts is not None else [0] * len(offs)
-    desc, bounds, grid = describe(offs, lens, starts, num_cus, ns, base)
+    desc, bounds, grid = describe(offs, lens, starts, num_cus, ns, base, weights)
     sp = spans(offs, lens, starts, base)
     covered = {}
     seg_bytes = []
@@ -86,9 +99,9 @@ def check(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000):
         assert np.all(np.diff(bounds.astype(np.int64)) >= 0)
         per = [sum(seg_bytes[bounds[g]:bounds[g + 1]]) for g in range(grid)]
         pool = seg_bytes[bounds[-1]:]
-        if grid >= 16:
-            # the pool: 12.5 % of the bytes (to a segment), small segments
-            assert abs(sum(pool) - T * 125 // 1000) <= max(seg_bytes) + 4096
+        if grid >= 16 and POOL_PM[0]:
+            # the pool: VSA_POOL_PM of the bytes (to a segment), small segments
+            assert abs(sum(pool) - T * POOL_PM[0] // 1000) <= max(seg_bytes) + 4096
         else:
             assert not pool
         return desc, bounds, grid, per, sum(per), seg_bytes
@@ -96,7 +109,7 @@ def check(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000):
 
 
 @pytest.mark.parametrize("mib,nblk", [(4096, 4), (512, 4), (512, 1), (64, 3), (1, 1)])
-def test_plan_large_blocks_equal_shares(mib, nblk):
+def test_plan_large_blocks_equal_shares(mib, nblk, pool):
     total = mib << 20
     bl = total // nblk
     desc, bounds, grid, per, T, segb = check([i * bl for i in range(nblk)], [bl] * nblk)
@@ -109,7 +122,7 @@ def test_plan_large_blocks_equal_shares(mib, nblk):
 
 
 @pytest.mark.parametrize("seed", range(6))
-def test_plan_random_layouts(seed):
+def test_plan_random_layouts(seed, pool):
     rng = random.Random(seed)
     offs, lens, starts = [], [], []
     pos = 0
@@ -132,7 +145,7 @@ def test_plan_random_layouts(seed):
         assert max(per) - share <= max(seg_bytes) + 4096
 
 
-def test_plan_back_to_back_small_blocks_pack_into_runs():
+def test_plan_back_to_back_small_blocks_pack_into_runs(pool):
     n = 65536
     desc, bounds, grid, per, T, seg_bytes = check([i * 16384 for i in range(n)], [16384] * n)
     groups = [d for d in desc.tolist() if d[0] >> 24]
@@ -146,3 +159,22 @@ def test_plan_drop_in_sizes_use_few_workgroups():
         desc, bounds, grid, per, T, _ = check([0], [ln])
         assert grid == max(1, min(256, -(-T // (15 * 1024))))
         assert bounds[-1] == len(desc)  # no pool for a few workgroups
+
+
+@pytest.mark.parametrize("mib,nblk", [(4096, 4), (512, 1), (300, 7)])
+def test_plan_feedback_weights(mib, nblk):
+    """Schedule feedback (runtime.hip take_feedback): per-workgroup weights
+    (here an XCD pattern, workgroup b on XCD b % 8, 0.85-1.15) give each
+    workgroup a static share in proportion to its weight, to the KiB plus a
+    sliver, and the segments still cover every block exactly once."""
+    total = mib << 20
+    bl = total // nblk
+    xw = [1.0, 0.9, 1.1, 1.0, 0.85, 1.15, 1.0, 1.0]
+    weights = [xw[b % 8] for b in range(256)]
+    desc, bounds, grid, per, T, segb = check([i * bl for i in range(nblk)], [bl] * nblk,
+                                             weights=weights)
+    assert grid == 256
+    wsum = sum(weights[:grid])
+    for b in range(grid):
+        want = T * weights[b] / wsum
+        assert abs(per[b] - want) <= 1024 * nblk + 4096 + 1024, (b, per[b], want)

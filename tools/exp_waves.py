@@ -24,13 +24,31 @@ vsa.lib.vsa_set_wave_log.argtypes = [ctypes.c_void_p]
 vsa.lib.vsa_set_wave_log(log.data_ptr())
 torch.cuda.synchronize()
 offs = [i * bl for i in range(4)]
+per_launch = []
 for i in range(22):
     log.zero_()
     ctx.scan_blocks(db, data.data_ptr(), offs, [bl] * 4)
+    if i >= 0:
+        # per-XCD workgroup done time (us from the first wave start) of
+        # this launch: is the XCD order stable launch to launch?
+        LL = log[:65536].view(-1, 8).cpu().numpy().astype(np.int64)
+        LL = LL[(LL[:, 0] != 0) & (LL[:, 1] != 0)]
+        tz = LL[:, 0].min()
+        xd = {}
+        for w, x, e in zip(LL[:, 4].tolist(), (LL[:, 6] & 0xf).tolist(), ((LL[:, 1] - tz) / 100.0).tolist()):
+            xd.setdefault(x, {}).setdefault(w, 0)
+            xd[x][w] = max(xd[x][w], e)
+        bx = {w: x for w, x in zip(LL[:, 4].tolist(), (LL[:, 6] & 0xf).tolist())}
+        rr = sum(1 for w, x in bx.items() if w % 8 == x)
+        per_launch.append("launch %d kernel %.4f ms; xcd p50 done: %s; wg%%8==xcc %d/%d" % (
+            i, ctx.kernel_ms(), " ".join("%d:%.1f" % (x, np.median(list(v.values())))
+                                        for x, v in sorted(xd.items())), rr, len(bx)))
 LA = log.cpu().numpy().astype(np.int64)
 L = LA[:65536].reshape(-1, 8)
 nev = int(LA[65535])
 EV = LA[65536:65536 + 4 * min(nev, 16000)].reshape(-1, 4)
+for line in per_launch:
+    print(line)
 L = L[L[:, 0] != 0]
 L = L[L[:, 1] != 0] if len(L) else L
 t0 = L[:, 0].min()

@@ -310,6 +310,25 @@ def derive_fdr4_table(blob, bits=15):
     return out[:n]
 
 
+_sig("vsa_derive_fdr4_pass", ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+     ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double))
+_sig("vsa_db_split", ctypes.c_int, ctypes.c_void_p)
+
+
+def derive_fdr4_pass(blob, par=-1):
+    """(table, estimated text candidate rate) of one split pass (par 0 / 1)
+    or of the one-pass table (par -1), 15-bit keys (host only; see
+    vsa_derive_fdr4_pass)"""
+    cap = 1 << 15
+    out = np.zeros(cap, np.uint32)
+    rate = ctypes.c_double()
+    n = lib.vsa_derive_fdr4_pass(blob.ptr, blob.size, par, out.ctypes.data, cap,
+                                 ctypes.byref(rate))
+    if n < 0:
+        raise BuildError("vsa_derive_fdr4_pass failed with %d" % n)
+    return out[:n], rate.value
+
+
 def engine_blob(blob):
     """Pointer to the engine inside an HWLM blob (HWLM_C_DATA, hwlm_internal.h:56)."""
     return blob.ptr + HWLM_HEADER
@@ -832,6 +851,11 @@ class Database:
     @property
     def engine(self):
         return lib.vsa_db_engine(self.ptr)
+
+    @property
+    def split(self):
+        """True when the database scans in split passes (large FDR sets)"""
+        return lib.vsa_db_split(self.ptr) == 1
 
     def close(self):
         if self.ptr:

@@ -118,6 +118,8 @@ struct VsaLitParams {
     const uint64_t *table;  /* FDR domain table / Teddy combined byte table */
     uint32_t table_entries;
     uint32_t dmask;
+    uint32_t end_par;       /* FDR4 split passes: 0 every end; 1 / 2 only the
+                               ends whose byte has bit 0 clear / set */
     uint64_t state_lo, state_hi; /* FDR start state (fdr->start) */
     const uint8_t *conf_base;    /* engine confBase (device) */
     uint32_t conf_off[16];       /* confBase[b], 0 = empty bucket */
@@ -157,6 +159,9 @@ struct VsaLitParams {
                                     VSA_SORT_BIN_MAX sets
                                     counters[VSA_CTR_BIN_OVERFLOW]); nullptr:
                                     the count-only histogram */
+    unsigned long long *wg_time;  /* schedule feedback (or null): [b] = xcc <<
+                                     60 | end of workgroup b's scanning
+                                     waves, [grid + b] = its entry (100 MHz) */
     unsigned long long *wave_log; /* diagnostic (dbg bit12): 8 u64 per scanning
                                      wave: start, end (100 MHz), segments,
                                      KiB iterations, workgroup, wave, XCC, HW_ID */

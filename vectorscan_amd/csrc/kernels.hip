@@ -999,15 +999,30 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
          * next lane's ends 0..2 (lane 63: the next chunk's) */
         u32 U[5];
         fdr4_conf<EDGE>(L, {d[0], d[1], d[2], d[3]}, pv3, look_m, U);
+        /* split passes (runtime.hip, large sets): this pass's ends are those
+         * whose byte has bit 0 == end_par - 1; the others are the other
+         * pass's, dead here (a uniform branch, off in one-pass scans) */
+        auto split_mask = [&]() {
+            if (P.end_par) {
+                const u32 fl = P.end_par == 1 ? 0u : 0x01010101u;
+#pragma unroll
+                for (int w = 0; w < 4; w++) {
+                    const u32 t = (d[w] ^ fl) & 0x01010101u;
+                    U[w] |= (t << 8) - t;
+                }
+            }
+        };
         if constexpr (EDGE) {
             const u32 s_in = writelane_u32<0>(lane_up1(U[4]), (u32)in.carry);
             out.carry = readlane_u32(U[4], WAVE - 1);
             U[0] |= s_in;
+            split_mask();
         } else {
             /* lane 0: the previous chunk's lane-63 U[4], rotated in last time */
             U[0] |= lane_up1_or_old(in.p4, U[4]);
             out.p4 = lane_ror1(U[4]);
             out.p5 = in.p5;
+            split_mask();
             const u32 nbm = ~bucket_mask;
             if (!__any(((U[0] & U[1] & U[2] & U[3]) | nbm) != 0xffffffffu)) return out;
         }
@@ -1702,6 +1717,9 @@ vsa_lit_scan(VsaLitParams P) {
         q_done = 0;
         wg_ctr = 0;
         pool_drained = 0;
+        /* the schedule's feedback (runtime.hip xcd_feedback): this
+         * workgroup's entry time */
+        if (P.wg_time) P.wg_time[gridDim.x + blockIdx.x] = t_entry;
     }
     if (tid < 8 * MAX_CONF_WAVES) prof_lds[tid] = 0;
     __syncthreads();
@@ -2268,6 +2286,14 @@ vsa_lit_scan(VsaLitParams P) {
                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
         if ((P.dbg & 2048) && prev + 1 == NS) /* diagnostic: earliest CU done */
             atomicMax(&P.counters[11], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+        if (P.wg_time && prev + 1 == NS) {
+            /* the schedule's feedback: when the workgroup's last scanning
+             * wave finished, and on which XCD (bits 60..63) */
+            u32 xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            P.wg_time[blockIdx.x] = ((unsigned long long)(xcc & 15u) << 60) |
+                                    (__builtin_amdgcn_s_memrealtime() & ((1ULL << 60) - 1));
+        }
     }
     if (P.counters && lane_id() == 0 && ncand_total)
         atomicAdd(&P.counters[2], (unsigned long long)ncand_total);

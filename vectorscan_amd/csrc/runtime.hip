@@ -33,6 +33,7 @@
 #include <thread>
 #include <vector>
 #include <chrono>
+#include <cmath>
 #include <sched.h>
 
 #include "../../include/vectorscan_amd.h"
@@ -209,6 +210,7 @@ struct vsa_ctx {
         const uint8_t *d_data = nullptr;
         uint64_t waves = 0;
         uint32_t nb = 0;
+        uint32_t fb_version = 0; /* the feedback weights it was built with */
         std::vector<uint64_t> in[5]; /* offs, lens, starts, hlens, rlos ({} = NULL) */
     } memo;
     bool host_sort = false; /* the last scan's records are left unsorted */
@@ -219,6 +221,18 @@ struct vsa_ctx {
     /* live plans of this context (vsa_ctx_destroy detaches them, so a plan
      * freed after its context never touches it) */
     std::vector<vsa_plan *> plans;
+    /* schedule feedback (xcd_feedback): per-XCD weights of the workgroups'
+     * static shares, learned from the workgroups' end times of large
+     * launches (the kernel writes them into fine-grained host memory) */
+    struct {
+        float w[8] = {1, 1, 1, 1, 1, 1, 1, 1};
+        uint8_t xcc[1024];       /* the XCD workgroup b ran on last time */
+        float wg[1024];          /* w[xcc[b]]: build_plan's share weights */
+        uint32_t version = 0;    /* bumped when w changes (plans rebuild) */
+        unsigned long long *h = nullptr, *d = nullptr; /* 2 x 1024 u64 */
+        bool armed = false;      /* the launch in flight records its times */
+        bool known = false;      /* xcc[] holds measured XCDs */
+    } fb;
 };
 
 /* A batch's block table and segment map built and uploaded once, then
@@ -254,6 +268,12 @@ struct vsa_db {
     uint32_t engine_id = 0;
     int mode = 0;                /* VsaLitMode */
     bool fdr4 = false;           /* FDR engine scanned with the 4-field first stage */
+    /* split passes (FDR4, large literal sets): two launches, one per bit 0
+     * of the end byte, each with the table of the literals that end in such
+     * a byte (derive_fdr4_table par 0 / 1; d_table2 = par 1) */
+    bool split = false;
+    uint32_t *d_table2 = nullptr;
+    double est_rate = 0.0;       /* fdr4_text_rate of the one-pass table */
     uint32_t table_entries = 0;
     uint32_t dmask = 0;
     uint64_t state_lo = 0, state_hi = 0;
@@ -655,6 +675,79 @@ int queue_bin_sort(vsa_ctx *c, hipStream_t st) {
     return VSA_OK;
 }
 
+/* Schedule feedback: the XCDs of a box do not run equally fast (measured
+ * 4-10 % apart on a 4 GiB scan: profiles/r04e_waves_4g.txt, r04g_waves_*),
+ * and with equal static shares the slowest sets the kernel's end.  A large
+ * per-workgroup-list launch (>= 64 workgroups, >= 256 MiB) records each
+ * workgroup's entry and end (and XCD) into fine-grained host memory; after
+ * it the host moves each XCD's weight toward the rate it showed (half the
+ * way, within 0.85-1.15 of the mean) and the next plan gives each
+ * workgroup a share in proportion (build_plan wg_w).  Results are
+ * unaffected (order-exact output); VSA_XCD_FEEDBACK=0 turns it off. */
+bool xcd_feedback_on() {
+    static const bool v = env_int("VSA_XCD_FEEDBACK", 1) != 0;
+    return v;
+}
+
+void arm_feedback(vsa_ctx *c) {
+    c->fb.armed = xcd_feedback_on() && c->fb.h && c->launch.grid >= 64 &&
+                  c->launch.grid <= 1024 && c->launch.bytes >= (256u << 20) &&
+                  !(c->launch.flags & SCAN_HOST_SORT_SMALL);
+    if (c->fb.armed) memset(c->fb.h, 0, 2 * c->launch.grid * sizeof(unsigned long long));
+}
+
+void take_feedback(vsa_ctx *c) {
+    if (!c->fb.armed) return;
+    c->fb.armed = false;
+    const uint32_t G = c->launch.grid;
+    const volatile unsigned long long *h = c->fb.h;
+    const unsigned long long M60 = (1ULL << 60) - 1;
+    unsigned long long t0 = ~0ULL;
+    for (uint32_t b = 0; b < G; b++) {
+        if (!h[b] || !h[G + b]) return; /* a workgroup without a record */
+        t0 = std::min(t0, (unsigned long long)h[G + b]);
+    }
+    double sum[8] = {0}, cnt[8] = {0};
+    for (uint32_t b = 0; b < G; b++) {
+        const uint32_t x = (uint32_t)(h[b] >> 60) & 7u;
+        const unsigned long long e = h[b] & M60;
+        if (e <= t0) return;
+        c->fb.xcc[b] = (uint8_t)x;
+        sum[x] += (double)(e - t0);
+        cnt[x] += 1;
+    }
+    double tm = 0, nx = 0;
+    for (int x = 0; x < 8; x++)
+        if (cnt[x]) {
+            tm += sum[x] / cnt[x];
+            nx += 1;
+        }
+    if (nx < 2) return;
+    tm /= nx;
+    float nw[8];
+    double mean = 0;
+    for (int x = 0; x < 8; x++) {
+        nw[x] = c->fb.w[x];
+        if (cnt[x]) {
+            const double tx = sum[x] / cnt[x];
+            nw[x] = (float)(0.5 * c->fb.w[x] + 0.5 * c->fb.w[x] * tm / tx);
+        }
+    }
+    for (int x = 0; x < 8; x++) mean += nw[x];
+    mean /= 8;
+    bool moved = false;
+    for (int x = 0; x < 8; x++) {
+        nw[x] = std::min(1.15f, std::max(0.85f, (float)(nw[x] / mean)));
+        moved = moved || std::fabs(nw[x] - c->fb.w[x]) > 0.002f;
+    }
+    const bool first = !c->fb.known;
+    c->fb.known = true;
+    if (!moved && !first) return;
+    memcpy(c->fb.w, nw, sizeof(nw));
+    for (int b = 0; b < 1024; b++) c->fb.wg[b] = c->fb.w[c->fb.xcc[b] & 7];
+    c->fb.version++;
+}
+
 /* diagnostic per-wave log (vsa_set_wave_log; the kernel writes it under
  * debug flag 4096) */
 static unsigned long long *g_wave_log = nullptr;
@@ -707,6 +800,7 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
      * timing and get their counters and records published (no copies) */
     const bool small = (c->launch.flags & SCAN_HOST_SORT_SMALL) != 0;
     if (!small) VSA_CHECK(hipEventRecord(c->ev0, c->stream));
+    arm_feedback(c);
     int r = launch_scan_kernel(c, db, d_data, nb, nsegs, seg_bytes);
     if (r != VSA_OK) return r;
     if (small) {
@@ -778,6 +872,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         P.bin_shift = bin_shift_for(c->launch.end_bits);
         P.bin_slots = c->launch.bins && !old_sort() ? w.d_bslots : nullptr;
         P.counters = w.d_counters;
+        P.wg_time = c->fb.armed ? c->fb.d : nullptr;
         P.wave_log = g_wave_log;
         {
             const char *e = getenv("VSA_DEBUG_FLAGS");
@@ -820,6 +915,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.bin_shift = bin_shift_for(c->launch.end_bits);
     P.bin_slots = c->launch.bins && !old_sort() ? w.d_bslots : nullptr;
     P.counters = w.d_counters;
+    P.wg_time = c->fb.armed ? c->fb.d : nullptr;
     P.wave_log = g_wave_log;
     {
         const char *e = getenv("VSA_DEBUG_FLAGS");
@@ -837,8 +933,24 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         P.nconf = launch_nconf(db, tb, ent, LDS_BUDGET);
         size_t lds = plan_lds(tb, db->slot_words, ent, &P.qcap, LDS_BUDGET, P.nconf);
         if (lds > LDS_BUDGET) return VSA_E_INVALID;
-        return xp ? launch_lit<VSA_MODE_FDR4, true, true>(c, P, lds)
-                  : launch_lit<VSA_MODE_FDR4, true>(c, P, lds);
+        auto go = [&](const VsaLitParams &Q) {
+            return xp ? launch_lit<VSA_MODE_FDR4, true, true>(c, Q, lds)
+                      : launch_lit<VSA_MODE_FDR4, true>(c, Q, lds);
+        };
+        if (!db->split) return go(P);
+        /* split passes: the ends whose byte has bit 0 clear, with the table
+         * of the literals ending in such a byte, then the others; each end
+         * is one pass's, and the confirm (the blob's, unchanged) can only
+         * accept a literal whose last byte is the end's, so no record is
+         * found twice.  The records of both go to the same output and bins.
+         * Between them the ticket counters (dynamic 1, the pool) restart. */
+        P.end_par = 1;
+        if (int r = go(P)) return r;
+        VSA_CHECK(hipMemsetAsync(w.d_counters + 16, 0, 128 * sizeof(unsigned long long),
+                                 c->stream));
+        P.end_par = 2;
+        P.table = (const uint64_t *)db->d_table2;
+        return go(P);
     }
     if (db->mode == VSA_MODE_FDR) {
         size_t tb = (size_t)db->table_entries * 8;
@@ -929,10 +1041,14 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     }
     uint64_t n = w.h_counters[0];
     c->last_cand = w.h_counters[2];
+    take_feedback(c);
     /* adapt the db's confirm-wave count to the measured candidate rate
      * (over a representative launch; not under diagnostic flags) */
     if (c->launch.db && c->launch.bytes >= (16u << 20) && !getenv("VSA_DEBUG_FLAGS")) {
-        const uint32_t want = nconf_for_rate((double)c->last_cand / (double)c->launch.bytes);
+        /* split passes: each launch confirms about half the candidates */
+        const double passes = c->launch.db->split ? 2.0 : 1.0;
+        const uint32_t want =
+            nconf_for_rate((double)c->last_cand / passes / (double)c->launch.bytes);
         uint32_t cur = c->launch.db->nconf.load(std::memory_order_relaxed);
         while (want > cur && !c->launch.db->nconf.compare_exchange_weak(cur, want)) {
         }
@@ -990,7 +1106,7 @@ constexpr uint32_t PLAN_MAX_BLOCKS = VSA_MAX_BLOCKS; /* 20-bit block field of th
 int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens,
                const uint64_t *starts, const uint64_t *hlens, const uint64_t *rlos,
                uint32_t nb, uint64_t waves, BatchPlan &pl, VsaBlock *out = nullptr,
-               uint64_t ns = LIT_WAVES - 1) {
+               uint64_t ns = LIT_WAVES - 1, const float *wg_w = nullptr) {
     if (nb > PLAN_MAX_BLOCKS) return VSA_E_INVALID;
     /* the block table goes to `out` (a pinned mirror) or pl.blocks */
     if (!out) {
@@ -1098,10 +1214,15 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
          * split into G equal shares, one list per workgroup; the rest is a
          * shared pool of small segments (region tickets, like the round-3
          * scheduler) that workgroups take from once their own list and
-         * their waves' stealing run dry.  The pool is what balances the
-         * XCDs: on some boxes one XCD runs ~10 % slower than another
+         * their waves' stealing run dry.  The pool is meant to balance the
+         * XCDs: on some boxes one XCD runs ~4-10 % slower than another
          * (profiles/r04e_waves_4g.txt: workgroups of XCD 7 done at 954 us,
-         * XCD 2 at 859 us, with equal shares).  With stealing, a large block
+         * XCD 2 at 859 us, with equal shares).  Off by default (VSA_POOL_PM
+         * = 0): measured, it costs more than it saves -- every wave of a
+         * workgroup holds a pool segment when the pool drains, so the
+         * workgroups' ends spread by a segment per wave (4 GiB: 892 against
+         * 870 us; 32 MiB: 47 against 28 us; cfg-3 Teddy 1 GiB: 0.253 against
+         * 0.238 ms; profiles/r04f_pool_sweep.jsonl, r04g_waves_*.txt).  With stealing, a large block
          * is cut into one segment per wave of the share; without it
          * (VSA_STEAL=0) into segments of clamp(r / (K x ns), min, max), r =
          * the bytes of the share still uncut (guided sizes).  Blocks shorter
@@ -1111,7 +1232,7 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
         static const uint64_t K = std::max(1, env_int("VSA_WG_K", 2));
         static const uint64_t smax = (uint64_t)std::max(1, env_int("VSA_WG_MAX_KIB", 256)) << 10;
         static const uint64_t smin0 = (uint64_t)std::max(1, env_int("VSA_WG_MIN_KIB", 4)) << 10;
-        static const uint64_t pool_pm = (uint64_t)std::min(900, std::max(0, env_int("VSA_POOL_PM", 125)));
+        const uint64_t pool_pm = (uint64_t)std::min(900, std::max(0, env_int("VSA_POOL_PM", 0)));
         const uint64_t smin = T <= (64u << 10) ? 1024u : smin0;
         const uint64_t gmax = std::max<uint64_t>(1, waves / ns);
         const uint64_t G = std::max<uint64_t>(1, std::min(gmax, (T + ns * smin - 1) / (ns * smin)));
@@ -1124,7 +1245,18 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
         uint64_t g = 0, acc = 0;
         bool in_pool = false;
         uint64_t pool_lo = 0;
-        auto cum = [&](uint64_t k) { return (uint64_t)((unsigned __int128)Tst * (k + 1) / G); };
+        /* the end of workgroup k's share: equal shares, or (schedule
+         * feedback, wg_w) shares weighted per workgroup */
+        std::vector<double> cw;
+        if (wg_w) {
+            cw.resize(G);
+            double a = 0;
+            for (uint64_t k = 0; k < G; k++) cw[k] = (a += wg_w[k]);
+        }
+        auto cum = [&](uint64_t k) {
+            if (!cw.empty()) return k + 1 >= G ? Tst : (uint64_t)((double)Tst * (cw[k] / cw[G - 1]));
+            return (uint64_t)((unsigned __int128)Tst * (k + 1) / G);
+        };
         auto advance = [&]() {
             while (g + 1 < G && acc >= cum(g)) wg_first[++g] = (uint32_t)pl.nsegs;
             if (pool_on && !in_pool && acc >= Tst) {
@@ -1258,7 +1390,8 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
     const uint64_t waves = (uint64_t)c->num_cus * (LIT_WAVES - db->nconf.load());
     const uint64_t *in[5] = {offs, lens, starts, hlens, rlos};
     auto &M = c->memo;
-    bool same = M.valid && M.d_data == d_data && M.nb == nb && M.waves == waves;
+    bool same = M.valid && M.d_data == d_data && M.nb == nb && M.waves == waves &&
+                M.fb_version == c->fb.version;
     for (int k = 0; same && k < 5; k++)
         same = in[k] ? (M.in[k].size() == nb && !memcmp(M.in[k].data(), in[k], nb * 8))
                      : M.in[k].empty();
@@ -1272,7 +1405,8 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         M.valid = false;
         if ((r = ensure_tables(c, nb, 0)) != VSA_OK) return r;
         if ((r = build_plan(d_data, offs, lens, starts, hlens, rlos, nb, waves, pl,
-                            w.h_blocks, LIT_WAVES - db->nconf.load())) != VSA_OK)
+                            w.h_blocks, LIT_WAVES - db->nconf.load(),
+                            c->fb.known ? c->fb.wg : nullptr)) != VSA_OK)
             return r;
         T1 = std::chrono::steady_clock::now();
         if ((r = ensure_tables(c, nb, pl.segblk.size(), true)) != VSA_OK) return r;
@@ -1285,6 +1419,7 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         M.d_data = d_data;
         M.nb = nb;
         M.waves = waves;
+        M.fb_version = c->fb.version;
         for (int k = 0; k < 5; k++) {
             if (in[k]) M.in[k].assign(in[k], in[k] + nb);
             else M.in[k].clear();
@@ -1778,6 +1913,13 @@ int vsa_ctx_create(int device, vsa_ctx_t **out) {
                             hipHostMallocCoherent | hipHostMallocMapped));
     memset(c->ws.h_pub, 0, PUB_WORDS * sizeof(unsigned long long));
     VSA_CHECK(hipHostGetDevicePointer((void **)&c->ws.d_pub, c->ws.h_pub, 0));
+    VSA_CHECK(hipHostMalloc((void **)&c->fb.h, 2048 * sizeof(unsigned long long),
+                            hipHostMallocCoherent | hipHostMallocMapped));
+    VSA_CHECK(hipHostGetDevicePointer((void **)&c->fb.d, c->fb.h, 0));
+    for (int b = 0; b < 1024; b++) {
+        c->fb.xcc[b] = (uint8_t)(b & 7);
+        c->fb.wg[b] = 1.0f;
+    }
     *out = c.release();
     return VSA_OK;
 }
@@ -1801,6 +1943,7 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (w.d_bslots) (void)hipFree(w.d_bslots);
     if (w.h_counters) (void)hipHostFree(w.h_counters);
     if (w.h_pub) (void)hipHostFree(w.h_pub);
+    if (c->fb.h) (void)hipHostFree(c->fb.h);
     if (w.h_in) (void)hipHostFree(w.h_in);
     if (w.d_blocks) (void)hipFree(w.d_blocks);
     if (w.h_blocks) (void)hipHostFree(w.h_blocks);
@@ -1912,7 +2055,7 @@ static void derive_fdr_table(const uint8_t *eng, const uint32_t conf_off[8], uin
  * 128 KiB, and its even positions alone leave 4.0 % of ends live against
  * 6.9 % (the two-level sweep's level 1). */
 static void derive_fdr4_table(const uint8_t *eng, const uint32_t conf_off[8], uint32_t bits,
-                              std::vector<uint32_t> &T) {
+                              std::vector<uint32_t> &T, int par = -1) {
     const uint32_t n = 1u << bits;
     T.assign(n, ~0u);
     uint32_t always = 0;
@@ -1948,6 +2091,10 @@ static void derive_fdr4_table(const uint8_t *eng, const uint32_t conf_off[8], ui
         offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
         for (uint32_t o : offs) {
             const LitInfo *L = (const LitInfo *)(fc + o);
+            /* split passes (par 0 / 1): only the literals whose last byte can
+             * have bit 0 == par (every end byte with that bit 0 is a pass's) */
+            if (par >= 0 && ((L->msk >> 56) & 1u) && (uint32_t)((L->v >> 56) & 1u) != (uint32_t)par)
+                continue;
             auto mv = [&](uint32_t back, uint8_t *m, uint8_t *v) {
                 /* the byte `back` before the end: byte 7 - back of the window */
                 *m = (uint8_t)(L->msk >> (8 * (7 - back)));
@@ -1974,6 +2121,41 @@ static void derive_fdr4_table(const uint8_t *eng, const uint32_t conf_off[8], ui
     if (always) {
         for (auto &t : T) t &= ~always;
     }
+}
+
+/* The candidate bits per byte a 4-field table (15-bit keys) passes on
+ * text, estimated as if its lookups were independent and the bytes uniform
+ * over 0x20..0x7e: sum over buckets of the product over fields of the live
+ * fraction of the keys.  Against tools/sim_filter.py on the cfg-4 sets
+ * (5k / 10k / 20k / 50k literals): 7.2e-5 / 7.3e-4 / 7.8e-3 / 0.142
+ * estimated, 1.7e-4 / - / 9.1e-3 / 0.148 simulated.  It only chooses the
+ * schedule (split_passes), never a result. */
+static double fdr4_text_rate(const std::vector<uint32_t> &T) {
+    uint32_t live[32] = {0}, n = 0;
+    for (uint32_t b2 = 0; b2 < 2; b2++)
+        for (uint32_t b0 = 0x20; b0 < 0x7f; b0++)
+            for (uint32_t b1 = 0x20; b1 < 0x7f; b1++) {
+                const uint32_t e = ~T[vsa_fdr4_key(b2, b1, b0, 15)];
+                n++;
+                for (int k = 0; k < 32; k++) live[k] += (e >> k) & 1u;
+            }
+    double s = 0.0;
+    for (int b = 0; b < 8; b++) {
+        double p = 1.0;
+        for (int f = 0; f < 4; f++) p *= (double)live[f * 8 + b] / n;
+        s += p;
+    }
+    return s;
+}
+
+/* split passes past this estimated rate (VSA_SPLIT=0 / 1 forces off / on).
+ * Measured, 4 GiB cfg-4 corpus, kernel ms one pass / split
+ * (profiles/r04h_split.jsonl): 20k literals (est 7.8e-3) 1.82 / 2.29, 30k
+ * (3.0e-2) 3.63 / 3.16, 50k (0.142) 11.4 / 5.44; confirm candidates 11.4M /
+ * 2.3M, 57.8M / 10.9M, 375M / 76M.  The crossover lies near 1.5e-2. */
+static bool split_passes(double est) {
+    if (const char *e = getenv("VSA_SPLIT")) return atoi(e) != 0;
+    return est > 0.015;
 }
 
 /* Teddy / Fat Teddy first stage, rebuilt at load like FDR's: bit (k * lb +
@@ -2139,6 +2321,16 @@ int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
         db->fdr4 = true;
         db->table_entries = 1u << bits;
         db->dmask = (1u << bits) - 1;
+        db->est_rate = fdr4_text_rate(T);
+        db->split = split_passes(db->est_rate);
+        if (db->split) {
+            /* pass 0's table in d_table, pass 1's in d_table2 */
+            std::vector<uint32_t> T1;
+            derive_fdr4_table(eng, db->conf_off, bits, T, 0);
+            derive_fdr4_table(eng, db->conf_off, bits, T1, 1);
+            VSA_CHECK(hipMalloc(&db->d_table2, T1.size() * 4));
+            VSA_CHECK(hipMemcpy(db->d_table2, T1.data(), T1.size() * 4, hipMemcpyHostToDevice));
+        }
         VSA_CHECK(hipMalloc(&db->d_table, T.size() * 4));
         VSA_CHECK(hipMemcpy(db->d_table, T.data(), T.size() * 4, hipMemcpyHostToDevice));
     } else if (db->mode == VSA_MODE_FDR) {
@@ -2171,6 +2363,7 @@ int vsa_db_free(vsa_db_t *db) {
     if (!db) return VSA_E_INVALID;
     if (db->d_blob) (void)hipFree(db->d_blob);
     if (db->d_table) (void)hipFree(db->d_table);
+    if (db->d_table2) (void)hipFree(db->d_table2);
     if (db->d_slots) (void)hipFree(db->d_slots);
     for (auto it = t_registry.begin(); it != t_registry.end(); ++it) {
         if (it->second == db) {
@@ -2236,6 +2429,34 @@ int vsa_derive_fdr4_table(const void *hwlm, size_t size, uint32_t bits, uint32_t
     const uint32_t n = (uint32_t)std::min<size_t>(cap, T.size());
     memcpy(table, T.data(), n * sizeof(uint32_t));
     return (int)n;
+}
+
+/* Host-only: the 15-bit 4-field table of one split pass (par 0 / 1: the
+ * literals whose last byte can have bit 0 == par; -1: the one-pass table)
+ * and, in *text_rate, fdr4_text_rate of it (the load's split_passes rule).
+ * Returns the entries written (<= cap) or a VSA_E_* code. */
+int vsa_derive_fdr4_pass(const void *hwlm, size_t size, int par, uint32_t *table, uint32_t cap,
+                         double *text_rate) {
+    if (!hwlm || size < VSA_ROUNDUP_CL(sizeof(HWLM)) || par < -1 || par > 1)
+        return VSA_E_INVALID;
+    const HWLM *h = (const HWLM *)hwlm;
+    if (h->type != HWLM_ENGINE_FDR) return VSA_E_INVALID;
+    const uint8_t *eng = (const uint8_t *)hwlm + VSA_ROUNDUP_CL(sizeof(HWLM));
+    if (((const uint32_t *)eng)[0] != VSA_ENGINE_FDR) return VSA_E_INVALID;
+    const uint32_t *confBase = (const uint32_t *)(eng + ((const uint32_t *)eng)[4]);
+    uint32_t conf_off[8];
+    for (int b = 0; b < 8; b++) conf_off[b] = confBase[b];
+    std::vector<uint32_t> T;
+    derive_fdr4_table(eng, conf_off, 15, T, par);
+    if (text_rate) *text_rate = fdr4_text_rate(T);
+    const uint32_t n = table ? (uint32_t)std::min<size_t>(cap, T.size()) : 0u;
+    if (n) memcpy(table, T.data(), n * sizeof(uint32_t));
+    return (int)n;
+}
+
+int vsa_db_split(const vsa_db_t *db) {
+    if (!db) return VSA_E_INVALID;
+    return db->split ? 1 : 0;
 }
 
 int vsa_db_engine(const vsa_db_t *db) {
@@ -3082,11 +3303,11 @@ int vsa_scan_blocks_stream(vsa_ctx_t *c, const vsa_db_t *db, const uint8_t *d_da
 int vsa_plan_describe(const uint8_t *d_data, const uint64_t *offsets, const uint64_t *lens,
                       const uint64_t *starts, const uint64_t *hlens, const uint64_t *report_lo,
                       uint32_t nblocks, uint32_t num_cus, uint32_t ns, uint32_t *words,
-                      uint64_t cap, uint64_t *nsegs, uint32_t *grid) {
+                      uint64_t cap, uint64_t *nsegs, uint32_t *grid, const float *wg_weights) {
     if (!offsets || !lens || !nblocks || !ns || !num_cus) return VSA_E_INVALID;
     BatchPlan pl;
     int r = build_plan(d_data, offsets, lens, starts, hlens, report_lo, nblocks,
-                       (uint64_t)num_cus * ns, pl, nullptr, ns);
+                       (uint64_t)num_cus * ns, pl, nullptr, ns, wg_weights);
     if (r != VSA_OK) return r;
     if (words) memcpy(words, pl.segblk.data(), std::min<uint64_t>(cap, pl.segblk.size()) * 4);
     if (nsegs) *nsegs = pl.nsegs;
