@@ -139,10 +139,10 @@ def test_gpu_report_lo_keeps_start_state(ctx):
 def test_gpu_large_literal_sets(ctx, nlits, monkeypatch):
     """Large FDR sets, where the confirm stage is the bound: the first launch
     (>= 16 MiB) measures the confirm-candidate rate and the next ones run
-    with two confirm waves per workgroup; one launch also forces a single
-    confirm wave and one three (VSA_NCONF).  From the second launch on the
-    scanning waves expand the candidates (scanner expansion, runtime.hip
-    use_xp); the last two launches force it off and on (VSA_XP).  The
+    with the scanning waves expanding the candidates (scanner expansion,
+    runtime.hip use_xp) and the confirm-wave count the rate asks for; one
+    launch also forces a single confirm wave and one three (VSA_NCONF); the
+    last two launches force expansion off and on (VSA_XP).  The
     database is loaded with the split passes at their default (on for 50k,
     runtime.hip split_passes) and forced off and on (VSA_SPLIT).  Every
     launch == the oracle."""

@@ -293,6 +293,9 @@ struct vsa_db {
      * threads.  It only grows (1 -> 2 -> 3) and feeds the segment sizes, so
      * a db's launch plans change at most twice. */
     mutable std::atomic<uint32_t> nconf{1};
+    /* scanner expansion (use_xp): on once a representative launch measured
+     * more than 1e-3 confirm candidates per byte; only turns on */
+    mutable std::atomic<bool> xp{false};
 };
 
 /* confirm waves for a measured confirm-candidate rate (candidates per
@@ -305,8 +308,15 @@ static uint32_t nconf_for_rate(double rate) {
      * 20k 2.47 / 2.32 / 2.70 ms at 1 / 2 / 3 waves, 50k 62.9 / 34.1 / 30.6
      * ms (profiles/r03_xp.jsonl; 4 fits no better than 3 beside a
      * domain-14 table) */
-    return rate > 0.05 ? 3u : rate > 1e-3 ? 2u : 1u;
+    /* Round 4, with scanner expansion on from 1e-3 (xp_for_rate), the
+     * confirm waves only confirm: 20k literals (2.7e-3) 1.80 / 1.85 / 1.99
+     * ms at 1 / 2 / 3 waves, 50k in split passes (8.9e-3 per pass) 6.22 /
+     * 5.34 / 6.13 (profiles/r04j_xp_cost.jsonl) */
+    return rate > 0.05 ? 3u : rate > 5e-3 ? 2u : 1u;
 }
+
+/* scanner expansion past this confirm-candidate rate (use_xp) */
+static bool xp_for_rate(double rate) { return rate > 1e-3; }
 
 /* VECTORSIZE of the reference build emulated where results depend on it:
  * shuftiDoubleExec's per-block lanes and the Teddy loop shape of the flood
@@ -590,12 +600,11 @@ uint32_t launch_nconf(const vsa_db *db, size_t tab, size_t ent, size_t budget) {
 
 /* Scanner expansion (kernels.hip xp_push) for large literal sets: the
  * scanning waves expand candidate bits and apply the slot-bitmap prefilter,
- * the confirm waves only confirm.  On when the db's measured candidate rate
- * asked for two confirm waves (> 1e-3 per byte, nconf_for_rate);
- * VSA_XP=0 / 1 forces it off / on. */
+ * the confirm waves only confirm.  On once the db's measured candidate rate
+ * passed 1e-3 per byte (xp_for_rate); VSA_XP=0 / 1 forces it off / on. */
 bool use_xp(const vsa_db *db) {
     if (const char *e = getenv("VSA_XP")) return atoi(e) != 0;
-    return db->nconf.load(std::memory_order_relaxed) >= 2;
+    return db->xp.load(std::memory_order_relaxed);
 }
 
 /* the binned sort (kernels.hip) replaces the library sort unless the
@@ -1047,11 +1056,12 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     if (c->launch.db && c->launch.bytes >= (16u << 20) && !getenv("VSA_DEBUG_FLAGS")) {
         /* split passes: each launch confirms about half the candidates */
         const double passes = c->launch.db->split ? 2.0 : 1.0;
-        const uint32_t want =
-            nconf_for_rate((double)c->last_cand / passes / (double)c->launch.bytes);
+        const double rate = (double)c->last_cand / passes / (double)c->launch.bytes;
+        const uint32_t want = nconf_for_rate(rate);
         uint32_t cur = c->launch.db->nconf.load(std::memory_order_relaxed);
         while (want > cur && !c->launch.db->nconf.compare_exchange_weak(cur, want)) {
         }
+        if (xp_for_rate(rate)) c->launch.db->xp.store(true, std::memory_order_relaxed);
     }
     if (getenv("VSA_DEBUG_FLAGS") && w.h_counters[3]) {
         fprintf(stderr, "vsa: %llu queued confirm keys differ from HBM\n",
