@@ -449,6 +449,11 @@ struct IterState {
     u32 ncand;  /* first-stage candidates so far (diagnostic, wave-uniform) */
     u32 tail_cache; /* last tail read from the confirm wave */
     u32 head;       /* entries this wave has pushed to its ring */
+    /* scanner expansion (xp_push): a batch of expanded candidates, one per
+     * lane in lanes [0, xn) -- match key (qm) and 8-byte confirm key --
+     * prefiltered and pushed together once 64 have gathered (xp_flush) */
+    u32 xs[4];
+    u32 xn;
 };
 
 struct SegCtx {
@@ -872,24 +877,46 @@ __device__ __forceinline__ u32 window4(const u32 (&s)[4], int o) {
 }
 
 /* Scanner expansion (XP, large literal sets): the scanning wave expands its
- * candidate bits itself -- each round every lane takes its lowest remaining
- * (end, bucket) bit, cuts the 8-byte confirm key from the bytes it holds,
- * and tests the bucket's LDS slot bitmap (litIndex[hash] == 0 rejects,
- * fdr_confirm_runtime.h:43-60) -- and pushes only the survivors, as
- * confirm-queue entries (QEnt), to its ring.  With thousands of literals per
- * bucket the first stage passes ~1e-2 candidate bits per byte; one confirm
- * wave expanding them one bit per lane per round was the bottleneck (20k
- * literals: 97 M bits, ~20 of 64 lanes busy per round), where 14 scanning
- * waves share the expansion and the confirm wave only confirms.
+ * candidate bits itself and pushes only the ones the bucket's slot bitmap
+ * passes (litIndex[hash] == 0 rejects, fdr_confirm_runtime.h:43-60), as
+ * confirm-queue entries (QEnt), to its ring; the confirm wave only
+ * confirms.  With thousands of literals per bucket the first stage passes
+ * ~1e-2 candidate bits per byte (20k literals: ~9 per 1 KiB iteration, in
+ * ~1.5 rounds of one bit per lane).
+ * Round 4: the rounds only extract -- each round every lane takes its
+ * lowest remaining (end, bucket) bit and cuts its 8-byte key from the bytes
+ * it holds (branch-free) -- and one ds_permute per word packs the round's
+ * bits into consecutive lanes of a batch (IterState xs / xn) that outlives
+ * the iteration; the prefilter (bucket record, hash, slot word: two
+ * dependent LDS reads) and the ring push run once per 64 candidates
+ * (xp_flush) instead of once per round with a few lanes busy.
  * c = candidate bits of ends 0..15 (byte i of c[w] = end 4 w + i, bit =
- * bucket); meta = p0 | blk << ENT_BLK_SHIFT; W0..W2 = bytes p0 - 8 .. p0 + 15. */
+ * bucket); meta = p0 | blk << ENT_BLK_SHIFT; D = bytes p0 - 8 .. p0 + 15. */
+template <typename ST>
+__device__ __forceinline__ void xp_flush(const VsaLitParams &P, const ConfLds &cl,
+                                         const LitShared &L, ST &st) {
+    const u32 n = st.xn;
+    if (n == 0) return;
+    const bool act = lane_id() < n;
+    const u64 key = ((u64)st.xs[3] << 32) | st.xs[2];
+    const u32 bb = st.xs[0] & 7u;
+    const PfRec pf = cl.pf[bb];
+    const bool chk = act && pf.slot_off != 0xffffffffu;
+    const u32 h = (u32)(((key & pf.andmsk) * P.pf_mult) >> pf.shift);
+    const u32 sw = chk ? lds_ld32(&L.slots[pf.slot_off + (h >> 5)]) : ~0u;
+    const bool push = act && ((sw >> (h & 31)) & 1u);
+    const u32 w[4] = {st.xs[0], st.xs[1], st.xs[2], st.xs[3]};
+    ring_push<1>(L, st, push, w);
+    st.xn = 0;
+}
+
 __device__ __forceinline__ void xp_push(const VsaLitParams &P, const ConfLds &cl,
                                         const LitShared &L, IterState &st, u32 (&c)[4],
                                         u64 meta, u32 pv2, u32 pv3, const u32 (&d)[5]) {
-    const u64 W0 = ((u64)pv3 << 32) | pv2, W1 = ((u64)d[1] << 32) | d[0],
-              W2 = ((u64)d[3] << 32) | d[2];
+    const u32 D[6] = {pv2, pv3, d[0], d[1], d[2], d[3]};
     const u64 p0 = meta & ENT_P0_MASK;
     const u64 blk4 = (meta >> ENT_BLK_SHIFT) << 4;
+    const u32 lane = lane_id();
     for (;;) {
         u32 word = 0, bits = c[0];
 #pragma unroll
@@ -899,27 +926,44 @@ __device__ __forceinline__ void xp_push(const VsaLitParams &P, const ConfLds &cl
             word = take ? (u32)k : word;
         }
         const bool have = bits != 0;
-        if (!__any(have)) break;
+        const u64 B = __ballot(have);
+        if (B == 0) break;
+        const u32 cnt = (u32)__popcll(B);
+        if (st.xn + cnt > WAVE) xp_flush(P, cl, L, st);
         const u32 bit = __ffs(bits) - 1;
 #pragma unroll
         for (int k = 0; k < 4; k++)
             if (have && word == (u32)k) c[k] &= c[k] - 1;
         const u32 jj = 4 * word + (bit >> 3), bb = bit & 7;
-        /* key = bytes [jj - 7, jj] = byte offset jj + 1 .. jj + 8 of W0:W1:W2 */
-        const u32 o = jj + 1;
-        u64 key;
-        if (o < 8) key = (W0 >> (8 * o)) | (W1 << (64 - 8 * o));
-        else if (o == 8) key = W1;
-        else if (o < 16) key = (W1 >> (8 * (o - 8))) | (W2 << (64 - 8 * (o - 8)));
-        else key = W2;
-        const PfRec pf = cl.pf[bb];
-        const bool chk = have && pf.slot_off != 0xffffffffu;
-        const u32 h = (u32)(((key & pf.andmsk) * P.pf_mult) >> pf.shift);
-        const u32 sw = chk ? lds_ld32(&L.slots[pf.slot_off + (h >> 5)]) : ~0u;
-        const bool push = have && ((sw >> (h & 31)) & 1u);
+        /* key = bytes [jj - 7, jj] = byte offset o = jj + 1 .. jj + 8 of D:
+         * dwords a, a + 1, a + 2 shifted by o & 3 */
+        const u32 o = jj + 1, a = o >> 2, sh = o & 3u;
+        u32 x0 = D[0], x1 = D[1], x2 = D[2];
+#pragma unroll
+        for (int k = 1; k < 5; k++) {
+            const bool sel = a == (u32)k;
+            x0 = sel ? D[k] : x0;
+            x1 = sel ? D[k + 1] : x1;
+            x2 = sel ? D[k + 2 < 6 ? k + 2 : 5] : x2;
+        }
+        const u32 key_lo = __builtin_amdgcn_alignbyte(x1, x0, sh);
+        const u32 key_hi = __builtin_amdgcn_alignbyte(x2, x1, sh);
         const u64 qm = ((p0 + jj) << 24) | blk4 | bb;
-        const u32 w[4] = {(u32)qm, (u32)(qm >> 32), (u32)key, (u32)(key >> 32)};
-        ring_push<1>(L, st, push, w);
+        /* the round's bits to lanes [xn, xn + cnt) of the batch; the other
+         * lanes fill the rest, so the permute is one-to-one */
+        const u32 rk = __builtin_amdgcn_mbcnt_hi((u32)(B >> 32), __builtin_amdgcn_mbcnt_lo((u32)B, 0));
+        const u32 dst = have ? st.xn + rk : (st.xn + cnt + (lane - rk)) & (WAVE - 1);
+        const int da = (int)(dst << 2);
+        const u32 r0 = (u32)__builtin_amdgcn_ds_permute(da, (int)(u32)qm);
+        const u32 r1 = (u32)__builtin_amdgcn_ds_permute(da, (int)(u32)(qm >> 32));
+        const u32 r2 = (u32)__builtin_amdgcn_ds_permute(da, (int)key_lo);
+        const u32 r3 = (u32)__builtin_amdgcn_ds_permute(da, (int)key_hi);
+        const bool mine = lane - st.xn < cnt;
+        st.xs[0] = mine ? r0 : st.xs[0];
+        st.xs[1] = mine ? r1 : st.xs[1];
+        st.xs[2] = mine ? r2 : st.xs[2];
+        st.xs[3] = mine ? r3 : st.xs[3];
+        st.xn += cnt;
     }
 }
 
@@ -988,6 +1032,9 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     out.ncand = in.ncand;
     out.tail_cache = in.tail_cache;
     out.head = in.head;
+#pragma unroll
+    for (int k = 0; k < 4; k++) out.xs[k] = in.xs[k];
+    out.xn = in.xn;
     if constexpr (PSTATE) {
         out.pbytes = (in.pbytes & 0xffffffff00000000ULL) | readlane_u32(d[2], WAVE - 1);
         out.carry = in.carry;
@@ -1779,6 +1826,9 @@ vsa_lit_scan(VsaLitParams P) {
     const u8 *A = P.data - mis;
     u32 ncand_total = 0;
     u32 ring_tail_cache = 0, ring_head = 0;
+    /* scanner expansion's batch (IterState xs / xn), carried across blocks
+     * and segments, flushed before the wave ends */
+    u32 xp_s[4] = {0, 0, 0, 0}, xp_n = 0;
 
     /* Segment scheduling.  The segments are split into NREG contiguous
      * regions; workgroup b works in region b % NREG first (workgroups are
@@ -2105,6 +2155,9 @@ vsa_lit_scan(VsaLitParams P) {
         is.ncand = ncand_total;
         is.tail_cache = ring_tail_cache;
         is.head = ring_head;
+#pragma unroll
+        for (int k = 0; k < 4; k++) is.xs[k] = xp_s[k];
+        is.xn = xp_n;
         {
             S_t x = 0;
             if (pro1_in) {
@@ -2255,11 +2308,24 @@ vsa_lit_scan(VsaLitParams P) {
         ncand_total = is.ncand;
         ring_tail_cache = is.tail_cache;
         ring_head = is.head;
+#pragma unroll
+        for (int k = 0; k < 4; k++) xp_s[k] = is.xs[k];
+        xp_n = is.xn;
         } /* blocks of the segment */
         n_seg++;
         /* after a stolen range or a pool segment, the list is known to be
          * exhausted */
         seg = (stolen || !from_list) ? (u32)P.nsegs : sched ? resolve(t_next) : seg + (u32)G;
+    }
+    if constexpr (XP) {
+        /* the last batch of expanded candidates, before this wave's done */
+        IterState fs;
+        fs.tail_cache = ring_tail_cache;
+        fs.head = ring_head;
+#pragma unroll
+        for (int k = 0; k < 4; k++) fs.xs[k] = xp_s[k];
+        fs.xn = xp_n;
+        xp_flush(P, cl, L, fs);
     }
     if ((P.dbg & 4096) && P.wave_log && lane < 8) {
         u32 xcc, hwid;
