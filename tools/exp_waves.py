@@ -14,7 +14,11 @@ import vectorscan_amd as vsa  # noqa: E402
 
 dev = torch.device("cuda", 0)
 ctx = vsa.Context(0)
-lits = bench.make_literals(5000, seed=12)
+# WORKLOAD=noodle: cfg 1's single literal (noodle engine); else cfg 4's set
+if os.environ.get("WORKLOAD") == "noodle":
+    lits = [vsa.HwlmLiteral(b"abcde", False, 1)]
+else:
+    lits = bench.make_literals(5000, seed=12)
 db = vsa.Database(ctx, vsa.hwlm_build(lits))
 total = int(float(os.environ.get("GIB", "4")) * (1 << 30))
 bl = total // 4

@@ -115,6 +115,7 @@ struct VsaLitParams {
     uint32_t steal;           /* dynamic 2: a wave out of segments steals sweep
                                  groups inside its workgroup when some wave
                                  has at least `steal` unclaimed (0: off) */
+    uint32_t steal_w;         /* weigh victims by issue age (VSA_STEAL_W) */
     const uint64_t *table;  /* FDR domain table / Teddy combined byte table */
     uint32_t table_entries;
     uint32_t dmask;

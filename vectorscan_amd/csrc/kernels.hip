@@ -1902,7 +1902,12 @@ vsa_lit_scan(VsaLitParams P) {
             unsigned long long w = 0;
             if (lane < NS) w = rng[lane];
             const u32 c = (u32)w & 0xfffffu, e = (u32)(w >> 20) & 0xfffffu;
-            u32 best = e > c ? e - c : 0u;
+            /* VSA_STEAL_W (P.steal_w): a victim's unclaimed groups count by
+             * its issue age (younger waves issue slower: x1 / 1.25 / 1.5 /
+             * 2.25 for waves 0-3 / 4-7 / 8-11 / 12+, quarter units), and the
+             * thief takes the share that would end both together */
+            const u32 wt = P.steal_w ? (lane < 4 ? 4u : lane < 8 ? 5u : lane < 12 ? 6u : 9u) : 4u;
+            u32 best = e > c ? (e - c) * wt : 0u;
             const u32 mine = best;
 #pragma unroll
             for (int dd = 32; dd >= 1; dd >>= 1) {
@@ -1910,14 +1915,20 @@ vsa_lit_scan(VsaLitParams P) {
                 best = o > best ? o : best;
             }
             best = readfirstlane_u32(best);
-            if (best < P.steal) return false;
+            if (best < 4u * P.steal) return false;
             const u64 mk = __ballot(mine == best);
             const u32 v = (u32)__ffsll((long long)mk) - 1;
             const unsigned long long wv =
                 ((unsigned long long)readlane_u32((u32)(w >> 32), (int)v) << 32) |
                 readlane_u32((u32)w, (int)v);
             const u32 vc = (u32)wv & 0xfffffu, ve = (u32)(wv >> 20) & 0xfffffu;
-            const u32 mid = vc + (ve - vc + 1) / 2;
+            u32 mid = vc + (ve - vc + 1) / 2;
+            if (P.steal_w) {
+                const u32 wv_ = v < 4 ? 4u : v < 8 ? 5u : v < 12 ? 6u : 9u;
+                const u32 wt_ = wave < 4 ? 4u : wave < 8 ? 5u : wave < 12 ? 6u : 9u;
+                mid = ve - ((ve - vc) * wv_ + (wv_ + wt_) / 2) / (wv_ + wt_);
+                mid = mid < ve ? mid : ve - 1; /* the thief takes at least one */
+            }
             const unsigned long long nw = (wv & ~(0xfffffULL << 20)) | ((unsigned long long)mid << 20);
             unsigned long long old = wv;
             if (lane == 0)

@@ -866,6 +866,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         P.seg_bytes = seg_bytes;
     P.dynamic = c->launch.grid ? 2u : getenv("VSA_STATIC_SEGS") ? 0u : 1u;
     P.steal = P.dynamic == 2 ? steal_min() : 0u;
+    P.steal_w = (uint32_t)env_int("VSA_STEAL_W", 0);
     P.nregions = 8;
     if (const char *e = getenv("VSA_REGIONS")) P.nregions = (uint32_t)std::min(8, std::max(1, atoi(e)));
         P.nsegs = nsegs;
@@ -902,6 +903,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.seg_bytes = seg_bytes;
     P.dynamic = c->launch.grid ? 2u : getenv("VSA_STATIC_SEGS") ? 0u : 1u;
     P.steal = P.dynamic == 2 ? steal_min() : 0u;
+    P.steal_w = (uint32_t)env_int("VSA_STEAL_W", 0);
     P.nregions = 8;
     if (const char *e = getenv("VSA_REGIONS")) P.nregions = (uint32_t)std::min(8, std::max(1, atoi(e)));
     P.nsegs = nsegs;
