@@ -1902,10 +1902,14 @@ vsa_lit_scan(VsaLitParams P) {
             unsigned long long w = 0;
             if (lane < NS) w = rng[lane];
             const u32 c = (u32)w & 0xfffffu, e = (u32)(w >> 20) & 0xfffffu;
-            /* VSA_STEAL_W (P.steal_w): a victim's unclaimed groups count by
-             * its issue age (younger waves issue slower: x1 / 1.25 / 1.5 /
-             * 2.25 for waves 0-3 / 4-7 / 8-11 / 12+, quarter units), and the
-             * thief takes the share that would end both together */
+            /* P.steal_w (VSA_STEAL_W, on): a victim's unclaimed groups count
+             * by its issue age (younger waves issue slower: x1 / 1.25 / 1.5 /
+             * 2.25 for waves 0-3 / 4-7 / 8-11 / 12+, quarter units; the
+             * per-wave rates of profiles/r04e_waves_4g.txt), and the thief
+             * takes the share that would end both together.  Measured
+             * (profiles/r04m_sweep.jsonl, kernel us, twice each): 4 GiB
+             * 850 / 848 against 864 / 857, 1 GiB 242 / 241 against 244 /
+             * 246, 512 MiB 136 / 137 against 137 / 138 */
             const u32 wt = P.steal_w ? (lane < 4 ? 4u : lane < 8 ? 5u : lane < 12 ? 6u : 9u) : 4u;
             u32 best = e > c ? (e - c) * wt : 0u;
             const u32 mine = best;

@@ -690,7 +690,9 @@ int queue_bin_sort(vsa_ctx *c, hipStream_t st) {
  * per-workgroup-list launch (>= 64 workgroups, >= 256 MiB) records each
  * workgroup's entry and end (and XCD) into fine-grained host memory; after
  * it the host moves each XCD's weight toward the rate it showed (half the
- * way, within 0.85-1.15 of the mean) and the next plan gives each
+ * way, within 0.7-1.3 of the mean: noodle at 1 GiB reached the earlier
+ * 0.85-1.15 clamp, its XCDs streaming 25 % apart, profiles/r04m_waves_noodle_1g.txt)
+ * and the next plan gives each
  * workgroup a share in proportion (build_plan wg_w).  Results are
  * unaffected (order-exact output); VSA_XCD_FEEDBACK=0 turns it off. */
 bool xcd_feedback_on() {
@@ -746,7 +748,7 @@ void take_feedback(vsa_ctx *c) {
     mean /= 8;
     bool moved = false;
     for (int x = 0; x < 8; x++) {
-        nw[x] = std::min(1.15f, std::max(0.85f, (float)(nw[x] / mean)));
+        nw[x] = std::min(1.3f, std::max(0.7f, (float)(nw[x] / mean)));
         moved = moved || std::fabs(nw[x] - c->fb.w[x]) > 0.002f;
     }
     const bool first = !c->fb.known;
@@ -866,7 +868,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         P.seg_bytes = seg_bytes;
     P.dynamic = c->launch.grid ? 2u : getenv("VSA_STATIC_SEGS") ? 0u : 1u;
     P.steal = P.dynamic == 2 ? steal_min() : 0u;
-    P.steal_w = (uint32_t)env_int("VSA_STEAL_W", 0);
+    P.steal_w = (uint32_t)env_int("VSA_STEAL_W", 1);
     P.nregions = 8;
     if (const char *e = getenv("VSA_REGIONS")) P.nregions = (uint32_t)std::min(8, std::max(1, atoi(e)));
         P.nsegs = nsegs;
@@ -903,7 +905,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.seg_bytes = seg_bytes;
     P.dynamic = c->launch.grid ? 2u : getenv("VSA_STATIC_SEGS") ? 0u : 1u;
     P.steal = P.dynamic == 2 ? steal_min() : 0u;
-    P.steal_w = (uint32_t)env_int("VSA_STEAL_W", 0);
+    P.steal_w = (uint32_t)env_int("VSA_STEAL_W", 1);
     P.nregions = 8;
     if (const char *e = getenv("VSA_REGIONS")) P.nregions = (uint32_t)std::min(8, std::max(1, atoi(e)));
     P.nsegs = nsegs;
