@@ -188,6 +188,11 @@ struct VsaClassParams {
     unsigned long long *count;     /* [slots] popcount of the bitmap */
     uint32_t slots;                /* workgroup b updates slot b % slots, at
                                       u64 index 16 * slot (one line each) */
+    const uint64_t *wg_lo;         /* LUT kernel: workgroup b scans [wg_lo[b],
+                                      wg_lo[b + 1]) (schedule feedback), or
+                                      null: equal spans */
+    unsigned long long *wg_time;   /* schedule feedback record (as
+                                      VsaLitParams.wg_time), or null */
 };
 
 /* Double shufti (shuftiDoubleExec): bucketed byte-pair test with the

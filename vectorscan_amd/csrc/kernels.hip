@@ -2922,12 +2922,14 @@ __device__ __forceinline__ u32 lds_ld8(u32 addr) { return *(lds_cu8_t *)(uintptr
 __global__ void __launch_bounds__(1024) vsa_class_scan_lut(VsaClassParams P, u64 wspan) {
     __shared__ __align__(16) u8 T[65536];
     __shared__ u8 mem[256];
-    __shared__ u32 gctr;
+    __shared__ u32 gctr, cdone;
     const u32 tid = threadIdx.x;
     const u32 lane = lane_id();
     const u32 wave = readfirstlane_u32(tid / WAVE);
-    const u64 lo = (u64)blockIdx.x * wspan;
-    const u64 hi = min(lo + wspan, (u64)P.len);
+    /* the workgroup's range: an equal span, or the schedule feedback's
+     * weighted bounds (4 KiB-aligned, runtime.hip vsa_class_scan) */
+    const u64 lo = P.wg_lo ? P.wg_lo[blockIdx.x] : (u64)blockIdx.x * wspan;
+    const u64 hi = min(P.wg_lo ? P.wg_lo[blockIdx.x + 1] : lo + wspan, (u64)P.len);
     /* iterations (1 KiB) of the range, the full ones, and its groups */
     const u32 nit = lo < hi ? (u32)((hi - lo + 1023) >> 10) : 0u;
     const u32 nfull = lo < hi ? (u32)min((u64)nit, ((u64)P.len - lo) >> 10) : 0u;
@@ -2943,7 +2945,11 @@ __global__ void __launch_bounds__(1024) vsa_class_scan_lut(VsaClassParams P, u64
         ring[k] = g < ngr && nfull ? load_wave_kib(sb, chunk_off(g * CLS_DEPTH + k, 0))
                                    : make_uint4(0, 0, 0, 0);
     if (tid < 256) mem[tid] = (u8)((P.cls[tid >> 5] >> (tid & 31)) & 1u);
-    if (tid == 0) gctr = 32;
+    if (tid == 0) {
+        gctr = 32;
+        cdone = 0;
+        if (P.wg_time) P.wg_time[gridDim.x + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    }
     __syncthreads();
     {
         /* dword i holds T[4i .. 4i+3]: low bytes 4i & 0xff .., high byte i >> 6 */
@@ -3019,5 +3025,16 @@ __global__ void __launch_bounds__(1024) vsa_class_scan_lut(VsaClassParams P, u64
         if (first != ~0ULL) atomicMin(P.first + sl, first);
         if (last) atomicMax(P.last + sl, last);
         if (cnt) atomicAdd(P.count + sl, cnt);
+        if (P.wg_time) {
+            /* the schedule feedback: the workgroup's last wave, its end and XCD */
+            const u32 prev = __hip_atomic_fetch_add(&cdone, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (prev + 1 == blockDim.x / WAVE) {
+                u32 xcc;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                P.wg_time[blockIdx.x] = ((unsigned long long)(xcc & 15u) << 60) |
+                                        (__builtin_amdgcn_s_memrealtime() & ((1ULL << 60) - 1));
+            }
+        }
     }
 }

@@ -210,7 +210,7 @@ struct vsa_ctx {
         const uint8_t *d_data = nullptr;
         uint64_t waves = 0;
         uint32_t nb = 0;
-        uint32_t fb_version = 0; /* the feedback weights it was built with */
+        uint64_t fb_key = 0; /* the feedback weights it was built with (fb_key_of) */
         std::vector<uint64_t> in[5]; /* offs, lens, starts, hlens, rlos ({} = NULL) */
     } memo;
     bool host_sort = false; /* the last scan's records are left unsorted */
@@ -221,17 +221,28 @@ struct vsa_ctx {
     /* live plans of this context (vsa_ctx_destroy detaches them, so a plan
      * freed after its context never touches it) */
     std::vector<vsa_plan *> plans;
-    /* schedule feedback (xcd_feedback): per-XCD weights of the workgroups'
-     * static shares, learned from the workgroups' end times of large
-     * launches (the kernel writes them into fine-grained host memory) */
-    struct {
+    /* the class scan's weighted workgroup bounds (device, pinned staging)
+     * and what they were built for: length, grid, weights version + 1 */
+    uint64_t *cls_bounds_d = nullptr, *cls_bounds_h = nullptr;
+    uint64_t cls_bounds_key[3] = {0, 0, 0};
+    /* schedule feedback (take_feedback): per-XCD weights of the
+     * workgroups' static shares, learned from the workgroups' end times of
+     * large launches (the kernels write them into fine-grained host
+     * memory); one set per kind of launch, as compute-bound and streaming
+     * scans see different XCD speeds: 0 = FDR / Teddy, 1 = noodle, 2 = the
+     * class scan */
+    struct FbSet {
         float w[8] = {1, 1, 1, 1, 1, 1, 1, 1};
         uint8_t xcc[1024];       /* the XCD workgroup b ran on last time */
-        float wg[1024];          /* w[xcc[b]]: build_plan's share weights */
+        float wg[1024];          /* w[xcc[b]]: the share weights */
         uint32_t version = 0;    /* bumped when w changes (plans rebuild) */
-        unsigned long long *h = nullptr, *d = nullptr; /* 2 x 1024 u64 */
-        bool armed = false;      /* the launch in flight records its times */
         bool known = false;      /* xcc[] holds measured XCDs */
+    };
+    struct {
+        FbSet set[3];
+        unsigned long long *h = nullptr, *d = nullptr; /* 2 x 1024 u64 */
+        int armed = -1;          /* the set the launch in flight records for */
+        uint32_t grid = 0;       /* ... and its workgroups */
     } fb;
 };
 
@@ -700,17 +711,29 @@ bool xcd_feedback_on() {
     return v;
 }
 
-void arm_feedback(vsa_ctx *c) {
-    c->fb.armed = xcd_feedback_on() && c->fb.h && c->launch.grid >= 64 &&
-                  c->launch.grid <= 1024 && c->launch.bytes >= (256u << 20) &&
-                  !(c->launch.flags & SCAN_HOST_SORT_SMALL);
-    if (c->fb.armed) memset(c->fb.h, 0, 2 * c->launch.grid * sizeof(unsigned long long));
+/* arm the feedback record of the next launch (set: FbSet kind) */
+void arm_feedback(vsa_ctx *c, int set, uint32_t grid, uint64_t bytes, bool small) {
+    c->fb.armed = xcd_feedback_on() && c->fb.h && grid >= 64 && grid <= 1024 &&
+                  bytes >= (256u << 20) && !small ? set : -1;
+    c->fb.grid = grid;
+    if (c->fb.armed >= 0) memset(c->fb.h, 0, 2 * grid * sizeof(unsigned long long));
+}
+
+/* the feedback kind of a literal scan */
+int fb_set_of(const vsa_db *db) { return db && db->type == HWLM_ENGINE_NOOD ? 1 : 0; }
+
+/* which weights a plan was built with: kind and version */
+uint64_t fb_key_of(const vsa_ctx *c, const vsa_db *db) {
+    const int si = fb_set_of(db);
+    return ((uint64_t)si << 32) | c->fb.set[si].version;
 }
 
 void take_feedback(vsa_ctx *c) {
-    if (!c->fb.armed) return;
-    c->fb.armed = false;
-    const uint32_t G = c->launch.grid;
+    const int si = c->fb.armed;
+    if (si < 0) return;
+    c->fb.armed = -1;
+    vsa_ctx::FbSet &F = c->fb.set[si];
+    const uint32_t G = c->fb.grid;
     const volatile unsigned long long *h = c->fb.h;
     const unsigned long long M60 = (1ULL << 60) - 1;
     unsigned long long t0 = ~0ULL;
@@ -719,14 +742,16 @@ void take_feedback(vsa_ctx *c) {
         t0 = std::min(t0, (unsigned long long)h[G + b]);
     }
     double sum[8] = {0}, cnt[8] = {0};
+    uint8_t xs[1024];
     for (uint32_t b = 0; b < G; b++) {
         const uint32_t x = (uint32_t)(h[b] >> 60) & 7u;
         const unsigned long long e = h[b] & M60;
         if (e <= t0) return;
-        c->fb.xcc[b] = (uint8_t)x;
+        xs[b] = (uint8_t)x;
         sum[x] += (double)(e - t0);
         cnt[x] += 1;
     }
+    memcpy(F.xcc, xs, G);
     double tm = 0, nx = 0;
     for (int x = 0; x < 8; x++)
         if (cnt[x]) {
@@ -738,10 +763,10 @@ void take_feedback(vsa_ctx *c) {
     float nw[8];
     double mean = 0;
     for (int x = 0; x < 8; x++) {
-        nw[x] = c->fb.w[x];
+        nw[x] = F.w[x];
         if (cnt[x]) {
             const double tx = sum[x] / cnt[x];
-            nw[x] = (float)(0.5 * c->fb.w[x] + 0.5 * c->fb.w[x] * tm / tx);
+            nw[x] = (float)(0.5 * F.w[x] + 0.5 * F.w[x] * tm / tx);
         }
     }
     for (int x = 0; x < 8; x++) mean += nw[x];
@@ -749,14 +774,14 @@ void take_feedback(vsa_ctx *c) {
     bool moved = false;
     for (int x = 0; x < 8; x++) {
         nw[x] = std::min(1.3f, std::max(0.7f, (float)(nw[x] / mean)));
-        moved = moved || std::fabs(nw[x] - c->fb.w[x]) > 0.002f;
+        moved = moved || std::fabs(nw[x] - F.w[x]) > 0.002f;
     }
-    const bool first = !c->fb.known;
-    c->fb.known = true;
+    const bool first = !F.known;
+    F.known = true;
     if (!moved && !first) return;
-    memcpy(c->fb.w, nw, sizeof(nw));
-    for (int b = 0; b < 1024; b++) c->fb.wg[b] = c->fb.w[c->fb.xcc[b] & 7];
-    c->fb.version++;
+    memcpy(F.w, nw, sizeof(nw));
+    for (int b = 0; b < 1024; b++) F.wg[b] = F.w[F.xcc[b] & 7];
+    F.version++;
 }
 
 /* diagnostic per-wave log (vsa_set_wave_log; the kernel writes it under
@@ -811,7 +836,7 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
      * timing and get their counters and records published (no copies) */
     const bool small = (c->launch.flags & SCAN_HOST_SORT_SMALL) != 0;
     if (!small) VSA_CHECK(hipEventRecord(c->ev0, c->stream));
-    arm_feedback(c);
+    arm_feedback(c, fb_set_of(db), c->launch.grid, c->launch.bytes, small);
     int r = launch_scan_kernel(c, db, d_data, nb, nsegs, seg_bytes);
     if (r != VSA_OK) return r;
     if (small) {
@@ -884,7 +909,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         P.bin_shift = bin_shift_for(c->launch.end_bits);
         P.bin_slots = c->launch.bins && !old_sort() ? w.d_bslots : nullptr;
         P.counters = w.d_counters;
-        P.wg_time = c->fb.armed ? c->fb.d : nullptr;
+        P.wg_time = c->fb.armed >= 0 ? c->fb.d : nullptr;
         P.wave_log = g_wave_log;
         {
             const char *e = getenv("VSA_DEBUG_FLAGS");
@@ -928,7 +953,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.bin_shift = bin_shift_for(c->launch.end_bits);
     P.bin_slots = c->launch.bins && !old_sort() ? w.d_bslots : nullptr;
     P.counters = w.d_counters;
-    P.wg_time = c->fb.armed ? c->fb.d : nullptr;
+    P.wg_time = c->fb.armed >= 0 ? c->fb.d : nullptr;
     P.wave_log = g_wave_log;
     {
         const char *e = getenv("VSA_DEBUG_FLAGS");
@@ -1405,7 +1430,7 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
     const uint64_t *in[5] = {offs, lens, starts, hlens, rlos};
     auto &M = c->memo;
     bool same = M.valid && M.d_data == d_data && M.nb == nb && M.waves == waves &&
-                M.fb_version == c->fb.version;
+                M.fb_key == fb_key_of(c, db);
     for (int k = 0; same && k < 5; k++)
         same = in[k] ? (M.in[k].size() == nb && !memcmp(M.in[k].data(), in[k], nb * 8))
                      : M.in[k].empty();
@@ -1420,7 +1445,8 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         if ((r = ensure_tables(c, nb, 0)) != VSA_OK) return r;
         if ((r = build_plan(d_data, offs, lens, starts, hlens, rlos, nb, waves, pl,
                             w.h_blocks, LIT_WAVES - db->nconf.load(),
-                            c->fb.known ? c->fb.wg : nullptr)) != VSA_OK)
+                            c->fb.set[fb_set_of(db)].known ? c->fb.set[fb_set_of(db)].wg
+                                                           : nullptr)) != VSA_OK)
             return r;
         T1 = std::chrono::steady_clock::now();
         if ((r = ensure_tables(c, nb, pl.segblk.size(), true)) != VSA_OK) return r;
@@ -1433,7 +1459,7 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         M.d_data = d_data;
         M.nb = nb;
         M.waves = waves;
-        M.fb_version = c->fb.version;
+        M.fb_key = fb_key_of(c, db);
         for (int k = 0; k < 5; k++) {
             if (in[k]) M.in[k].assign(in[k], in[k] + nb);
             else M.in[k].clear();
@@ -1930,10 +1956,11 @@ int vsa_ctx_create(int device, vsa_ctx_t **out) {
     VSA_CHECK(hipHostMalloc((void **)&c->fb.h, 2048 * sizeof(unsigned long long),
                             hipHostMallocCoherent | hipHostMallocMapped));
     VSA_CHECK(hipHostGetDevicePointer((void **)&c->fb.d, c->fb.h, 0));
-    for (int b = 0; b < 1024; b++) {
-        c->fb.xcc[b] = (uint8_t)(b & 7);
-        c->fb.wg[b] = 1.0f;
-    }
+    for (auto &F : c->fb.set)
+        for (int b = 0; b < 1024; b++) {
+            F.xcc[b] = (uint8_t)(b & 7);
+            F.wg[b] = 1.0f;
+        }
     *out = c.release();
     return VSA_OK;
 }
@@ -1958,6 +1985,8 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (w.h_counters) (void)hipHostFree(w.h_counters);
     if (w.h_pub) (void)hipHostFree(w.h_pub);
     if (c->fb.h) (void)hipHostFree(c->fb.h);
+    if (c->cls_bounds_d) (void)hipFree(c->cls_bounds_d);
+    if (c->cls_bounds_h) (void)hipHostFree(c->cls_bounds_h);
     if (w.h_in) (void)hipHostFree(w.h_in);
     if (w.d_blocks) (void)hipFree(w.d_blocks);
     if (w.h_blocks) (void)hipHostFree(w.h_blocks);
@@ -2672,6 +2701,39 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
         const uint64_t G = (uint64_t)c->num_cus;
         const uint64_t wspan = ((len + G - 1) / G + 4095) & ~(uint64_t)4095;
         const uint32_t grid = (uint32_t)((len + wspan - 1) / wspan);
+        /* schedule feedback (take_feedback, kind 2): weighted 4 KiB-aligned
+         * bounds per workgroup, uploaded when they change */
+        vsa_ctx::FbSet &F = c->fb.set[2];
+        if (xcd_feedback_on() && F.known && grid == G && grid <= 1024) {
+            if (!c->cls_bounds_d) {
+                VSA_CHECK(hipMalloc(&c->cls_bounds_d, 1025 * sizeof(uint64_t)));
+                VSA_CHECK(hipHostMalloc((void **)&c->cls_bounds_h, 1025 * sizeof(uint64_t),
+                                        hipHostMallocDefault));
+            }
+            if (c->cls_bounds_key[0] != len || c->cls_bounds_key[1] != grid ||
+                c->cls_bounds_key[2] != F.version + 1) {
+                double tw = 0, a = 0;
+                for (uint32_t b = 0; b < grid; b++) tw += F.wg[b];
+                c->cls_bounds_h[0] = 0;
+                for (uint32_t b = 0; b < grid; b++) {
+                    a += F.wg[b];
+                    const uint64_t e = b + 1 == grid ? len
+                                                     : std::min<uint64_t>(
+                                                           len, ((uint64_t)((double)len * a / tw) + 2048) &
+                                                                    ~(uint64_t)4095);
+                    c->cls_bounds_h[b + 1] = std::max<uint64_t>(c->cls_bounds_h[b], e);
+                }
+                VSA_CHECK(hipMemcpyAsync(c->cls_bounds_d, c->cls_bounds_h, (grid + 1) * 8,
+                                         hipMemcpyHostToDevice, c->stream));
+                c->cls_bounds_key[0] = len;
+                c->cls_bounds_key[1] = grid;
+                c->cls_bounds_key[2] = F.version + 1;
+            }
+            P.wg_lo = c->cls_bounds_d;
+        }
+        /* (an asynchronous literal scan still in flight keeps its record) */
+        if (c->fb.armed < 0) arm_feedback(c, 2, grid, len, false);
+        P.wg_time = c->fb.armed == 2 ? c->fb.d : nullptr;
         hipLaunchKernelGGL(vsa_class_scan_lut, dim3(grid), dim3(1024), 0, c->stream, P, wspan);
     } else {
         uint64_t chunks = (len + 15) / 16;
@@ -2685,6 +2747,7 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
     VSA_CHECK(hipMemcpyAsync(w.h_counters + CLASS_BASE, part, 16 * CLASS_SLOTS * 8,
                              hipMemcpyDeviceToHost, c->stream));
     VSA_CHECK(hipStreamSynchronize(c->stream));
+    take_feedback(c);
     {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_kernel_ms = ms;
