@@ -232,6 +232,46 @@ def test_gpu_fdr_5k_64mib(ctx):
     assert len(m) >= (64 << 20) // (64 << 10)
 
 
+def test_gpu_schedule_feedback_512mib(ctx):
+    """Schedule feedback (runtime.hip take_feedback / refresh_plan): 512 MiB
+    in 4 blocks scanned 8 times through one prebuilt plan and 8 times per
+    call (scan_blocks), so the XCD weights are learned and the plans rebuilt
+    with weighted shares between launches: every launch's records equal the
+    first one's, and that one's digest equals the oracle's."""
+    import bench
+    import torch
+    lits = bench.make_literals(5000, seed=12)
+    blob = vsa.hwlm_build(lits)
+    db = vsa.Database(ctx, blob)
+    n = 512 << 20
+    bl = n // 4
+    offs = [i * bl for i in range(4)]
+    dev = torch.device("cuda", 0)
+    data = bench.make_corpus_device(torch, 0, n, n, lits, 5, 64 << 10, dev)
+    torch.cuda.synchronize()
+    first = None
+    plan = ctx.plan(data.data_ptr(), offs, [bl] * 4)
+    try:
+        for k in range(16):
+            m = (ctx.scan_plan(db, plan) if k < 8 else
+                 ctx.scan_blocks(db, data.data_ptr(), offs, [bl] * 4))
+            res = ctx.results(m)
+            cur = (res["key"].copy(), res["id"].copy())
+            if first is None:
+                first = cur
+                host = data.cpu().numpy()
+                want = oracle.digest_mt(vsa.engine_blob(blob), host, 16)
+                assert oracle.digest_of(res["key"] >> np.uint64(24), res["id"]) == want
+                del host
+            else:
+                assert np.array_equal(cur[0], first[0]) and np.array_equal(cur[1], first[1]), k
+    finally:
+        plan.close()
+        db.close()
+        del data
+        torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("kind", ["shufti", "truffle"])
 def test_gpu_class_scan_256mib(ctx, kind):
     """cfg-2: 256 MiB uniform bytes, class A, driven by the shufti / truffle

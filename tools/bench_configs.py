@@ -42,6 +42,16 @@ def lits_printable(n, seed, minlen=4, maxlen=8):
 
 
 def timed(fn, steps, warmup, ctx):
+    # clock settle first, as bench.py: between configs the host-side parity
+    # checks leave the GPU idle long enough for its clock to drop, and 20
+    # warmup launches of 0.05-0.25 ms do not bring it back (untimed launches
+    # until the last 8 kernel times agree within 2 %, 40-400 of them, <= 3 s)
+    hist, t0 = [], time.perf_counter()
+    while len(hist) < 400 and time.perf_counter() - t0 < 3.0:
+        fn()
+        hist.append(ctx.kernel_ms())
+        if len(hist) >= 40 and max(hist[-8:]) <= 1.02 * min(hist[-8:]):
+            break
     for _ in range(warmup):
         fn()
     ks, t0 = [], time.perf_counter()

@@ -232,10 +232,11 @@ struct vsa_ctx {
      * scans see different XCD speeds: 0 = FDR / Teddy, 1 = noodle, 2 = the
      * class scan */
     struct FbSet {
-        float w[8] = {1, 1, 1, 1, 1, 1, 1, 1};
+        float w[8] = {1, 1, 1, 1, 1, 1, 1, 1};  /* the running estimate */
+        float wa[8] = {1, 1, 1, 1, 1, 1, 1, 1}; /* the weights plans use */
         uint8_t xcc[1024];       /* the XCD workgroup b ran on last time */
-        float wg[1024];          /* w[xcc[b]]: the share weights */
-        uint32_t version = 0;    /* bumped when w changes (plans rebuild) */
+        float wg[1024];          /* wa[xcc[b]]: the share weights */
+        uint32_t version = 0;    /* bumped when wa changes (plans rebuild) */
         bool known = false;      /* xcc[] holds measured XCDs */
     };
     struct {
@@ -261,6 +262,12 @@ struct vsa_plan {
     uint64_t bytes = 0;
     VsaBlock *d_blocks = nullptr;
     uint32_t *d_segblk = nullptr;
+    /* schedule feedback: the inputs (to rebuild the segment map with the
+     * context's current weights), the words d_segblk holds room for, and
+     * the weights it was built with (fb_key_of; ~0: equal shares) */
+    std::vector<uint64_t> in[5];
+    size_t segblk_cap = 0;
+    uint64_t fb_key = ~0ULL;
 };
 
 /* drop-in scans: results of at most HOST_SORT_MAX records are sorted on the
@@ -771,16 +778,21 @@ void take_feedback(vsa_ctx *c) {
     }
     for (int x = 0; x < 8; x++) mean += nw[x];
     mean /= 8;
+    /* the estimate moves every launch; the weights plans are built with
+     * only when it left them by more than 1 % (per-launch noise is ~0.5 %,
+     * and a changed plan means a rebuild, for a prebuilt plan a device
+     * upload: vsa_scan_plan) */
     bool moved = false;
     for (int x = 0; x < 8; x++) {
         nw[x] = std::min(1.3f, std::max(0.7f, (float)(nw[x] / mean)));
-        moved = moved || std::fabs(nw[x] - F.w[x]) > 0.002f;
+        moved = moved || std::fabs(nw[x] - F.wa[x]) > 0.01f;
     }
+    memcpy(F.w, nw, sizeof(nw));
     const bool first = !F.known;
     F.known = true;
     if (!moved && !first) return;
-    memcpy(F.w, nw, sizeof(nw));
-    for (int b = 0; b < 1024; b++) F.wg[b] = F.w[F.xcc[b] & 7];
+    memcpy(F.wa, nw, sizeof(nw));
+    for (int b = 0; b < 1024; b++) F.wg[b] = F.wa[F.xcc[b] & 7];
     F.version++;
 }
 
@@ -3411,10 +3423,14 @@ int vsa_plan_create(vsa_ctx_t *c, const uint8_t *d_data, const uint64_t *offsets
     p->grid = pl.grid;
     p->end_bits = pl.end_bits;
     p->bytes = pl.bytes;
+    const uint64_t *ins[5] = {offsets, lens, starts, hlens, report_lo};
+    for (int k = 0; k < 5; k++)
+        if (ins[k]) p->in[k].assign(ins[k], ins[k] + nblocks);
+    /* room for a rebuilt map: weighted shares can cut a few more pieces */
+    p->segblk_cap = std::max<size_t>(1, pl.segblk.size() + pl.segblk.size() / 4 + 4 * 1024);
     if (hipSetDevice(c->device) != hipSuccess ||
         hipMalloc(&p->d_blocks, nblocks * sizeof(VsaBlock)) != hipSuccess ||
-        hipMalloc(&p->d_segblk, std::max<size_t>(1, pl.segblk.size()) * sizeof(uint32_t)) !=
-            hipSuccess ||
+        hipMalloc(&p->d_segblk, p->segblk_cap * sizeof(uint32_t)) != hipSuccess ||
         upload_plan(c, pl, p->d_blocks, p->d_segblk) != VSA_OK ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
         vsa_plan_free(p);
@@ -3444,10 +3460,42 @@ int vsa_plan_free(vsa_plan_t *p) {
     return r;
 }
 
+/* A prebuilt plan follows the context's schedule feedback: when the
+ * weights for this kind of scan changed since the plan's segment map was
+ * built, the map is rebuilt and uploaded before the launch (the context's
+ * previous scan is complete, and only this context's scans read the plan;
+ * the weights move by > 1 % steps, so this happens a few times while they
+ * settle).  A map that would outgrow its buffer keeps the old one. */
+int refresh_plan(vsa_ctx *c, const vsa_db *db, vsa_plan *p) {
+    if (!xcd_feedback_on() || p->grid < 64 || p->in[0].empty()) return VSA_OK;
+    const int si = fb_set_of(db);
+    if (!c->fb.set[si].known) return VSA_OK;
+    const uint64_t key = fb_key_of(c, db);
+    if (key == p->fb_key) return VSA_OK;
+    BatchPlan pl;
+    auto in = [&](int k) { return p->in[k].empty() ? nullptr : p->in[k].data(); };
+    int r = build_plan(p->d_data, in(0), in(1), in(2), in(3), in(4), p->nb,
+                       (uint64_t)c->num_cus * (LIT_WAVES - 1), pl, nullptr, LIT_WAVES - 1,
+                       c->fb.set[si].wg);
+    if (r != VSA_OK) return r;
+    p->fb_key = key;
+    if (pl.segblk.size() > p->segblk_cap || pl.blocks.size() != p->nb) return VSA_OK;
+    VSA_CHECK(hipMemcpyAsync(p->d_blocks, pl.blocks.data(), pl.blocks.size() * sizeof(VsaBlock),
+                             hipMemcpyHostToDevice, c->stream));
+    VSA_CHECK(hipMemcpyAsync(p->d_segblk, pl.segblk.data(), pl.segblk.size() * sizeof(uint32_t),
+                             hipMemcpyHostToDevice, c->stream));
+    /* pageable sources: wait for the copies before pl goes */
+    VSA_CHECK(hipStreamSynchronize(c->stream));
+    p->segs = pl.nsegs;
+    p->grid = pl.grid;
+    return VSA_OK;
+}
+
 int vsa_scan_plan(vsa_ctx_t *c, const vsa_db_t *db, const vsa_plan_t *p, uint32_t flags,
                   uint64_t *n_matches) {
     if (!c || !db || !p || p->ctx != c) return VSA_E_INVALID;
     if (int r0 = finish_pending(c)) return r0;
+    if (int r1 = refresh_plan(c, db, const_cast<vsa_plan *>(p))) return r1;
     uint64_t dummy;
     return launch_planned(c, db, p->d_data, p->d_blocks, p->d_segblk, p->nb, p->segs,
                           p->seg_bytes, p->grid, p->end_bits, p->bytes, flags,
