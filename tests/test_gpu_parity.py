@@ -239,37 +239,34 @@ def test_gpu_schedule_feedback_512mib(ctx):
     with weighted shares between launches: every launch's records equal the
     first one's, and that one's digest equals the oracle's."""
     import bench
-    import torch
     lits = bench.make_literals(5000, seed=12)
     blob = vsa.hwlm_build(lits)
     db = vsa.Database(ctx, blob)
     n = 512 << 20
     bl = n // 4
     offs = [i * bl for i in range(4)]
-    dev = torch.device("cuda", 0)
-    data = bench.make_corpus_device(torch, 0, n, n, lits, 5, 64 << 10, dev)
-    torch.cuda.synchronize()
+    host = bench.make_corpus(n, lits, seed=5, plant_every=64 << 10)
+    d = ctx.malloc(n + 64)
     first = None
-    plan = ctx.plan(data.data_ptr(), offs, [bl] * 4)
+    plan = None
     try:
+        ctx.h2d(d, host)
+        plan = ctx.plan(d, offs, [bl] * 4)
         for k in range(16):
-            m = (ctx.scan_plan(db, plan) if k < 8 else
-                 ctx.scan_blocks(db, data.data_ptr(), offs, [bl] * 4))
+            m = ctx.scan_plan(db, plan) if k < 8 else ctx.scan_blocks(db, d, offs, [bl] * 4)
             res = ctx.results(m)
             cur = (res["key"].copy(), res["id"].copy())
             if first is None:
                 first = cur
-                host = data.cpu().numpy()
                 want = oracle.digest_mt(vsa.engine_blob(blob), host, 16)
                 assert oracle.digest_of(res["key"] >> np.uint64(24), res["id"]) == want
-                del host
             else:
                 assert np.array_equal(cur[0], first[0]) and np.array_equal(cur[1], first[1]), k
     finally:
-        plan.close()
+        if plan is not None:
+            plan.close()
         db.close()
-        del data
-        torch.cuda.empty_cache()
+        ctx.free(d)
 
 
 @pytest.mark.parametrize("kind", ["shufti", "truffle"])

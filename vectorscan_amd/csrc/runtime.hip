@@ -268,6 +268,7 @@ struct vsa_plan {
     std::vector<uint64_t> in[5];
     size_t segblk_cap = 0;
     uint64_t fb_key = ~0ULL;
+    void *h_stage = nullptr; /* pinned staging of a rebuilt block table + map */
 };
 
 /* drop-in scans: results of at most HOST_SORT_MAX records are sorted on the
@@ -2705,48 +2706,54 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
     P.last = part + 1;
     P.count = part + 2;
     P.slots = CLASS_SLOTS;
+    const bool lut = !cls2 && len >= ((uint64_t)8 << 20) && !getenv("VSA_CLASS_SIMPLE");
+    const uint64_t G = (uint64_t)c->num_cus;
+    const uint64_t wspan = ((len + G - 1) / G + 4095) & ~(uint64_t)4095;
+    const uint32_t lgrid = (uint32_t)((len + wspan - 1) / wspan);
+    /* schedule feedback for the class scan (kind 2): weighted 4 KiB-aligned
+     * bounds per workgroup, uploaded (before the timed region) when they
+     * change.  Off by default (VSA_CLASS_FEEDBACK=1): at 256 MiB it measured
+     * no gain, 0.0592 / 0.0597 / 0.0566 ms against 0.0593 / 0.0587 / 0.0580
+     * without (profiles/r04p_configs.jsonl, r04p_cfg2_nofb.jsonl) */
+    static const bool cls_fb = env_int("VSA_CLASS_FEEDBACK", 0) != 0;
+    vsa_ctx::FbSet &F = c->fb.set[2];
+    if (lut && cls_fb && xcd_feedback_on() && F.known && lgrid == G && lgrid <= 1024) {
+        if (!c->cls_bounds_d) {
+            VSA_CHECK(hipMalloc(&c->cls_bounds_d, 1025 * sizeof(uint64_t)));
+            VSA_CHECK(hipHostMalloc((void **)&c->cls_bounds_h, 1025 * sizeof(uint64_t),
+                                    hipHostMallocDefault));
+        }
+        if (c->cls_bounds_key[0] != len || c->cls_bounds_key[1] != lgrid ||
+            c->cls_bounds_key[2] != F.version + 1) {
+            double tw = 0, a = 0;
+            for (uint32_t b = 0; b < lgrid; b++) tw += F.wg[b];
+            c->cls_bounds_h[0] = 0;
+            for (uint32_t b = 0; b < lgrid; b++) {
+                a += F.wg[b];
+                const uint64_t e =
+                    b + 1 == lgrid
+                        ? len
+                        : std::min<uint64_t>(len, ((uint64_t)((double)len * a / tw) + 2048) &
+                                                      ~(uint64_t)4095);
+                c->cls_bounds_h[b + 1] = std::max<uint64_t>(c->cls_bounds_h[b], e);
+            }
+            VSA_CHECK(hipMemcpyAsync(c->cls_bounds_d, c->cls_bounds_h, (lgrid + 1) * 8,
+                                     hipMemcpyHostToDevice, c->stream));
+            c->cls_bounds_key[0] = len;
+            c->cls_bounds_key[1] = lgrid;
+            c->cls_bounds_key[2] = F.version + 1;
+        }
+        P.wg_lo = c->cls_bounds_d;
+    }
     VSA_CHECK(hipEventRecord(c->ev0, c->stream));
-    if (!cls2 && len >= ((uint64_t)8 << 20) && !getenv("VSA_CLASS_SIMPLE")) {
+    if (lut) {
         /* large buffers: pair-LUT kernel, one 1024-thread workgroup per CU,
          * an equal 4 KiB-aligned share per workgroup, taken by its waves in
          * 4 KiB groups (kernels.hip vsa_class_scan_lut) */
-        const uint64_t G = (uint64_t)c->num_cus;
-        const uint64_t wspan = ((len + G - 1) / G + 4095) & ~(uint64_t)4095;
-        const uint32_t grid = (uint32_t)((len + wspan - 1) / wspan);
-        /* schedule feedback (take_feedback, kind 2): weighted 4 KiB-aligned
-         * bounds per workgroup, uploaded when they change */
-        vsa_ctx::FbSet &F = c->fb.set[2];
-        if (xcd_feedback_on() && F.known && grid == G && grid <= 1024) {
-            if (!c->cls_bounds_d) {
-                VSA_CHECK(hipMalloc(&c->cls_bounds_d, 1025 * sizeof(uint64_t)));
-                VSA_CHECK(hipHostMalloc((void **)&c->cls_bounds_h, 1025 * sizeof(uint64_t),
-                                        hipHostMallocDefault));
-            }
-            if (c->cls_bounds_key[0] != len || c->cls_bounds_key[1] != grid ||
-                c->cls_bounds_key[2] != F.version + 1) {
-                double tw = 0, a = 0;
-                for (uint32_t b = 0; b < grid; b++) tw += F.wg[b];
-                c->cls_bounds_h[0] = 0;
-                for (uint32_t b = 0; b < grid; b++) {
-                    a += F.wg[b];
-                    const uint64_t e = b + 1 == grid ? len
-                                                     : std::min<uint64_t>(
-                                                           len, ((uint64_t)((double)len * a / tw) + 2048) &
-                                                                    ~(uint64_t)4095);
-                    c->cls_bounds_h[b + 1] = std::max<uint64_t>(c->cls_bounds_h[b], e);
-                }
-                VSA_CHECK(hipMemcpyAsync(c->cls_bounds_d, c->cls_bounds_h, (grid + 1) * 8,
-                                         hipMemcpyHostToDevice, c->stream));
-                c->cls_bounds_key[0] = len;
-                c->cls_bounds_key[1] = grid;
-                c->cls_bounds_key[2] = F.version + 1;
-            }
-            P.wg_lo = c->cls_bounds_d;
-        }
         /* (an asynchronous literal scan still in flight keeps its record) */
-        if (c->fb.armed < 0) arm_feedback(c, 2, grid, len, false);
+        if (cls_fb && c->fb.armed < 0) arm_feedback(c, 2, lgrid, len, false);
         P.wg_time = c->fb.armed == 2 ? c->fb.d : nullptr;
-        hipLaunchKernelGGL(vsa_class_scan_lut, dim3(grid), dim3(1024), 0, c->stream, P, wspan);
+        hipLaunchKernelGGL(vsa_class_scan_lut, dim3(lgrid), dim3(1024), 0, c->stream, P, wspan);
     } else {
         uint64_t chunks = (len + 15) / 16;
         uint64_t want = (chunks + 255) / 256;
@@ -3456,6 +3463,7 @@ int vsa_plan_free(vsa_plan_t *p) {
     }
     if (p->d_blocks) (void)hipFree(p->d_blocks);
     if (p->d_segblk) (void)hipFree(p->d_segblk);
+    if (p->h_stage) (void)hipHostFree(p->h_stage);
     delete p;
     return r;
 }
@@ -3480,12 +3488,20 @@ int refresh_plan(vsa_ctx *c, const vsa_db *db, vsa_plan *p) {
     if (r != VSA_OK) return r;
     p->fb_key = key;
     if (pl.segblk.size() > p->segblk_cap || pl.blocks.size() != p->nb) return VSA_OK;
-    VSA_CHECK(hipMemcpyAsync(p->d_blocks, pl.blocks.data(), pl.blocks.size() * sizeof(VsaBlock),
+    /* through a pinned staging buffer, queued on the scan stream: no host
+     * wait.  The staging is rewritten only at this plan's next refresh, by
+     * then this context's next scan -- queued behind these copies -- has
+     * completed (finish_pending), so the copies have run */
+    const size_t bb = (size_t)p->nb * sizeof(VsaBlock);
+    if (!p->h_stage)
+        VSA_CHECK(hipHostMalloc(&p->h_stage, bb + p->segblk_cap * sizeof(uint32_t),
+                                hipHostMallocDefault));
+    uint8_t *hs = (uint8_t *)p->h_stage;
+    memcpy(hs, pl.blocks.data(), bb);
+    memcpy(hs + bb, pl.segblk.data(), pl.segblk.size() * sizeof(uint32_t));
+    VSA_CHECK(hipMemcpyAsync(p->d_blocks, hs, bb, hipMemcpyHostToDevice, c->stream));
+    VSA_CHECK(hipMemcpyAsync(p->d_segblk, hs + bb, pl.segblk.size() * sizeof(uint32_t),
                              hipMemcpyHostToDevice, c->stream));
-    VSA_CHECK(hipMemcpyAsync(p->d_segblk, pl.segblk.data(), pl.segblk.size() * sizeof(uint32_t),
-                             hipMemcpyHostToDevice, c->stream));
-    /* pageable sources: wait for the copies before pl goes */
-    VSA_CHECK(hipStreamSynchronize(c->stream));
     p->segs = pl.nsegs;
     p->grid = pl.grid;
     return VSA_OK;
