@@ -243,6 +243,7 @@ struct vsa_ctx {
         FbSet set[3];
         unsigned long long *h = nullptr, *d = nullptr; /* 2 x 1024 u64 */
         int armed = -1;          /* the set the launch in flight records for */
+        uint32_t tick = 0;       /* eligible launches (VSA_FB_PERIOD) */
         uint32_t grid = 0;       /* ... and its workgroups */
     } fb;
 };
@@ -721,8 +722,11 @@ bool xcd_feedback_on() {
 
 /* arm the feedback record of the next launch (set: FbSet kind) */
 void arm_feedback(vsa_ctx *c, int set, uint32_t grid, uint64_t bytes, bool small) {
+    /* VSA_FB_PERIOD (A/B knob): record every n-th eligible launch */
+    static const uint32_t period = (uint32_t)std::max(1, env_int("VSA_FB_PERIOD", 1));
+    const bool due = (c->fb.tick++ % period) == 0 || !c->fb.set[set].known;
     c->fb.armed = xcd_feedback_on() && c->fb.h && grid >= 64 && grid <= 1024 &&
-                  bytes >= (256u << 20) && !small ? set : -1;
+                  bytes >= (256u << 20) && !small && due ? set : -1;
     c->fb.grid = grid;
     if (c->fb.armed >= 0) memset(c->fb.h, 0, 2 * grid * sizeof(unsigned long long));
 }
@@ -3475,7 +3479,8 @@ int vsa_plan_free(vsa_plan_t *p) {
  * the weights move by > 1 % steps, so this happens a few times while they
  * settle).  A map that would outgrow its buffer keeps the old one. */
 int refresh_plan(vsa_ctx *c, const vsa_db *db, vsa_plan *p) {
-    if (!xcd_feedback_on() || p->grid < 64 || p->in[0].empty()) return VSA_OK;
+    static const bool refresh = env_int("VSA_FB_REFRESH", 1) != 0; /* A/B knob */
+    if (!refresh || !xcd_feedback_on() || p->grid < 64 || p->in[0].empty()) return VSA_OK;
     const int si = fb_set_of(db);
     if (!c->fb.set[si].known) return VSA_OK;
     const uint64_t key = fb_key_of(c, db);
