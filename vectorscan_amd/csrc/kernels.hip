@@ -2570,9 +2570,14 @@ __device__ __forceinline__ void publish_body(unsigned long long *ctr, unsigned l
 /* publish_body for one wave (no workgroup barrier): wave 0 of
  * vsa_bin_finish's first workgroup publishes while its other waves sort */
 __device__ __forceinline__ void publish_wave(unsigned long long *ctr, unsigned long long *h,
-                                             unsigned long long seq, uint32_t nzero) {
+                                             unsigned long long seq, uint32_t nzero,
+                                             const unsigned long long *fb = nullptr,
+                                             unsigned long long *hfb = nullptr, u32 nfb = 0) {
     const u32 l = lane_id();
     const unsigned long long v = l < 16 ? ctr[l] : 0ULL;
+    /* the scan's schedule-feedback record (device memory) rides along to
+     * the host, before the sequence store releases it */
+    for (u32 i = l; i < nfb; i += WAVE) hfb[i] = fb[i];
     /* every read above before any zeroing below (one wave: program order
      * and a wait for the loads) */
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2620,7 +2625,9 @@ __global__ void __launch_bounds__(1024) vsa_bin_finish(const uint32_t *counts, u
                                                      uint32_t *oids,
                                                      uint64_t out_cap, unsigned long long *ctr,
                                                      unsigned long long *h,
-                                                     unsigned long long seq) {
+                                                     unsigned long long seq,
+                                                     const unsigned long long *fb,
+                                                     unsigned long long *hfb, uint32_t nfb) {
     __shared__ u32 red[16], cnt[FIN_BINS], off[FIN_BINS];
     const u32 t = threadIdx.x, wv = t / WAVE, lane = lane_id();
     const u32 b0 = blockIdx.x * FIN_BINS;
@@ -2647,7 +2654,7 @@ __global__ void __launch_bounds__(1024) vsa_bin_finish(const uint32_t *counts, u
         off[lane] = base + e;
     }
     __syncthreads();
-    if (blockIdx.x == 0 && wv == 0) publish_wave(ctr, h, seq, 144u);
+    if (blockIdx.x == 0 && wv == 0) publish_wave(ctr, h, seq, 144u, fb, hfb, nfb);
     /* this wave's 4 bins */
     const u32 lb = wv * 4;
     u32 m[4], mmax = 0;

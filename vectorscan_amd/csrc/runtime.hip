@@ -56,7 +56,9 @@ __global__ void vsa_bin_finish(const uint32_t *counts, uint32_t *counts_next,
                                const uint32_t *slots, const uint64_t *ikeys, const uint32_t *iids,
                                uint64_t *okeys, uint32_t *oids, uint64_t out_cap,
                                unsigned long long *ctr,
-                               unsigned long long *h, unsigned long long seq);
+                               unsigned long long *h, unsigned long long seq,
+                               const unsigned long long *fb, unsigned long long *hfb,
+                               uint32_t nfb);
 __global__ void vsa_class_scan_lut(VsaClassParams P, uint64_t span);
 __global__ void vsa_publish(unsigned long long *ctr, unsigned long long *h, unsigned long long seq,
                             uint32_t nzero, const uint64_t *keys, const uint32_t *ids,
@@ -243,6 +245,10 @@ struct vsa_ctx {
         FbSet set[3];
         unsigned long long *h = nullptr, *d = nullptr; /* 2 x 1024 u64 */
         int armed = -1;          /* the set the launch in flight records for */
+        /* ... into device memory (d_rec), published with the counters by
+         * vsa_bin_finish, instead of stores to host memory from the scan */
+        bool dev = false;
+        unsigned long long *d_rec = nullptr;
         uint32_t tick = 0;       /* eligible launches (VSA_FB_PERIOD) */
         uint32_t grid = 0;       /* ... and its workgroups */
     } fb;
@@ -674,10 +680,13 @@ int queue_bin_sort(vsa_ctx *c, hipStream_t st) {
     Workspace &w = c->ws;
     if (!old_sort()) {
         const uint32_t par = c->bin_par;
+        const bool fbd = c->fb.armed >= 0 && c->fb.dev;
         hipLaunchKernelGGL(vsa_bin_finish, dim3(VSA_SORT_BINS / 64), dim3(1024), 0, st,
                            bin_counts_of(c, par), bin_counts_of(c, par ^ 1u), w.d_bslots,
                            w.d_keys[0], w.d_ids[0], w.d_keys[1], w.d_ids[1], (uint64_t)w.out_cap,
-                           c->ws.d_counters, c->ws.d_pub, (unsigned long long)++c->pub_seq);
+                           c->ws.d_counters, c->ws.d_pub, (unsigned long long)++c->pub_seq,
+                           fbd ? c->fb.d_rec : nullptr, fbd ? c->fb.d : nullptr,
+                           fbd ? 2 * c->fb.grid : 0u);
         VSA_CHECK(hipGetLastError());
         c->bins_clean[par ^ 1u] = true;
         c->bin_par = par ^ 1u;
@@ -728,6 +737,11 @@ void arm_feedback(vsa_ctx *c, int set, uint32_t grid, uint64_t bytes, bool small
     c->fb.armed = xcd_feedback_on() && c->fb.h && grid >= 64 && grid <= 1024 &&
                   bytes >= (256u << 20) && !small && due ? set : -1;
     c->fb.grid = grid;
+    /* a literal scan whose counters vsa_bin_finish publishes records in
+     * device memory and rides on the publish (VSA_FB_DEV=0: host stores) */
+    static const bool dev_ok = env_int("VSA_FB_DEV", 1) != 0;
+    c->fb.dev = c->fb.armed >= 0 && c->fb.armed != 2 && dev_ok && c->fb.d_rec &&
+                c->launch.bins && !old_sort() && !small;
     if (c->fb.armed >= 0) memset(c->fb.h, 0, 2 * grid * sizeof(unsigned long long));
 }
 
@@ -926,7 +940,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         P.bin_shift = bin_shift_for(c->launch.end_bits);
         P.bin_slots = c->launch.bins && !old_sort() ? w.d_bslots : nullptr;
         P.counters = w.d_counters;
-        P.wg_time = c->fb.armed >= 0 ? c->fb.d : nullptr;
+        P.wg_time = c->fb.armed >= 0 ? (c->fb.dev ? c->fb.d_rec : c->fb.d) : nullptr;
         P.wave_log = g_wave_log;
         {
             const char *e = getenv("VSA_DEBUG_FLAGS");
@@ -970,7 +984,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.bin_shift = bin_shift_for(c->launch.end_bits);
     P.bin_slots = c->launch.bins && !old_sort() ? w.d_bslots : nullptr;
     P.counters = w.d_counters;
-    P.wg_time = c->fb.armed >= 0 ? c->fb.d : nullptr;
+    P.wg_time = c->fb.armed >= 0 ? (c->fb.dev ? c->fb.d_rec : c->fb.d) : nullptr;
     P.wave_log = g_wave_log;
     {
         const char *e = getenv("VSA_DEBUG_FLAGS");
@@ -1973,6 +1987,7 @@ int vsa_ctx_create(int device, vsa_ctx_t **out) {
     VSA_CHECK(hipHostMalloc((void **)&c->fb.h, 2048 * sizeof(unsigned long long),
                             hipHostMallocCoherent | hipHostMallocMapped));
     VSA_CHECK(hipHostGetDevicePointer((void **)&c->fb.d, c->fb.h, 0));
+    VSA_CHECK(hipMalloc(&c->fb.d_rec, 2048 * sizeof(unsigned long long)));
     for (auto &F : c->fb.set)
         for (int b = 0; b < 1024; b++) {
             F.xcc[b] = (uint8_t)(b & 7);
@@ -2002,6 +2017,7 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (w.h_counters) (void)hipHostFree(w.h_counters);
     if (w.h_pub) (void)hipHostFree(w.h_pub);
     if (c->fb.h) (void)hipHostFree(c->fb.h);
+    if (c->fb.d_rec) (void)hipFree(c->fb.d_rec);
     if (c->cls_bounds_d) (void)hipFree(c->cls_bounds_d);
     if (c->cls_bounds_h) (void)hipHostFree(c->cls_bounds_h);
     if (w.h_in) (void)hipHostFree(w.h_in);
