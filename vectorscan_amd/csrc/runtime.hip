@@ -239,6 +239,7 @@ struct vsa_ctx {
         uint8_t xcc[1024];       /* the XCD workgroup b ran on last time */
         float wg[1024];          /* wa[xcc[b]]: the share weights */
         uint32_t version = 0;    /* bumped when wa changes (plans rebuild) */
+        uint32_t since = 0;      /* records taken since wa last changed */
         bool known = false;      /* xcc[] holds measured XCDs */
     };
     struct {
@@ -276,6 +277,9 @@ struct vsa_plan {
     size_t segblk_cap = 0;
     uint64_t fb_key = ~0ULL;
     void *h_stage = nullptr; /* pinned staging of a rebuilt block table + map */
+    std::vector<uint32_t> flags; /* the block flags on the device (the only
+                                    block field a rebuild can change that the
+                                    kernel reads: VSA_BLK_RUN) */
 };
 
 /* drop-in scans: results of at most HOST_SORT_MAX records are sorted on the
@@ -798,18 +802,24 @@ void take_feedback(vsa_ctx *c) {
     for (int x = 0; x < 8; x++) mean += nw[x];
     mean /= 8;
     /* the estimate moves every launch; the weights plans are built with
-     * only when it left them by more than 1 % (per-launch noise is ~0.5 %,
-     * and a changed plan means a rebuild, for a prebuilt plan a device
-     * upload: vsa_scan_plan) */
+     * follow it only when it left them by more than 2 % (per-launch noise
+     * is ~1 %), and then at most once per 16 records after the first few:
+     * a changed plan is a rebuild, for a prebuilt plan two uploads queued on
+     * the scan stream (vsa_scan_plan), measured at ~10-20 us of step time
+     * each (profiles/r04r/: applied at every > 1 % move, step - kernel grew
+     * from 14 to 20-28 us) */
     bool moved = false;
     for (int x = 0; x < 8; x++) {
         nw[x] = std::min(1.3f, std::max(0.7f, (float)(nw[x] / mean)));
-        moved = moved || std::fabs(nw[x] - F.wa[x]) > 0.01f;
+        moved = moved || std::fabs(nw[x] - F.wa[x]) > 0.02f;
     }
     memcpy(F.w, nw, sizeof(nw));
     const bool first = !F.known;
     F.known = true;
-    if (!moved && !first) return;
+    F.since++;
+    const bool settling = F.version < 4;
+    if (!first && (!moved || (!settling && F.since < 16))) return;
+    F.since = 0;
     memcpy(F.wa, nw, sizeof(nw));
     for (int b = 0; b < 1024; b++) F.wg[b] = F.wa[F.xcc[b] & 7];
     F.version++;
@@ -3455,6 +3465,8 @@ int vsa_plan_create(vsa_ctx_t *c, const uint8_t *d_data, const uint64_t *offsets
         if (ins[k]) p->in[k].assign(ins[k], ins[k] + nblocks);
     /* room for a rebuilt map: weighted shares can cut a few more pieces */
     p->segblk_cap = std::max<size_t>(1, pl.segblk.size() + pl.segblk.size() / 4 + 4 * 1024);
+    p->flags.resize(nblocks);
+    for (uint32_t i = 0; i < nblocks; i++) p->flags[i] = pl.blocks[i].flags;
     if (hipSetDevice(c->device) != hipSuccess ||
         hipMalloc(&p->d_blocks, nblocks * sizeof(VsaBlock)) != hipSuccess ||
         hipMalloc(&p->d_segblk, p->segblk_cap * sizeof(uint32_t)) != hipSuccess ||
@@ -3518,9 +3530,16 @@ int refresh_plan(vsa_ctx *c, const vsa_db *db, vsa_plan *p) {
         VSA_CHECK(hipHostMalloc(&p->h_stage, bb + p->segblk_cap * sizeof(uint32_t),
                                 hipHostMallocDefault));
     uint8_t *hs = (uint8_t *)p->h_stage;
-    memcpy(hs, pl.blocks.data(), bb);
+    bool blocks_same = p->flags.size() == p->nb;
+    for (uint32_t i = 0; blocks_same && i < p->nb; i++)
+        blocks_same = p->flags[i] == pl.blocks[i].flags;
+    if (!blocks_same) {
+        memcpy(hs, pl.blocks.data(), bb);
+        VSA_CHECK(hipMemcpyAsync(p->d_blocks, hs, bb, hipMemcpyHostToDevice, c->stream));
+        p->flags.resize(p->nb);
+        for (uint32_t i = 0; i < p->nb; i++) p->flags[i] = pl.blocks[i].flags;
+    }
     memcpy(hs + bb, pl.segblk.data(), pl.segblk.size() * sizeof(uint32_t));
-    VSA_CHECK(hipMemcpyAsync(p->d_blocks, hs, bb, hipMemcpyHostToDevice, c->stream));
     VSA_CHECK(hipMemcpyAsync(p->d_segblk, hs + bb, pl.segblk.size() * sizeof(uint32_t),
                              hipMemcpyHostToDevice, c->stream));
     p->segs = pl.nsegs;
