@@ -734,6 +734,28 @@ def test_gpu_split_passes(ctx, nlits, monkeypatch):
             rb[k + 1][:len(s) - cut] = s[cut:]
     want = [oracle.hwlm_exec(blob.ptr, bytes(b), cap=1 << 18)[1] for b in rb]
     assert run_layout_scan(ctx, blob, rb, 3) == want
+    # one stream cut into writes of ragged sizes, each with up to 16 history
+    # bytes before it: the same records as the whole buffer in one block
+    whole = b"".join(bytes(b) for b in rb)
+    cuts = [0]
+    while cuts[-1] < len(whole):
+        cuts.append(min(len(whole), cuts[-1] + rng.choice([1, 7, 100, 1023, 1024, 5000, 40000])))
+    offs = np.array(cuts[:-1], np.uint64)
+    lens = np.diff(np.array(cuts, np.uint64))
+    hl = np.minimum(offs, 16).astype(np.uint64)
+    host = np.frombuffer(whole, np.uint8)
+    d = ctx.malloc(len(host) + 64)
+    try:
+        ctx.h2d(d, host)
+        db = vsa.Database(ctx, blob)
+        k = ctx.scan_blocks_stream(db, d, offs, lens, hl)
+        got = ctx.results(k)
+        db.close()
+    finally:
+        ctx.free(d)
+    st, m = oracle.hwlm_exec(blob.ptr, whole, cap=1 << 20)
+    ends = (got["key"] >> np.uint64(24)).tolist()
+    assert list(zip(ends, got["id"].tolist())) == m
 
 
 def test_gpu_plan_free_after_async_overflow():

@@ -792,11 +792,15 @@ void take_feedback(vsa_ctx *c) {
     tm /= nx;
     float nw[8];
     double mean = 0;
+    /* the launch ran with the applied weights wa: the weights that would
+     * have ended every XCD together are wa * tm / tx; the estimate w moves
+     * half-way toward them (an average over launches, not a walk: basing
+     * it on w itself while wa lagged ran w into the clamps) */
     for (int x = 0; x < 8; x++) {
         nw[x] = F.w[x];
         if (cnt[x]) {
             const double tx = sum[x] / cnt[x];
-            nw[x] = (float)(0.5 * F.w[x] + 0.5 * F.w[x] * tm / tx);
+            nw[x] = (float)(0.5 * F.w[x] + 0.5 * F.wa[x] * tm / tx);
         }
     }
     for (int x = 0; x < 8; x++) mean += nw[x];
