@@ -266,6 +266,13 @@ int vsa_plan_describe(const uint8_t *d_data, const uint64_t *offsets, const uint
                       uint32_t nblocks, uint32_t num_cus, uint32_t ns, uint32_t *words,
                       uint64_t cap, uint64_t *nsegs, uint32_t *grid,
                       const float *wg_weights);
+
+/* Host-only (tests): the schedule feedback's per-XCD weight updates over
+ * `launches` synthetic launches of `grid` workgroups (b on XCD b % 8) whose
+ * XCDs run at rate[0..7], with relative timing noise `jitter`; the applied
+ * weights go to w_out[8], the return value counts their changes. */
+int vsa_feedback_simulate(const double *rate, uint32_t grid, uint32_t launches, double jitter,
+                          float *w_out);
 int vsa_plan_create(vsa_ctx_t *ctx, const uint8_t *d_data, const uint64_t *offsets,
                     const uint64_t *lens, const uint64_t *starts, const uint64_t *hlens,
                     const uint64_t *report_lo, uint32_t nblocks, vsa_plan_t **plan);

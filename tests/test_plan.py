@@ -178,3 +178,39 @@ def test_plan_feedback_weights(mib, nblk):
     for b in range(grid):
         want = T * weights[b] / wsum
         assert abs(per[b] - want) <= 1024 * nblk + 4096 + 1024, (b, per[b], want)
+
+
+lib.vsa_feedback_simulate.restype = ctypes.c_int
+lib.vsa_feedback_simulate.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_double, ctypes.c_void_p]
+
+
+def simulate_feedback(rates, launches, jitter, grid=256):
+    r = np.ascontiguousarray(rates, np.float64)
+    w = np.zeros(8, np.float32)
+    n = lib.vsa_feedback_simulate(r.ctypes.data, grid, launches, jitter, w.ctypes.data)
+    assert n >= 0
+    return w, n
+
+
+@pytest.mark.parametrize("rates", [
+    [1, 1, 0.9, 0.9, 1.1, 1.1, 0.95, 1.05],      # compute-bound FDR: a few % apart
+    [1.25, 1.25, 1.0, 1.0, 1.0, 1.0, 1.2, 1.2],  # streaming noodle: 25 % apart
+])
+def test_feedback_converges_to_the_xcd_rates(rates):
+    """Schedule feedback (runtime.hip feedback_update): with XCDs running at
+    fixed rates and 1 % timing noise, the applied weights settle to the
+    rates (the shares that end every XCD together) within 3 %, with a
+    bounded number of changes (each is a plan rebuild / upload)."""
+    w, n = simulate_feedback(rates, 300, 0.01)
+    want = np.array(rates) / np.mean(rates)
+    assert np.max(np.abs(w - want)) < 0.03, (w, want)
+    assert n <= 24, n
+
+
+def test_feedback_equal_rates_do_not_churn():
+    """Equal XCDs and 1 % noise: the weights stay at 1 and the plans are
+    rebuilt at most a couple of times (not on every launch)."""
+    w, n = simulate_feedback([1.0] * 8, 300, 0.01)
+    assert np.max(np.abs(w - 1.0)) < 0.03, w
+    assert n <= 3, n

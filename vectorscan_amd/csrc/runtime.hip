@@ -758,17 +758,13 @@ uint64_t fb_key_of(const vsa_ctx *c, const vsa_db *db) {
     return ((uint64_t)si << 32) | c->fb.set[si].version;
 }
 
-void take_feedback(vsa_ctx *c) {
-    const int si = c->fb.armed;
-    if (si < 0) return;
-    c->fb.armed = -1;
-    vsa_ctx::FbSet &F = c->fb.set[si];
-    const uint32_t G = c->fb.grid;
-    const volatile unsigned long long *h = c->fb.h;
+/* One feedback record (h: [b] = xcc << 60 | end, [G + b] = entry, 100 MHz)
+ * into a weight set; false if the record is incomplete. */
+bool feedback_update(vsa_ctx::FbSet &F, const volatile unsigned long long *h, uint32_t G) {
     const unsigned long long M60 = (1ULL << 60) - 1;
     unsigned long long t0 = ~0ULL;
     for (uint32_t b = 0; b < G; b++) {
-        if (!h[b] || !h[G + b]) return; /* a workgroup without a record */
+        if (!h[b] || !h[G + b]) return false; /* a workgroup without a record */
         t0 = std::min(t0, (unsigned long long)h[G + b]);
     }
     double sum[8] = {0}, cnt[8] = {0};
@@ -776,7 +772,7 @@ void take_feedback(vsa_ctx *c) {
     for (uint32_t b = 0; b < G; b++) {
         const uint32_t x = (uint32_t)(h[b] >> 60) & 7u;
         const unsigned long long e = h[b] & M60;
-        if (e <= t0) return;
+        if (e <= t0) return false;
         xs[b] = (uint8_t)x;
         sum[x] += (double)(e - t0);
         cnt[x] += 1;
@@ -788,14 +784,14 @@ void take_feedback(vsa_ctx *c) {
             tm += sum[x] / cnt[x];
             nx += 1;
         }
-    if (nx < 2) return;
+    if (nx < 2) return false;
     tm /= nx;
     float nw[8];
     double mean = 0;
     /* the launch ran with the applied weights wa: the weights that would
      * have ended every XCD together are wa * tm / tx; the estimate w moves
      * half-way toward them (an average over launches, not a walk: basing
-     * it on w itself while wa lagged ran w into the clamps) */
+     * it on w itself while wa lagged ran w into the clamps, r04s) */
     for (int x = 0; x < 8; x++) {
         nw[x] = F.w[x];
         if (cnt[x]) {
@@ -808,7 +804,7 @@ void take_feedback(vsa_ctx *c) {
     /* the estimate moves every launch; the weights plans are built with
      * follow it only when it left them by more than 2 % (per-launch noise
      * is ~1 %), and then at most once per 16 records after the first few:
-     * a changed plan is a rebuild, for a prebuilt plan two uploads queued on
+     * a changed plan is a rebuild, for a prebuilt plan an upload queued on
      * the scan stream (vsa_scan_plan), measured at ~10-20 us of step time
      * each (profiles/r04r/: applied at every > 1 % move, step - kernel grew
      * from 14 to 20-28 us) */
@@ -822,11 +818,19 @@ void take_feedback(vsa_ctx *c) {
     F.known = true;
     F.since++;
     const bool settling = F.version < 4;
-    if (!first && (!moved || (!settling && F.since < 16))) return;
+    if (!first && (!moved || (!settling && F.since < 16))) return true;
     F.since = 0;
     memcpy(F.wa, nw, sizeof(nw));
     for (int b = 0; b < 1024; b++) F.wg[b] = F.wa[F.xcc[b] & 7];
     F.version++;
+    return true;
+}
+
+void take_feedback(vsa_ctx *c) {
+    const int si = c->fb.armed;
+    if (si < 0) return;
+    c->fb.armed = -1;
+    (void)feedback_update(c->fb.set[si], c->fb.h, c->fb.grid);
 }
 
 /* diagnostic per-wave log (vsa_set_wave_log; the kernel writes it under
@@ -3443,6 +3447,44 @@ int vsa_plan_describe(const uint8_t *d_data, const uint64_t *offsets, const uint
     if (nsegs) *nsegs = pl.nsegs;
     if (grid) *grid = pl.grid;
     return (int)pl.segblk.size();
+}
+
+/* Host-only (tests): the schedule feedback's weight updates over `launches`
+ * synthetic launches of `grid` workgroups (workgroup b on XCD b % 8) whose
+ * XCDs stream at rate[x] (any unit; a workgroup's time = its share / its
+ * XCD's rate, plus noise x jitter), each workgroup's share in proportion to
+ * the applied weights.  Writes the applied weights to w_out[8]; returns how
+ * many times they changed (plan rebuilds). */
+int vsa_feedback_simulate(const double *rate, uint32_t grid, uint32_t launches, double jitter,
+                          float *w_out) {
+    if (!rate || !w_out || grid < 8 || grid > 1024) return VSA_E_INVALID;
+    vsa_ctx::FbSet F;
+    for (int b = 0; b < 1024; b++) {
+        F.xcc[b] = (uint8_t)(b & 7);
+        F.wg[b] = 1.0f;
+    }
+    std::vector<unsigned long long> h(2 * grid);
+    uint64_t rs = 0x9e3779b97f4a7c15ULL;
+    auto rnd = [&]() {
+        rs ^= rs << 13;
+        rs ^= rs >> 7;
+        rs ^= rs << 17;
+        return (double)(rs >> 11) / 9007199254740992.0 * 2.0 - 1.0;
+    };
+    uint32_t v0 = F.version;
+    for (uint32_t l = 0; l < launches; l++) {
+        double tw = 0;
+        for (uint32_t b = 0; b < grid; b++) tw += F.wg[b];
+        for (uint32_t b = 0; b < grid; b++) {
+            const double share = F.wg[b] / tw;
+            const double t = share / rate[b & 7] * (1.0 + jitter * rnd());
+            h[grid + b] = 1000;
+            h[b] = ((unsigned long long)(b & 7) << 60) | (1000 + (unsigned long long)(t * 1e9));
+        }
+        (void)feedback_update(F, h.data(), grid);
+    }
+    memcpy(w_out, F.wa, sizeof(F.wa));
+    return (int)(F.version - v0);
 }
 
 int vsa_plan_create(vsa_ctx_t *c, const uint8_t *d_data, const uint64_t *offsets,
