@@ -15,14 +15,21 @@ import vectorscan_amd as vsa  # noqa: E402
 dev = torch.device("cuda", 0)
 ctx = vsa.Context(0)
 # WORKLOAD=noodle: cfg 1's single literal (noodle engine); else cfg 4's set
+# WORKLOAD=teddy: cfg 3's 48 literals (seed 55, Teddy), planted every 4 KiB
+plant = 64 << 10
+hint = -1
 if os.environ.get("WORKLOAD") == "noodle":
     lits = [vsa.HwlmLiteral(b"abcde", False, 1)]
+elif os.environ.get("WORKLOAD") == "teddy":
+    import tools.bench_configs as bc
+    lits = bc.lits_printable(48, 55)
+    plant = 4 << 10
 else:
     lits = bench.make_literals(5000, seed=12)
-db = vsa.Database(ctx, vsa.hwlm_build(lits))
+db = vsa.Database(ctx, vsa.hwlm_build(lits, engine_hint=hint))
 total = int(float(os.environ.get("GIB", "4")) * (1 << 30))
 bl = total // 4
-data = bench.make_corpus_device(torch, 0, total, total, lits, 5, 64 << 10, dev)
+data = bench.make_corpus_device(torch, 0, total, total, lits, 5, plant, dev)
 log = torch.zeros(1024 * 16 * 8, dtype=torch.int64, device=dev)
 vsa.lib.vsa_set_wave_log.argtypes = [ctypes.c_void_p]
 vsa.lib.vsa_set_wave_log(log.data_ptr())
