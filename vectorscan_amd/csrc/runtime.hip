@@ -71,7 +71,7 @@ __global__ void vsa_pair_scan(VsaPairParams P);
     do {                                                                      \
         hipError_t e_ = (x);                                                  \
         if (e_ != hipSuccess) {                                               \
-            if (getenv("VSA_DEBUG"))                                          \
+            if (!getenv("VSA_QUIET"))                                         \
                 fprintf(stderr, "vsa: %s failed: %s (%s:%d)\n", #x,           \
                         hipGetErrorString(e_), __FILE__, __LINE__);           \
             return VSA_E_DEVICE;                                              \
