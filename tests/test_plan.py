@@ -214,3 +214,31 @@ def test_feedback_equal_rates_do_not_churn():
     w, n = simulate_feedback([1.0] * 8, 300, 0.01)
     assert np.max(np.abs(w - 1.0)) < 0.03, w
     assert n <= 3, n
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_plan_random_layouts_weighted(seed):
+    """Weighted shares (schedule feedback: weights learned on a full-size
+    launch apply to every later plan of the context, whatever its size or
+    layout): ragged, packed, back-to-back and started blocks are still
+    covered exactly once and in order, and every workgroup's share follows
+    its weight within a packed group or a sliver."""
+    rng = random.Random(100 + seed)
+    offs, lens, starts = [], [], []
+    pos = 0
+    for _ in range(rng.choice([3, 40, 300, 2000])):
+        kind = rng.random()
+        ln = (rng.randint(0, 600) if kind < 0.3 else rng.randint(1000, 40000) if kind < 0.8
+              else rng.randint(1 << 20, 8 << 20))
+        pos += rng.choice([0, 0, 0, rng.randint(1, 5000)])
+        offs.append(pos)
+        lens.append(ln)
+        starts.append(rng.choice([0, 0, 0, rng.randint(0, ln)]) if ln else 0)
+        pos += ln
+    weights = [rng.uniform(0.7, 1.3) for _ in range(256)]
+    desc, bounds, grid, per, T, seg_bytes = check(offs, lens, starts, base=0x10000 +
+                                                  rng.randint(0, 15), weights=weights)
+    if grid:
+        wsum = sum(weights[:grid])
+        for b in range(grid):
+            assert abs(per[b] - T * weights[b] / wsum) <= max(seg_bytes) + 8192, (b, per[b])

@@ -595,6 +595,9 @@ int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds) {
      * 1 KiB drop-in, profiles/r03_dropin_waves.txt) */
     VsaLitParams Q = P;
     if (Q.dynamic == 1 && Q.nsegs <= (uint64_t)grid * ns) Q.dynamic = 0;
+    /* the check below is for this launch: a stale non-fatal error of an
+     * earlier call (the thread's last error) must not fail it */
+    (void)hipGetLastError();
     hipLaunchKernelGGL(fn, dim3(grid), dim3(LIT_THREADS), lds, c->stream, Q);
     VSA_CHECK(hipGetLastError());
     return VSA_OK;
@@ -685,6 +688,7 @@ int queue_bin_sort(vsa_ctx *c, hipStream_t st) {
     if (!old_sort()) {
         const uint32_t par = c->bin_par;
         const bool fbd = c->fb.armed >= 0 && c->fb.dev;
+        (void)hipGetLastError(); /* checks below are for this launch */
         hipLaunchKernelGGL(vsa_bin_finish, dim3(VSA_SORT_BINS / 64), dim3(1024), 0, st,
                            bin_counts_of(c, par), bin_counts_of(c, par ^ 1u), w.d_bslots,
                            w.d_keys[0], w.d_ids[0], w.d_keys[1], w.d_ids[1], (uint64_t)w.out_cap,
@@ -698,6 +702,7 @@ int queue_bin_sort(vsa_ctx *c, hipStream_t st) {
     }
     uint32_t *counts = w.d_bins, *cursor = w.d_bins + VSA_SORT_BINS;
     const uint32_t shift = bin_shift_for(c->launch.end_bits);
+    (void)hipGetLastError(); /* the check below is for this chain of launches */
     if (sep_hist())
         hipLaunchKernelGGL(vsa_bin_hist, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, st,
                            w.d_keys[0], (const uint64_t *)w.d_counters, (uint64_t)w.out_cap,
@@ -889,6 +894,7 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
     int r = launch_scan_kernel(c, db, d_data, nb, nsegs, seg_bytes);
     if (r != VSA_OK) return r;
     if (small) {
+        (void)hipGetLastError(); /* checks below are for this launch */
         hipLaunchKernelGGL(vsa_publish, dim3(1), dim3(256), 0, c->stream, c->ws.d_counters,
                            c->ws.d_pub, (unsigned long long)++c->pub_seq, 144u,
                            (const uint64_t *)c->ws.d_keys[0], (const uint32_t *)c->ws.d_ids[0],
@@ -1148,6 +1154,10 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     if (!(flags & SCAN_HOST_SORT_SMALL)) {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_kernel_ms = ms;
+        /* a not-yet-observed event (the published path completes on the
+         * publish, not on ev1) must not leave hipErrorNotReady as the
+         * thread's last error for the next launch check */
+        (void)hipGetLastError();
     }
     if (n > w.out_cap) return VSA_E_OVERFLOW;
     c->cur = 0;
@@ -1929,6 +1939,7 @@ int64_t pair_host(const uint8_t *lo1, const uint8_t *hi1, const uint8_t *lo2,
     P.first = first;
     uint64_t want = (len + 255) / 256;
     uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * 4));
+    (void)hipGetLastError(); /* checks below are for this launch */
     hipLaunchKernelGGL(vsa_pair_scan, dim3(grid), dim3(256), 0, c->stream, P);
     if (hipGetLastError() != hipSuccess) return -2;
     if (hipMemcpyAsync(w.h_counters + PAIR_BASE, first, 48 * 8, hipMemcpyDeviceToHost,
@@ -2624,6 +2635,7 @@ int vsa_scan_pack(vsa_ctx_t *c, void *d_dst, uint64_t cap) {
         /* the async binned scan's sorted records (buffer 1) and the counters
          * vsa_publish keeps on the device: queued behind it, no wait */
         if (int r0 = join_sort(c)) return r0;
+        (void)hipGetLastError(); /* checks below are for this launch */
         hipLaunchKernelGGL(vsa_pack, dim3(grid), dim3(256), 0, c->stream,
                            (const unsigned long long *)c->ws.d_counters + 144,
                            (uint64_t)c->ws.out_cap, (const uint64_t *)c->ws.d_keys[1],
@@ -2637,6 +2649,7 @@ int vsa_scan_pack(vsa_ctx_t *c, void *d_dst, uint64_t cap) {
     unsigned long long *save = c->ws.d_counters + 144;
     unsigned long long hv[16] = {c->last_n, 0};
     VSA_CHECK(hipMemcpyAsync(save, hv, sizeof(hv), hipMemcpyHostToDevice, c->stream));
+    (void)hipGetLastError(); /* checks below are for this launch */
     hipLaunchKernelGGL(vsa_pack, dim3(grid), dim3(256), 0, c->stream,
                        (const unsigned long long *)save, (uint64_t)c->ws.out_cap,
                        (const uint64_t *)c->ws.d_keys[c->cur], (const uint32_t *)c->ws.d_ids[c->cur],
@@ -2791,12 +2804,14 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
         /* (an asynchronous literal scan still in flight keeps its record) */
         if (cls_fb && c->fb.armed < 0) arm_feedback(c, 2, lgrid, len, false);
         P.wg_time = c->fb.armed == 2 ? c->fb.d : nullptr;
+        (void)hipGetLastError(); /* checks below are for this launch */
         hipLaunchKernelGGL(vsa_class_scan_lut, dim3(lgrid), dim3(1024), 0, c->stream, P, wspan);
     } else {
         uint64_t chunks = (len + 15) / 16;
         uint64_t want = (chunks + 255) / 256;
         uint64_t cap = (uint64_t)c->num_cus * 8;
         uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
+        (void)hipGetLastError(); /* checks below are for this launch */
         hipLaunchKernelGGL(vsa_class_scan, dim3(grid), dim3(256), 0, c->stream, P);
     }
     VSA_CHECK(hipGetLastError());
@@ -2808,6 +2823,10 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
     {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_kernel_ms = ms;
+        /* a not-yet-observed event (the published path completes on the
+         * publish, not on ev1) must not leave hipErrorNotReady as the
+         * thread's last error for the next launch check */
+        (void)hipGetLastError();
     }
     const unsigned long long *h = w.h_counters + CLASS_BASE;
     uint64_t f = ~0ULL, l = 0, n = 0;
