@@ -2060,6 +2060,7 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (c->sort_stream) (void)hipStreamDestroy(c->sort_stream);
     if (t_ctx == c) t_ctx = nullptr;
     delete c; /* drops its hold on the stream */
+    (void)hipGetLastError(); /* ignored statuses do not outlive the call */
     return VSA_OK;
 }
 
@@ -2477,6 +2478,9 @@ int vsa_db_free(vsa_db_t *db) {
         }
     }
     delete db;
+    /* the frees' statuses are ignored: none stays the thread's last error
+     * (a later launch check would read it) */
+    (void)hipGetLastError();
     return VSA_OK;
 }
 
@@ -3562,6 +3566,7 @@ int vsa_plan_free(vsa_plan_t *p) {
     if (p->d_segblk) (void)hipFree(p->d_segblk);
     if (p->h_stage) (void)hipHostFree(p->h_stage);
     delete p;
+    (void)hipGetLastError(); /* ignored statuses do not outlive the call */
     return r;
 }
 
