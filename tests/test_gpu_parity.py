@@ -744,18 +744,20 @@ def test_gpu_split_passes(ctx, nlits, monkeypatch):
     lens = np.diff(np.array(cuts, np.uint64))
     hl = np.minimum(offs, 16).astype(np.uint64)
     host = np.frombuffer(whole, np.uint8)
+    st, m = oracle.hwlm_exec(blob.ptr, whole, cap=1 << 22)
     d = ctx.malloc(len(host) + 64)
     try:
         ctx.h2d(d, host)
-        db = vsa.Database(ctx, blob)
-        k = ctx.scan_blocks_stream(db, d, offs, lens, hl)
-        got = ctx.results(k)
-        db.close()
+        for split in ("0", "1"):
+            monkeypatch.setenv("VSA_SPLIT", split)
+            db = vsa.Database(ctx, blob)
+            k = ctx.scan_blocks_stream(db, d, offs, lens, hl)
+            got = ctx.results(k)
+            db.close()
+            ends = (got["key"] >> np.uint64(24)).tolist()
+            assert list(zip(ends, got["id"].tolist())) == m, split
     finally:
         ctx.free(d)
-    st, m = oracle.hwlm_exec(blob.ptr, whole, cap=1 << 20)
-    ends = (got["key"] >> np.uint64(24)).tolist()
-    assert list(zip(ends, got["id"].tolist())) == m
 
 
 def test_gpu_plan_free_after_async_overflow():

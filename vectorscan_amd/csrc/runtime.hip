@@ -595,6 +595,15 @@ int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds) {
      * 1 KiB drop-in, profiles/r03_dropin_waves.txt) */
     VsaLitParams Q = P;
     if (Q.dynamic == 1 && Q.nsegs <= (uint64_t)grid * ns) Q.dynamic = 0;
+    /* diagnostic (VSA_PRINT_LAUNCH=1): every literal-scan launch's shape */
+    static const bool print_launch = getenv("VSA_PRINT_LAUNCH") != nullptr;
+    if (print_launch)
+        fprintf(stderr,
+                "vsa launch: mode %d xp %d grid %u nsegs %llu nblocks %u lds %zu qcap %u nconf %u "
+                "dynamic %u end_par %u data %p blocks %p seg_desc %p out_cap %llu bins %p\n",
+                MODE, (int)XP, grid, (unsigned long long)P.nsegs, P.nblocks, lds, P.qcap, P.nconf,
+                P.dynamic, P.end_par, (const void *)P.data, (const void *)P.blocks,
+                (const void *)P.seg_desc, (unsigned long long)P.out_cap, (void *)P.bin_counts);
     /* the check below is for this launch: a stale non-fatal error of an
      * earlier call (the thread's last error) must not fail it */
     (void)hipGetLastError();
