@@ -25,7 +25,7 @@ struct VsaBlock {
                            scanned from its own first byte, stripe.py) */
     uint64_t hlen;      /* streaming: len_history (confirm overhang bound,
                            fdr_confirm_runtime.h:79-88); 0 = block mode */
-    uint32_t hist;      /* bytes readable before base (16 when streaming) */
+    uint32_t hist;      /* bytes readable before base (min(hlen, 16)) */
     uint32_t flags;     /* VSA_BLK_* */
 };
 

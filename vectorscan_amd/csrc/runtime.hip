@@ -1240,7 +1240,11 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
         b.seg_first = 0;
         const int64_t len = (int64_t)b.len, st = (int64_t)b.start;
         b.hlen = hlens ? hlens[i] : 0;
-        b.hist = b.hlen ? 16 : 0;
+        /* only the history is readable before the block: a write at offset
+         * 1 with 1 history byte must not load the 15 bytes before the
+         * buffer (the prologue's masked loads reach base - 8; a buffer at the
+         * start of a mapping faulted, test_gpu_split_passes' stream part) */
+        b.hist = (uint32_t)std::min<uint64_t>(b.hlen, 16);
         b.flags = b.hlen ? VSA_BLK_STREAM : 0;
         /* prepareZones fdr.c:625-659: short zone anchors at len - 16; with
          * history the look-back also covers start - 1 (getInitState) */
