@@ -22,12 +22,15 @@ sizes = [int(x) for x in (sys.argv[1:] or ["20000"])]
 settings = [{}, {"VSA_DEBUG_FLAGS": "8", "VSA_NCONF": "2", "VSA_XP": "1"},
             {"VSA_NCONF": "1", "VSA_XP": "1"}, {"VSA_NCONF": "2", "VSA_XP": "1"},
             {"VSA_NCONF": "3", "VSA_XP": "1"}, {"VSA_NCONF": "2", "VSA_XP": "0"}]
+rounds = 2
+if os.environ.get("XP_COST_QUICK"):  # the default setting only, one round (library A/B)
+    settings, rounds = [{}], 1
 for nl in sizes:
     lits = bench.make_literals(nl, seed=12)
     blob = vsa.hwlm_build(lits)
     data = bench.make_corpus_device(torch, 0, n, n, lits, 5, 64 << 10, torch.device("cuda", 0))
     torch.cuda.synchronize()
-    for rnd in range(2):
+    for rnd in range(rounds):
         for st in settings:
             for k, v in st.items():
                 os.environ[k] = v
@@ -37,7 +40,8 @@ for nl in sizes:
             for i in range(12):
                 m = ctx.scan_blocks(db, data.data_ptr(), [0, bl, 2 * bl, 3 * bl], [bl] * 4)
                 ks.append(ctx.kernel_ms())
-            print(json.dumps({"lits": nl, "setting": st, "split": db.split, "round": rnd,
+            print(json.dumps({"lits": nl, "lib": os.environ.get("VSA_LIB_VARIANT", "default"),
+                              "setting": st, "split": db.split, "round": rnd,
                               "kernel_ms": round(float(np.mean(ks[4:])), 4),
                               "candidates": int(ctx.candidates()), "matches": int(m)}),
                   flush=True)

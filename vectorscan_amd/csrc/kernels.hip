@@ -917,24 +917,25 @@ __device__ __forceinline__ void xp_push(const VsaLitParams &P, const ConfLds &cl
     const u64 p0 = meta & ENT_P0_MASK;
     const u64 blk4 = (meta >> ENT_BLK_SHIFT) << 4;
     const u32 lane = lane_id();
+    /* the 128 candidate bits as two 64-bit halves: bit b is end b >> 3,
+     * bucket b & 7 (byte i of c[w] = end 4 w + i), so a round's lowest bit
+     * is one 64-bit find-first and its clear one 64-bit a & (a - 1), with no
+     * per-word select */
+    u64 lo = ((u64)c[1] << 32) | c[0];
+    u64 hi = ((u64)c[3] << 32) | c[2];
     for (;;) {
-        u32 word = 0, bits = c[0];
-#pragma unroll
-        for (int k = 1; k < 4; k++) {
-            const bool take = bits == 0;
-            bits = take ? c[k] : bits;
-            word = take ? (u32)k : word;
-        }
-        const bool have = bits != 0;
+        const bool have = (lo | hi) != 0;
         const u64 B = __ballot(have);
         if (B == 0) break;
         const u32 cnt = (u32)__popcll(B);
         if (st.xn + cnt > WAVE) xp_flush(P, cl, L, st);
-        const u32 bit = __ffs(bits) - 1;
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            if (have && word == (u32)k) c[k] &= c[k] - 1;
-        const u32 jj = 4 * word + (bit >> 3), bb = bit & 7;
+        const bool inlo = lo != 0;
+        const u64 cur = inlo ? lo : hi;
+        const u32 b = (inlo ? 0u : 64u) + (u32)__builtin_ctzll(cur | (1ull << 63));
+        const u64 nxt = cur & (cur - 1);
+        lo = inlo ? nxt : lo;
+        hi = inlo ? hi : nxt;
+        const u32 jj = b >> 3, bb = b & 7;
         /* key = bytes [jj - 7, jj] = byte offset o = jj + 1 .. jj + 8 of D:
          * dwords a, a + 1, a + 2 shifted by o & 3 */
         const u32 o = jj + 1, a = o >> 2, sh = o & 3u;
