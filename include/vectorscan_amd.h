@@ -242,8 +242,8 @@ int vsa_scan_blocks_ex(vsa_ctx_t *ctx, const vsa_db_t *db, const uint8_t *d_data
                        const uint64_t *starts, const uint64_t *report_lo,
                        uint32_t nblocks, uint32_t flags, uint64_t *n_matches);
 /* As vsa_scan_blocks, each block a streaming call: hlens[i] bytes of
- * history sit immediately before offsets[i] in d_data (at least 16 bytes
- * before each block with hlens[i] > 0 must be readable); hlens[i] = 0 is a
+ * history sit immediately before offsets[i] in d_data (only those bytes are
+ * read before the block, at most 16 of them); hlens[i] = 0 is a
  * block-mode scan.  A stream cut into consecutive chunks is scanned as one
  * launch this way. */
 int vsa_scan_blocks_stream(vsa_ctx_t *ctx, const vsa_db_t *db, const uint8_t *d_data,
