@@ -1340,7 +1340,11 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
          * than half the current size are packed whole as before. */
         uint64_t T = 0;
         for (int64_t sp : live) T += (uint64_t)sp;
-        static const uint64_t K = std::max(1, env_int("VSA_WG_K", 2));
+        /* K = 1: packed groups of small blocks up to a wave's share of the
+         * list (~1 group per wave); K = 2 (round 4 until r04af) measured
+         * 4-13 % slower on 2-64 KiB blocks at 128 MiB-1 GiB and no better
+         * at 32 MiB (profiles/r04af_wg_k.txt, r04ag_wg_k_small.txt) */
+        static const uint64_t K = std::max(1, env_int("VSA_WG_K", 1));
         static const uint64_t smax = (uint64_t)std::max(1, env_int("VSA_WG_MAX_KIB", 256)) << 10;
         static const uint64_t smin0 = (uint64_t)std::max(1, env_int("VSA_WG_MIN_KIB", 4)) << 10;
         const uint64_t pool_pm = (uint64_t)std::min(900, std::max(0, env_int("VSA_POOL_PM", 0)));
