@@ -121,6 +121,17 @@ def test_plan_large_blocks_equal_shares(mib, nblk, pool):
     assert share - min(per) <= 1024 * nblk + 4096 + 1024, (min(per), share)
 
 
+@pytest.mark.parametrize("mib,kib", [(256, 1), (64, 1), (512, 2), (256, 3)])
+def test_plan_back_to_back_groups_stay_runs(mib, kib):
+    """Back-to-back blocks of >= 1 KiB scanned from byte 0 can be runs
+    (kernels.h VSA_RUN_MAX, at most 128 blocks): a packed group of them is cut
+    at 128 blocks, not at the 255 of a plain group (runtime.hip build_plan)."""
+    n = (mib << 20) // (kib << 10)
+    desc, bounds, grid, per, T, segb = check([i * (kib << 10) for i in range(n)], [kib << 10] * n)
+    cnts = [info >> 24 for info in desc[:, 0].tolist() if info >> 24]
+    assert cnts and max(cnts) <= 128, max(cnts)
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_plan_random_layouts(seed, pool):
     rng = random.Random(seed)

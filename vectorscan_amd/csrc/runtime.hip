@@ -1266,6 +1266,7 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
     const bool group = !getenv("VSA_NO_GROUPS");
     const bool no_runs = getenv("VSA_NO_RUNS") != nullptr;
     uint32_t g_first = 0, g_n = 0;
+    bool g_run = false; /* the open group can still be a run (wgl lists) */
     int64_t g_span = 0;
     pl.nsegs = 0;
     pl.grid = 0;
@@ -1396,10 +1397,20 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
             }
             uint64_t sz = size_now();
             if (group && 2 * (uint64_t)sp <= sz) {
-                if (g_n && (g_span + sp > (int64_t)sz || g_n == SEG_GROUP_MAX)) {
+                /* a group that can still be a run (runnable) is cut at
+                 * VSA_RUN_MAX blocks, so back-to-back 1 KiB blocks scan as
+                 * runs of 128 rather than as groups of 255 single blocks */
+                const VsaBlock &bi = out[i];
+                const bool elig = !no_runs && !bi.start && !bi.rlo && bi.len >= VSA_RUN_MIN_LEN;
+                const bool cont = g_n && g_run && elig &&
+                                  bi.base == out[i - 1].base + out[i - 1].len;
+                const uint32_t gmax = cont ? VSA_RUN_MAX : SEG_GROUP_MAX;
+                if (g_n && (g_span + sp > (int64_t)sz || g_n >= gmax)) {
                     flush();
                     advance();
                 }
+                if (!g_n) g_run = elig;
+                else g_run = g_run && elig && bi.base == out[i - 1].base + out[i - 1].len;
                 if (!g_n) g_first = i;
                 out[i].seg_first = pl.nsegs;
                 g_n++;
