@@ -324,7 +324,7 @@ struct vsa_db {
      * a db's launch plans change at most twice. */
     mutable std::atomic<uint32_t> nconf{1};
     /* scanner expansion (use_xp): on once a representative launch measured
-     * more than 1e-3 confirm candidates per byte; only turns on */
+     * more than 4e-4 confirm candidates per byte; only turns on */
     mutable std::atomic<bool> xp{false};
 };
 
@@ -338,15 +338,18 @@ static uint32_t nconf_for_rate(double rate) {
      * 20k 2.47 / 2.32 / 2.70 ms at 1 / 2 / 3 waves, 50k 62.9 / 34.1 / 30.6
      * ms (profiles/r03_xp.jsonl; 4 fits no better than 3 beside a
      * domain-14 table) */
-    /* Round 4, with scanner expansion on from 1e-3 (xp_for_rate), the
+    /* Round 4, with scanner expansion on from 4e-4 (1e-3 until late round 4) (xp_for_rate), the
      * confirm waves only confirm: 20k literals (2.7e-3) 1.80 / 1.85 / 1.99
      * ms at 1 / 2 / 3 waves, 50k in split passes (8.9e-3 per pass) 6.22 /
      * 5.34 / 6.13 (profiles/r04j_xp_cost.jsonl) */
     return rate > 0.05 ? 3u : rate > 5e-3 ? 2u : 1u;
 }
 
-/* scanner expansion past this confirm-candidate rate (use_xp) */
-static bool xp_for_rate(double rate) { return rate > 1e-3; }
+/* scanner expansion past this confirm-candidate rate (use_xp): 4 GiB
+ * cfg-4 corpus, one confirm wave, expansion off / on
+ * (profiles/r04al_xp_10k.jsonl): 10k literals (1.4e-4) 1.18 / 1.27 ms, 15k
+ * (6.6e-4) 1.51-1.53 / 1.47 ms, 20k (2.7e-3) 2.49 / 1.80 (r04j) */
+static bool xp_for_rate(double rate) { return rate > 4e-4; }
 
 /* VECTORSIZE of the reference build emulated where results depend on it:
  * shuftiDoubleExec's per-block lanes and the Teddy loop shape of the flood
@@ -643,7 +646,7 @@ uint32_t launch_nconf(const vsa_db *db, size_t tab, size_t ent, size_t budget) {
 /* Scanner expansion (kernels.hip xp_push) for large literal sets: the
  * scanning waves expand candidate bits and apply the slot-bitmap prefilter,
  * the confirm waves only confirm.  On once the db's measured candidate rate
- * passed 1e-3 per byte (xp_for_rate); VSA_XP=0 / 1 forces it off / on. */
+ * passed 4e-4 per byte (xp_for_rate); VSA_XP=0 / 1 forces it off / on. */
 bool use_xp(const vsa_db *db) {
     if (const char *e = getenv("VSA_XP")) return atoi(e) != 0;
     return db->xp.load(std::memory_order_relaxed);
