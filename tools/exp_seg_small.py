@@ -22,10 +22,12 @@ data = bench.make_corpus_device(torch, 0, total, total, lits, 5, 64 << 10, dev)
 offs = [i * bl for i in range(4)]
 torch.cuda.synchronize()
 ks = []
-for i in range(60):
+settle = int(os.environ.get("SETTLE", "20"))  # untimed launches (GPU clock ramp)
+for i in range(settle + 40):
     n = ctx.scan_blocks(db, data.data_ptr(), offs, [bl] * 4)
-    if i >= 20:
+    if i >= settle:
         ks.append(ctx.kernel_ms())
-print("MiB %d seg_kb %s kernel median %.4f ms min %.4f matches %d" % (
-    mib, os.environ.get("VSA_SEG_KB", "auto"), float(np.median(ks)), min(ks), n),
+print("MiB %d seg_kb %s steal %s steal_w %s kernel median %.4f ms min %.4f matches %d" % (
+    mib, os.environ.get("VSA_SEG_KB", "auto"), os.environ.get("VSA_STEAL", "-"),
+    os.environ.get("VSA_STEAL_W", "-"), float(np.median(ks)), min(ks), n),
     flush=True)
