@@ -582,7 +582,78 @@ def fdr_flood_cases():
     return out
 
 
+# ------------------------------------------------------- hs behaviour
+def hs_behaviour_cases():
+    """unit/hyperscan/behaviour.cpp, the rows whose pattern is a pure
+    literal (no regex syntax, so hs_compile builds the same database as
+    hs_compile_lit_multi of the literal with the same flags).  Inputs are
+    the tests' construction rules (a zero-filled block with a pre-block and
+    a post-block, runs of 'a', the corpus strings) with every size spelled
+    out; expected values are the tests' own assertions.  Rows with regex
+    syntax (foobar\\z, hatstand.*teakettle, ...) are out of scope: the
+    pure-literal API refuses them."""
+    HS_SCAN_TERMINATED = -3
+    CASELESS = 1
+    gig = [  # behaviour.cpp:301-303 (the pure-literal rows of gigTests)
+        {"pattern": "foobar", "flags": 0, "pre": "flibble", "post": "foobar"},
+        {"pattern": "longliteralislongerthanlong", "flags": 0, "pre": "precursor",
+         "post": "longliteralislongerthanlong"},
+    ]
+    kib = [1, 4, 8, 16, 32, 64, 128, 256, 512, 1024]  # :261-265
+    block = []
+    for g in gig:
+        # allocAndScanBlock :211-235: calloc(len), pre at 0, post at
+        # len - strlen(post), hs_scan -> HS_SUCCESS and lastMatchTo == len;
+        # three lengths per size :284-292
+        lens = []
+        for k in kib:
+            b = k * 1024
+            lens += [b, b + 4, b + len(g["post"])]
+        block.append(dict(g, src="behaviour.cpp:241-299 (allocAndScanBlock :211-235)",
+                          lens=lens, expected_status=0, expected_last_to=lens))
+    # BIG_BLOCKS sizes (:266-273): 4, 32, 128, 512 MiB, 1, 2, 3 GiB, each
+    # below UINT_MAX with the post-block (:280-282)
+    big = [4 << 20, 32 << 20, 128 << 20, 512 << 20, 1 << 30, 2 << 30, 3 << 30]
+    big_block = [dict(g, src="behaviour.cpp:266-273 (BIG_BLOCKS), :284-292", lens=big,
+                      expected_status=0, expected_last_to=big) for g in gig]
+    # StreamingMatch :137-208: pre-block, gb * 1024 writes of 1 MiB of 'X',
+    # post-block, close; lastMatchTo stays 0 until the post-block; after the
+    # close it equals pre + gb GiB + post.  gb = 1, 2 (debug build; 1..8
+    # under NDEBUG)
+    stream = []
+    for g in gig:
+        for gb in (1, 2):
+            total = len(g["pre"]) + gb * 1024 * (1 << 20) + len(g["post"])
+            stream.append(dict(g, src="behaviour.cpp:137-208", fill="X", chunk=1 << 20,
+                               chunks=gb * 1024, expected_status=0,
+                               expected_last_to_before_post=0,
+                               expected_last_to_after_close=total))
+    # LiteralLength FloatingBlock :404-440, sizes :481-483: pattern 'a' * L,
+    # data 'a' * (L + 4): 5 matches; data[5:]: 0 matches
+    lens = [1, 2, 3, 4, 8, 16, 17, 32, 100, 200, 400, 1000, 4096, 8192, 15000, 15999]
+    floating = [{"src": "behaviour.cpp:404-440, 481-483", "literal_len": L, "data_len": L + 4,
+                 "fill": "a", "expected_count": 5, "expected_count_from5": 0} for L in lens]
+    # CallbackReturnStop Block / Streaming / Vectored :494-594, rows :596-599:
+    # exactly one match and HS_SCAN_TERMINATED (the stream's close: HS_SUCCESS)
+    stop = [{"src": "behaviour.cpp:494-599", "pattern": p, "flags": f, "corpus": c,
+             "expected_count": 1, "expected_status": HS_SCAN_TERMINATED,
+             "expected_close_status": 0}
+            for p, f, c in [("foobar", 0, "xxxfoobarxxxfoobarxxxfoobar"),
+                            ("a", 0, "xxxaaaaaaaaaaaaaaaaaaa"),
+                            ("a", CASELESS, "xxxAaAaAaAa")]]
+    # SerializedDogfood1 :613-662: serialize, free, deserialize; same
+    # database size; hs_scan of "delicious puppy treats!" -> lastMatchTo = len
+    dog = [{"src": "behaviour.cpp:613-662", "pattern": "puppy treats!", "flags": 0,
+            "data": "delicious puppy treats!", "expected_size_equal": True,
+            "expected_last_to": len("delicious puppy treats!")}]
+    return {"block_gigabytes": block, "big_block": big_block, "stream_gigabytes": stream,
+            "literal_length_floating": floating, "callback_stop": stop,
+            "serialized_dogfood": dog}
+
+
 def main():
+    with open(os.path.join(HERE, "hs_behaviour.json"), "w") as f:
+        json.dump(hs_behaviour_cases(), f, indent=1)
     with open(os.path.join(HERE, "noodle.json"), "w") as f:
         json.dump(noodle_cases(), f)
     with open(os.path.join(HERE, "fdr.json"), "w") as f:
