@@ -266,6 +266,13 @@ int vsa_plan_describe(const uint8_t *d_data, const uint64_t *offsets, const uint
                       uint32_t nblocks, uint32_t num_cus, uint32_t ns, uint32_t *words,
                       uint64_t cap, uint64_t *nsegs, uint32_t *grid,
                       const float *wg_weights);
+/* Host-only (tests): the block table the planner builds for a batch (one
+ * 72-byte record per block, kernels.h struct VsaBlock: base, len, start,
+ * seg_first, zbase, org, rlo, hlen, hist, flags) into out[nblocks]; d_data
+ * only sets the alignment.  Returns VSA_OK or a VSA_E_* code. */
+int vsa_plan_blocks(const uint8_t *d_data, const uint64_t *offsets, const uint64_t *lens,
+                    const uint64_t *starts, const uint64_t *hlens, const uint64_t *report_lo,
+                    uint32_t nblocks, void *out);
 
 /* Host-only (tests): the schedule feedback's per-XCD weight updates over
  * `launches` synthetic launches of `grid` workgroups (b on XCD b % 8) whose
@@ -277,11 +284,16 @@ int vsa_plan_create(vsa_ctx_t *ctx, const uint8_t *d_data, const uint64_t *offse
                     const uint64_t *lens, const uint64_t *starts, const uint64_t *hlens,
                     const uint64_t *report_lo, uint32_t nblocks, vsa_plan_t **plan);
 int vsa_plan_free(vsa_plan_t *plan);
+/* Segment maps a plan rebuilt so far to follow the schedule feedback's
+ * weights (tests: the feedback reaches prebuilt plans). */
+uint32_t vsa_plan_rebuilds(const vsa_plan_t *plan);
 /* vsa_scan_blocks over a plan (same flags, results and waiting) */
 int vsa_scan_plan(vsa_ctx_t *ctx, const vsa_db_t *db, const vsa_plan_t *plan, uint32_t flags,
                   uint64_t *n_matches);
 int vsa_scan_wait(vsa_ctx_t *ctx, uint64_t *n_matches);
-/* Device pointers to the last scan's sorted keys (u64) and ids (u32). */
+/* Device pointers to the last scan's sorted keys (u64) and ids (u32).  The
+ * scan is completed and the context's stream synchronized first, so the
+ * pointers can be read on any stream. */
 /* Pack the last scan's sorted records for a collective, into caller device
  * memory d_dst (u64 words): [header | keys (cap) | ids (cap x u32, i.e.
  * cap / 2 words)], header = record count, bit 62 set when the records are

@@ -1,11 +1,10 @@
 """CPU tests of the scan schedule (runtime.hip build_plan, through the
 host-only vsa_plan_describe): whatever the block layout, the segments cover
 every live block's span exactly once, in order; the per-workgroup lists
-(kernels.hip dynamic 2: one list per workgroup, handed out in LDS) give
-every workgroup an equal share of the static bytes -- stealing balances
-waves only inside a workgroup -- and the rest (VSA_POOL_PM per mille, off
-by default, 125 in the pool tests) is a pool of small segments after the
-lists, shared by all workgroups."""
+(kernels.hip: one list per workgroup, handed out in LDS) give every
+workgroup an equal (or weighted) share of the bytes -- stealing balances
+waves only inside a workgroup.  The block table keeps every load of the
+kernel inside the buffer (vsa_plan_blocks)."""
 import ctypes
 import random
 
@@ -54,17 +53,6 @@ def spans(offs, lens, starts, base):
     return out
 
 
-POOL_PM = [0]
-
-
-@pytest.fixture(params=[0, 125], ids=["no_pool", "pool125"])
-def pool(request, monkeypatch):
-    monkeypatch.setenv("VSA_POOL_PM", str(request.param))
-    POOL_PM[0] = request.param
-    yield request.param
-    POOL_PM[0] = 0
-
-
 def check(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000, weights=None):
     starts = list(starts) if starts is not None else [0] * len(offs)
     desc, bounds, grid = describe(offs, lens, starts, num_cus, ns, base, weights)
@@ -98,23 +86,17 @@ def check(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000, weights=Non
         assert bounds[0] == 0 and bounds[-1] <= len(desc)
         assert np.all(np.diff(bounds.astype(np.int64)) >= 0)
         per = [sum(seg_bytes[bounds[g]:bounds[g + 1]]) for g in range(grid)]
-        pool = seg_bytes[bounds[-1]:]
-        if grid >= 16 and POOL_PM[0]:
-            # the pool: VSA_POOL_PM of the bytes (to a segment), small segments
-            assert abs(sum(pool) - T * POOL_PM[0] // 1000) <= max(seg_bytes) + 4096
-        else:
-            assert not pool
+        assert bounds[-1] == len(desc)  # every segment is on some list
         return desc, bounds, grid, per, sum(per), seg_bytes
     return desc, None, 0, None, T, seg_bytes
 
 
 @pytest.mark.parametrize("mib,nblk", [(4096, 4), (512, 4), (512, 1), (64, 3), (1, 1)])
-def test_plan_large_blocks_equal_shares(mib, nblk, pool):
+def test_plan_large_blocks_equal_shares(mib, nblk):
     total = mib << 20
     bl = total // nblk
     desc, bounds, grid, per, T, segb = check([i * bl for i in range(nblk)], [bl] * nblk)
     assert grid == min(256, -(-total // (15 * 4096)))
-    assert all(b <= 128 << 10 for b in segb[bounds[-1]:])
     share = T / grid
     # every share to the KiB, plus at most one sliver (< the 4 KiB minimum)
     assert max(per) - share <= 1024 * nblk + 4096 + 1024, (max(per), share)
@@ -133,7 +115,7 @@ def test_plan_back_to_back_groups_stay_runs(mib, kib):
 
 
 @pytest.mark.parametrize("seed", range(6))
-def test_plan_random_layouts(seed, pool):
+def test_plan_random_layouts(seed):
     rng = random.Random(seed)
     offs, lens, starts = [], [], []
     pos = 0
@@ -156,7 +138,7 @@ def test_plan_random_layouts(seed, pool):
         assert max(per) - share <= max(seg_bytes) + 4096
 
 
-def test_plan_back_to_back_small_blocks_pack_into_runs(pool):
+def test_plan_back_to_back_small_blocks_pack_into_runs():
     n = 65536
     desc, bounds, grid, per, T, seg_bytes = check([i * 16384 for i in range(n)], [16384] * n)
     groups = [d for d in desc.tolist() if d[0] >> 24]
@@ -253,3 +235,54 @@ def test_plan_random_layouts_weighted(seed):
         wsum = sum(weights[:grid])
         for b in range(grid):
             assert abs(per[b] - T * weights[b] / wsum) <= max(seg_bytes) + 8192, (b, per[b])
+
+
+BLOCK_DT = np.dtype([("base", "<u8"), ("len", "<u8"), ("start", "<u8"), ("seg_first", "<u8"),
+                     ("zbase", "<i8"), ("org", "<i8"), ("rlo", "<i8"), ("hlen", "<u8"),
+                     ("hist", "<u4"), ("flags", "<u4")])
+assert BLOCK_DT.itemsize == 72
+lib.vsa_plan_blocks.restype = ctypes.c_int
+lib.vsa_plan_blocks.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_void_p]
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_plan_blocks_read_only_inside_the_buffer(seed):
+    """The round-4 fault (an illegal address in the GPU suite, fixed by
+    hist = min(hlen, 16)): every load of a block stays inside the buffer.
+    Random block and stream layouts whose history lies before each write in
+    the same buffer (the caller's contract: base >= hlen), at every
+    alignment: the history the kernel may read is min(hlen, 16) bytes, the
+    masked byte loads start at base - hist >= 0, and the chunk loads start at
+    a 1 KiB-aligned origin inside [aligned buffer start, first scanned byte]
+    (offsets relative to the 16-byte-aligned start, kernels.hip `A`)."""
+    rng = random.Random(5000 + seed)
+    n = rng.choice([1, 7, 60, 500])
+    offs, lens, starts, hlens = [], [], [], []
+    pos = rng.choice([0, 0, 1, 15, 16, 100])
+    for _ in range(n):
+        ln = rng.choice([0, 1, 2, 15, 16, 17, 100, 1023, 1024, 5000, 70000])
+        hl = rng.choice([0, 0, 1, 3, 15, 16, 17, 1000])
+        hl = min(hl, pos)  # the history is in the buffer, right before the write
+        offs.append(pos)
+        lens.append(ln)
+        starts.append(rng.choice([0, 0, rng.randint(0, max(0, ln - 1))]) if ln else 0)
+        hlens.append(hl)
+        pos += ln + rng.choice([0, 0, rng.randint(1, 3000)])
+    for mis in (0, 1, 7, 15):
+        base = 0x100000 + mis
+        o = np.ascontiguousarray(offs, np.uint64)
+        ln = np.ascontiguousarray(lens, np.uint64)
+        st = np.ascontiguousarray(starts, np.uint64)
+        hl = np.ascontiguousarray(hlens, np.uint64)
+        out = np.zeros(n, BLOCK_DT)
+        rc = lib.vsa_plan_blocks(base, o.ctypes.data, ln.ctypes.data, st.ctypes.data,
+                                 hl.ctypes.data, None, n, out.ctypes.data)
+        assert rc == 0
+        for i, b in enumerate(out):
+            assert b["hist"] == min(hlens[i], 16), (i, b)
+            assert b["hist"] <= b["hlen"]
+            blo = offs[i] + mis  # A-relative first byte of the block
+            assert blo - int(b["hist"]) >= 0, (i, b)  # masked byte loads
+            org = int(b["org"])
+            assert org >= 0 and org % 1024 == 0, (i, org)  # chunk loads
+            assert org <= blo + max(0, starts[i] - 16), (i, org, blo)

@@ -28,6 +28,9 @@ struct VsaBlock {
     uint32_t hist;      /* bytes readable before base (min(hlen, 16)) */
     uint32_t flags;     /* VSA_BLK_* */
 };
+#ifdef __cplusplus
+static_assert(sizeof(VsaBlock) == 72, "VsaBlock layout (vsa_plan_blocks, tests/test_plan.py)");
+#endif
 
 /* The block is a streaming call with history (fdrExecStreaming fdr.c:827,
  * len_history > 0): no FDR start state, the look-back starts one byte
@@ -54,35 +57,20 @@ struct VsaBlock {
 #define VSA_KEY_BUCKET_SHIFT 20
 #define VSA_KEY_LI_MASK 0xfffffu
 
-/* Key of the derived FDR first stage (runtime.hip derive_fdr_table) for the
- * byte pair (b0, b1) at positions (p, p + 1), dmask = 2^bits - 1: the low
- * 7 bits of b0 and the low bits - 7 bits of b1, except at 13 bits: the low
- * 6 bits of b0 and 7 of b1.  Both are "first byte under a mask, second
- * byte's low 7 bits shifted up", which the kernels compute two keys per
- * dword in two packed ops (kernels.hip fdr_key2: v_pk_lshrrev_b16 of the
- * 7-bit bytes by 1 or 2, v_bfi_b32 with the first-byte mask). */
-#ifdef __HIPCC__
-__host__ __device__
-#endif
-static inline uint32_t vsa_fdr_key(uint32_t b0, uint32_t b1, uint32_t dmask) {
-    if (dmask == 0x1fffu) return (b0 & 0x3fu) | ((b1 & 0x7fu) << 6);
-    return (b0 & 0x7fu) | ((b1 << 7) & dmask & ~0x7fu);
-}
-
 /* Key of the 4-field derived FDR first stage (VSA_MODE_FDR4, runtime.hip
  * derive_fdr4_table) at position p, from the bytes b2 = b[p-2], b1 =
- * b[p-1], b0 = b[p]: the low 7 bits of b1 and of b0 and, at 15 bits, bit 0
- * of b2 on top.  The kernels build it two keys per dword: bit 0 of b[p-2]
- * is funnel-shifted into bit 7 of b[p]'s (masked) byte, then fdr_key2. */
+ * b[p-1], b0 = b[p]: 15 bits, the low 7 bits of b1, bit 0 of b2, then the
+ * low 7 bits of b0 -- the 16-bit pair (b1, b0) as it lies in memory with its
+ * two bit-7s replaced (kernels.hip fdr4_keys builds two per dword in three
+ * ops). */
 #ifdef __HIPCC__
 __host__ __device__
 #endif
-static inline uint32_t vsa_fdr4_key(uint32_t b2, uint32_t b1, uint32_t b0, uint32_t bits) {
-    return (b1 & 0x7fu) | ((b0 & 0x7fu) << 7) | (bits >= 15 ? (b2 & 1u) << 14 : 0u);
+static inline uint32_t vsa_fdr4_key(uint32_t b2, uint32_t b1, uint32_t b0) {
+    return (b1 & 0x7fu) | ((b2 & 1u) << 7) | ((b0 & 0x7fu) << 8);
 }
 
 enum VsaLitMode {
-    VSA_MODE_FDR = 0,   /* 8 lanes x 8 buckets, 2-byte key & domainMask */
     VSA_MODE_TEDDY = 1, /* 4 lanes x 8 buckets, 1-byte key */
     VSA_MODE_FAT = 2,   /* 4 lanes x 16 buckets, 1-byte key */
     VSA_MODE_NOOD = 3,  /* noodle: masked compare of the <= 8 bytes ending at e */
@@ -100,23 +88,16 @@ struct VsaLitParams {
     const uint8_t *data;
     const VsaBlock *blocks;
     uint32_t nblocks;
-    uint32_t seg_bytes;     /* nominal segment size (multiple of 1 KiB) */
-    uint32_t dynamic;       /* 0: static (wave g takes g, g + G, ..); 1:
-                               atomic ticket per region; 2: per-workgroup
-                               segment lists (wg_seg) handed out in LDS */
-    uint32_t nregions;      /* ticket regions (counters[16 + 16 r], one
-                               128-B line each), <= 8 */
     uint64_t nsegs;
     const uint32_t *seg_desc; /* 4 words per segment: first block | count <<
                                  24, offset and length in KiB from the block
                                  origin (a part of one block), 0 */
-    const uint32_t *wg_seg;   /* dynamic 2: workgroup b's segments are
-                                 [wg_seg[b], wg_seg[b + 1]) */
-    uint32_t steal;           /* dynamic 2: a wave out of segments steals sweep
-                                 groups inside its workgroup when some wave
-                                 has at least `steal` unclaimed (0: off) */
-    uint32_t steal_w;         /* weigh victims by issue age (VSA_STEAL_W) */
-    const uint64_t *table;  /* FDR domain table / Teddy combined byte table */
+    const uint32_t *wg_seg;   /* workgroup b's segments are [wg_seg[b],
+                                 wg_seg[b + 1]), handed out in LDS */
+    uint32_t steal;           /* a wave out of segments steals sweep groups
+                                 inside its workgroup when some wave has at
+                                 least `steal` unclaimed (0: off) */
+    const uint64_t *table;  /* FDR4 table (u32 entries) / Teddy byte table */
     uint32_t table_entries;
     uint32_t dmask;
     uint32_t end_par;       /* FDR4 split passes: 0 every end; 1 / 2 only the
@@ -150,25 +131,23 @@ struct VsaLitParams {
     uint64_t out_cap;
     uint32_t *bin_counts;        /* binned sort: records per bin of end >>
                                     bin_shift, counted as they are emitted
-                                    (nullptr: no binned sort, or the separate
-                                    histogram launch) */
+                                    (nullptr: no binned sort) */
     uint32_t bin_shift;
     uint32_t *bin_slots;         /* staged binned sort (vsa_bin_finish): the
                                     output slot of record s of bin b goes to
                                     [b * VSA_SORT_BIN_MAX + s] (s from the
                                     returning count atomic; a bin past
                                     VSA_SORT_BIN_MAX sets
-                                    counters[VSA_CTR_BIN_OVERFLOW]); nullptr:
-                                    the count-only histogram */
+                                    counters[VSA_CTR_BIN_OVERFLOW]) */
     unsigned long long *wg_time;  /* schedule feedback (or null): [b] = xcc <<
                                      60 | end of workgroup b's scanning
                                      waves, [grid + b] = its entry (100 MHz) */
     unsigned long long *wave_log; /* diagnostic (dbg bit12): 8 u64 per scanning
                                      wave: start, end (100 MHz), segments,
                                      KiB iterations, workgroup, wave, XCC, HW_ID */
-    unsigned long long *counters; /* [0] matches, [16 + 16 r] region tickets,
-                                     [2] candidates handed to confirm (after
-                                     the slot prefilter; diagnostic) */
+    unsigned long long *counters; /* [0] matches, [2] candidates handed to
+                                     confirm (after the slot prefilter;
+                                     diagnostic) */
 };
 
 
@@ -188,11 +167,6 @@ struct VsaClassParams {
     unsigned long long *count;     /* [slots] popcount of the bitmap */
     uint32_t slots;                /* workgroup b updates slot b % slots, at
                                       u64 index 16 * slot (one line each) */
-    const uint64_t *wg_lo;         /* LUT kernel: workgroup b scans [wg_lo[b],
-                                      wg_lo[b + 1]) (schedule feedback), or
-                                      null: equal spans */
-    unsigned long long *wg_time;   /* schedule feedback record (as
-                                      VsaLitParams.wg_time), or null */
 };
 
 /* Double shufti (shuftiDoubleExec): bucketed byte-pair test with the

@@ -13,12 +13,12 @@
  *                      vermicelli_simd.cpp) -> 1 bit/byte bitmap + first/last.
  *
  * Work decomposition (literal scan): the batch is a list of blocks (each one
- * hwlmExec call); a block is cut into segments of seg_bytes end positions
- * (host-sized so every scanning wave gets the same number of segments);
- * scanning wave g owns segments g, g + G, ... (static, G = all scanning
- * waves), sweeping each in 1 KiB iterations: lane l loads 16 bytes at
- * iteration_base + 16 l with one global_load_dwordx4 (fully coalesced), so
- * HBM is read once plus a 1 KiB-aligned halo per segment.
+ * hwlmExec call) cut into segments by the host (runtime.hip build_plan);
+ * workgroup b owns a list of segments holding an equal share of the bytes
+ * and its scanning waves take them in turn from an LDS counter, sweeping
+ * each in 1 KiB iterations: lane l loads 16 bytes at iteration_base + 16 l
+ * with one global_load_dwordx4 (fully coalesced), so HBM is read once plus
+ * a 1 KiB-aligned halo per segment.
  *
  * FDR / Teddy filter (the reference's stride-1 shift-or, restated per lane):
  * for end e, conf(e) = OR_k field_k(T[key(e-k)]); a zero bit b means
@@ -93,30 +93,6 @@ __device__ __forceinline__ u32 writelane_u32(u32 v, u32 s) {
     asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(readfirstlane_u32(s)), "n"(L));
     return v;
 }
-/* vsa_fdr_key of the byte pairs (0, 1) and (2, 3) of z, one per 16-bit half,
- * for 14- and 13-bit tables: z = the bytes with bit 7 clear (every byte
- * AND 0x7f, shared by all keys of a dword); the packed shift moves each
- * half's second byte down by kshift (1 or 2: its low 7 bits land right
- * above the first byte's kf bits, its bit 7 is 0 and bit 15 is zero-filled)
- * and v_bfi_b32 keeps the first byte's bits under kf (0x007f007f or
- * 0x003f003f).  Two VALU ops per two keys. */
-__device__ __forceinline__ u32 fdr_key2(u32 z, u32 kf, u32 kshift2) {
-    u32 y, r;
-    asm("v_pk_lshrrev_b16 %0, %1, %2" : "=v"(y) : "s"(kshift2), "v"(z));
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(kf), "v"(z), "v"(y));
-    return r;
-}
-/* LDS byte address of an 8-byte table entry: base + 8 * (16-bit half H of
- * w) in one op (v_mad_u32_u16 with op_sel picks the half, no bfe/shift) */
-template <int H>
-__device__ __forceinline__ u32 tab_addr16(u32 w, u32 base) {
-    u32 r;
-    if constexpr (H == 0)
-        asm("v_mad_u32_u16 %0, %1, 8, %2" : "=v"(r) : "v"(w), "s"(base));
-    else
-        asm("v_mad_u32_u16 %0, %1, 8, %2 op_sel:[1,0,0,0]" : "=v"(r) : "v"(w), "s"(base));
-    return r;
-}
 typedef const __attribute__((address_space(3))) u64 lds_u64_t;
 typedef const __attribute__((address_space(3))) u8 lds_u8_t;
 __device__ __forceinline__ u64 lds_ld64(u32 addr) { return *(lds_u64_t *)(uintptr_t)addr; }
@@ -138,6 +114,10 @@ __device__ __forceinline__ u32 shfl_xor_u32(u32 v, int m) {
 __device__ __forceinline__ u32 shfl_down_u32(u32 v, unsigned d) {
     return (u32)__shfl_down((int)v, d, WAVE);
 }
+
+/* any lane's c: one v_cmp into a scalar mask and a scalar test (__any's
+ * lowering re-materialized the mask as a lane value and compared again) */
+__device__ __forceinline__ bool wave_any(bool c) { return __builtin_amdgcn_ballot_w64(c) != 0; }
 
 /* wave-wide exclusive prefix sum of a small per-lane count */
 __device__ __forceinline__ u32 wave_excl_scan(u32 v, u32 *total) {
@@ -162,15 +142,6 @@ __device__ __forceinline__ u8 load_byte_masked(const u8 *A, int64_t aoff,
 template <int MODE>
 struct LitTraits;
 
-template <>
-struct LitTraits<VSA_MODE_FDR> {
-    static constexpr int LB = 8;   /* bits per lane field (= buckets) */
-    static constexpr int NL = 8;   /* lanes (positions looked back) */
-    static constexpr int CW = 4;   /* conf dwords for 16 ends */
-    static constexpr int EW = 3;   /* uint4 words per candidate chunk entry */
-    static constexpr bool KEY16 = true;
-    typedef u64 S_t;
-};
 /* Teddy: the first stage is an exact per-byte table derived from the
  * confirm records (runtime.hip derive_teddy_table), 8 positions x 8
  * buckets; the reference's nibble masks (teddy_compile.cpp:439) admit up to
@@ -181,7 +152,6 @@ struct LitTraits<VSA_MODE_TEDDY> {
     static constexpr int NL = 8;
     static constexpr int CW = 4;
     static constexpr int EW = 3;
-    static constexpr bool KEY16 = false;
     typedef u64 S_t;
 };
 template <>
@@ -190,7 +160,6 @@ struct LitTraits<VSA_MODE_NOOD> {
     static constexpr int NL = 1; /* no look-back state */
     static constexpr int CW = 1;
     static constexpr int EW = 2; /* {meta}, {hits} */
-    static constexpr bool KEY16 = false;
     typedef u32 S_t;
 };
 template <>
@@ -199,7 +168,6 @@ struct LitTraits<VSA_MODE_FAT> {
     static constexpr int NL = 4;
     static constexpr int CW = 8;
     static constexpr int EW = 4;
-    static constexpr bool KEY16 = false;
     typedef u64 S_t;
 };
 /* FDR engines, 4-field first stage (runtime.hip derive_fdr4_table): u32
@@ -211,7 +179,6 @@ struct LitTraits<VSA_MODE_FDR4> {
     static constexpr int NL = 4;
     static constexpr int CW = 4;
     static constexpr int EW = 3;
-    static constexpr bool KEY16 = false;
     typedef u32 S_t;
 };
 
@@ -261,8 +228,6 @@ struct QEnt {
 struct LitShared {
     const void *tab;
     u32 tab_lds;     /* LDS byte address of tab (LDS tables) */
-    u32 kf;          /* FDR key: first-byte mask in both halves (fdr_key2) */
-    u32 kshift2;     /* FDR key: second-byte shift in both halves */
     u32 tsel;        /* Teddy: TEDDY_TAB_LDS | this lane's copy offset */
     uint4 *ring;     /* this wave's ring */
     const u32 *tail; /* this ring's consumed position (written by the confirm wave) */
@@ -395,11 +360,6 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
                         P.bin_slots[bix[i] * VSA_SORT_BIN_MAX + bslot[i]] = (u32)slot;
                     else
                         P.counters[VSA_CTR_BIN_OVERFLOW] = 1;
-                } else if (mt[i] && P.bin_counts) {
-                    /* the count-only histogram (an overflowed launch's counts
-                     * are zeroed by its sort launch and never used) */
-                    __hip_atomic_fetch_add(&P.bin_counts[(u32)((base[i] + (u64)e[i]) >> P.bin_shift)],
-                                           1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
         }
@@ -412,12 +372,9 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
     }
 }
 
-template <int MODE, bool LDS_TABLE>
+template <int MODE>
 __device__ __forceinline__ u64 lit_lookup(const void *tab, u32 key, u32 lane) {
-    if constexpr (MODE == VSA_MODE_FDR) {
-        (void)lane;
-        return ((const u64 *)tab)[key];
-    } else if constexpr (MODE == VSA_MODE_FDR4) {
+    if constexpr (MODE == VSA_MODE_FDR4) {
         (void)lane;
         return ((const u32 *)tab)[key];
     } else {
@@ -425,27 +382,13 @@ __device__ __forceinline__ u64 lit_lookup(const void *tab, u32 key, u32 lane) {
     }
 }
 
-/* key of position j (0..15) of the lane's chunk d[0..3] (d[4] = next byte) */
-template <int MODE>
-__device__ __forceinline__ u32 lit_key(const u32 d[5], int j, u32 dmask) {
-    if constexpr (LitTraits<MODE>::KEY16) {
-        /* vsa_fdr_key of bytes j, j + 1 (the derived table's key) */
-        const u32 w = (j & 3) != 3 ? d[j >> 2] >> (8 * (j & 3))
-                                   : __builtin_amdgcn_alignbyte(d[(j >> 2) + 1], d[j >> 2], 3);
-        return vsa_fdr_key(w & 0xff, (w >> 8) & 0xff, dmask);
-    } else {
-        (void)dmask;
-        return (d[j >> 2] >> (8 * (j & 3))) & 0xff;
-    }
-}
-
 struct IterState {
     u64 carry;  /* pending table contributions into the next chunk's first ends */
     u64 pbytes; /* the 8 bytes before the next chunk (lane 63's d[2..3]) */
-    /* FDR sweep: lane 0 holds the previous chunk's lane-63 d[3] / U[4] /
-     * U[5] (lane_ror1 of them); carry and pbytes' high half are refreshed
-     * from these only when the sweep ends (sweep_enter / sweep_leave) */
-    u32 p3, p4, p5;
+    /* FDR4 sweep: lane 0 holds the previous chunk's lane-63 d[3] / U[4]
+     * (lane_ror1 of them); carry and pbytes' high half are refreshed from
+     * these only when the sweep ends (sweep_enter / sweep_leave) */
+    u32 p3, p4;
     u32 ncand;  /* first-stage candidates so far (diagnostic, wave-uniform) */
     u32 tail_cache; /* last tail read from the confirm wave */
     u32 head;       /* entries this wave has pushed to its ring */
@@ -567,58 +510,6 @@ __device__ __forceinline__ void conf_accumulate(const typename LitTraits<MODE>::
     }
 }
 
-/* OR-into-place of the FDR entries of the residue groups in RM (bit r: the
- * slots j = 4 w + r), the LB == 8 case of conf_accumulate split by residue:
- * F[0..5] = the conf dwords of positions -1 .. 22 (byte i of F[w] = end
- * 4 w + i - 1; F[4..5] spill into the next lane), before the look-back
- * shift. */
-template <int RM, bool ACC = false>
-__device__ __forceinline__ void fdr_acc_groups(const u64 (&x)[16], u32 (&F)[6]) {
-    auto lo = [&](int j) { return (u32)x[j]; };
-    auto hi = [&](int j) { return (u32)(x[j] >> 32); };
-    constexpr bool R0 = RM & 1, R1 = RM & 2, R2 = RM & 4, R3 = RM & 8;
-    u32 A[4][5];
-#pragma unroll
-    for (int r = 1; r < 4; r++) {
-        A[r][0] = lo(r);
-        A[r][1] = hi(r) | lo(4 + r);
-        A[r][2] = hi(4 + r) | lo(8 + r);
-        A[r][3] = hi(8 + r) | lo(12 + r);
-        A[r][4] = hi(12 + r);
-    }
-    /* ACC: OR into F (the previous level's dwords ride in the or3's spare
-     * operand) */
-    u32 f0 = ACC ? F[0] : 0u;
-    if (R0) f0 |= lo(0);
-    if (R1) f0 |= A[1][0] << 8;
-    if (R2) f0 |= A[2][0] << 16;
-    if (R3) f0 |= A[3][0] << 24;
-    F[0] = f0;
-#pragma unroll
-    for (int i = 1; i < 5; i++) {
-        u32 a = ACC ? F[i] : 0u, b = 0, c = 0;
-        if (R0) a |= hi(4 * (i - 1)) | (i < 4 ? lo(4 * i) : 0u);
-        if (R1) b = __builtin_amdgcn_alignbyte(A[1][i], A[1][i - 1], 3);
-        if (R2) c = __builtin_amdgcn_alignbyte(A[2][i], A[2][i - 1], 2);
-        if (R3) c |= __builtin_amdgcn_alignbyte(A[3][i], A[3][i - 1], 1);
-        F[i] = or3(a, b, c);
-    }
-    u32 f5 = ACC ? F[5] : 0u;
-    if (R1) f5 |= A[1][4] >> 24;
-    if (R2) f5 |= A[2][4] >> 16;
-    if (R3) f5 |= A[3][4] >> 8;
-    F[5] = f5;
-}
-
-
-/* the look-back shift (lit_iter): byte i of c[w] = end 4 w + i; s = the
- * spill into ends 16 .. 22 */
-__device__ __forceinline__ void fdr_shift1(const u32 (&F)[6], u32 (&c)[4], u64 &s) {
-#pragma unroll
-    for (int w = 0; w < 4; w++) c[w] = __builtin_amdgcn_alignbyte(F[w + 1], F[w], 1);
-    s = ((u64)(F[5] >> 8) << 32) | __builtin_amdgcn_alignbyte(F[5], F[4], 1);
-}
-
 /* ---- FDR4: the 4-field first stage (VSA_MODE_FDR4) ----
  * Lane l looks up positions 0 .. 15 of its chunk; the key of position p is
  * vsa_fdr4_key(b[p-2], b[p-1], b[p]) (bytes -2, -1: the previous lane's, or
@@ -626,28 +517,38 @@ __device__ __forceinline__ void fdr_shift1(const u32 (&F)[6], u32 (&c)[4], u64 &
  * U[0..3] = the conf bytes of ends 0 .. 15, U[4] bytes 0..2 = ends 16..18,
  * which are the next lane's ends 0..2 (spilled once per iteration).
  *
- * Keys, two per dword (fdr_key2 on 16-bit halves, raw bytes): the even positions (4w,
- * 4w + 2) from t = bytes 4w-1 .. 4w+2, the odd ones (4w + 1, 4w + 3) from
- * bytes 4w .. 4w+3; bit 0 of each key's b[p-2] goes into bit 7 of b[p]'s
- * masked byte (bits 15 / 31 of the dword) by a funnel shift (v_alignbit) and
- * one v_bfi, so fdr_key2 lands it at key bit 14 (15-bit keys only: a
- * database whose slot bitmaps leave no room for the 128 KiB table scans
- * with the 8-field table, runtime.hip). */
-__device__ __forceinline__ void fdr4_keys(const u32 (&z)[4], u32 zp, u32 (&ke)[4],
+ * Keys, two per dword, one per 16-bit half: [b[p-1] & 0x7f | (b[p-2] & 1)
+ * << 7, b[p] & 0x7f] (vsa_fdr4_key's bit order: the halves of the 7-bit
+ * bytes as they lie in memory, with bit 0 of the byte before them in the
+ * first byte's free bit 7).  From z = the chunk's bytes & 0x7f: the even
+ * positions (4w, 4w + 2) take t = bytes 4w-1 .. 4w+2 (v_alignbyte) and the
+ * odd ones (4w + 1, 4w + 3) z[w] itself; the b[p-2] bits come by one
+ * funnel shift (v_alignbit) and one v_bfi each.  Six VALU ops per four keys
+ * (nine with the round-3 key order, which shifted each half by one). */
+__device__ __forceinline__ u32 bfi_b32(u32 m, u32 a, u32 b) {
+    u32 r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ void fdr4_keys(const u32 (&d)[4], u32 pv3, u32 (&ke)[4],
                                           u32 (&ko)[4]) {
-    const u32 kf = 0x007f007fu, ks = 0x00010001u;
+    /* the byte mask kept in a VGPR: v_and_b32 with two VGPR operands issues
+     * in half the cycles of one with a constant (tools/probe_issue.hip) */
+    u32 m7;
+    asm("v_mov_b32 %0, 0x7f7f7f7f" : "=v"(m7));
+    u32 z[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) asm("v_and_b32 %0, %1, %2" : "=v"(z[w]) : "v"(m7), "v"(d[w]));
+    u32 zp;
+    asm("v_and_b32 %0, %1, %2" : "=v"(zp) : "v"(m7), "v"(pv3));
 #pragma unroll
     for (int w = 0; w < 4; w++) {
         const u32 zq = w ? z[w - 1] : zp;
-        const u32 t = __builtin_amdgcn_alignbyte(z[w], zq, 3);
-        /* bit 15 = b(4w-2), bit 31 = b(4w) (even); b(4w-1), b(4w+1) (odd) */
-        u32 te, to;
-        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(te) : "s"(0x80008000u),
-            "v"(__builtin_amdgcn_alignbit(z[w], zq, 1)), "v"(t));
-        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(to) : "s"(0x80008000u),
-            "v"(__builtin_amdgcn_alignbit(z[w], zq, 9)), "v"(z[w]));
-        ke[w] = fdr_key2(te, kf, ks);
-        ko[w] = fdr_key2(to, kf, ks);
+        /* bit 7 = bit 0 of b(4w-2), bit 23 = of b(4w) (even); b(4w-1),
+         * b(4w+1) (odd) */
+        ke[w] = bfi_b32(0x00800080u, __builtin_amdgcn_alignbit(z[w], zq, 9),
+                        __builtin_amdgcn_alignbyte(z[w], zq, 3));
+        ko[w] = bfi_b32(0x00800080u, __builtin_amdgcn_alignbit(z[w], zq, 17), z[w]);
     }
 }
 /* LDS byte address of a u32 entry: base + 4 * (16-bit half H of w) */
@@ -662,6 +563,27 @@ __device__ __forceinline__ u32 tab_addr16x4(u32 w, u32 base) {
 }
 __device__ __forceinline__ u32 lds_ld32a(u32 addr) {
     return *(const __attribute__((address_space(3))) u32 *)(uintptr_t)addr;
+}
+/* Two LDS reads in the lanes of m only (EXEC = m around them; a lane
+ * outside m keeps whatever its registers held, which only ever reaches ends
+ * that are already dead).  The compiler does not see these reads: the
+ * caller waits for them (lds_wait8) before the values are used.  Reads the
+ * compiler issued are counted with them, so its own waits stay correct, if
+ * conservative. */
+__device__ __forceinline__ void lds_ld32x2_masked(u64 m, u32 a0, u32 a1, u32 &x0, u32 &x1) {
+    u64 sv;
+    asm volatile("s_mov_b64 %2, exec\n\t"
+                 "s_mov_b64 exec, %5\n\t"
+                 "ds_read_b32 %0, %3\n\t"
+                 "ds_read_b32 %1, %4\n\t"
+                 "s_mov_b64 exec, %2"
+                 : "=&v"(x0), "=&v"(x1), "=&s"(sv)
+                 : "v"(a0), "v"(a1), "s"(m));
+}
+__device__ __forceinline__ void lds_wait8(u32 (&x)[16]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(x[1]), "+v"(x[3]), "+v"(x[5]), "+v"(x[7]), "+v"(x[9]), "+v"(x[11]),
+                   "+v"(x[13]), "+v"(x[15]));
 }
 /* OR-into-place: field f of x[p] onto end p + f.  EVEN: x[0, 2, .., 14]
  * (the first writes of U); ODD: x[1, 3, .., 15] OR-ed on top. */
@@ -681,16 +603,14 @@ __device__ __forceinline__ void fdr4_acc_odd(const u32 (&x)[16], u32 (&U)[5]) {
 }
 /* One chunk's conf bytes (before the previous lane's spill into U[0]).
  * Sweep (LOOKM == false): two levels -- the even positions for every lane,
- * then the odd ones with their real keys only in lanes where a conf dword
- * they reach is still live (else key 0: an LDS broadcast; its entry is
- * OR-ed only into ends already dead, so the result is the one-level
- * filter's).  Edge iterations (LOOKM): one level, position p looked up
- * only where bit p of look_m is set. */
+ * then the odd ones only in lanes where a conf dword they reach is still
+ * live (EXEC-masked reads: a lane left out takes no LDS bank and no VALU
+ * op; its stale value is OR-ed only into ends already dead, so the result
+ * is the one-level filter's).  Edge iterations (LOOKM): one level, position
+ * p looked up only where bit p of look_m is set. */
 template <bool LOOKM>
 __device__ __forceinline__ void fdr4_conf(const LitShared &L, const u32 (&d)[4], u32 pv3,
                                           u32 look_m, u32 (&U)[5]) {
-    /* no 7-bit masking: fdr_key2 keeps 7 bits of each pair's first byte,
-     * and the injected bit replaces bit 7 of its second byte */
     u32 ke[4], ko[4], x[16];
     fdr4_keys(d, pv3, ke, ko);
     auto ld = [&](int p, u32 a) {
@@ -702,12 +622,7 @@ __device__ __forceinline__ void fdr4_conf(const LitShared &L, const u32 (&d)[4],
         ld(4 * w, tab_addr16x4<0>(ke[w], L.tab_lds));
         ld(4 * w + 2, tab_addr16x4<1>(ke[w], L.tab_lds));
     }
-#ifdef VSA_FDR4_ONE_LEVEL /* A/B: every lookup in every lane */
-    constexpr bool ONE = true;
-#else
-    constexpr bool ONE = LOOKM;
-#endif
-    if (ONE) {
+    if (LOOKM) {
 #pragma unroll
         for (int w = 0; w < 4; w++) {
             ld(4 * w + 1, tab_addr16x4<0>(ko[w], L.tab_lds));
@@ -726,122 +641,15 @@ __device__ __forceinline__ void fdr4_conf(const LitShared &L, const u32 (&d)[4],
      * conflicts it saves (profiles/r03_fdr4_gate_ab.txt). */
     u64 m[5];
 #pragma unroll
-    for (int k = 0; k < 5; k++) m[k] = __ballot(U[k] != 0xffffffffu);
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-        const u32 k = __builtin_amdgcn_inverse_ballot_w64(m[w] | m[w + 1]) ? ko[w] : 0u;
-        x[4 * w + 1] = lds_ld32a(tab_addr16x4<0>(k, L.tab_lds));
-        x[4 * w + 3] = lds_ld32a(tab_addr16x4<1>(k, L.tab_lds));
-    }
-    fdr4_acc_odd(x, U);
-}
-
-/* FDR sweep (LDS table, interior iteration): the 16 lookups in two levels.
- * Level 1 looks up the 8 even slots (positions -1, 1, .., 13).  Level 2
- * looks up the odd slots (positions 0, 2, .., 14) with their real keys only
- * in the lanes where a conf dword the pair of slots reaches still has a
- * live end after level 1; the other lanes look up key 0, one address for
- * all of them (an LDS broadcast, no bank conflict).  On cfg-4 text 3.5 % of
- * ends survive the even slots, so ~35 % of level 2's lanes carry real keys
- * and the model of the LDS array cycles per KiB falls from ~113 to ~90
- * (tools/sim_lds.py): the random lookups' bank conflicts are what bound
- * this kernel.  The result is exactly the full filter's: a dead lane's
- * entry is OR-ed only into ends that are already dead (every bucket bit
- * set), which stay dead, and lane 63, whose reach crosses into the next
- * chunk, always looks up. */
-template <bool TWO>
-__device__ __forceinline__ void fdr_sweep_conf(const LitShared &L, const u32 (&d)[4], u32 pv3,
-                                               u32 &p4, u32 &p5, u32 (&U)[6]) {
-    u64 x[16];
-    u32 ko[4], km[4], z[4];
-#pragma unroll
-    for (int w = 0; w < 4; w++) z[w] = d[w] & 0x7f7f7f7fu;
-    /* byte -1 (pv3's top byte) is only ever a first byte: fdr_key2 keeps
-     * its low kf bits, so it needs no mask */
+    for (int k = 0; k < 4; k++) m[k] = __builtin_amdgcn_ballot_w64(U[k] != 0xffffffffu);
+    /* U[4]: ends 16..18 (the next lane's 0..2); its byte 3 is never set */
+    m[4] = __builtin_amdgcn_ballot_w64((U[4] | 0xff000000u) != 0xffffffffu);
 #pragma unroll
     for (int w = 0; w < 4; w++)
-        ko[w] = fdr_key2(__builtin_amdgcn_alignbyte(z[w], w ? z[w - 1] : pv3, 3), L.kf, L.kshift2);
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-        x[4 * w] = lds_ld64(tab_addr16<0>(ko[w], L.tab_lds));
-        x[4 * w + 2] = lds_ld64(tab_addr16<1>(ko[w], L.tab_lds));
-    }
-    if (!TWO) {
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-            km[w] = fdr_key2(z[w], L.kf, L.kshift2);
-            x[4 * w + 1] = lds_ld64(tab_addr16<0>(km[w], L.tab_lds));
-            x[4 * w + 3] = lds_ld64(tab_addr16<1>(km[w], L.tab_lds));
-        }
-    }
-    /* Level 1, before the look-back shift: byte i of U[w] = end 4 w + i - 1,
-     * U[4..5] = ends 15 .. 22 (byte 0 of U[4] is this lane's end 15, the
-     * rest spills into the next lane).  The previous lane's U[4..5] land on
-     * this lane's U[0..1] as they are (its end 15 = this lane's end -1);
-     * lane 0 takes the previous chunk's carry in the same form. */
-    fdr_acc_groups<0x5>(x, U);
-    if (!TWO) fdr_acc_groups<0xA, true>(x, U);
-    /* The previous lane's U[4..5] (lane 0: the previous chunk's lane 63)
-     * land on this lane's U[0..1] once, after the last level (spill()).
-     * Level 2's lane masks are taken before it: a dword then counts as live
-     * whenever this lane's own slots leave it live, which keeps them
-     * conservative and saves a second cross-lane spill. */
-    auto spill = [&]() {
-        const u32 x4 = lane_ror1(U[4]), x5 = lane_ror1(U[5]);
-        U[0] |= lane_up1_or_old(p4, U[4]);
-        U[1] |= lane_up1_or_old(p5, U[5]);
-        p4 = x4;
-        p5 = x5;
-    };
-    if (!TWO) {
-        spill();
-        return;
-    }
-#ifdef VSA_SPILL_TIGHT /* experiment: spill before the masks too (tighter level 2) */
-    U[0] |= lane_up1_or_old(p4, U[4]);
-    U[1] |= lane_up1_or_old(p5, U[5]);
-#endif
-    /* conf dwords with a live end after level 1 (lane masks; an absent
-     * bucket's bit is set in every entry, derive_fdr_table).  The next
-     * lane's U[0] / U[1] cover ends 15 .. 22 (its U[0] byte 0 = this lane's
-     * end 15); lane 63's successor is the next chunk: always live. */
-    const u64 m0 = __ballot(U[0] != 0xffffffffu);
-    const u64 m1 = __ballot(U[1] != 0xffffffffu);
-    const u64 m2 = __ballot(U[2] != 0xffffffffu);
-    const u64 m3 = __ballot(U[3] != 0xffffffffu);
-    const u64 top = 1ULL << 63;
-    const u64 n0 = (m0 >> 1) | top, n1 = (m1 >> 1) | top;
-    /* slots 2 i + 1 and 2 i + 3 (i even: positions 2 i, 2 i + 2, one key
-     * dword km[i / 2]) reach ends 2 i .. 2 i + 9 = U bytes 2 i + 1 .. 2 i + 10:
-     * dwords i / 2 .. i / 2 + 2 */
-    const u64 m12 = m1 | m2, m3n0 = m3 | n0;
-    const u64 act[4] = {m0 | m12, m12 | m3, m2 | m3n0, m3n0 | n1};
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-        /* a dead pair reads entry 0 (a broadcast: no bank conflict); any
-         * entry serves a dead end */
-        const u32 k = fdr_key2(z[w], L.kf, L.kshift2);
-        km[w] = __builtin_amdgcn_inverse_ballot_w64(act[w]) ? k : 0u;
-    }
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-        x[4 * w + 1] = lds_ld64(tab_addr16<0>(km[w], L.tab_lds));
-        x[4 * w + 3] = lds_ld64(tab_addr16<1>(km[w], L.tab_lds));
-    }
-    fdr_acc_groups<0xA, true>(x, U);
-#ifdef VSA_EXTRA_VALU
-    /* experiment build: VSA_EXTRA_VALU dependent VALU ops per iteration */
-#pragma unroll
-    for (int i = 0; i < VSA_EXTRA_VALU; i++) asm volatile("v_or_b32 %0, %0, %0" : "+v"(U[i & 3]));
-#endif
-#ifdef VSA_SPILL_TIGHT
-    U[0] |= lane_up1(U[4]); /* lane 0: its carry is in already */
-    U[1] |= lane_up1(U[5]);
-    p4 = lane_ror1(U[4]);
-    p5 = lane_ror1(U[5]);
-#else
-    spill();
-#endif
+        lds_ld32x2_masked(m[w] | m[w + 1], tab_addr16x4<0>(ko[w], L.tab_lds),
+                          tab_addr16x4<1>(ko[w], L.tab_lds), x[4 * w + 1], x[4 * w + 3]);
+    lds_wait8(x);
+    fdr4_acc_odd(x, U);
 }
 
 /* Block-edge masks: position j (0..16) of a lane's chunk is end / byte
@@ -912,7 +720,7 @@ __device__ __forceinline__ void xp_flush(const VsaLitParams &P, const ConfLds &c
 
 __device__ __forceinline__ void xp_push(const VsaLitParams &P, const ConfLds &cl,
                                         const LitShared &L, IterState &st, u32 (&c)[4],
-                                        u64 meta, u32 pv2, u32 pv3, const u32 (&d)[5]) {
+                                        u64 meta, u32 pv2, u32 pv3, const u32 (&d)[4]) {
     const u32 D[6] = {pv2, pv3, d[0], d[1], d[2], d[3]};
     const u64 p0 = meta & ENT_P0_MASK;
     const u64 blk4 = (meta >> ENT_BLK_SHIFT) << 4;
@@ -968,24 +776,22 @@ __device__ __forceinline__ void xp_push(const VsaLitParams &P, const ConfLds &cl
     }
 }
 
-/* One 1 KiB iteration at aoff `ib`: lane l owns bytes [ib + 16 l, +16).
- * d = the lane's 16 bytes, nxt0 = first byte of the following chunk (for
- * lane 63's last 2-byte key). */
-template <int MODE, bool LDS_TABLE, bool EDGE, bool XP>
+/* One 1 KiB iteration at aoff `ib`: lane l owns bytes [ib + 16 l, +16),
+ * d = the lane's 16 bytes.  Every key looks back (FDR4: the two bytes before
+ * a position; Teddy: the position's own byte), so no key needs the byte
+ * after the chunk and an iteration never waits on the next chunk's load. */
+template <int MODE, bool EDGE, bool XP, bool SPLIT>
 __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfLds &cl,
                                               const LitShared &L, const SegCtx &S,
                                               u32 mis, int64_t ib, uint4 chunk,
-                                              u32 nxt0, IterState in, u32 bucket_mask) {
+                                              IterState in, u32 bucket_mask) {
     typedef LitTraits<MODE> T;
     typedef typename T::S_t S_t;
     const u32 lane = lane_id();
     const int64_t p0 = ib + 16 * (int64_t)lane;
     const int64_t q0 = p0 - S.blo;
 
-    u32 d[5] = {chunk.x, chunk.y, chunk.z, chunk.w, 0};
-    /* next byte (only byte 0 of d[4] reaches a key: the 16-bit key of
-     * position 15 is bytes 15..16, masked to <= 16 bits) */
-    d[4] = writelane_u32<WAVE - 1>(lane_down1(d[0]), nxt0);
+    u32 d[4] = {chunk.x, chunk.y, chunk.z, chunk.w};
     /* edge iterations: readable bytes [vlo, bhi) and looked-up positions */
     u32 look_m = 0xffffu;
     if (EDGE) {
@@ -993,24 +799,12 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
         const u32 bm = range_mask(rel32(S.vlo - S.blo, q0), r_len);
 #pragma unroll
         for (int w = 0; w < 4; w++) d[w] &= nib_to_bytes(bm >> (4 * w));
-        if (!((bm >> 16) & 1u)) d[4] = 0;
-        look_m = range_mask(rel32((MODE == VSA_MODE_FDR || MODE == VSA_MODE_FDR4) ? S.zbase
-                                                                                 : S.qlo, q0),
-                            r_len);
+        look_m = range_mask(rel32(MODE == VSA_MODE_FDR4 ? S.zbase : S.qlo, q0), r_len);
     }
 
-    /* FDR (LDS table): the lane looks up positions -1 .. 14, keyed by the
-     * byte pairs (j - 1, j), so no key needs the byte after its chunk and
-     * the sweep never waits on the next chunk's load; byte -1 is the previous
-     * lane's last byte (lane 0: the previous chunk's, in.pbytes).  Position
-     * 15 is the next lane's (or chunk's) position -1.  Only field 0 of end -1
-     * is left out: a one-byte constraint on b[e] that field 1 (b[e - 1],
-     * b[e]) implies (derive_fdr_table) — the filter stays a superset. */
-    constexpr bool FDR_BACK = MODE == VSA_MODE_FDR && LDS_TABLE;
-    constexpr bool SWEEP = FDR_BACK && !EDGE;
     constexpr bool F4 = MODE == VSA_MODE_FDR4;
-    /* sweep state in lane-rotated registers (p3 / p4 / p5) */
-    constexpr bool PSTATE = (FDR_BACK || F4) && !EDGE;
+    /* sweep state in lane-rotated registers (p3 / p4) */
+    constexpr bool PSTATE = F4 && !EDGE;
     u32 pv3;
     IterState out;
     if constexpr (PSTATE) {
@@ -1020,15 +814,6 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     } else {
         pv3 = writelane_u32<0>(lane_up1(d[3]), (u32)(in.pbytes >> 32));
     }
-    if constexpr (FDR_BACK) {
-        if (EDGE) look_m = range_mask(rel32(S.zbase, q0) + 1, rel32(S.len, q0) + 1);
-    }
-
-#ifdef VSA_FDR_ONE_LEVEL /* experiment build: every lookup in every lane */
-    constexpr bool TWO_LVL = false;
-#else
-    constexpr bool TWO_LVL = true;
-#endif
     u32 c[T::CW];
     out.ncand = in.ncand;
     out.tail_cache = in.tail_cache;
@@ -1047,11 +832,11 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
          * next lane's ends 0..2 (lane 63: the next chunk's) */
         u32 U[5];
         fdr4_conf<EDGE>(L, {d[0], d[1], d[2], d[3]}, pv3, look_m, U);
-        /* split passes (runtime.hip, large sets): this pass's ends are those
-         * whose byte has bit 0 == end_par - 1; the others are the other
-         * pass's, dead here (a uniform branch, off in one-pass scans) */
+        /* split passes (runtime.hip, large sets; their own kernels): this
+         * pass's ends are those whose byte has bit 0 == end_par - 1; the
+         * others are the other pass's, dead here */
         auto split_mask = [&]() {
-            if (P.end_par) {
+            if constexpr (SPLIT) {
                 const u32 fl = P.end_par == 1 ? 0u : 0x01010101u;
 #pragma unroll
                 for (int w = 0; w < 4; w++) {
@@ -1069,86 +854,28 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
             /* lane 0: the previous chunk's lane-63 U[4], rotated in last time */
             U[0] |= lane_up1_or_old(in.p4, U[4]);
             out.p4 = lane_ror1(U[4]);
-            out.p5 = in.p5;
             split_mask();
             const u32 nbm = ~bucket_mask;
-            if (!__any(((U[0] & U[1] & U[2] & U[3]) | nbm) != 0xffffffffu)) return out;
+            if (!wave_any(((U[0] & U[1] & U[2] & U[3]) | nbm) != 0xffffffffu)) return out;
         }
 #pragma unroll
         for (int w = 0; w < 4; w++) c[w] = U[w];
-    } else if constexpr (SWEEP) {
-        /* interior FDR iteration (fdr_sweep_conf): the candidate test runs on
-         * the unshifted dwords (this lane's ends are U[0] bytes 1..3, U[1..3]
-         * and U[4] byte 0); the shift to end order is done only for a push */
-        u32 U[6];
-        out.p4 = in.p4;
-        out.p5 = in.p5;
-        fdr_sweep_conf<TWO_LVL>(L, {d[0], d[1], d[2], d[3]}, pv3, out.p4, out.p5, U);
-        const u32 nbm = ~bucket_mask;
-        /* this lane's ends: U[0] bytes 1..3 and U[4] byte 0 (one v_bfi) */
-        const u32 a123 = U[1] & U[2] & U[3];
-        u32 a04;
-        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(a04) : "s"(0xffu), "v"(U[4]), "v"(U[0]));
-        if (!__any(((a04 & a123) | nbm) != 0xffffffffu)) return out;
-#pragma unroll
-        for (int w = 0; w < 4; w++) c[w] = __builtin_amdgcn_alignbyte(U[w + 1], U[w], 1);
     } else {
-    /* own contributions: the lane's 16 lookups ... */
+    /* Teddy / Fat Teddy: the lane's 16 lookups ... */
     S_t x[16];
-    u32 km[4], ko[4]; /* FDR/LDS: keys of even / odd positions, two per dword */
-    if constexpr (FDR_BACK) {
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-            /* km: positions 4w, 4w + 2; ko: 4w - 1, 4w + 1 */
-            const u32 zw = d[w] & 0x7f7f7f7fu;
-            const u32 zp = w ? d[w - 1] & 0x7f7f7f7fu : pv3;
-            km[w] = fdr_key2(zw, L.kf, L.kshift2);
-            ko[w] = fdr_key2(__builtin_amdgcn_alignbyte(zw, zp, 3), L.kf, L.kshift2);
-        }
-    }
 #pragma unroll
     for (int j = 0; j < 16; j++) {
-        if constexpr (FDR_BACK) {
-            /* x[j] = position j - 1 = 4w + r - 1: ko[w] (r even) or km[w]
-             * (r odd), 16-bit half r >> 1 */
-            const u32 kw = (j & 1) ? km[j >> 2] : ko[j >> 2];
-            const u32 a = (j & 2) ? tab_addr16<1>(kw, L.tab_lds) : tab_addr16<0>(kw, L.tab_lds);
-            x[j] = lds_ld64(a);
-        } else if constexpr (MODE == VSA_MODE_TEDDY || MODE == VSA_MODE_FAT) {
-            /* byte r of d[w] -> address byte 1, L.tsel = 0x10000 | lane slot */
-            const u32 sel = 0x0c020000u | ((4u + (j & 3)) << 8);
-            const u32 a = __builtin_amdgcn_perm(d[j >> 2], L.tsel, sel);
-            x[j] = lds_ld64(a);
-        } else {
-            u32 key = lit_key<MODE>(d, j, P.dmask);
-            x[j] = (S_t)lit_lookup<MODE, LDS_TABLE>(L.tab, key, lane);
-        }
+        /* byte r of d[w] -> address byte 1, L.tsel = 0x10000 | lane slot */
+        const u32 sel = 0x0c020000u | ((4u + (j & 3)) << 8);
+        const u32 a = __builtin_amdgcn_perm(d[j >> 2], L.tsel, sel);
+        x[j] = lds_ld64(a);
         if (EDGE) {
             if (!((look_m >> j) & 1u)) x[j] = 0;
         }
     }
-#ifdef VSA_EXTRA_VALU
-    /* experiment build: VSA_EXTRA_VALU dependent VALU ops per iteration */
-#pragma unroll
-    for (int i = 0; i < VSA_EXTRA_VALU; i++) asm volatile("v_or_b32 %0, %0, %0" : "+v"(d[i & 3]));
-#endif
     /* ... OR-ed into place: field k of x[j] lands on end j + k */
     u64 s_out;
     conf_accumulate<MODE>(x, c, s_out);
-    if constexpr (FDR_BACK) {
-        /* x[j] sat at position j - 1: every end one byte down (end -1, the
-         * byte shifted out, held only field 0 of position -1) */
-        const u32 f4 = (u32)s_out, f5 = (u32)(s_out >> 32);
-        const u32 c0 = __builtin_amdgcn_alignbyte(c[1], c[0], 1);
-        const u32 c1 = __builtin_amdgcn_alignbyte(c[2], c[1], 1);
-        const u32 c2 = __builtin_amdgcn_alignbyte(c[3], c[2], 1);
-        const u32 c3 = __builtin_amdgcn_alignbyte(f4, c[3], 1);
-        c[0] = c0;
-        c[1] = c1;
-        c[2] = c2;
-        c[3] = c3;
-        s_out = ((u64)(f5 >> 8) << 32) | __builtin_amdgcn_alignbyte(f5, f4, 1);
-    }
     /* spill from the previous lane (lane 0: from the previous chunk) */
     const u32 s_in_lo = writelane_u32<0>(lane_up1((u32)s_out), (u32)in.carry);
     const u32 s_in_hi = sizeof(S_t) == 8
@@ -1159,9 +886,9 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
                 readlane_u32((u32)s_out, WAVE - 1);
     c[0] |= (u32)s_in;
     if constexpr (sizeof(S_t) == 8) c[1] |= (u32)(s_in >> 32);
-    } /* one-level lookups */
+    } /* Teddy lookups */
     if (EDGE) {
-        if constexpr (MODE == VSA_MODE_FDR || MODE == VSA_MODE_FDR4) if (!S.stream) {
+        if constexpr (MODE == VSA_MODE_FDR4) if (!S.stream) {
             /* start state: byte i applies to end start + i (the short zone
              * shifts fdr->start by 16 - (len - start) against a scan from
              * len - 16, fdr.c:372-440 and :712-720, landing on start too):
@@ -1194,7 +921,7 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     u32 all = c[0];
 #pragma unroll
     for (int i = 1; i < T::CW; i++) all &= c[i];
-    if (!__any((all | ~bucket_mask) != 0xffffffffu)) return out;
+    if (!wave_any((all | ~bucket_mask) != 0xffffffffu)) return out;
     u32 any = 0;
 #pragma unroll
     for (int i = 0; i < T::CW; i++) {
@@ -1285,7 +1012,7 @@ __device__ __forceinline__ IterState nood_iter(const VsaLitParams &P, const LitS
             const u32 t = or3((d[k] & M2) ^ C2, (p1 & M1) ^ C1, (p2 & M0) ^ C0);
             z |= (t - 0x01010101u) & ~t;
         }
-        if (!__any((z & 0x80808080u) != 0)) return out;
+        if (!wave_any((z & 0x80808080u) != 0)) return out;
     }
     const u32 w[6] = {pv2, pv3, d[0], d[1], d[2], d[3]};
     const u32 mlo = (u32)P.nood_msk, mhi = (u32)(P.nood_msk >> 32);
@@ -1311,22 +1038,22 @@ __device__ __forceinline__ IterState nood_iter(const VsaLitParams &P, const LitS
         const int64_t elo = S.start + (int64_t)P.nood_len - 1 + S.qlo;
         hits &= range_mask(rel32(elo > S.rlo ? elo : S.rlo, q0), rel32(S.len, q0));
     }
-    if (!__any(hits != 0)) return out;
+    if (!wave_any(hits != 0)) return out;
     const u64 meta = (u64)p0 | ((u64)S.blk << ENT_BLK_SHIFT);
     const u32 ent[8] = {(u32)meta, (u32)(meta >> 32), 0, 0, hits, 0, 0, 0};
     ring_push<2>(L, out, hits != 0, ent);
     return out;
 }
 
-template <int MODE, bool LDS_TABLE, bool EDGE, bool XP>
+template <int MODE, bool EDGE, bool XP, bool SPLIT>
 __device__ __forceinline__ IterState scan_iter(const VsaLitParams &P, const ConfLds &cl,
                                                const LitShared &L, const SegCtx &S,
                                                u32 mis, int64_t ib, uint4 chunk,
-                                               u32 nxt0, IterState in, u32 bucket_mask) {
+                                               IterState in, u32 bucket_mask) {
     if constexpr (MODE == VSA_MODE_NOOD) {
         return nood_iter<EDGE>(P, L, S, ib, chunk, in);
     } else {
-        return lit_iter<MODE, LDS_TABLE, EDGE, XP>(P, cl, L, S, mis, ib, chunk, nxt0, in,
+        return lit_iter<MODE, EDGE, XP, SPLIT>(P, cl, L, S, mis, ib, chunk, in,
                                                    bucket_mask);
     }
 }
@@ -1367,9 +1094,10 @@ __device__ __forceinline__ uint4 load_wave_kib(const u8 *base, u32 off) {
     return make_uint4(t.x, t.y, t.z, t.w);
 }
 
-#ifndef LIT_DEPTH
 #define LIT_DEPTH 4 /* chunks in flight per scanning wave (1 KiB each) */
-#endif
+/* s_waitcnt immediate (gfx9 encoding): vmcnt 0, expcnt and lgkmcnt left at
+ * their maximum (no wait) */
+#define VMCNT0 0x0f70
 
 /* A workgroup's confirm wave (one, or several for large literal sets, each
  * serving every nc-th ring): gathers up to 64 chunk entries per round from
@@ -1541,22 +1269,16 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                         P.out_keys[slot] = key;
                         P.out_ids[slot] = P.nood_id;
                     }
-                    if (P.bin_counts) {
+                    if (P.bin_slots) {
+                        /* staged binned sort (vsa_bin_finish) */
                         const u32 bin = (u32)((p0 + j - mis) >> P.bin_shift);
-                        if (P.bin_slots) {
-                            /* staged binned sort (vsa_bin_finish) */
-                            const u32 s = __hip_atomic_fetch_add(&P.bin_counts[bin], 1u,
-                                                                 __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_AGENT);
-                            if (s < VSA_SORT_BIN_MAX) {
-                                P.bin_slots[(size_t)bin * VSA_SORT_BIN_MAX + s] = (u32)slot;
-                            } else {
-                                P.counters[VSA_CTR_BIN_OVERFLOW] = 1;
-                            }
-                        } else {
-                            __hip_atomic_fetch_add(&P.bin_counts[bin], 1u, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-                        }
+                        const u32 s = __hip_atomic_fetch_add(&P.bin_counts[bin], 1u,
+                                                             __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+                        if (s < VSA_SORT_BIN_MAX)
+                            P.bin_slots[(size_t)bin * VSA_SORT_BIN_MAX + s] = (u32)slot;
+                        else
+                            P.counters[VSA_CTR_BIN_OVERFLOW] = 1;
                     }
                 }
             }
@@ -1679,7 +1401,7 @@ __device__ __forceinline__ void stage_lds(TV *dst, u32 n, u32 tid, F &&src) {
     }
 }
 
-template <int MODE, bool LDS_TABLE, bool XP>
+template <int MODE, bool XP, bool SPLIT>
 __global__ void __launch_bounds__(LIT_THREADS)
 vsa_lit_scan(VsaLitParams P) {
     typedef LitTraits<MODE> T;
@@ -1693,7 +1415,6 @@ vsa_lit_scan(VsaLitParams P) {
      * current segment it has not claimed yet: seg << 40 | end << 20 | cur
      * (groups of LIT_DEPTH iterations; cur = the next group to claim) */
     __shared__ unsigned long long rng[16];
-    __shared__ u32 pool_drained; /* pool regions this workgroup found empty */
     __shared__ u64 prof_lds[8 * MAX_CONF_WAVES]; /* confirm-wave profile (dbg & 64) */
     const u32 tid = threadIdx.x;
     const u32 lane = lane_id();
@@ -1706,15 +1427,11 @@ vsa_lit_scan(VsaLitParams P) {
     /* ---- stage tables into LDS ---- */
     u32 tab_bytes = 0;
     const void *tab;
-    if constexpr (MODE == VSA_MODE_FDR || MODE == VSA_MODE_FDR4) {
-        if (LDS_TABLE) {
-            tab_bytes = P.table_entries * (MODE == VSA_MODE_FDR4 ? 4 : 8);
-            const uint4 *src = (const uint4 *)P.table;
-            stage_lds<8>((uint4 *)smem, tab_bytes / 16, tid, [&](u32 i) { return src[i]; });
-            tab = smem;
-        } else {
-            tab = P.table;
-        }
+    if constexpr (MODE == VSA_MODE_FDR4) {
+        tab_bytes = P.table_entries * 4;
+        const uint4 *src = (const uint4 *)P.table;
+        stage_lds<8>((uint4 *)smem, tab_bytes / 16, tid, [&](u32 i) { return src[i]; });
+        tab = smem;
     } else if constexpr (MODE == VSA_MODE_NOOD) {
         tab = nullptr;
     } else {
@@ -1764,7 +1481,6 @@ vsa_lit_scan(VsaLitParams P) {
     if (tid == 0) {
         q_done = 0;
         wg_ctr = 0;
-        pool_drained = 0;
         /* the schedule's feedback (runtime.hip xcd_feedback): this
          * workgroup's entry time */
         if (P.wg_time) P.wg_time[gridDim.x + blockIdx.x] = t_entry;
@@ -1775,7 +1491,6 @@ vsa_lit_scan(VsaLitParams P) {
     const u32 mis = (u32)((uintptr_t)P.data & 15);
     if (wave >= NS) {
         const u32 cw = wave - NS;
-#ifndef VSA_EXP_NO_CONFIRM /* experiment: VGPR use of the scanning path alone */
         if (NC == 1)
             confirm_wave<MODE, 4, XP>(P, cl, rings, 31 - __clz(P.qcap), q_tails, q_heads, &q_done,
                                   mis, slots, pqx, 0, 1, prof_lds);
@@ -1783,7 +1498,6 @@ vsa_lit_scan(VsaLitParams P) {
             confirm_wave<MODE, 2, XP>(P, cl, rings, 31 - __clz(P.qcap), q_tails, q_heads, &q_done,
                                   mis, slots, pqx + (size_t)cw * PQ_ENTRIES(2), cw, NC,
                                   prof_lds + 8 * cw);
-#endif
         if ((P.dbg & 8192) && P.wave_log && lane < 8) {
             /* diagnostic: a confirm wave's entry and end */
             const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
@@ -1809,9 +1523,6 @@ vsa_lit_scan(VsaLitParams P) {
     LitShared L;
     L.tab = tab;
     L.tab_lds = (u32)(uintptr_t)(lds_u8_t *)smem;
-    /* fdr_key2's parameters for the table's key width (vsa_fdr_key) */
-    L.kf = P.dmask == 0x1fffu ? 0x003f003fu : 0x007f007fu;
-    L.kshift2 = P.dmask == 0x1fffu ? 0x00020002u : 0x00010001u;
     L.tsel = TEDDY_TAB_LDS | ((lane & 31) << 3);
     L.ring = rings + (size_t)wave * P.qcap * REW;
     L.slots = slots;
@@ -1831,64 +1542,36 @@ vsa_lit_scan(VsaLitParams P) {
      * and segments, flushed before the wave ends */
     u32 xp_s[4] = {0, 0, 0, 0}, xp_n = 0;
 
-    /* Segment scheduling.  The segments are split into NREG contiguous
-     * regions; workgroup b works in region b % NREG first (workgroups are
-     * dispatched round-robin over the 8 XCDs, so a region streams through
-     * one XCD's L2 and the segments in flight stay adjacent in memory), taking
-     * segments by atomic ticket from the region's own counter, then moves on
-     * to the next regions when its own is exhausted (balancing across CUs).
-     * One ticket address per region keeps the atomics from serializing the
-     * grid (a single-address ticket capped streaming at ~4.4 TB/s,
-     * tools/probe_stream.hip).  P.dynamic == 0: plain static assignment
-     * (wave g takes g, g + G, ...).
-     * P.dynamic == 2 (the default): workgroup b owns the host-built list
-     * [wg_seg[b], wg_seg[b + 1]) -- an equal share of the bytes (runtime.hip
-     * build_plan) -- and its scanning waves take the next segment from an
-     * LDS counter: no global atomics at all (dynamic tickets measured 50
-     * us of contention at 32 MiB and ~0.15 us of CU time per segment at 4
-     * GiB, profiles/r04c_launch_sweep.jsonl).  The CU's waves, whose issue
-     * rates differ ~3x by age, balance by stealing sweep groups from each
-     * other (below), so a large block is cut into one segment per wave;
-     * without stealing (VSA_STEAL=0) the list's segments shrink toward its
-     * end instead (guided sizes). */
-    const u64 G = (u64)gridDim.x * NS;
-    const u32 sched = P.dynamic;
-    const u32 nreg = sched == 1 ? P.nregions : 1u;
-    u32 reg_i = 0; /* regions tried so far */
-    u32 reg = blockIdx.x % nreg;
-    auto region_lo = [&](u32 r) { return P.nsegs * r / nreg; };
-    /* the next ticket is taken (lane 0, returning atomic) during the last
-     * group of the current segment's sweep, so its latency hides behind
-     * that group without one wave holding a whole segment ahead */
+    /* Segment scheduling: workgroup b owns the host-built list [wg_seg[b],
+     * wg_seg[b + 1]) -- an equal share of the bytes (runtime.hip build_plan)
+     * -- and its scanning waves take the next segment from an LDS counter:
+     * no global atomics in the sweep (dynamic tickets measured 50 us of
+     * contention at 32 MiB and ~0.15 us of CU time per segment at 4 GiB,
+     * profiles/r04c_launch_sweep.jsonl; and a returning global atomic in
+     * the sweep loop made the compiler wait for every chunk in flight,
+     * vmcnt(0), at each group start).  The CU's waves, whose issue rates
+     * differ ~3x by age, balance by stealing sweep groups from each other
+     * (below), so a large block is cut into one segment per wave; without
+     * stealing (VSA_STEAL=0) the list's segments shrink toward its end
+     * instead (guided sizes). */
+    /* the next ticket is taken (lane 0, LDS atomic) during the last group of
+     * the current segment's sweep, so its latency hides behind that group
+     * without one wave holding a whole segment ahead */
     auto take = [&]() -> u32 {
         u32 t = 0;
-        if (sched == 2) {
-            if (lane == 0)
-                t = __hip_atomic_fetch_add(&wg_ctr, 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else if (lane == 0) {
-            t = (u32)atomicAdd(&P.counters[16 + 16 * reg], 1ULL);
-        }
+        if (lane == 0)
+            t = __hip_atomic_fetch_add(&wg_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         return t;
     };
     auto resolve = [&](u32 t0) -> u32 {
-        u32 t = readlane_u32(t0, 0);
-        if (sched == 2) {
-            /* reloaded per segment (scalar loads) rather than held: the
-             * sweep needs the SGPRs */
-            const u32 wg_lo = readfirstlane_u32(P.wg_seg[blockIdx.x]);
-            const u32 wg_hi = readfirstlane_u32(P.wg_seg[blockIdx.x + 1]);
-            return wg_lo + t < wg_hi ? wg_lo + t : (u32)P.nsegs;
-        }
-        for (;;) {
-            const u64 sg = region_lo(reg) + t;
-            if (sg < region_lo(reg + 1)) return (u32)sg;
-            if (++reg_i == nreg) return (u32)P.nsegs; /* every region drained */
-            reg = (reg + 1) % nreg;
-            t = readlane_u32(take(), 0);
-        }
+        const u32 t = readlane_u32(t0, 0);
+        /* reloaded per segment (scalar loads) rather than held: the sweep
+         * needs the SGPRs */
+        const u32 wg_lo = readfirstlane_u32(P.wg_seg[blockIdx.x]);
+        const u32 wg_hi = readfirstlane_u32(P.wg_seg[blockIdx.x + 1]);
+        return wg_lo + t < wg_hi ? wg_lo + t : (u32)P.nsegs;
     };
-    /* Work stealing inside the workgroup (dynamic 2, P.steal): a wave whose
+    /* Work stealing inside the workgroup (P.steal): a wave whose
      * list is exhausted takes the back half of the unclaimed sweep groups of
      * the scanning wave with the most left (one LDS compare-and-swap on the
      * victim's rng word; the victim claims each next group with an LDS
@@ -1897,21 +1580,20 @@ vsa_lit_scan(VsaLitParams P) {
      * the range start, and the segment's last checked iterations when its
      * range reaches the segment end.  Only parts of one block (not packed
      * groups or runs) are stolen. */
-    const bool steal_on = sched == 2 && P.steal != 0;
+    const bool steal_on = P.steal != 0;
     auto steal = [&](u32 &sg, u32 &gs, u32 &ge) -> bool {
         for (int tries = 0; tries < 64; tries++) {
             unsigned long long w = 0;
             if (lane < NS) w = rng[lane];
             const u32 c = (u32)w & 0xfffffu, e = (u32)(w >> 20) & 0xfffffu;
-            /* P.steal_w (VSA_STEAL_W, on): a victim's unclaimed groups count
-             * by its issue age (younger waves issue slower: x1 / 1.25 / 1.5 /
-             * 2.25 for waves 0-3 / 4-7 / 8-11 / 12+, quarter units; the
-             * per-wave rates of profiles/r04e_waves_4g.txt), and the thief
-             * takes the share that would end both together.  Measured
-             * (profiles/r04m_sweep.jsonl, kernel us, twice each): 4 GiB
-             * 850 / 848 against 864 / 857, 1 GiB 242 / 241 against 244 /
-             * 246, 512 MiB 136 / 137 against 137 / 138 */
-            const u32 wt = P.steal_w ? (lane < 4 ? 4u : lane < 8 ? 5u : lane < 12 ? 6u : 9u) : 4u;
+            /* a victim's unclaimed groups count by its issue age (younger
+             * waves issue slower: x1 / 1.25 / 1.5 / 2.25 for waves 0-3 / 4-7
+             * / 8-11 / 12+, quarter units; the per-wave rates of
+             * profiles/r04e_waves_4g.txt), and the thief takes the share that
+             * would end both together.  Measured against equal weights
+             * (profiles/r04m_sweep.jsonl, kernel us, twice each): 4 GiB 850 /
+             * 848 against 864 / 857, 1 GiB 242 / 241 against 244 / 246 */
+            const u32 wt = lane < 4 ? 4u : lane < 8 ? 5u : lane < 12 ? 6u : 9u;
             u32 best = e > c ? (e - c) * wt : 0u;
             const u32 mine = best;
 #pragma unroll
@@ -1927,13 +1609,10 @@ vsa_lit_scan(VsaLitParams P) {
                 ((unsigned long long)readlane_u32((u32)(w >> 32), (int)v) << 32) |
                 readlane_u32((u32)w, (int)v);
             const u32 vc = (u32)wv & 0xfffffu, ve = (u32)(wv >> 20) & 0xfffffu;
-            u32 mid = vc + (ve - vc + 1) / 2;
-            if (P.steal_w) {
-                const u32 wv_ = v < 4 ? 4u : v < 8 ? 5u : v < 12 ? 6u : 9u;
-                const u32 wt_ = wave < 4 ? 4u : wave < 8 ? 5u : wave < 12 ? 6u : 9u;
-                mid = ve - ((ve - vc) * wv_ + (wv_ + wt_) / 2) / (wv_ + wt_);
-                mid = mid < ve ? mid : ve - 1; /* the thief takes at least one */
-            }
+            const u32 wv_ = v < 4 ? 4u : v < 8 ? 5u : v < 12 ? 6u : 9u;
+            const u32 wt_ = wave < 4 ? 4u : wave < 8 ? 5u : wave < 12 ? 6u : 9u;
+            u32 mid = ve - ((ve - vc) * wv_ + (wv_ + wt_) / 2) / (wv_ + wt_);
+            mid = mid < ve ? mid : ve - 1; /* the thief takes at least one */
             const unsigned long long nw = (wv & ~(0xfffffULL << 20)) | ((unsigned long long)mid << 20);
             unsigned long long old = wv;
             if (lane == 0)
@@ -1950,62 +1629,24 @@ vsa_lit_scan(VsaLitParams P) {
         }
         return false;
     };
-    /* The shared pool (dynamic 2): segments [wg_seg[G], nsegs) in 8
-     * regions of tickets (counters[16 + 16 r]), this workgroup's XCD region
-     * first; a region found empty is remembered in LDS, so a workgroup walks
-     * the drained regions once, not once per wave. */
-    auto pool_take = [&]() -> u32 {
-        const u32 pool_lo = readfirstlane_u32(P.wg_seg[gridDim.x]);
-        const u32 npool = (u32)P.nsegs - pool_lo;
-        u32 r = blockIdx.x & 7u;
-        for (int i = 0; npool && i < 8; i++, r = (r + 1) & 7u) {
-            if ((lds_ld32(&pool_drained) >> r) & 1u) continue;
-            unsigned long long t0 = 0;
-            if (lane == 0) t0 = atomicAdd(&P.counters[16 + 16 * r], 1ULL);
-            const u64 t = ((u64)readlane_u32((u32)(t0 >> 32), 0) << 32) | readlane_u32((u32)t0, 0);
-            const u64 lo = pool_lo + (u64)npool * r / 8, hi = pool_lo + (u64)npool * (r + 1) / 8;
-            if (lo + t < hi) {
-                if ((P.dbg & 16384) && P.wave_log && lane == 0) {
-                    /* diagnostic: pool take events (time, workgroup, wave,
-                     * segment) after the per-wave records */
-                    unsigned long long *ev = (unsigned long long *)P.wave_log + 65536;
-                    const unsigned long long k = atomicAdd(&ev[-1], 1ULL);
-                    if (k < 16000) {
-                        ev[4 * k] = __builtin_amdgcn_s_memrealtime();
-                        ev[4 * k + 1] = blockIdx.x;
-                        ev[4 * k + 2] = wave;
-                        ev[4 * k + 3] = lo + t;
-                    }
-                }
-                return (u32)(lo + t);
-            }
-            if (lane == 0)
-                __hip_atomic_fetch_or(&pool_drained, 1u << r, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        return (u32)P.nsegs;
-    };
     /* segment indices are 32-bit (the plan's descriptors; the kernel's
      * SGPRs are scarce) */
-    u32 seg = sched ? resolve(take()) : blockIdx.x * NS + wave;
+    u32 seg = resolve(take());
     u32 st_gs = 0, st_ge = 0; /* a stolen range: sweep groups [st_gs, st_ge) */
     bool from_list = true;     /* seg came from the workgroup's list */
     for (;;) {
         bool stolen = false;
         if (seg >= P.nsegs) {
-            /* out of list work: help the workgroup's waves, then the pool,
-             * then (the pool empty) the workgroup again */
+            /* out of list work: help the workgroup's waves */
             from_list = false;
             if (steal_on && steal(seg, st_gs, st_ge)) stolen = true;
-            else if (sched == 2 && (seg = pool_take()) < P.nsegs) stolen = false;
-            else if (steal_on && steal(seg, st_gs, st_ge)) stolen = true;
             else break;
         }
         u32 t_next = 0;
         bool have_next = false;
         bool lastb = true;
         auto prefetch_ticket = [&]() {
-            if (sched && !have_next && lastb) {
+            if (!have_next && lastb) {
                 t_next = take();
                 have_next = true;
             }
@@ -2093,7 +1734,7 @@ vsa_lit_scan(VsaLitParams P) {
         const int64_t s_hi =
             (!gcount && s_lo + ((int64_t)d_len << 10) < S.bhi) ? s_lo + ((int64_t)d_len << 10) : S.bhi;
         const u32 niters = (u32)((s_hi - s_lo + 1023) >> 10);
-        const int64_t zlo = (MODE == VSA_MODE_FDR || MODE == VSA_MODE_FDR4) ? B.zbase : S.qlo;
+        const int64_t zlo = MODE == VSA_MODE_FDR4 ? B.zbase : S.qlo;
 
         /* iterations [f0, f1) are interior ("fast"): no byte of the 1 KiB
          * chunk or its successor byte lies outside the block, and the FDR
@@ -2112,7 +1753,6 @@ vsa_lit_scan(VsaLitParams P) {
         const u32 nf = f1 - f0;
         const int64_t fb = s_lo + 1024 * (int64_t)f0;
         uint4 ring[LIT_DEPTH];
-        u32 after = 0;
         /* The range's first loads are issued together: the prologue bytes,
          * the first checked iteration's chunk (ring[0]) and, when there is
          * no sweep, the last checked iteration's chunk (ring[1]), so a small
@@ -2130,7 +1770,6 @@ vsa_lit_scan(VsaLitParams P) {
         const int64_t pp = pro_lo - (T::NL - 1) + (int64_t)lane;
         const bool pro1_in = pro1 && pp - S.blo >= zlo && pp - S.blo < S.len;
         const u8 pb0 = pro1_in ? load_byte_masked(A, pp, S.vlo, S.bhi) : (u8)0;
-        const u8 pb1 = (T::KEY16 && pro1_in) ? load_byte_masked(A, pp + 1, S.vlo, S.bhi) : (u8)0;
         /* FDR4 keys also need the two bytes before each position: issued
          * with the others (one memory round trip for the whole prologue) */
         const bool F4P = MODE == VSA_MODE_FDR4;
@@ -2147,16 +1786,13 @@ vsa_lit_scan(VsaLitParams P) {
 #pragma unroll
             for (int k = 0; k < LIT_DEPTH; k++)
                 ring[k] = load_wave_kib(sb, it0 + (u32)k < nf ? 1024u * (it0 + k) : 1024u * it0);
-            after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.vlo, S.bhi);
         }
-        u32 nxt_f = 0, nxt_t = 0;
         if (!early) {
             ring[0] = make_uint4(0, 0, 0, 0);
             ring[1] = make_uint4(0, 0, 0, 0);
         }
         if (f0 > 0 && !stolen) {
             ring[0] = load_chunk(A, s_lo + 16 * (int64_t)lane, S.bhi);
-            nxt_f = load_byte_masked(A, s_lo + 1024, S.vlo, S.bhi);
         }
         /* the tail's first chunk is preloaded only without a sweep (f1 is
          * then max(f0, ...) and the tail starts right after the f0 loop) */
@@ -2164,7 +1800,6 @@ vsa_lit_scan(VsaLitParams P) {
         if (tail_pre) {
             const int64_t ibt = s_lo + 1024 * (int64_t)f1;
             ring[1] = load_chunk(A, ibt + 16 * (int64_t)lane, S.bhi);
-            nxt_t = load_byte_masked(A, ibt + 1024, S.vlo, S.bhi);
         }
         /* prologue 1: table spill from positions s_lo-NL+1 .. s_lo-1 */
         IterState is;
@@ -2178,11 +1813,9 @@ vsa_lit_scan(VsaLitParams P) {
             S_t x = 0;
             if (pro1_in) {
                 u32 key;
-                if constexpr (T::KEY16) key = vsa_fdr_key(pb0, pb1, P.dmask);
-                else if constexpr (MODE == VSA_MODE_FDR4)
-                    key = vsa_fdr4_key(pm2, pm1, pb0, 15u);
+                if constexpr (MODE == VSA_MODE_FDR4) key = vsa_fdr4_key(pm2, pm1, pb0);
                 else key = pb0;
-                x = (S_t)lit_lookup<MODE, LDS_TABLE>(tab, key, lane);
+                x = (S_t)lit_lookup<MODE>(tab, key, lane);
                 x >>= T::LB * (pro_lo - pp);
             }
             u64 xv = (u64)x;
@@ -2206,44 +1839,40 @@ vsa_lit_scan(VsaLitParams P) {
         for (u32 it = 0; it < (stolen ? 0u : f0); it++) {
             const int64_t ib = s_lo + 1024 * (int64_t)it;
             uint4 cur = ring[0];
-            u32 nxt0 = nxt_f;
-            if (it > 0) {
-                cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
-                nxt0 = load_byte_masked(A, ib + 1024, S.vlo, S.bhi);
-            }
-            is = scan_iter<MODE, LDS_TABLE, true, XP>(P, cl, L, S, mis, ib, cur, nxt0, is,
-                                                 bucket_mask);
+            if (it > 0) cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
+            is = scan_iter<MODE, true, XP, SPLIT>(P, cl, L, S, mis, ib, cur, is, bucket_mask);
             run_adv(ib);
         }
         bool tail_mine = true; /* a stolen-from range leaves its tail to the thief */
         u32 swept = 0;         /* sweep iterations scanned (diagnostic) */
         if (nf > 0) {
-            if constexpr (MODE == VSA_MODE_FDR && LDS_TABLE) {
-                /* sweep_enter: the carry and the previous chunk's last dword
-                 * move to lane 0 of p3..p5 (IterState) */
-                const u64 cu = is.carry << 8;
-                is.p3 = (u32)(is.pbytes >> 32);
-                is.p4 = (u32)cu;
-                is.p5 = (u32)(cu >> 32);
-            }
             if constexpr (MODE == VSA_MODE_FDR4) {
-                /* the carry (ends 0..2 of the chunk) is U[4]'s form */
+                /* sweep_enter: the carry (ends 0..2 of the chunk, U[4]'s form)
+                 * and the previous chunk's last dword move to lane 0 of p4 /
+                 * p3 (IterState) */
                 is.p3 = (u32)(is.pbytes >> 32);
                 is.p4 = (u32)is.carry;
-                is.p5 = 0;
             }
             /* main sweep: LIT_DEPTH chunks in flight per wave.  ring[k] is
              * consumed and then refilled in place (no register rotation), so
-             * each step waits only for the load issued LIT_DEPTH-1 steps ago
-             * (the next chunk's first byte).  Every load is unconditional (an
+             * each step waits only for its own chunk, the load issued
+             * LIT_DEPTH steps ago.  Every load is unconditional (an
              * out-of-range prefetch re-reads the current chunk) so the wait
              * counters stay exact. */
             /* segment base in SGPRs, 32-bit offsets */
+            /* Nothing but the sweep's own chunks in flight when it starts
+             * (an early range's were issued with its prologue, long done;
+             * otherwise they are issued right below): the compiler's wait
+             * bookkeeping then sees the same LIT_DEPTH loads, in the same
+             * order, on every way into the loop and waits vmcnt(LIT_DEPTH
+             * - 1) per iteration.  Without this it merged the paths into a
+             * vmcnt(0) at every group start: each group waited for the load
+             * issued just before it. */
+            __builtin_amdgcn_s_waitcnt(VMCNT0);
             if (!early) {
 #pragma unroll
                 for (int k = 0; k < LIT_DEPTH; k++)
                     ring[k] = load_wave_kib(sb, (u32)k < nf ? 1024u * k : 0u);
-                after = load_byte_masked(A, fb + 1024 * (int64_t)nf, S.vlo, S.bhi);
             }
             /* the groups this wave scans: all (or the stolen [gs, ge));
              * with stealing on, each next group is claimed one group ahead
@@ -2262,10 +1891,7 @@ vsa_lit_scan(VsaLitParams P) {
                 for (int k = 0; k < LIT_DEPTH; k++) {
                     const u32 it = g * LIT_DEPTH + k;
                     const int64_t ib = fb + 1024 * (int64_t)it;
-                    const u32 nb = readlane_u32(ring[(k + 1) % LIT_DEPTH].x, 0);
-                    const u32 nxt0 = (it + 1 < nf) ? nb : after;
-                    is = scan_iter<MODE, LDS_TABLE, false, XP>(P, cl, L, S, mis, ib, ring[k], nxt0,
-                                                          is, bucket_mask);
+                    is = scan_iter<MODE, false, XP, SPLIT>(P, cl, L, S, mis, ib, ring[k], is, bucket_mask);
                     run_adv(ib);
                     const u32 itn = (it + LIT_DEPTH < nf) ? it + LIT_DEPTH : it;
                     ring[k] = load_wave_kib(sb, 1024u * itn);
@@ -2290,19 +1916,12 @@ vsa_lit_scan(VsaLitParams P) {
                 if ((u32)k < rem) {
                     const u32 it = ng * LIT_DEPTH + k;
                     const int64_t ib = fb + 1024 * (int64_t)it;
-                    const u32 nb = readlane_u32(ring[(k + 1) % LIT_DEPTH].x, 0);
-                    const u32 nxt0 = (it + 1 < nf) ? nb : after;
-                    is = scan_iter<MODE, LDS_TABLE, false, XP>(P, cl, L, S, mis, ib, ring[k], nxt0,
-                                                          is, bucket_mask);
+                    is = scan_iter<MODE, false, XP, SPLIT>(P, cl, L, S, mis, ib, ring[k], is, bucket_mask);
                     run_adv(ib);
                 }
             }
-            if constexpr (MODE == VSA_MODE_FDR && LDS_TABLE) {
-                /* sweep_leave: back to the scalar carry / pbytes */
-                is.pbytes = ((u64)readlane_u32(is.p3, 0) << 32) | (u32)is.pbytes;
-                is.carry = (((u64)readlane_u32(is.p5, 0) << 32) | readlane_u32(is.p4, 0)) >> 8;
-            }
             if constexpr (MODE == VSA_MODE_FDR4) {
+                /* sweep_leave: back to the scalar carry / pbytes */
                 is.pbytes = ((u64)readlane_u32(is.p3, 0) << 32) | (u32)is.pbytes;
                 is.carry = readlane_u32(is.p4, 0);
             }
@@ -2311,13 +1930,8 @@ vsa_lit_scan(VsaLitParams P) {
         for (u32 it = f1; tail_mine && it < niters; it++) {
             const int64_t ib = s_lo + 1024 * (int64_t)it;
             uint4 cur = ring[1];
-            u32 nxt0 = nxt_t;
-            if (it > f1 || !tail_pre) {
-                cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
-                nxt0 = load_byte_masked(A, ib + 1024, S.vlo, S.bhi);
-            }
-            is = scan_iter<MODE, LDS_TABLE, true, XP>(P, cl, L, S, mis, ib, cur, nxt0, is,
-                                                 bucket_mask);
+            if (it > f1 || !tail_pre) cur = load_chunk(A, ib + 16 * (int64_t)lane, S.bhi);
+            is = scan_iter<MODE, true, XP, SPLIT>(P, cl, L, S, mis, ib, cur, is, bucket_mask);
             run_adv(ib);
         }
         n_iter += (stolen ? 0u : f0) + swept + (tail_mine ? niters - f1 : 0u);
@@ -2329,9 +1943,8 @@ vsa_lit_scan(VsaLitParams P) {
         xp_n = is.xn;
         } /* blocks of the segment */
         n_seg++;
-        /* after a stolen range or a pool segment, the list is known to be
-         * exhausted */
-        seg = (stolen || !from_list) ? (u32)P.nsegs : sched ? resolve(t_next) : seg + (u32)G;
+        /* after a stolen range, the list is known to be exhausted */
+        seg = (stolen || !from_list) ? (u32)P.nsegs : resolve(t_next);
     }
     if constexpr (XP) {
         /* the last batch of expanded candidates, before this wave's done */
@@ -2381,153 +1994,22 @@ vsa_lit_scan(VsaLitParams P) {
         atomicAdd(&P.counters[2], (unsigned long long)ncand_total);
 }
 
-template __global__ void vsa_lit_scan<VSA_MODE_FDR, true, false>(VsaLitParams);
-template __global__ void vsa_lit_scan<VSA_MODE_FDR, true, true>(VsaLitParams);
+template __global__ void vsa_lit_scan<VSA_MODE_FDR4, false, false>(VsaLitParams);
 template __global__ void vsa_lit_scan<VSA_MODE_FDR4, true, false>(VsaLitParams);
+template __global__ void vsa_lit_scan<VSA_MODE_FDR4, false, true>(VsaLitParams);
 template __global__ void vsa_lit_scan<VSA_MODE_FDR4, true, true>(VsaLitParams);
-template __global__ void vsa_lit_scan<VSA_MODE_FDR, false, false>(VsaLitParams);
-template __global__ void vsa_lit_scan<VSA_MODE_TEDDY, true, false>(VsaLitParams);
-template __global__ void vsa_lit_scan<VSA_MODE_FAT, true, false>(VsaLitParams);
+template __global__ void vsa_lit_scan<VSA_MODE_TEDDY, false, false>(VsaLitParams);
+template __global__ void vsa_lit_scan<VSA_MODE_FAT, false, false>(VsaLitParams);
 template __global__ void vsa_lit_scan<VSA_MODE_NOOD, false, false>(VsaLitParams);
 
 /* ====================================================== binned sort === */
 
-/* Match records sorted in three short launches instead of a library sort's
- * dozen (runtime.hip queue_bin_sort): bins = VSA_SORT_BINS ranges of end
- * positions; (1) the scan kernel counts each record into its bin as it
- * emits it (one non-returning atomic per record: at cfg 4 that is cheaper
- * than the separate histogram launch vsa_bin_hist, kept for A/B), (2)
- * exclusive scan of the counts, (3) scatter into bin order, (4) one wave
- * sorts each bin (<= 64 records: a register bitonic sort on the full key).
- * Keys are unique (end, bucket, LitInfo), so the result equals the full
- * sort. */
-__global__ void __launch_bounds__(256) vsa_bin_hist(const uint64_t *keys, const uint64_t *ctr,
-                                                    uint64_t cap, uint32_t bin_shift,
-                                                    uint32_t *counts) {
-    const uint64_t n0 = ctr[0];
-    const uint64_t n = n0 > cap ? 0 : n0; /* an overflowed launch runs again */
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * 256)
-        __hip_atomic_fetch_add(&counts[(uint32_t)((keys[i] >> VSA_KEY_END_SHIFT) >> bin_shift)],
-                               1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ void __launch_bounds__(1024) vsa_bin_scan(const uint32_t *counts, uint32_t *cursor,
-                                                    uint64_t *ctr) {
-    /* thread t owns bins [16 t, 16 t + 16) (four dwordx4 loads); a wave scan
-     * of the threads' sums, then one of the 16 waves' totals: two barriers */
-    __shared__ uint32_t wsum[16];
-    const uint32_t t = threadIdx.x, wv = t / WAVE;
-    constexpr uint32_t PER = VSA_SORT_BINS / 1024;
-    static_assert(PER == 16, "four uint4 per thread");
-    uint4 v[4];
-    uint32_t sum = 0, big = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        v[k] = ((const uint4 *)counts)[t * 4 + k];
-        sum += v[k].x + v[k].y + v[k].z + v[k].w;
-        big |= (v[k].x > VSA_SORT_BIN_MAX) | (v[k].y > VSA_SORT_BIN_MAX) |
-               (v[k].z > VSA_SORT_BIN_MAX) | (v[k].w > VSA_SORT_BIN_MAX);
-    }
-    /* a crowded bin: the scatter and sort stand down (bin_records) and the
-     * host sorts with the library */
-    if (big) ctr[VSA_CTR_BIN_OVERFLOW] = 1;
-    u32 wtot;
-    const u32 ex = wave_excl_scan(sum, &wtot);
-    if (lane_id() == 0) wsum[wv] = wtot;
-    __syncthreads();
-    u32 base = 0;
-    if (wv == 0) {
-        u32 tot;
-        const u32 x = lane_id() < 16 ? wsum[lane_id()] : 0u;
-        const u32 e = wave_excl_scan(x, &tot);
-        if (lane_id() < 16) wsum[lane_id()] = e;
-    }
-    __syncthreads();
-    base = wsum[wv];
-    uint32_t run = base + ex; /* exclusive prefix of this thread's bins */
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        uint4 o;
-        o.x = run; run += v[k].x;
-        o.y = run; run += v[k].y;
-        o.z = run; run += v[k].z;
-        o.w = run; run += v[k].w;
-        ((uint4 *)cursor)[t * 4 + k] = o;
-    }
-}
-
-/* the scan's record count and overflow flag, read on the device (the sort
- * is queued before the host has seen them): 0 when the launch overflowed its
- * output (it runs again) or a bin (the library sort runs instead) */
-__device__ __forceinline__ uint64_t bin_records(const uint64_t *ctr, uint64_t cap) {
-    const uint64_t n = ctr[0];
-    return (n > cap || ctr[VSA_CTR_BIN_OVERFLOW]) ? 0 : n;
-}
-
-__global__ void __launch_bounds__(256) vsa_bin_scatter(const uint64_t *keys, const uint32_t *ids,
-                                                       const uint64_t *ctr, uint64_t cap,
-                                                       uint32_t bin_shift, uint32_t *cursor,
-                                                       uint64_t *okeys, uint32_t *oids) {
-    const uint64_t n = bin_records(ctr, cap);
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * 256) {
-        const uint64_t k = keys[i];
-        const uint32_t pos = atomicAdd(&cursor[(uint32_t)((k >> VSA_KEY_END_SHIFT) >> bin_shift)], 1u);
-        okeys[pos] = k;
-        oids[pos] = ids[i];
-    }
-}
-
-/* one wave per bin; after the scatter cursor[b] = the bin's end */
-__device__ __forceinline__ void bin_sort_wave(const uint64_t *ctr, uint64_t cap, uint32_t *counts,
-                                              const uint32_t *cursor, uint64_t *keys,
-                                              uint32_t *ids) {
-    const uint32_t bin = blockIdx.x * 4 + threadIdx.x / WAVE;
-    const u32 lane = lane_id();
-    const uint32_t m = counts[bin];
-    /* ready for the next scan, whether or not this one sorts (an overflowed
-     * or crowded launch leaves its counts behind too) */
-    if (lane_id() == 0) counts[bin] = 0;
-    if (bin_records(ctr, cap) < 2) return;
-    if (m < 2) return;
-    const uint32_t base = cursor[bin] - m;
-    u64 k = ~0ULL;
-    u32 id = 0;
-    if (lane < m) {
-        k = keys[base + lane];
-        id = ids[base + lane];
-    }
-#pragma unroll
-    for (u32 size = 2; size <= WAVE; size <<= 1) {
-#pragma unroll
-        for (u32 j = size >> 1; j > 0; j >>= 1) {
-            const u32 plo = shfl_xor_u32((u32)k, (int)j);
-            const u32 phi = shfl_xor_u32((u32)(k >> 32), (int)j);
-            const u32 pid = shfl_xor_u32(id, (int)j);
-            const u64 pk = ((u64)phi << 32) | plo;
-            const bool up = (lane & size) == 0;
-            const bool lower = (lane & j) == 0;
-            /* keep the smaller key where (lower == up) */
-            const bool take = (lower == up) ? (pk < k) : (pk > k);
-            if (take) {
-                k = pk;
-                id = pid;
-            }
-        }
-    }
-    if (lane < m) {
-        keys[base + lane] = k;
-        ids[base + lane] = id;
-    }
-}
-
-__global__ void __launch_bounds__(256) vsa_bin_sort(const uint64_t *ctr, uint64_t cap,
-                                                    uint32_t *counts,
-                                                    const uint32_t *cursor, uint64_t *keys,
-                                                    uint32_t *ids) {
-    bin_sort_wave(ctr, cap, counts, cursor, keys, ids);
-}
+/* Match records sorted without a library sort (runtime.hip
+ * queue_bin_sort): bins = VSA_SORT_BINS ranges of end positions; the scan
+ * kernel stages each record's output slot in its bin as it emits it
+ * (confirm_multi), and one vsa_bin_finish launch sorts every bin (<= 64
+ * records: a register bitonic sort on the full key) into place.  Keys are
+ * unique (end, bucket, LitInfo), so the result equals the full sort. */
 
 /* The last launch of a binned scan: the scan's counters [0, 16) go to
  * host memory (fine-grained, h[1..16]) and then h[0] = seq with a
@@ -2930,14 +2412,13 @@ __device__ __forceinline__ u32 lds_ld8(u32 addr) { return *(lds_cu8_t *)(uintptr
 __global__ void __launch_bounds__(1024) vsa_class_scan_lut(VsaClassParams P, u64 wspan) {
     __shared__ __align__(16) u8 T[65536];
     __shared__ u8 mem[256];
-    __shared__ u32 gctr, cdone;
+    __shared__ u32 gctr;
     const u32 tid = threadIdx.x;
     const u32 lane = lane_id();
     const u32 wave = readfirstlane_u32(tid / WAVE);
-    /* the workgroup's range: an equal span, or the schedule feedback's
-     * weighted bounds (4 KiB-aligned, runtime.hip vsa_class_scan) */
-    const u64 lo = P.wg_lo ? P.wg_lo[blockIdx.x] : (u64)blockIdx.x * wspan;
-    const u64 hi = min(P.wg_lo ? P.wg_lo[blockIdx.x + 1] : lo + wspan, (u64)P.len);
+    /* the workgroup's range: an equal span */
+    const u64 lo = (u64)blockIdx.x * wspan;
+    const u64 hi = min(lo + wspan, (u64)P.len);
     /* iterations (1 KiB) of the range, the full ones, and its groups */
     const u32 nit = lo < hi ? (u32)((hi - lo + 1023) >> 10) : 0u;
     const u32 nfull = lo < hi ? (u32)min((u64)nit, ((u64)P.len - lo) >> 10) : 0u;
@@ -2955,8 +2436,6 @@ __global__ void __launch_bounds__(1024) vsa_class_scan_lut(VsaClassParams P, u64
     if (tid < 256) mem[tid] = (u8)((P.cls[tid >> 5] >> (tid & 31)) & 1u);
     if (tid == 0) {
         gctr = 32;
-        cdone = 0;
-        if (P.wg_time) P.wg_time[gridDim.x + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     {
@@ -3033,16 +2512,5 @@ __global__ void __launch_bounds__(1024) vsa_class_scan_lut(VsaClassParams P, u64
         if (first != ~0ULL) atomicMin(P.first + sl, first);
         if (last) atomicMax(P.last + sl, last);
         if (cnt) atomicAdd(P.count + sl, cnt);
-        if (P.wg_time) {
-            /* the schedule feedback: the workgroup's last wave, its end and XCD */
-            const u32 prev = __hip_atomic_fetch_add(&cdone, 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (prev + 1 == blockDim.x / WAVE) {
-                u32 xcc;
-                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-                P.wg_time[blockIdx.x] = ((unsigned long long)(xcc & 15u) << 60) |
-                                        (__builtin_amdgcn_s_memrealtime() & ((1ULL << 60) - 1));
-            }
-        }
     }
 }

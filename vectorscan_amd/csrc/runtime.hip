@@ -41,17 +41,9 @@
 #include "kernels.h"
 #include "vsa_internal.h"
 
-template <int MODE, bool LDS_TABLE, bool XP>
+template <int MODE, bool XP, bool SPLIT>
 __global__ void vsa_lit_scan(VsaLitParams P);
 __global__ void vsa_class_scan(VsaClassParams P);
-__global__ void vsa_bin_hist(const uint64_t *keys, const uint64_t *ctr, uint64_t cap,
-                             uint32_t bin_shift, uint32_t *counts);
-__global__ void vsa_bin_scan(const uint32_t *counts, uint32_t *cursor, uint64_t *ctr);
-__global__ void vsa_bin_scatter(const uint64_t *keys, const uint32_t *ids, const uint64_t *ctr,
-                                uint64_t cap, uint32_t bin_shift, uint32_t *cursor,
-                                uint64_t *okeys, uint32_t *oids);
-__global__ void vsa_bin_sort(const uint64_t *ctr, uint64_t cap, uint32_t *counts,
-                             const uint32_t *cursor, uint64_t *keys, uint32_t *ids);
 __global__ void vsa_bin_finish(const uint32_t *counts, uint32_t *counts_next,
                                const uint32_t *slots, const uint64_t *ikeys, const uint32_t *iids,
                                uint64_t *okeys, uint32_t *oids, uint64_t out_cap,
@@ -87,9 +79,9 @@ const size_t LDS_BUDGET = 160 * 1024 - 4096; /* minus static LDS (confirm params
 const uint32_t SLOT_WORDS_MAX = 3072;        /* 12 KiB of slot bitmaps (coarsened
                                                 beyond, see vsa_db_load) */
 
-/* d_counters layout (u64): [0..7] scan counters, [16 + 16 r] region
- * tickets (one 128-B line each), [PAIR_BASE + 16 k] double-shufti stage
- * results, [CLASS_BASE + 16 s + {0,1,2}] class-scan
+/* d_counters layout (u64): [0..15] scan counters, [144..159] the last
+ * binned scan's counters kept for vsa_pack, [PAIR_BASE + 16 k]
+ * double-shufti stage results, [CLASS_BASE + 16 s + {0,1,2}] class-scan
  * first / last / count partials of slot s (one line per slot) */
 constexpr int CLASS_SLOTS = 64;
 constexpr int PAIR_BASE = 160; /* double-shufti stage results, 16 apart */
@@ -112,9 +104,8 @@ struct Workspace {
     size_t tmp_bytes = 0;
     unsigned long long *d_counters = nullptr; /* layout above */
     uint32_t *d_bins = nullptr; /* binned sort: two count buffers of
-                                   VSA_SORT_BINS, used in turn (staged sort,
-                                   vsa_bin_finish) or counts + cursor (the
-                                   scatter chain, VSA_OLD_SORT) */
+                                   VSA_SORT_BINS, used in turn (vsa_bin_finish
+                                   reads one and clears the other) */
     /* staged output slots of the binned sort: VSA_SORT_BIN_MAX per bin */
     uint32_t *d_bslots = nullptr;
     unsigned long long *h_counters = nullptr; /* pinned mirror */
@@ -139,12 +130,11 @@ struct Workspace {
  * count << 24 (count 0: part of one block). */
 struct BatchPlan {
     std::vector<VsaBlock> blocks;
-    /* 4 words per segment (kernels.h seg_desc), then for per-workgroup
-     * lists (grid != 0) grid + 1 list bounds */
+    /* 4 words per segment (kernels.h seg_desc), then grid + 1 list
+     * bounds */
     std::vector<uint32_t> segblk;
     uint64_t nsegs = 0;
-    uint32_t grid = 0; /* workgroups of a per-workgroup-list plan, else 0 */
-    uint32_t seg_bytes = 0;
+    uint32_t grid = 0; /* workgroups (one segment list each) */
     int end_bits = 0;
     uint64_t bytes = 0; /* scanned bytes (len - start summed) */
     std::vector<int64_t> spans, live; /* build_plan scratch */
@@ -172,8 +162,7 @@ struct vsa_ctx {
         const uint8_t *d_data = nullptr;
         uint32_t nb = 0;
         uint64_t segs = 0;
-        uint32_t seg_bytes = 0;
-        uint32_t grid = 0; /* per-workgroup lists: the plan's workgroups */
+        uint32_t grid = 0; /* the plan's workgroups (one segment list each) */
         int end_bits = 0;
         uint32_t flags = 0;
         bool bins = false;     /* the scan counts records into the sort bins */
@@ -188,13 +177,6 @@ struct vsa_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_done = nullptr; /* polled by wait_stream */
     hipEvent_t ev_rec = nullptr;  /* records_fetch_async's copies done */
-    /* side-stream sort (side_sort): the binned sort of this context's scan
-     * runs on its own stream, so the next scan queued on a shared stream
-     * overlaps it; ev_sorted = its last launch, joined (sort_join) before
-     * this context's next use of the scan stream */
-    hipStream_t sort_stream = nullptr;
-    hipEvent_t ev_sorted = nullptr;
-    bool sort_join = false;
     double last_kernel_ms = 0.0;
     uint32_t bin_skip = 0;   /* launches left without the binned sort */
     bool bins_clean[2] = {false, false}; /* bin count buffer b is zero (no memset) */
@@ -223,16 +205,11 @@ struct vsa_ctx {
     /* live plans of this context (vsa_ctx_destroy detaches them, so a plan
      * freed after its context never touches it) */
     std::vector<vsa_plan *> plans;
-    /* the class scan's weighted workgroup bounds (device, pinned staging)
-     * and what they were built for: length, grid, weights version + 1 */
-    uint64_t *cls_bounds_d = nullptr, *cls_bounds_h = nullptr;
-    uint64_t cls_bounds_key[3] = {0, 0, 0};
     /* schedule feedback (take_feedback): per-XCD weights of the
      * workgroups' static shares, learned from the workgroups' end times of
      * large launches (the kernels write them into fine-grained host
      * memory); one set per kind of launch, as compute-bound and streaming
-     * scans see different XCD speeds: 0 = FDR / Teddy, 1 = noodle, 2 = the
-     * class scan */
+     * scans see different XCD speeds: 0 = FDR / Teddy, 1 = noodle */
     struct FbSet {
         float w[8] = {1, 1, 1, 1, 1, 1, 1, 1};  /* the running estimate */
         float wa[8] = {1, 1, 1, 1, 1, 1, 1, 1}; /* the weights plans use */
@@ -243,15 +220,14 @@ struct vsa_ctx {
         bool known = false;      /* xcc[] holds measured XCDs */
     };
     struct {
-        FbSet set[3];
+        FbSet set[2];
         unsigned long long *h = nullptr, *d = nullptr; /* 2 x 1024 u64 */
         int armed = -1;          /* the set the launch in flight records for */
         /* ... into device memory (d_rec), published with the counters by
          * vsa_bin_finish, instead of stores to host memory from the scan */
         bool dev = false;
         unsigned long long *d_rec = nullptr;
-        uint32_t tick = 0;       /* eligible launches (VSA_FB_PERIOD) */
-        uint32_t grid = 0;       /* ... and its workgroups */
+        uint32_t grid = 0;       /* the launch's workgroups */
     } fb;
 };
 
@@ -264,10 +240,10 @@ struct vsa_plan {
     const uint8_t *d_data = nullptr;
     uint32_t nb = 0;
     uint64_t segs = 0;
-    uint32_t seg_bytes = 0;
     uint32_t grid = 0;
     int end_bits = 0;
     uint64_t bytes = 0;
+    uint32_t rebuilds = 0; /* segment maps rebuilt for the feedback weights */
     VsaBlock *d_blocks = nullptr;
     uint32_t *d_segblk = nullptr;
     /* schedule feedback: the inputs (to rebuild the segment map with the
@@ -297,7 +273,6 @@ struct vsa_db {
     int type = 0;                /* HWLM_ENGINE_NOOD / FDR */
     uint32_t engine_id = 0;
     int mode = 0;                /* VsaLitMode */
-    bool fdr4 = false;           /* FDR engine scanned with the 4-field first stage */
     /* split passes (FDR4, large literal sets): two launches, one per bit 0
      * of the end byte, each with the table of the literals that end in such
      * a byte (derive_fdr4_table par 0 / 1; d_table2 = par 1) */
@@ -438,130 +413,18 @@ int ensure_tables(vsa_ctx *c, uint32_t nb, uint64_t nsegs, bool keep_blocks = fa
     return VSA_OK;
 }
 
-/* Segment size (bytes, multiple of 1 KiB) for the literal-scan kernel's
- * assignment: at most 128 KiB (VSA_SEG_MAX_KIB), at least 4 KiB, and sized so the
- * segment count is just under a multiple of the scanning-wave count
- * (every wave gets k or k-1 segments, no long tail).  spans[] are the
- * per-block byte spans from their 1 KiB-aligned origins. */
-/* segments build_plan makes of spans[first, first + n) at segment size seg */
-uint64_t count_range(const std::vector<int64_t> &spans, size_t first, size_t n, uint64_t seg) {
-    uint64_t cnt = 0, gn = 0;
-    int64_t gs = 0;
-    for (size_t i = first; i < first + n; i++) {
-        const int64_t sp = spans[i];
-        if (2 * sp <= (int64_t)seg) {
-            if (gn && (gs + sp > (int64_t)seg || gn == 255)) {
-                cnt++;
-                gn = 0;
-                gs = 0;
-            }
-            gn++;
-            gs += sp;
-            continue;
-        }
-        if (gn) {
-            cnt++;
-            gn = 0;
-            gs = 0;
-        }
-        cnt += (uint64_t)((sp + (int64_t)seg - 1) / (int64_t)seg);
-    }
-    return cnt + (gn ? 1 : 0);
-}
-
 int env_int(const char *name, int dflt) {
     const char *e = getenv(name);
     return e ? atoi(e) : dflt;
 }
 
-/* The scan's schedule: per-workgroup segment lists handed out in LDS
- * (build_plan, kernels.hip dynamic 2), unless one of the A/B knobs of the
- * region-ticket scheduler asks for it (VSA_SCHED_OLD, VSA_STATIC_SEGS,
- * VSA_SEG_KB, VSA_REGIONS, VSA_SEG_MAX_KIB) */
-bool sched_wg_lists() {
-    static const bool v = !getenv("VSA_SCHED_OLD") && !getenv("VSA_STATIC_SEGS") &&
-                          !getenv("VSA_SEG_KB") && !getenv("VSA_REGIONS") &&
-                          !getenv("VSA_SEG_MAX_KIB");
-    return v;
-}
-
-/* work stealing inside a workgroup (kernels.hip, dynamic 2): a wave out of
- * segments steals when another has at least this many sweep groups (4 KiB)
+/* work stealing inside a workgroup (kernels.hip): a wave out of segments
+ * steals when another has at least this many sweep groups (4 KiB)
  * unclaimed; VSA_STEAL=0 turns it off (the plan then cuts large blocks into
  * shrinking segments instead) */
 uint32_t steal_min() {
     static const uint32_t v = (uint32_t)std::max(0, env_int("VSA_STEAL", 4));
     return v;
-}
-
-uint64_t pick_seg_bytes(const std::vector<int64_t> &spans, uint64_t waves) {
-    /* segments of a candidate size, blocks of at most half a segment packed
-     * whole (up to 255 per segment) as build_plan does.  Past 64 Ki blocks
-     * the count is estimated from 64 runs of 1024 consecutive blocks spread
-     * over the batch, scaled by bytes (it only balances the schedule) */
-    const size_t ns = spans.size();
-    const size_t RUNS = 64, RUN = 1024;
-    const bool sampled = ns > 65536;
-    uint64_t all_bytes = 0, sample_bytes = 0;
-    if (sampled) {
-        for (int64_t sp : spans) all_bytes += (uint64_t)sp;
-        for (size_t r = 0; r < RUNS; r++)
-            for (size_t i = r * (ns / RUNS); i < r * (ns / RUNS) + RUN; i++)
-                sample_bytes += (uint64_t)spans[i];
-    }
-    auto count = [&](uint64_t seg) {
-        if (!sampled) return count_range(spans, 0, ns, seg);
-        uint64_t n = 0;
-        for (size_t r = 0; r < RUNS; r++) n += count_range(spans, r * (ns / RUNS), RUN, seg);
-        return (uint64_t)((double)n * (double)all_bytes / (double)std::max<uint64_t>(1, sample_bytes));
-    };
-    uint64_t total = 0;
-    for (int64_t sp : spans) total += (uint64_t)sp;
-    uint64_t seg = 128 << 10; /* 64-256 KiB measured equal for FDR, 128 KiB
-                                 5-8 % faster for Teddy / noodle at 1 GiB */
-    /* 16-192 KiB per scanning wave (the 2-8-GPU stripes of the 4 GiB corpus
-     * are 512 MiB-2 GiB, 136-546 KiB a wave): ~1.4 segments per wave.  A CU's waves scan at rates set by their age
-     * (issue priority, 1.82 down to 0.69 KiB/us), so its 8 oldest waves take
-     * two segments and the rest one; the balanced >= 2 rounds below pays
-     * more segment starts and ends on a young wave's last segment.  At 512
-     * MiB: 96 KiB segments 0.149 ms against 0.159 for 46 KiB (3 rounds);
-     * 64 / 128 / 192 / 256 MiB: -8 / -16 / -21 / -14 %; from 768 MiB up the
-     * rules tie (profiles/r03_seg_stripes.txt).  VSA_SEG_ROUNDS_OLD=1: the
-     * old rule. */
-    static const bool old_rule = getenv("VSA_SEG_ROUNDS_OLD") != nullptr;
-    if (!old_rule && !getenv("VSA_SEG_MAX_KIB") && ns <= 64 && total >= 16 * 1024 * waves &&
-        total <= 192 * 1024 * waves) {
-        uint64_t s = (uint64_t)((double)total / (1.42 * (double)waves));
-        s = (s + 1023) & ~(uint64_t)1023;
-        bool large = true; /* every block spans several such segments */
-        for (int64_t sp : spans) large = large && (uint64_t)sp >= 4 * s;
-        if (large) return s;
-    }
-    if (const char *e = getenv("VSA_SEG_MAX_KIB"))
-        seg = (uint64_t)std::max(4, std::min(4096, atoi(e))) << 10;
-    /* 1 KiB segments for inputs up to 64 KiB (the drop-ins: one short
-     * segment per scanning wave), else at least 4 KiB */
-    const uint64_t min_seg = total <= (64u << 10) ? (1u << 10) : (4u << 10);
-    while (seg > min_seg && count(seg) < 2 * waves) seg >>= 1;
-    const uint64_t k = (count(seg) + waves - 1) / waves; /* rounds per wave */
-    if (k >= 2) {
-        uint64_t bal = (total + k * waves - 1) / (k * waves);
-        bal = (bal + 1023) & ~(uint64_t)1023;
-        if (bal < seg && count(bal) > k * waves) {
-            /* smallest 1 KiB multiple in (bal, seg] keeping k rounds (per
-             * block rounding; binary search, count falls as size grows) */
-            uint64_t lo = bal, hi = seg;
-            while (hi - lo > 1024) {
-                const uint64_t mid = ((lo + hi) / 2) & ~(uint64_t)1023;
-                if (mid <= lo) break;
-                if (count(mid) > k * waves) lo = mid;
-                else hi = mid;
-            }
-            bal = hi;
-        }
-        if (bal <= seg) seg = bal;
-    }
-    return seg;
 }
 
 int bits_for(uint64_t v) {
@@ -573,9 +436,9 @@ int bits_for(uint64_t v) {
     return b;
 }
 
-template <int MODE, bool LDS, bool XP = false>
+template <int MODE, bool XP = false, bool SPLIT = false>
 int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds) {
-    auto fn = vsa_lit_scan<MODE, LDS, XP>;
+    auto fn = vsa_lit_scan<MODE, XP, SPLIT>;
     /* the dynamic-LDS limit is raised once per device and kernel (the call
      * costs a few us, a drop-in scan ~25 us) */
     static std::atomic<int> lds_set[64];
@@ -587,30 +450,19 @@ int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds) {
         while (cur < (int)lds && !ls.compare_exchange_weak(cur, (int)lds)) {
         }
     }
-    const uint64_t ns = LIT_WAVES - P.nconf; /* scanning waves per workgroup */
-    uint64_t want = (P.nsegs + ns - 1) / ns;
-    uint64_t cap = (uint64_t)c->num_cus; /* persistent: one 16-wave WG per CU */
-    uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
-    if (P.dynamic == 2) grid = c->launch.grid; /* one workgroup per list */
-    /* at most one segment per scanning wave (small scans, the drop-ins):
-     * static assignment.  Dynamic tickets would cost every wave a walk over
-     * the drained regions, one returning atomic each (~5.5 us measured on a
-     * 1 KiB drop-in, profiles/r03_dropin_waves.txt) */
-    VsaLitParams Q = P;
-    if (Q.dynamic == 1 && Q.nsegs <= (uint64_t)grid * ns) Q.dynamic = 0;
+    /* one persistent 16-wave workgroup per segment list (at most one per
+     * CU: build_plan) */
+    const uint32_t grid = std::max<uint32_t>(1, c->launch.grid);
     /* diagnostic (VSA_PRINT_LAUNCH=1): every literal-scan launch's shape */
     static const bool print_launch = getenv("VSA_PRINT_LAUNCH") != nullptr;
     if (print_launch)
         fprintf(stderr,
                 "vsa launch: mode %d xp %d grid %u nsegs %llu nblocks %u lds %zu qcap %u nconf %u "
-                "dynamic %u end_par %u data %p blocks %p seg_desc %p out_cap %llu bins %p\n",
+                "end_par %u data %p blocks %p seg_desc %p out_cap %llu bins %p\n",
                 MODE, (int)XP, grid, (unsigned long long)P.nsegs, P.nblocks, lds, P.qcap, P.nconf,
-                P.dynamic, P.end_par, (const void *)P.data, (const void *)P.blocks,
+                P.end_par, (const void *)P.data, (const void *)P.blocks,
                 (const void *)P.seg_desc, (unsigned long long)P.out_cap, (void *)P.bin_counts);
-    /* the check below is for this launch: a stale non-fatal error of an
-     * earlier call (the thread's last error) must not fail it */
-    (void)hipGetLastError();
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(LIT_THREADS), lds, c->stream, Q);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(LIT_THREADS), lds, c->stream, P);
     VSA_CHECK(hipGetLastError());
     return VSA_OK;
 }
@@ -652,11 +504,11 @@ bool use_xp(const vsa_db *db) {
     return db->xp.load(std::memory_order_relaxed);
 }
 
-/* the binned sort (kernels.hip) replaces the library sort unless the
- * caller wants the records unsorted or VSA_LIB_SORT is set */
+/* the binned sort (kernels.hip vsa_bin_finish) replaces the library sort
+ * unless the caller wants the records unsorted (or a recent launch crowded
+ * a bin, bin_skip) */
 bool use_bins(const vsa_ctx *c) {
-    static const bool lib_sort = getenv("VSA_LIB_SORT") != nullptr;
-    return !lib_sort && !(c->launch.flags & VSA_SCAN_UNSORTED) && c->bin_skip == 0;
+    return !(c->launch.flags & VSA_SCAN_UNSORTED) && c->bin_skip == 0;
 }
 
 /* bins of 2^bin_shift end positions, at most VSA_SORT_BINS over the span */
@@ -664,73 +516,33 @@ uint32_t bin_shift_for(int end_bits) {
     return end_bits > (int)VSA_SORT_BIN_BITS ? (uint32_t)end_bits - VSA_SORT_BIN_BITS : 0u;
 }
 
-/* the binned sort behind the scan (kernels.hip): the scan kernel counts
- * its records into the bins as it emits them (VsaLitParams.bin_counts),
- * then: scan of the counts, scatter, per-bin sorts, publish -- four short
- * launches.  They read the record count and the overflow flag from
- * d_counters, so they are queued before the host has seen either (an
- * overflowed launch leaves them idle).
- * VSA_SEP_HIST=1 (A/B knob): the histogram as its own launch over the
- * records instead (round 2's five launches).
- * Measured and dropped: histogram + scan and sort + publish fused behind a
- * last-workgroup ticket (three launches) -- 107 us + 342 us against ~30 us
- * for all five (profiles/r03_sort_fused_trace.csv): every workgroup's
- * agent-scope release + acq_rel ticket serializes (~85-100 ns each over
- * 1,024 / 4,096 workgroups; the XCDs' L2s are written back for it). */
-bool sep_hist() {
-    static const bool v = getenv("VSA_SEP_HIST") != nullptr;
-    return v;
-}
+uint32_t *bin_counts_of(vsa_ctx *c, uint32_t par) { return c->ws.d_bins + par * VSA_SORT_BINS; }
 
-/* VSA_OLD_SORT=1 (A/B knob): the round-3 chain behind a binned scan --
- * count-only histogram in the scan, then vsa_bin_scan, vsa_bin_scatter,
- * vsa_bin_sort and vsa_publish (four launches) -- instead of the staged
- * sort (records staged per bin by the scan, one vsa_bin_finish launch) */
-bool old_sort() {
-    static const bool v = getenv("VSA_OLD_SORT") != nullptr || sep_hist();
-    return v;
-}
-
-uint32_t *bin_counts_of(vsa_ctx *c, uint32_t par) {
-    return c->ws.d_bins + (old_sort() ? 0u : par * VSA_SORT_BINS);
-}
-
-int queue_bin_sort(vsa_ctx *c, hipStream_t st) {
+/* The binned sort behind the scan: the scan kernel stages each record's
+ * output slot in its bin as it emits it (VsaLitParams.bin_slots), and one
+ * vsa_bin_finish launch sorts the bins into place, clears the other count
+ * buffer for the next launch and publishes the counters to the host.  It
+ * reads the record count and the overflow flags from d_counters, so it is
+ * queued before the host has seen either (an overflowed launch leaves it
+ * idle).  Measured and dropped (rounds 3-4): the four-launch chain (count,
+ * scan, scatter, per-bin sort; 29 us against 18 us of step - kernel,
+ * profiles/r04c_sort_ab.jsonl), its histogram as a separate launch, a side
+ * stream for the sort (no gain, profiles/r03_sidesort.jsonl), and fused
+ * launches behind a last-workgroup ticket (107 + 342 us: every workgroup's
+ * agent-scope release serializes, profiles/r03_sort_fused_trace.csv). */
+int queue_bin_sort(vsa_ctx *c) {
     Workspace &w = c->ws;
-    if (!old_sort()) {
-        const uint32_t par = c->bin_par;
-        const bool fbd = c->fb.armed >= 0 && c->fb.dev;
-        (void)hipGetLastError(); /* checks below are for this launch */
-        hipLaunchKernelGGL(vsa_bin_finish, dim3(VSA_SORT_BINS / 64), dim3(1024), 0, st,
-                           bin_counts_of(c, par), bin_counts_of(c, par ^ 1u), w.d_bslots,
-                           w.d_keys[0], w.d_ids[0], w.d_keys[1], w.d_ids[1], (uint64_t)w.out_cap,
-                           c->ws.d_counters, c->ws.d_pub, (unsigned long long)++c->pub_seq,
-                           fbd ? c->fb.d_rec : nullptr, fbd ? c->fb.d : nullptr,
-                           fbd ? 2 * c->fb.grid : 0u);
-        VSA_CHECK(hipGetLastError());
-        c->bins_clean[par ^ 1u] = true;
-        c->bin_par = par ^ 1u;
-        return VSA_OK;
-    }
-    uint32_t *counts = w.d_bins, *cursor = w.d_bins + VSA_SORT_BINS;
-    const uint32_t shift = bin_shift_for(c->launch.end_bits);
-    (void)hipGetLastError(); /* the check below is for this chain of launches */
-    if (sep_hist())
-        hipLaunchKernelGGL(vsa_bin_hist, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, st,
-                           w.d_keys[0], (const uint64_t *)w.d_counters, (uint64_t)w.out_cap,
-                           shift, counts);
-    hipLaunchKernelGGL(vsa_bin_scan, dim3(1), dim3(1024), 0, st, counts, cursor,
-                       (uint64_t *)w.d_counters);
-    hipLaunchKernelGGL(vsa_bin_scatter, dim3((uint32_t)c->num_cus * 4), dim3(256), 0, st,
-                       w.d_keys[0], w.d_ids[0], (const uint64_t *)w.d_counters,
-                       (uint64_t)w.out_cap, shift, cursor, w.d_keys[1], w.d_ids[1]);
-    hipLaunchKernelGGL(vsa_bin_sort, dim3(VSA_SORT_BINS / 4), dim3(256), 0, st,
-                       (const uint64_t *)w.d_counters, (uint64_t)w.out_cap, counts, cursor,
-                       w.d_keys[1], w.d_ids[1]);
-    hipLaunchKernelGGL(vsa_publish, dim3(1), dim3(256), 0, st, c->ws.d_counters,
-                       c->ws.d_pub, (unsigned long long)++c->pub_seq, 144u,
-                       (const uint64_t *)nullptr, (const uint32_t *)nullptr, 0u);
+    const uint32_t par = c->bin_par;
+    const bool fbd = c->fb.armed >= 0 && c->fb.dev;
+    hipLaunchKernelGGL(vsa_bin_finish, dim3(VSA_SORT_BINS / 64), dim3(1024), 0, c->stream,
+                       bin_counts_of(c, par), bin_counts_of(c, par ^ 1u), w.d_bslots,
+                       w.d_keys[0], w.d_ids[0], w.d_keys[1], w.d_ids[1], (uint64_t)w.out_cap,
+                       c->ws.d_counters, c->ws.d_pub, (unsigned long long)++c->pub_seq,
+                       fbd ? c->fb.d_rec : nullptr, fbd ? c->fb.d : nullptr,
+                       fbd ? 2 * c->fb.grid : 0u);
     VSA_CHECK(hipGetLastError());
+    c->bins_clean[par ^ 1u] = true;
+    c->bin_par = par ^ 1u;
     return VSA_OK;
 }
 
@@ -752,17 +564,12 @@ bool xcd_feedback_on() {
 
 /* arm the feedback record of the next launch (set: FbSet kind) */
 void arm_feedback(vsa_ctx *c, int set, uint32_t grid, uint64_t bytes, bool small) {
-    /* VSA_FB_PERIOD (A/B knob): record every n-th eligible launch */
-    static const uint32_t period = (uint32_t)std::max(1, env_int("VSA_FB_PERIOD", 1));
-    const bool due = (c->fb.tick++ % period) == 0 || !c->fb.set[set].known;
     c->fb.armed = xcd_feedback_on() && c->fb.h && grid >= 64 && grid <= 1024 &&
-                  bytes >= (256u << 20) && !small && due ? set : -1;
+                  bytes >= (256u << 20) && !small ? set : -1;
     c->fb.grid = grid;
-    /* a literal scan whose counters vsa_bin_finish publishes records in
-     * device memory and rides on the publish (VSA_FB_DEV=0: host stores) */
-    static const bool dev_ok = env_int("VSA_FB_DEV", 1) != 0;
-    c->fb.dev = c->fb.armed >= 0 && c->fb.armed != 2 && dev_ok && c->fb.d_rec &&
-                c->launch.bins && !old_sort() && !small;
+    /* a scan whose counters vsa_bin_finish publishes records in device
+     * memory and rides on the publish; otherwise host stores */
+    c->fb.dev = c->fb.armed >= 0 && c->fb.d_rec && c->launch.bins && !small;
     if (c->fb.armed >= 0) memset(c->fb.h, 0, 2 * grid * sizeof(unsigned long long));
 }
 
@@ -855,34 +662,10 @@ void take_feedback(vsa_ctx *c) {
 static unsigned long long *g_wave_log = nullptr;
 
 int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
-                       uint64_t nsegs, uint32_t seg_bytes);
-
-/* the previous side-stream sort of this context before its next use of the
- * scan stream (a no-op once the host has seen its publish) */
-int join_sort(vsa_ctx *c) {
-    if (c->sort_join) {
-        VSA_CHECK(hipStreamWaitEvent(c->stream, c->ev_sorted, 0));
-        c->sort_join = false;
-    }
-    return VSA_OK;
-}
-
-/* VSA_SIDE_SORT=1 (A/B knob, off by default): the binned sort goes to a
- * side stream, so the next pipelined context's scan, queued behind this one
- * on the shared stream, runs while this one's sort does.  Measured: no gain
- * (cfg 4 step 1.019-1.075 ms against 1.005-1.014 ms on the same box; 512
- * MiB rank step 0.187 either way): the sort's workgroups co-run with the
- * scan's persistent ones and the scan kernel grows by what the step saves
- * (profiles/r03_sidesort.jsonl). */
-bool side_sort(const vsa_ctx *c) {
-    static const char *e = getenv("VSA_SIDE_SORT");
-    (void)c;
-    return e && atoi(e) != 0;
-}
+                       uint64_t nsegs);
 
 int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
-                uint64_t nsegs, uint32_t seg_bytes) {
-    if (int r0 = join_sort(c)) return r0;
+                uint64_t nsegs) {
     if (!c->ctr_clean)
         VSA_CHECK(hipMemsetAsync(c->ws.d_counters, 0, 144 * sizeof(unsigned long long), c->stream));
     c->ctr_clean = false;
@@ -890,10 +673,10 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
     /* not for the drop-in calls, whose few records the host sorts (a
      * larger result takes the library sort) */
     c->launch.bins = use_bins(c) && !(c->launch.flags & SCAN_HOST_SORT_SMALL);
-    if (c->launch.bins && !old_sort() && !c->ws.d_bslots)
+    if (c->launch.bins && !c->ws.d_bslots)
         VSA_CHECK(hipMalloc(&c->ws.d_bslots,
                             (size_t)VSA_SORT_BINS * VSA_SORT_BIN_MAX * sizeof(uint32_t)));
-    const uint32_t par = old_sort() ? 0u : c->bin_par;
+    const uint32_t par = c->bin_par;
     if (c->launch.bins && !c->bins_clean[par])
         VSA_CHECK(hipMemsetAsync(bin_counts_of(c, par), 0, VSA_SORT_BINS * sizeof(uint32_t),
                                  c->stream));
@@ -903,10 +686,9 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
     const bool small = (c->launch.flags & SCAN_HOST_SORT_SMALL) != 0;
     if (!small) VSA_CHECK(hipEventRecord(c->ev0, c->stream));
     arm_feedback(c, fb_set_of(db), c->launch.grid, c->launch.bytes, small);
-    int r = launch_scan_kernel(c, db, d_data, nb, nsegs, seg_bytes);
+    int r = launch_scan_kernel(c, db, d_data, nb, nsegs);
     if (r != VSA_OK) return r;
     if (small) {
-        (void)hipGetLastError(); /* checks below are for this launch */
         hipLaunchKernelGGL(vsa_publish, dim3(1), dim3(256), 0, c->stream, c->ws.d_counters,
                            c->ws.d_pub, (unsigned long long)++c->pub_seq, 144u,
                            (const uint64_t *)c->ws.d_keys[0], (const uint32_t *)c->ws.d_ids[0],
@@ -923,102 +705,33 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
      * (finish_scan falls back to the library sort if a bin overflowed) */
     c->launch.dev_sort = c->launch.bins;
     if (!c->launch.dev_sort) return VSA_OK;
-    /* the sort zeroes every bin count; the publish hands the counters to
-     * the host and zeroes them */
-    hipStream_t st = c->stream;
-    if (side_sort(c)) {
-        if (!c->sort_stream) {
-            VSA_CHECK(hipStreamCreateWithFlags(&c->sort_stream, hipStreamNonBlocking));
-            VSA_CHECK(hipEventCreateWithFlags(&c->ev_sorted, hipEventDisableTiming));
-        }
-        VSA_CHECK(hipStreamWaitEvent(c->sort_stream, c->ev1, 0));
-        st = c->sort_stream;
-    }
-    int r2 = queue_bin_sort(c, st);
+    /* the sort zeroes the next launch's bin counts and publishes the
+     * counters to the host, zeroing them */
+    int r2 = queue_bin_sort(c);
     if (r2 != VSA_OK) return r2;
-    if (st != c->stream) {
-        VSA_CHECK(hipEventRecord(c->ev_sorted, st));
-        c->sort_join = true;
-    }
-    if (old_sort()) c->bins_clean[0] = true; /* vsa_bin_sort zeroed the counts */
     c->launch.published = true;
     c->ctr_clean = true;
     return VSA_OK;
 }
 
 int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
-                       uint64_t nsegs, uint32_t seg_bytes) {
+                       uint64_t nsegs) {
     Workspace &w = c->ws;
-    if (db->type == HWLM_ENGINE_NOOD) {
-        VsaLitParams P;
-        memset(&P, 0, sizeof(P));
-        P.data = d_data;
-        P.blocks = c->launch.d_blocks;
-        P.seg_desc = c->launch.d_segblk;
-        P.wg_seg = c->launch.grid ? c->launch.d_segblk + 4 * nsegs : nullptr;
-        P.nblocks = nb;
-        P.seg_bytes = seg_bytes;
-    P.dynamic = c->launch.grid ? 2u : getenv("VSA_STATIC_SEGS") ? 0u : 1u;
-    P.steal = P.dynamic == 2 ? steal_min() : 0u;
-    P.steal_w = (uint32_t)env_int("VSA_STEAL_W", 1);
-    P.nregions = 8;
-    if (const char *e = getenv("VSA_REGIONS")) P.nregions = (uint32_t)std::min(8, std::max(1, atoi(e)));
-        P.nsegs = nsegs;
-        const uint32_t ml = db->nood.msk_len; /* 1..8 */
-        P.nood_msk = db->nood.msk << (8 * (8 - ml));
-        P.nood_cmp = db->nood.cmp << (8 * (8 - ml));
-        P.nood_len = ml;
-        P.nood_id = db->nood.id;
-        P.out_keys = w.d_keys[0];
-        P.out_ids = w.d_ids[0];
-        P.out_cap = w.out_cap;
-        P.bin_counts = c->launch.bins && !sep_hist() ? bin_counts_of(c, c->bin_par) : nullptr;
-        P.bin_shift = bin_shift_for(c->launch.end_bits);
-        P.bin_slots = c->launch.bins && !old_sort() ? w.d_bslots : nullptr;
-        P.counters = w.d_counters;
-        P.wg_time = c->fb.armed >= 0 ? (c->fb.dev ? c->fb.d_rec : c->fb.d) : nullptr;
-        P.wave_log = g_wave_log;
-        {
-            const char *e = getenv("VSA_DEBUG_FLAGS");
-            P.dbg = e ? (uint32_t)atoi(e) : 0u;
-        }
-        for (int b = 0; b < 16; b++) P.slot_off[b] = 0xffffffffu;
-        P.nconf = 1;
-        size_t lds = plan_lds(0, 0, 32, &P.qcap);
-        return launch_lit<VSA_MODE_NOOD, false>(c, P, lds);
-    }
     VsaLitParams P;
     memset(&P, 0, sizeof(P));
     P.data = d_data;
     P.blocks = c->launch.d_blocks;
     P.seg_desc = c->launch.d_segblk;
-        P.wg_seg = c->launch.grid ? c->launch.d_segblk + 4 * nsegs : nullptr;
+    P.wg_seg = c->launch.d_segblk + 4 * nsegs;
     P.nblocks = nb;
-    P.seg_bytes = seg_bytes;
-    P.dynamic = c->launch.grid ? 2u : getenv("VSA_STATIC_SEGS") ? 0u : 1u;
-    P.steal = P.dynamic == 2 ? steal_min() : 0u;
-    P.steal_w = (uint32_t)env_int("VSA_STEAL_W", 1);
-    P.nregions = 8;
-    if (const char *e = getenv("VSA_REGIONS")) P.nregions = (uint32_t)std::min(8, std::max(1, atoi(e)));
+    P.steal = steal_min();
     P.nsegs = nsegs;
-    const uint8_t *d_eng = db->d_blob + VSA_ROUNDUP_CL(sizeof(HWLM));
-    P.table = db->d_table; /* derived FDR table / combined Teddy table */
-    P.table_entries = db->table_entries;
-    P.dmask = db->dmask;
-    /* experiment only (wrong results): every FDR lookup hits entry 0, a
-     * broadcast, so the run shows the filter without LDS bank conflicts */
-    if (getenv("VSA_EXP_DMASK_ZERO")) P.dmask = 0;
-    P.state_lo = db->state_lo;
-    P.state_hi = db->state_hi;
-    const uint32_t conf_offset_in_eng = ((const uint32_t *)(db->hblob + VSA_ROUNDUP_CL(sizeof(HWLM))))[4];
-    P.conf_base = d_eng + conf_offset_in_eng;
-    memcpy(P.conf_off, db->conf_off, sizeof(P.conf_off));
     P.out_keys = w.d_keys[0];
     P.out_ids = w.d_ids[0];
     P.out_cap = w.out_cap;
-    P.bin_counts = c->launch.bins && !sep_hist() ? bin_counts_of(c, c->bin_par) : nullptr;
+    P.bin_counts = c->launch.bins ? bin_counts_of(c, c->bin_par) : nullptr;
     P.bin_shift = bin_shift_for(c->launch.end_bits);
-    P.bin_slots = c->launch.bins && !old_sort() ? w.d_bslots : nullptr;
+    P.bin_slots = c->launch.bins ? w.d_bslots : nullptr;
     P.counters = w.d_counters;
     P.wg_time = c->fb.armed >= 0 ? (c->fb.dev ? c->fb.d_rec : c->fb.d) : nullptr;
     P.wave_log = g_wave_log;
@@ -1026,51 +739,55 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         const char *e = getenv("VSA_DEBUG_FLAGS");
         P.dbg = e ? (uint32_t)atoi(e) : 0u;
     }
+    if (db->type == HWLM_ENGINE_NOOD) {
+        const uint32_t ml = db->nood.msk_len; /* 1..8 */
+        P.nood_msk = db->nood.msk << (8 * (8 - ml));
+        P.nood_cmp = db->nood.cmp << (8 * (8 - ml));
+        P.nood_len = ml;
+        P.nood_id = db->nood.id;
+        for (int b = 0; b < 16; b++) P.slot_off[b] = 0xffffffffu;
+        P.nconf = 1;
+        size_t lds = plan_lds(0, 0, 32, &P.qcap);
+        return launch_lit<VSA_MODE_NOOD>(c, P, lds);
+    }
+    const uint8_t *d_eng = db->d_blob + VSA_ROUNDUP_CL(sizeof(HWLM));
+    P.table = db->d_table; /* derived FDR4 table / Teddy byte table */
+    P.table_entries = db->table_entries;
+    P.dmask = db->dmask;
+    P.state_lo = db->state_lo;
+    P.state_hi = db->state_hi;
+    const uint32_t conf_offset_in_eng = ((const uint32_t *)(db->hblob + VSA_ROUNDUP_CL(sizeof(HWLM))))[4];
+    P.conf_base = d_eng + conf_offset_in_eng;
+    memcpy(P.conf_off, db->conf_off, sizeof(P.conf_off));
     P.slotmap = db->d_slots;
     P.slot_words = db->slot_words;
     memcpy(P.slot_off, db->slot_off, sizeof(P.slot_off));
     memcpy(P.slot_bits, db->slot_bits, sizeof(P.slot_bits));
     P.pf_mult = db->pf_mult;
-    if (db->mode == VSA_MODE_FDR && db->fdr4) {
+    if (db->mode == VSA_MODE_FDR4) {
         const size_t tb = (size_t)db->table_entries * 4;
         const bool xp = use_xp(db);
         const size_t ent = xp ? 16 : 48; /* QEnt or chunk entries */
         P.nconf = launch_nconf(db, tb, ent, LDS_BUDGET);
         size_t lds = plan_lds(tb, db->slot_words, ent, &P.qcap, LDS_BUDGET, P.nconf);
         if (lds > LDS_BUDGET) return VSA_E_INVALID;
+        if (!db->split)
+            return xp ? launch_lit<VSA_MODE_FDR4, true>(c, P, lds)
+                      : launch_lit<VSA_MODE_FDR4>(c, P, lds);
         auto go = [&](const VsaLitParams &Q) {
             return xp ? launch_lit<VSA_MODE_FDR4, true, true>(c, Q, lds)
-                      : launch_lit<VSA_MODE_FDR4, true>(c, Q, lds);
+                      : launch_lit<VSA_MODE_FDR4, false, true>(c, Q, lds);
         };
-        if (!db->split) return go(P);
         /* split passes: the ends whose byte has bit 0 clear, with the table
          * of the literals ending in such a byte, then the others; each end
          * is one pass's, and the confirm (the blob's, unchanged) can only
          * accept a literal whose last byte is the end's, so no record is
-         * found twice.  The records of both go to the same output and bins.
-         * Between them the ticket counters (dynamic 1, the pool) restart. */
+         * found twice.  The records of both go to the same output and bins. */
         P.end_par = 1;
         if (int r = go(P)) return r;
-        VSA_CHECK(hipMemsetAsync(w.d_counters + 16, 0, 128 * sizeof(unsigned long long),
-                                 c->stream));
         P.end_par = 2;
         P.table = (const uint64_t *)db->d_table2;
         return go(P);
-    }
-    if (db->mode == VSA_MODE_FDR) {
-        size_t tb = (size_t)db->table_entries * 8;
-        if (tb <= 128 * 1024) {
-            const bool xp = use_xp(db);
-            const size_t ent = xp ? 16 : 48; /* QEnt or chunk entries */
-            P.nconf = launch_nconf(db, tb, ent, LDS_BUDGET);
-            size_t lds = plan_lds(tb, db->slot_words, ent, &P.qcap, LDS_BUDGET, P.nconf);
-            if (lds <= LDS_BUDGET)
-                return xp ? launch_lit<VSA_MODE_FDR, true, true>(c, P, lds)
-                          : launch_lit<VSA_MODE_FDR, true>(c, P, lds);
-        }
-        P.nconf = launch_nconf(db, 0, 48, LDS_BUDGET);
-        size_t lds = plan_lds(0, db->slot_words, 48, &P.qcap, LDS_BUDGET, P.nconf);
-        return launch_lit<VSA_MODE_FDR, false>(c, P, lds);
     }
     /* Teddy / Fat Teddy: the 64 KiB table sits at LDS 0x10000 (kernels.hip
      * TEDDY_TAB_LDS), ring + slot bitmaps below it after the static LDS */
@@ -1079,22 +796,18 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     if (db->mode == VSA_MODE_TEDDY) {
         P.nconf = launch_nconf(db, 0, 48, below);
         if (plan_lds(0, db->slot_words, 48, &P.qcap, below, P.nconf) > below) return VSA_E_INVALID;
-        return launch_lit<VSA_MODE_TEDDY, true>(c, P, teddy_dyn);
+        return launch_lit<VSA_MODE_TEDDY>(c, P, teddy_dyn);
     }
     P.nconf = launch_nconf(db, 0, 64, below);
     if (plan_lds(0, db->slot_words, 64, &P.qcap, below, P.nconf) > below) return VSA_E_INVALID;
-    size_t lds = teddy_dyn;
-    return launch_lit<VSA_MODE_FAT, true>(c, P, lds);
+    return launch_lit<VSA_MODE_FAT>(c, P, teddy_dyn);
 }
 
 /* wait for the scan stream by polling an event: a blocking wait wakes on a
  * coarse tick (measured ~1 ms after a 0.3 ms scan), which would set the
  * wall time of every scan shorter than that.  Past 50 ms of polling the
- * wait blocks (long scans do not need the precision).  VSA_SYNC_BLOCK:
- * always block. */
+ * wait blocks (long scans do not need the precision). */
 hipError_t wait_stream(vsa_ctx *c) {
-    static const bool block = getenv("VSA_SYNC_BLOCK") != nullptr;
-    if (block) return hipStreamSynchronize(c->stream);
     hipError_t e = hipEventRecord(c->ev_done, c->stream);
     if (e != hipSuccess) return e;
     /* spin ~100 us, then yield the core between polls (the host replay
@@ -1103,6 +816,9 @@ hipError_t wait_stream(vsa_ctx *c) {
     for (uint32_t i = 0;; i++) {
         e = hipEventQuery(c->ev_done);
         if (e != hipErrorNotReady) return e;
+        /* not ready is a poll's answer, not an error: it must not stay the
+         * thread's last error for the next launch check */
+        (void)hipGetLastError();
         if ((i & 15) == 15) {
             const auto dt = std::chrono::steady_clock::now() - t0;
             if (dt > std::chrono::milliseconds(50)) return hipStreamSynchronize(c->stream);
@@ -1121,7 +837,7 @@ hipError_t wait_published(vsa_ctx *c, uint64_t seq) {
         if ((i & 15) == 15) {
             const auto dt = std::chrono::steady_clock::now() - t0;
             if (dt > std::chrono::milliseconds(50)) {
-                hipError_t e = hipStreamSynchronize(c->sort_join ? c->sort_stream : c->stream);
+                hipError_t e = hipStreamSynchronize(c->stream);
                 if (e != hipSuccess) return e;
                 if (h[0] != seq) return hipErrorUnknown;
                 break;
@@ -1138,7 +854,6 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     if (c->launch.published) {
         VSA_CHECK(wait_published(c, c->pub_seq));
         for (int i = 0; i < 16; i++) w.h_counters[i] = w.h_pub[1 + i];
-        if (int r0 = join_sort(c)) return r0; /* later work on the scan stream follows the sort */
     } else {
         VSA_CHECK(hipMemcpyAsync(w.h_counters, w.d_counters, 16 * sizeof(unsigned long long),
                                  hipMemcpyDeviceToHost, c->stream));
@@ -1183,7 +898,7 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     if (n > 1 && !(flags & VSA_SCAN_UNSORTED) && !c->host_sort && c->launch.dev_sort &&
         !w.h_counters[VSA_CTR_BIN_OVERFLOW]) {
         /* sorted by the binned sort queued in launch_scan (its overflow
-         * flag, set by vsa_bin_scan, is in the counters just read) */
+         * flag, set by the scan, is in the counters just read) */
         c->cur = 1;
     } else if (n > 1 && !(flags & VSA_SCAN_UNSORTED) && !c->host_sort) {
         hipcub::DoubleBuffer<uint64_t> kb(w.d_keys[0], w.d_keys[1]);
@@ -1246,7 +961,8 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
         /* only the history is readable before the block: a write at offset
          * 1 with 1 history byte must not load the 15 bytes before the
          * buffer (the prologue's masked loads reach base - 8; a buffer at the
-         * start of a mapping faulted, test_gpu_split_passes' stream part) */
+         * start of a mapping faulted, test_gpu_split_passes' stream part;
+         * tests/test_plan.py checks the bound) */
         b.hist = (uint32_t)std::min<uint64_t>(b.hlen, 16);
         b.flags = b.hlen ? VSA_BLK_STREAM : 0;
         /* prepareZones fdr.c:625-659: short zone anchors at len - 16; with
@@ -1263,13 +979,12 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
             pl.bytes += (uint64_t)(len - st);
         }
     }
-    const bool wgl = sched_wg_lists();
-    uint64_t seg = live.empty() ? (64u << 10) : pick_seg_bytes(live, waves);
-    if (const char *e = getenv("VSA_SEG_KB")) seg = (uint64_t)std::max(1, atoi(e)) << 10;
+    /* VSA_SEG_KB (tests): every piece and packed group at most this size */
+    const uint64_t seg_kb = (uint64_t)std::max(0, env_int("VSA_SEG_KB", 0)) << 10;
     const bool group = !getenv("VSA_NO_GROUPS");
     const bool no_runs = getenv("VSA_NO_RUNS") != nullptr;
     uint32_t g_first = 0, g_n = 0;
-    bool g_run = false; /* the open group can still be a run (wgl lists) */
+    bool g_run = false; /* the open group can still be a run */
     int64_t g_span = 0;
     pl.nsegs = 0;
     pl.grid = 0;
@@ -1302,160 +1017,109 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
         g_n = 0;
         g_span = 0;
     };
-    if (!wgl) {
-        /* fixed-size segments for the region tickets / static assignment */
-        for (uint32_t i = 0; i < nb; i++) {
-            const int64_t sp = spans[i];
-            if (sp < 0) {
-                flush();
-                continue;
-            }
-            if (group && 2 * sp <= (int64_t)seg) {
-                if (g_n && (g_span + sp > (int64_t)seg || g_n == SEG_GROUP_MAX)) flush();
-                if (!g_n) g_first = i;
-                out[i].seg_first = pl.nsegs;
-                g_n++;
-                g_span += sp;
-                continue;
-            }
+    /* Per-workgroup lists (kernels.hip): the live bytes, in block order, are
+     * split into G equal shares (or shares weighted per workgroup: schedule
+     * feedback, wg_w), one list per workgroup.  With stealing a large block
+     * is cut into one segment per wave of the share; without it
+     * (VSA_STEAL=0) into segments of clamp(r / ns, min, max), r = the bytes
+     * of the share still uncut (guided sizes).  Blocks shorter than half the
+     * current size are packed whole (groups of up to SEG_GROUP_MAX blocks,
+     * runs of up to VSA_RUN_MAX).  A wave's share of the list per group
+     * (K = 1) measured 4-13 % faster on 2-64 KiB blocks than K = 2
+     * (profiles/r04af_wg_k.txt).  A shared pool of small segments after the
+     * lists (round 4) measured slower: 4 GiB 892 against 870 us, 32 MiB 47
+     * against 28 us (profiles/r04f_pool_sweep.jsonl). */
+    uint64_t T = 0;
+    for (int64_t sp : live) T += (uint64_t)sp;
+    const uint64_t smax = seg_kb ? seg_kb : (256u << 10);
+    const uint64_t smin = seg_kb ? seg_kb : T <= (64u << 10) ? 1024u : (4u << 10);
+    const uint64_t gmax = std::max<uint64_t>(1, waves / ns);
+    const uint64_t G = std::max<uint64_t>(1, std::min(gmax, (T + ns * smin - 1) / (ns * smin)));
+    std::vector<uint32_t> wg_first(G + 1, 0);
+    uint64_t g = 0, acc = 0;
+    /* the end of workgroup k's share: equal shares, or weighted per
+     * workgroup */
+    std::vector<double> cw;
+    if (wg_w) {
+        cw.resize(G);
+        double a = 0;
+        for (uint64_t k = 0; k < G; k++) cw[k] = (a += wg_w[k]);
+    }
+    auto cum = [&](uint64_t k) {
+        if (!cw.empty()) return k + 1 >= G ? T : (uint64_t)((double)T * (cw[k] / cw[G - 1]));
+        return (uint64_t)((unsigned __int128)T * (k + 1) / G);
+    };
+    auto advance = [&]() {
+        while (g + 1 < G && acc >= cum(g)) wg_first[++g] = (uint32_t)pl.nsegs;
+    };
+    const uint64_t big = seg_kb ? seg_kb
+                                : std::min<uint64_t>(16u << 20,
+                                                     std::max(smin, ((T / G / ns) + 1023) &
+                                                                        ~(uint64_t)1023));
+    auto size_now = [&]() -> uint64_t {
+        const uint64_t c = cum(g);
+        const uint64_t r = c > acc ? c - acc : 0;
+        uint64_t v = (r / ns + 1023) & ~(uint64_t)1023;
+        return std::min(smax, std::max(smin, v));
+    };
+    for (uint32_t i = 0; i < nb; i++) {
+        const int64_t sp = spans[i];
+        if (sp < 0) {
             flush();
-            out[i].seg_first = pl.nsegs;
-            for (int64_t off = 0; off < sp; off += (int64_t)seg) push_desc(i, (uint64_t)off, seg);
+            continue;
         }
-        flush();
-    } else {
-        /* Per-workgroup lists (kernels.hip, dynamic 2).  The first
-         * (1 - VSA_POOL_PM / 1000) of the live bytes, in block order, are
-         * split into G equal shares, one list per workgroup; the rest is a
-         * shared pool of small segments (region tickets, like the round-3
-         * scheduler) that workgroups take from once their own list and
-         * their waves' stealing run dry.  The pool is meant to balance the
-         * XCDs: on some boxes one XCD runs ~4-10 % slower than another
-         * (profiles/r04e_waves_4g.txt: workgroups of XCD 7 done at 954 us,
-         * XCD 2 at 859 us, with equal shares).  Off by default (VSA_POOL_PM
-         * = 0): measured, it costs more than it saves -- every wave of a
-         * workgroup holds a pool segment when the pool drains, so the
-         * workgroups' ends spread by a segment per wave (4 GiB: 892 against
-         * 870 us; 32 MiB: 47 against 28 us; cfg-3 Teddy 1 GiB: 0.253 against
-         * 0.238 ms; profiles/r04f_pool_sweep.jsonl, r04g_waves_*.txt).  With stealing, a large block
-         * is cut into one segment per wave of the share; without it
-         * (VSA_STEAL=0) into segments of clamp(r / (K x ns), min, max), r =
-         * the bytes of the share still uncut (guided sizes).  Blocks shorter
-         * than half the current size are packed whole as before. */
-        uint64_t T = 0;
-        for (int64_t sp : live) T += (uint64_t)sp;
-        /* K = 1: packed groups of small blocks up to a wave's share of the
-         * list (~1 group per wave); K = 2 (round 4 until r04af) measured
-         * 4-13 % slower on 2-64 KiB blocks at 128 MiB-1 GiB and no better
-         * at 32 MiB (profiles/r04af_wg_k.txt, r04ag_wg_k_small.txt) */
-        static const uint64_t K = std::max(1, env_int("VSA_WG_K", 1));
-        static const uint64_t smax = (uint64_t)std::max(1, env_int("VSA_WG_MAX_KIB", 256)) << 10;
-        static const uint64_t smin0 = (uint64_t)std::max(1, env_int("VSA_WG_MIN_KIB", 4)) << 10;
-        const uint64_t pool_pm = (uint64_t)std::min(900, std::max(0, env_int("VSA_POOL_PM", 0)));
-        const uint64_t smin = T <= (64u << 10) ? 1024u : smin0;
-        const uint64_t gmax = std::max<uint64_t>(1, waves / ns);
-        const uint64_t G = std::max<uint64_t>(1, std::min(gmax, (T + ns * smin - 1) / (ns * smin)));
-        /* the pool: only for a grid wide enough to be unbalanced */
-        const bool pool_on = G >= 16 && pool_pm > 0;
-        const uint64_t Tst = pool_on ? T - T * pool_pm / 1000 : T;
-        const uint64_t ps = std::min<uint64_t>(
-            128u << 10, std::max<uint64_t>(16u << 10, (((T - Tst) / (8 * G)) + 1023) & ~(uint64_t)1023));
-        std::vector<uint32_t> wg_first(G + 1, 0);
-        uint64_t g = 0, acc = 0;
-        bool in_pool = false;
-        uint64_t pool_lo = 0;
-        /* the end of workgroup k's share: equal shares, or (schedule
-         * feedback, wg_w) shares weighted per workgroup */
-        std::vector<double> cw;
-        if (wg_w) {
-            cw.resize(G);
-            double a = 0;
-            for (uint64_t k = 0; k < G; k++) cw[k] = (a += wg_w[k]);
-        }
-        auto cum = [&](uint64_t k) {
-            if (!cw.empty()) return k + 1 >= G ? Tst : (uint64_t)((double)Tst * (cw[k] / cw[G - 1]));
-            return (uint64_t)((unsigned __int128)Tst * (k + 1) / G);
-        };
-        auto advance = [&]() {
-            while (g + 1 < G && acc >= cum(g)) wg_first[++g] = (uint32_t)pl.nsegs;
-            if (pool_on && !in_pool && acc >= Tst) {
-                in_pool = true;
-                pool_lo = pl.nsegs;
-            }
-        };
-        static const uint64_t bmax = (uint64_t)std::max(4, env_int("VSA_WG_BIG_MAX_KIB", 16384)) << 10;
-        const uint64_t big = std::min(bmax, std::max(smin, ((Tst / G / ns) + 1023) & ~(uint64_t)1023));
-        auto size_now = [&]() -> uint64_t {
-            if (in_pool) return ps;
-            const uint64_t c = cum(g);
-            const uint64_t r = c > acc ? c - acc : 0;
-            uint64_t v = (r / (K * ns) + 1023) & ~(uint64_t)1023;
-            return std::min(smax, std::max(smin, v));
-        };
-        for (uint32_t i = 0; i < nb; i++) {
-            const int64_t sp = spans[i];
-            if (sp < 0) {
+        uint64_t sz = size_now();
+        if (group && 2 * (uint64_t)sp <= sz) {
+            /* a group that can still be a run (runnable) is cut at
+             * VSA_RUN_MAX blocks, so back-to-back 1 KiB blocks scan as runs
+             * of 128 rather than as groups of 255 single blocks */
+            const VsaBlock &bi = out[i];
+            const bool elig = !no_runs && !bi.start && !bi.rlo && bi.len >= VSA_RUN_MIN_LEN;
+            const bool cont = g_n && g_run && elig && bi.base == out[i - 1].base + out[i - 1].len;
+            const uint32_t gcap = cont ? VSA_RUN_MAX : SEG_GROUP_MAX;
+            if (g_n && (g_span + sp > (int64_t)sz || g_n >= gcap)) {
                 flush();
-                continue;
-            }
-            uint64_t sz = size_now();
-            if (group && 2 * (uint64_t)sp <= sz) {
-                /* a group that can still be a run (runnable) is cut at
-                 * VSA_RUN_MAX blocks, so back-to-back 1 KiB blocks scan as
-                 * runs of 128 rather than as groups of 255 single blocks */
-                const VsaBlock &bi = out[i];
-                const bool elig = !no_runs && !bi.start && !bi.rlo && bi.len >= VSA_RUN_MIN_LEN;
-                const bool cont = g_n && g_run && elig &&
-                                  bi.base == out[i - 1].base + out[i - 1].len;
-                const uint32_t gmax = cont ? VSA_RUN_MAX : SEG_GROUP_MAX;
-                if (g_n && (g_span + sp > (int64_t)sz || g_n >= gmax)) {
-                    flush();
-                    advance();
-                }
-                if (!g_n) g_run = elig;
-                else g_run = g_run && elig && bi.base == out[i - 1].base + out[i - 1].len;
-                if (!g_n) g_first = i;
-                out[i].seg_first = pl.nsegs;
-                g_n++;
-                g_span += sp;
-                acc += (uint64_t)sp;
-                if (!in_pool && acc >= cum(g)) { /* the share ends here */
-                    flush();
-                    advance();
-                }
-                continue;
-            }
-            flush();
-            advance();
-            out[i].seg_first = pl.nsegs;
-            for (uint64_t off = 0; off < (uint64_t)sp;) {
-                /* with stealing, a part of a large block is one wave's share
-                 * of its workgroup's bytes: the waves balance by stealing
-                 * sweep groups, so no segment needs to be small (fewer
-                 * segment starts); without it, the guided size; in the pool,
-                 * the pool's size */
-                sz = in_pool ? ps : steal_min() ? big : size_now();
-                /* a piece ends at its share's end: every workgroup gets its
-                 * share to the KiB */
-                const uint64_t cg = cum(g);
-                if (!in_pool && cg > acc) sz = std::min(sz, (cg - acc + 1023) & ~(uint64_t)1023);
-                uint64_t piece = std::min<uint64_t>(sz, (uint64_t)sp - off);
-                /* no sliver shorter than the minimum after this piece */
-                if ((uint64_t)sp - off - piece < smin) piece = (uint64_t)sp - off;
-                push_desc(i, off, piece);
-                off += piece;
-                acc += piece;
                 advance();
             }
+            if (!g_n) g_run = elig;
+            else g_run = g_run && elig && bi.base == out[i - 1].base + out[i - 1].len;
+            if (!g_n) g_first = i;
+            out[i].seg_first = pl.nsegs;
+            g_n++;
+            g_span += sp;
+            acc += (uint64_t)sp;
+            if (acc >= cum(g)) { /* the share ends here */
+                flush();
+                advance();
+            }
+            continue;
         }
         flush();
-        if (!in_pool) pool_lo = pl.nsegs;
-        for (uint64_t k = g + 1; k <= G; k++) wg_first[k] = (uint32_t)pool_lo;
-        wg_first[G] = (uint32_t)pool_lo; /* the pool: segments [wg_first[G], nsegs) */
-        pl.grid = (uint32_t)G;
-        pl.segblk.insert(pl.segblk.end(), wg_first.begin(), wg_first.end());
+        advance();
+        out[i].seg_first = pl.nsegs;
+        for (uint64_t off = 0; off < (uint64_t)sp;) {
+            /* with stealing, a part of a large block is one wave's share of
+             * its workgroup's bytes: the waves balance by stealing sweep
+             * groups, so no segment needs to be small (fewer segment
+             * starts); without it, the guided size */
+            sz = steal_min() ? big : size_now();
+            /* a piece ends at its share's end: every workgroup gets its
+             * share to the KiB */
+            const uint64_t cg = cum(g);
+            if (cg > acc) sz = std::min(sz, (cg - acc + 1023) & ~(uint64_t)1023);
+            uint64_t piece = std::min<uint64_t>(sz, (uint64_t)sp - off);
+            /* no sliver shorter than the minimum after this piece */
+            if ((uint64_t)sp - off - piece < smin) piece = (uint64_t)sp - off;
+            push_desc(i, off, piece);
+            off += piece;
+            acc += piece;
+            advance();
+        }
     }
-    pl.seg_bytes = (uint32_t)seg;
+    flush();
+    for (uint64_t k = g + 1; k <= G; k++) wg_first[k] = (uint32_t)pl.nsegs;
+    pl.grid = (uint32_t)G;
+    pl.segblk.insert(pl.segblk.end(), wg_first.begin(), wg_first.end());
     pl.end_bits = bits_for(span);
     return VSA_OK;
 }
@@ -1475,7 +1139,7 @@ int upload_plan(vsa_ctx *c, const BatchPlan &pl, VsaBlock *d_blocks, uint32_t *d
 
 /* launch a planned batch whose tables are on the device */
 int launch_planned(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, const VsaBlock *d_blocks,
-                   const uint32_t *d_segblk, uint32_t nb, uint64_t segs, uint32_t seg_bytes,
+                   const uint32_t *d_segblk, uint32_t nb, uint64_t segs,
                    uint32_t grid, int end_bits, uint64_t bytes, uint32_t flags, uint64_t *n_out) {
     int r;
     if ((r = ensure_out(c, 1)) != VSA_OK) return r;
@@ -1491,12 +1155,11 @@ int launch_planned(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, const Vs
     c->launch.d_segblk = d_segblk;
     c->launch.nb = nb;
     c->launch.segs = segs;
-    c->launch.seg_bytes = seg_bytes;
     c->launch.grid = grid;
     c->launch.end_bits = end_bits;
     c->launch.bytes = bytes;
     c->launch.flags = flags;
-    if ((r = launch_scan(c, db, d_data, nb, segs, seg_bytes)) != VSA_OK) return r;
+    if ((r = launch_scan(c, db, d_data, nb, segs)) != VSA_OK) return r;
     if (flags & VSA_SCAN_ASYNC) {
         c->pending = true;
         *n_out = 0;
@@ -1516,7 +1179,11 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
     if (int r0 = finish_pending(c)) return r0;
     BatchPlan &pl = c->plan;
     auto T0 = std::chrono::steady_clock::now();
-    const uint64_t waves = (uint64_t)c->num_cus * (LIT_WAVES - db->nconf.load());
+    /* one load of the confirm-wave count (another context may raise it):
+     * the plan's waves and scanning waves per workgroup must agree, or its
+     * workgroup count would exceed the CUs */
+    const uint64_t ns_plan = LIT_WAVES - db->nconf.load();
+    const uint64_t waves = (uint64_t)c->num_cus * ns_plan;
     const uint64_t *in[5] = {offs, lens, starts, hlens, rlos};
     auto &M = c->memo;
     bool same = M.valid && M.d_data == d_data && M.nb == nb && M.waves == waves &&
@@ -1534,7 +1201,7 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         M.valid = false;
         if ((r = ensure_tables(c, nb, 0)) != VSA_OK) return r;
         if ((r = build_plan(d_data, offs, lens, starts, hlens, rlos, nb, waves, pl,
-                            w.h_blocks, LIT_WAVES - db->nconf.load(),
+                            w.h_blocks, ns_plan,
                             c->fb.set[fb_set_of(db)].known ? c->fb.set[fb_set_of(db)].wg
                                                            : nullptr)) != VSA_OK)
             return r;
@@ -1557,7 +1224,7 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         M.valid = true;
     }
     int rr = launch_planned(c, db, d_data, c->ws.d_blocks, c->ws.d_segblk, nb, pl.nsegs,
-                          pl.seg_bytes, pl.grid, pl.end_bits, pl.bytes, flags, n_out);
+                          pl.grid, pl.end_bits, pl.bytes, flags, n_out);
     auto T3 = std::chrono::steady_clock::now();
     /* diagnostic: host-side cost of a per-call plan (tools/exp_host.py) */
     static const bool timing = getenv("VSA_HOST_TIMING") != nullptr;
@@ -1579,8 +1246,8 @@ int complete_scan(vsa_ctx *c, uint64_t *n_out) {
         /* the rescan reads the launch's tables: gone if its plan was freed */
         if (!c->launch.d_blocks || !c->launch.d_segblk) return VSA_E_INVALID;
         if ((r = ensure_out(c, c->ws.h_counters[0])) != VSA_OK) return r;
-        if ((r = launch_scan(c, c->launch.db, c->launch.d_data, c->launch.nb, c->launch.segs,
-                             c->launch.seg_bytes)) != VSA_OK)
+        if ((r = launch_scan(c, c->launch.db, c->launch.d_data, c->launch.nb, c->launch.segs)) !=
+            VSA_OK)
             return r;
     }
     return VSA_E_OVERFLOW;
@@ -1780,7 +1447,7 @@ hwlm_error_t replay_lit(const vsa_db *db, const uint64_t *keys, uint64_t n,
                         bool scratch_is_real = true) {
     const uint8_t *eng = db->hblob + VSA_ROUNDUP_CL(sizeof(HWLM));
     const uint8_t *confBase = eng + ((const uint32_t *)eng)[4];
-    const bool squash_ok = scratch && scratch_is_real && db->mode == VSA_MODE_FDR;
+    const bool squash_ok = scratch && scratch_is_real && db->mode == VSA_MODE_FDR4;
     const long co = g_fdr_conf_off.load(), coo = g_fdr_conf_offset_off.load();
     const size_t nf = floods ? floods->size() : 0;
     size_t fe = 0;
@@ -1970,7 +1637,6 @@ int64_t pair_host(const uint8_t *lo1, const uint8_t *hi1, const uint8_t *lo2,
     P.first = first;
     uint64_t want = (len + 255) / 256;
     uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * 4));
-    (void)hipGetLastError(); /* checks below are for this launch */
     hipLaunchKernelGGL(vsa_pair_scan, dim3(grid), dim3(256), 0, c->stream, P);
     if (hipGetLastError() != hipSuccess) return -2;
     if (hipMemcpyAsync(w.h_counters + PAIR_BASE, first, 48 * 8, hipMemcpyDeviceToHost,
@@ -2061,7 +1727,6 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (!c) return VSA_E_INVALID;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    if (c->sort_stream) (void)hipStreamSynchronize(c->sort_stream);
     /* plans outliving the context keep only their own device tables */
     for (vsa_plan *p : c->plans) p->ctx = nullptr;
     Workspace &w = c->ws;
@@ -2078,8 +1743,6 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (w.h_pub) (void)hipHostFree(w.h_pub);
     if (c->fb.h) (void)hipHostFree(c->fb.h);
     if (c->fb.d_rec) (void)hipFree(c->fb.d_rec);
-    if (c->cls_bounds_d) (void)hipFree(c->cls_bounds_d);
-    if (c->cls_bounds_h) (void)hipHostFree(c->cls_bounds_h);
     if (w.h_in) (void)hipHostFree(w.h_in);
     if (w.d_blocks) (void)hipFree(w.d_blocks);
     if (w.h_blocks) (void)hipHostFree(w.h_blocks);
@@ -2087,11 +1750,8 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->ev_rec) (void)hipEventDestroy(c->ev_rec);
-    if (c->ev_sorted) (void)hipEventDestroy(c->ev_sorted);
-    if (c->sort_stream) (void)hipStreamDestroy(c->sort_stream);
     if (t_ctx == c) t_ctx = nullptr;
     delete c; /* drops its hold on the stream */
-    (void)hipGetLastError(); /* ignored statuses do not outlive the call */
     return VSA_OK;
 }
 
@@ -2111,82 +1771,18 @@ void *vsa_ctx_stream(vsa_ctx_t *c) { return c ? (void *)c->stream : nullptr; }
 
 /* ------------------------------------------- derived FDR first stage -- */
 
-/* The device first stage for an FDR engine is a stride-1 shift-or table
- * rebuilt from the engine's own confirm records (every LitInfo's v / msk,
- * fdr_confirm.h:57-65), in the reference's bucket layout: bit (k * 8 + b)
- * of T[key] is 0 when some literal of bucket b is consistent with the two
- * bytes sitting k bytes before its end (getMultiEntriesAtPosition,
- * fdr_compile.cpp:520-600, restated over the 8-byte confirm window; the
- * byte after the end is a don't-care).  Every literal the confirm accepts is
- * consistent at every window, so the set of confirmed matches is exactly the
- * reference's, for any stride / domain of the bytecode and any key function.
- * The key is fdr_key (kernels.h): 7 bits of each byte, the two halves of a
- * printable pair exactly (the reference's domainMask keeps the first byte
- * whole and cuts the second, fdr_compile.cpp:185-187); on the cfg-4 set
- * this admits 2.8x fewer first-stage candidates than 8 + 6 bits. */
-static void derive_fdr_table(const uint8_t *eng, const uint32_t conf_off[8], uint32_t bits,
-                             std::vector<uint64_t> &T) {
-    const uint32_t n = 1u << bits;
-    T.assign(n, ~0ULL);
-    uint64_t always = 0; /* (k, b) columns open for every key */
-    const uint8_t *confBase = eng + ((const uint32_t *)eng)[4];
-    for (uint32_t b = 0; b < 8; b++) {
-        if (!conf_off[b]) continue;
-        const uint8_t *fc = confBase + conf_off[b];
-        const FDRConfirm *cf = (const FDRConfirm *)fc;
-        const uint32_t *li = (const uint32_t *)(fc + sizeof(FDRConfirm));
-        std::vector<uint32_t> offs;
-        for (uint32_t h = 0; h < (1u << cf->nBits); h++) {
-            uint32_t o = li[h];
-            if (!o) continue;
-            for (;;) {
-                offs.push_back(o);
-                const LitInfo *L = (const LitInfo *)(fc + o);
-                if (!L->next) break;
-                o += sizeof(LitInfo);
-            }
-        }
-        std::sort(offs.begin(), offs.end());
-        offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
-        for (uint32_t o : offs) {
-            const LitInfo *L = (const LitInfo *)(fc + o);
-            for (uint32_t k = 0; k < 8; k++) {
-                const uint64_t bit = 1ULL << (k * 8 + b);
-                /* first key byte: k bytes before the end (byte 7 - k of v) */
-                const uint8_t m0 = (uint8_t)(L->msk >> (8 * (7 - k)));
-                const uint8_t v0 = (uint8_t)(L->v >> (8 * (7 - k))) & m0;
-                /* second key byte: k - 1 before the end (k = 0: past it) */
-                uint8_t m1 = 0, v1 = 0;
-                if (k >= 1) {
-                    m1 = (uint8_t)(L->msk >> (8 * (8 - k)));
-                    v1 = (uint8_t)(L->v >> (8 * (8 - k))) & m1;
-                }
-                /* every (x0, x1) consistent with the literal -> its key */
-                std::vector<uint32_t> c0, c1;
-                for (uint32_t x = 0; x < 256; x++) {
-                    if ((x & m0) == v0) c0.push_back(x);
-                    if ((x & m1) == v1) c1.push_back(x);
-                }
-                if (c0.size() * c1.size() >= 65536) {
-                    always |= bit; /* no constraint at this position */
-                    continue;
-                }
-                for (uint32_t x0 : c0)
-                    for (uint32_t x1 : c1) T[vsa_fdr_key(x0, x1, n - 1)] &= ~bit;
-            }
-        }
-    }
-    if (always) {
-        for (auto &t : T) t &= ~always;
-    }
-}
-
-/* The 4-field FDR first stage (VSA_MODE_FDR4), derived like
- * derive_fdr_table: bit (f * 8 + b) of T[key] is 0 when some literal of
+/* The device first stage of an FDR engine, rebuilt at load time from the
+ * engine's own confirm records (every LitInfo's v / msk, fdr_confirm.h:
+ * 57-65), in the reference's bucket layout.  The reference's first stages
+ * are filters whose only contract is "no false negatives": every literal
+ * the confirm accepts is consistent at every window, so the set of
+ * confirmed matches is exactly the reference's for any stride / domain of
+ * the bytecode and any key function.  The 4-field table (VSA_MODE_FDR4):
+ * bit (f * 8 + b) of T[key] is 0 when some literal of
  * bucket b is consistent with the three bytes ending f bytes before its end
  * (back offsets f + 2, f + 1, f; bytes before the literal are don't-cares,
- * msk 0), keyed by vsa_fdr4_key (kernels.h: 7 + 7 bits of the last two and,
- * at 15 bits, bit 0 of the first).  u32 entries, 4 fields.  On the cfg-4
+ * msk 0), keyed by vsa_fdr4_key (kernels.h: 15 bits, 7 + 7 of the last
+ * two and bit 0 of the first).  u32 entries, 4 fields.  On the cfg-4
  * set it passes half the candidate bits of the 8-field pair table (1.7e-4
  * against 3.3e-4 per byte, tools/sim_filter.py s1_tri177_f4) from the same
  * 128 KiB, and its even positions alone leave 4.0 % of ends live against
@@ -2244,14 +1840,14 @@ static void derive_fdr4_table(const uint8_t *eng, const uint32_t conf_off[8], ui
                 mv(f + 1, &m1, &v1);
                 mv(f + 2, &m2, &v2);
                 const auto c0 = proj(m0, v0, 0x7f), c1 = proj(m1, v1, 0x7f);
-                const auto c2 = proj(m2, v2, bits >= 15 ? 1u : 0u);
+                const auto c2 = proj(m2, v2, 1u);
                 if (c0.size() * c1.size() * c2.size() >= n) {
                     always |= bit;
                     continue;
                 }
                 for (uint32_t x2 : c2)
                     for (uint32_t x1 : c1)
-                        for (uint32_t x0 : c0) T[vsa_fdr4_key(x2, x1, x0, bits)] &= ~bit;
+                        for (uint32_t x0 : c0) T[vsa_fdr4_key(x2, x1, x0)] &= ~bit;
             }
         }
     }
@@ -2272,7 +1868,7 @@ static double fdr4_text_rate(const std::vector<uint32_t> &T) {
     for (uint32_t b2 = 0; b2 < 2; b2++)
         for (uint32_t b0 = 0x20; b0 < 0x7f; b0++)
             for (uint32_t b1 = 0x20; b1 < 0x7f; b1++) {
-                const uint32_t e = ~T[vsa_fdr4_key(b2, b1, b0, 15)];
+                const uint32_t e = ~T[vsa_fdr4_key(b2, b1, b0)];
                 n++;
                 for (int k = 0; k < 32; k++) live[k] += (e >> k) & 1u;
             }
@@ -2362,9 +1958,7 @@ int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
         if (db->engine_id == VSA_ENGINE_FDR) {
             const FDR *f = (const FDR *)eng;
             if (f->domain < 9 || f->domain > 15) return VSA_E_INVALID;
-            db->mode = VSA_MODE_FDR;
-            db->table_entries = 1u << f->domain;
-            db->dmask = f->domainMask;
+            db->mode = VSA_MODE_FDR4;
             memcpy(&db->state_lo, f->start.b, 8);
             memcpy(&db->state_hi, f->start.b + 8, 8);
             db->nbuckets = 8;
@@ -2393,14 +1987,13 @@ int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
         /* prefilter bitmaps: bit h of bucket b = (litIndex_b[h] != 0) */
         std::vector<uint32_t> slots;
         for (uint32_t b = 0; b < 16; b++) db->slot_off[b] = 0xffffffffu;
-        const bool no_pf = getenv("VSA_NO_PREFILTER") != nullptr;
         db->pf_mult = 0;
         /* eligible buckets (one kernel-wide multiplier); when the exact
          * bitmaps exceed SLOT_WORDS_MAX the largest are coarsened: bit h >> k
          * of a 2^(nbits - k)-bit map = OR of the exact bits it covers (the
          * hash's top nbits - k bits), still a no-false-negative prefilter */
         uint32_t nb_full[16] = {0}, nb_use[16] = {0};
-        for (uint32_t b = 0; b < db->nbuckets && !no_pf; b++) {
+        for (uint32_t b = 0; b < db->nbuckets; b++) {
             if (!db->conf_off[b]) continue;
             const uint8_t *fc = (const uint8_t *)confBase + db->conf_off[b];
             const uint32_t nbits = *(const uint32_t *)(fc + 16);
@@ -2446,16 +2039,13 @@ int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
     VSA_CHECK(hipSetDevice(c->device));
     VSA_CHECK(hipMalloc(&db->d_blob, size));
     VSA_CHECK(hipMemcpy(db->d_blob, db->hblob, size, hipMemcpyHostToDevice));
-    uint32_t qc4 = 0;
-    if (db->mode == VSA_MODE_FDR && !getenv("VSA_FDR8") &&
-        plan_lds((size_t)4 << 15, db->slot_words, 48, &qc4) <= LDS_BUDGET) {
-        /* the 4-field first stage (derive_fdr4_table, 15-bit keys) when the
-         * 128 KiB table fits in LDS beside the rings and slot bitmaps; else,
-         * or with VSA_FDR8=1 (A/B), the 8-field pair table below */
+    if (db->mode == VSA_MODE_FDR4) {
+        /* the 4-field first stage (derive_fdr4_table, 15-bit keys): its 128
+         * KiB always fit in LDS beside the rings and the slot bitmaps (<= 12
+         * KiB, SLOT_WORDS_MAX) */
         const uint32_t bits = 15;
         std::vector<uint32_t> T;
         derive_fdr4_table(eng, db->conf_off, bits, T);
-        db->fdr4 = true;
         db->table_entries = 1u << bits;
         db->dmask = (1u << bits) - 1;
         db->est_rate = fdr4_text_rate(T);
@@ -2470,19 +2060,6 @@ int vsa_db_load(vsa_ctx_t *c, const void *hwlm, size_t size, vsa_db_t **out) {
         }
         VSA_CHECK(hipMalloc(&db->d_table, T.size() * 4));
         VSA_CHECK(hipMemcpy(db->d_table, T.data(), T.size() * 4, hipMemcpyHostToDevice));
-    } else if (db->mode == VSA_MODE_FDR) {
-        /* derived stride-1 first stage: domain 14 when it fits in LDS beside
-         * the rings and slot bitmaps, else 13 (see derive_fdr_table) */
-        uint32_t qc = 0;
-        uint32_t bits = 14;
-        if (getenv("VSA_FDR_DOMAIN")) bits = (uint32_t)std::min(15, std::max(13, atoi(getenv("VSA_FDR_DOMAIN"))));
-        else if (plan_lds((size_t)8 << 14, db->slot_words, 48, &qc) > LDS_BUDGET) bits = 13;
-        std::vector<uint64_t> T;
-        derive_fdr_table(eng, db->conf_off, bits, T);
-        db->table_entries = 1u << bits;
-        db->dmask = (1u << bits) - 1;
-        VSA_CHECK(hipMalloc(&db->d_table, T.size() * 8));
-        VSA_CHECK(hipMemcpy(db->d_table, T.data(), T.size() * 8, hipMemcpyHostToDevice));
     }
     if (db->mode == VSA_MODE_TEDDY || db->mode == VSA_MODE_FAT) {
         /* exact byte table from the confirm records (derive_teddy_table) */
@@ -2509,17 +2086,14 @@ int vsa_db_free(vsa_db_t *db) {
         }
     }
     delete db;
-    /* the frees' statuses are ignored: none stays the thread's last error
-     * (a later launch check would read it) */
-    (void)hipGetLastError();
     return VSA_OK;
 }
 
-/* Host-only: the first stage vsa_db_load derives for an HWLM blob (FDR:
- * 2^bits stride-1 entries keyed by b[p] | (b[p+1] & mask) << 8; Teddy / Fat
- * Teddy: 256 byte entries), for tests and tools.  *key_bits = 14 for FDR,
- * 8 for Teddy; *field_bits = buckets per field (8 or 16).  Returns the
- * number of entries written (<= cap), or a VSA_E_* code. */
+/* Host-only: the first stage vsa_db_load derives for a Teddy / Fat Teddy
+ * blob (256 byte entries), for tests and tools (FDR engines:
+ * vsa_derive_fdr4_table).  *key_bits = 8; *field_bits = buckets per field
+ * (8 or 16).  Returns the number of entries written (<= cap), or a VSA_E_*
+ * code. */
 int vsa_derive_first_stage(const void *hwlm, size_t size, uint64_t *table, uint32_t cap,
                            uint32_t *key_bits, uint32_t *field_bits) {
     if (!hwlm || !table || size < VSA_ROUNDUP_CL(sizeof(HWLM))) return VSA_E_INVALID;
@@ -2530,12 +2104,7 @@ int vsa_derive_first_stage(const void *hwlm, size_t size, uint64_t *table, uint3
     const uint32_t *confBase = (const uint32_t *)(eng + ((const uint32_t *)eng)[4]);
     uint32_t conf_off[16] = {0};
     std::vector<uint64_t> T;
-    if (id == VSA_ENGINE_FDR) {
-        for (int b = 0; b < 8; b++) conf_off[b] = confBase[b];
-        derive_fdr_table(eng, conf_off, 14, T);
-        *key_bits = 14;
-        *field_bits = 8;
-    } else if (vsa_engine_is_teddy(id)) {
+    if (vsa_engine_is_teddy(id)) {
         const bool fat = vsa_engine_is_fat(id);
         for (int b = 0; b < (fat ? 16 : 8); b++) conf_off[b] = confBase[b];
         if (fat) derive_teddy_table(eng, conf_off, 16, 4, 16, T);
@@ -2550,12 +2119,12 @@ int vsa_derive_first_stage(const void *hwlm, size_t size, uint64_t *table, uint3
     return (int)n;
 }
 
-/* Host-only: the 4-field first stage (derive_fdr4_table) of an FDR blob at
- * `bits` (14 or 15) key bits, for tests and tools.  Returns the entries
- * written (<= cap) or a VSA_E_* code. */
+/* Host-only: the 4-field first stage (derive_fdr4_table) of an FDR blob,
+ * for tests and tools (bits must be 15: vsa_fdr4_key).  Returns the
+ * entries written (<= cap) or a VSA_E_* code. */
 int vsa_derive_fdr4_table(const void *hwlm, size_t size, uint32_t bits, uint32_t *table,
                           uint32_t cap) {
-    if (!hwlm || !table || size < VSA_ROUNDUP_CL(sizeof(HWLM)) || bits < 14 || bits > 15)
+    if (!hwlm || !table || size < VSA_ROUNDUP_CL(sizeof(HWLM)) || bits != 15)
         return VSA_E_INVALID;
     const HWLM *h = (const HWLM *)hwlm;
     if (h->type != HWLM_ENGINE_FDR) return VSA_E_INVALID;
@@ -2657,6 +2226,12 @@ int vsa_scan_wait(vsa_ctx_t *c, uint64_t *n_matches) {
 
 int vsa_scan_results(vsa_ctx_t *c, const uint64_t **k, const uint32_t **ids) {
     if (!c) return VSA_E_INVALID;
+    /* The pointers go to callers that read them on any stream (or the
+     * host): the scan is completed and its whole queue (the binned sort
+     * publishes the counters from its first workgroup, before the others
+     * have written their bins) has finished before they are handed out. */
+    if (int r = finish_pending(c)) return r;
+    VSA_CHECK(hipStreamSynchronize(c->stream));
     if (k) *k = c->ws.d_keys[c->cur];
     if (ids) *ids = c->ws.d_ids[c->cur];
     return VSA_OK;
@@ -2669,8 +2244,6 @@ int vsa_scan_pack(vsa_ctx_t *c, void *d_dst, uint64_t cap) {
     if (c->pending && c->launch.published && c->launch.dev_sort) {
         /* the async binned scan's sorted records (buffer 1) and the counters
          * vsa_publish keeps on the device: queued behind it, no wait */
-        if (int r0 = join_sort(c)) return r0;
-        (void)hipGetLastError(); /* checks below are for this launch */
         hipLaunchKernelGGL(vsa_pack, dim3(grid), dim3(256), 0, c->stream,
                            (const unsigned long long *)c->ws.d_counters + 144,
                            (uint64_t)c->ws.out_cap, (const uint64_t *)c->ws.d_keys[1],
@@ -2684,7 +2257,6 @@ int vsa_scan_pack(vsa_ctx_t *c, void *d_dst, uint64_t cap) {
     unsigned long long *save = c->ws.d_counters + 144;
     unsigned long long hv[16] = {c->last_n, 0};
     VSA_CHECK(hipMemcpyAsync(save, hv, sizeof(hv), hipMemcpyHostToDevice, c->stream));
-    (void)hipGetLastError(); /* checks below are for this launch */
     hipLaunchKernelGGL(vsa_pack, dim3(grid), dim3(256), 0, c->stream,
                        (const unsigned long long *)save, (uint64_t)c->ws.out_cap,
                        (const uint64_t *)c->ws.d_keys[c->cur], (const uint32_t *)c->ws.d_ids[c->cur],
@@ -2792,61 +2364,25 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
     P.last = part + 1;
     P.count = part + 2;
     P.slots = CLASS_SLOTS;
-    const bool lut = !cls2 && len >= ((uint64_t)8 << 20) && !getenv("VSA_CLASS_SIMPLE");
+    const bool lut = !cls2 && len >= ((uint64_t)8 << 20);
     const uint64_t G = (uint64_t)c->num_cus;
     const uint64_t wspan = ((len + G - 1) / G + 4095) & ~(uint64_t)4095;
     const uint32_t lgrid = (uint32_t)((len + wspan - 1) / wspan);
-    /* schedule feedback for the class scan (kind 2): weighted 4 KiB-aligned
-     * bounds per workgroup, uploaded (before the timed region) when they
-     * change.  Off by default (VSA_CLASS_FEEDBACK=1): at 256 MiB it measured
-     * no gain, 0.0592 / 0.0597 / 0.0566 ms against 0.0593 / 0.0587 / 0.0580
-     * without (profiles/r04p_configs.jsonl, r04p_cfg2_nofb.jsonl) */
-    static const bool cls_fb = env_int("VSA_CLASS_FEEDBACK", 0) != 0;
-    vsa_ctx::FbSet &F = c->fb.set[2];
-    if (lut && cls_fb && xcd_feedback_on() && F.known && lgrid == G && lgrid <= 1024) {
-        if (!c->cls_bounds_d) {
-            VSA_CHECK(hipMalloc(&c->cls_bounds_d, 1025 * sizeof(uint64_t)));
-            VSA_CHECK(hipHostMalloc((void **)&c->cls_bounds_h, 1025 * sizeof(uint64_t),
-                                    hipHostMallocDefault));
-        }
-        if (c->cls_bounds_key[0] != len || c->cls_bounds_key[1] != lgrid ||
-            c->cls_bounds_key[2] != F.version + 1) {
-            double tw = 0, a = 0;
-            for (uint32_t b = 0; b < lgrid; b++) tw += F.wg[b];
-            c->cls_bounds_h[0] = 0;
-            for (uint32_t b = 0; b < lgrid; b++) {
-                a += F.wg[b];
-                const uint64_t e =
-                    b + 1 == lgrid
-                        ? len
-                        : std::min<uint64_t>(len, ((uint64_t)((double)len * a / tw) + 2048) &
-                                                      ~(uint64_t)4095);
-                c->cls_bounds_h[b + 1] = std::max<uint64_t>(c->cls_bounds_h[b], e);
-            }
-            VSA_CHECK(hipMemcpyAsync(c->cls_bounds_d, c->cls_bounds_h, (lgrid + 1) * 8,
-                                     hipMemcpyHostToDevice, c->stream));
-            c->cls_bounds_key[0] = len;
-            c->cls_bounds_key[1] = lgrid;
-            c->cls_bounds_key[2] = F.version + 1;
-        }
-        P.wg_lo = c->cls_bounds_d;
-    }
+    /* Schedule feedback (per-XCD weighted bounds) for the class scan measured
+     * no gain at 256 MiB (0.0592 / 0.0597 / 0.0566 ms against 0.0593 /
+     * 0.0587 / 0.0580, profiles/r04p_configs.jsonl, r04p_cfg2_nofb.jsonl)
+     * and was removed in round 5: equal spans. */
     VSA_CHECK(hipEventRecord(c->ev0, c->stream));
     if (lut) {
         /* large buffers: pair-LUT kernel, one 1024-thread workgroup per CU,
          * an equal 4 KiB-aligned share per workgroup, taken by its waves in
          * 4 KiB groups (kernels.hip vsa_class_scan_lut) */
-        /* (an asynchronous literal scan still in flight keeps its record) */
-        if (cls_fb && c->fb.armed < 0) arm_feedback(c, 2, lgrid, len, false);
-        P.wg_time = c->fb.armed == 2 ? c->fb.d : nullptr;
-        (void)hipGetLastError(); /* checks below are for this launch */
         hipLaunchKernelGGL(vsa_class_scan_lut, dim3(lgrid), dim3(1024), 0, c->stream, P, wspan);
     } else {
         uint64_t chunks = (len + 15) / 16;
         uint64_t want = (chunks + 255) / 256;
         uint64_t cap = (uint64_t)c->num_cus * 8;
         uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
-        (void)hipGetLastError(); /* checks below are for this launch */
         hipLaunchKernelGGL(vsa_class_scan, dim3(grid), dim3(256), 0, c->stream, P);
     }
     VSA_CHECK(hipGetLastError());
@@ -2854,12 +2390,10 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
     VSA_CHECK(hipMemcpyAsync(w.h_counters + CLASS_BASE, part, 16 * CLASS_SLOTS * 8,
                              hipMemcpyDeviceToHost, c->stream));
     VSA_CHECK(hipStreamSynchronize(c->stream));
-    take_feedback(c);
     {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_kernel_ms = ms;
-        /* a not-yet-observed event (the published path completes on the
-         * publish, not on ev1) must not leave hipErrorNotReady as the
+        /* a not-ready event status is not an error: it must not stay the
          * thread's last error for the next launch check */
         (void)hipGetLastError();
     }
@@ -3503,6 +3037,18 @@ int vsa_plan_describe(const uint8_t *d_data, const uint64_t *offsets, const uint
     return (int)pl.segblk.size();
 }
 
+int vsa_plan_blocks(const uint8_t *d_data, const uint64_t *offsets, const uint64_t *lens,
+                    const uint64_t *starts, const uint64_t *hlens, const uint64_t *report_lo,
+                    uint32_t nblocks, void *out) {
+    if (!offsets || !lens || !nblocks || !out) return VSA_E_INVALID;
+    BatchPlan pl;
+    int r = build_plan(d_data, offsets, lens, starts, hlens, report_lo, nblocks,
+                       (uint64_t)256 * (LIT_WAVES - 1), pl);
+    if (r != VSA_OK) return r;
+    memcpy(out, pl.blocks.data(), (size_t)nblocks * sizeof(VsaBlock));
+    return VSA_OK;
+}
+
 /* Host-only (tests): the schedule feedback's weight updates over `launches`
  * synthetic launches of `grid` workgroups (workgroup b on XCD b % 8) whose
  * XCDs stream at rate[x] (any unit; a workgroup's time = its share / its
@@ -3556,7 +3102,6 @@ int vsa_plan_create(vsa_ctx_t *c, const uint8_t *d_data, const uint64_t *offsets
     p->d_data = d_data;
     p->nb = nblocks;
     p->segs = pl.nsegs;
-    p->seg_bytes = pl.seg_bytes;
     p->grid = pl.grid;
     p->end_bits = pl.end_bits;
     p->bytes = pl.bytes;
@@ -3597,7 +3142,6 @@ int vsa_plan_free(vsa_plan_t *p) {
     if (p->d_segblk) (void)hipFree(p->d_segblk);
     if (p->h_stage) (void)hipHostFree(p->h_stage);
     delete p;
-    (void)hipGetLastError(); /* ignored statuses do not outlive the call */
     return r;
 }
 
@@ -3608,8 +3152,7 @@ int vsa_plan_free(vsa_plan_t *p) {
  * the weights move by > 1 % steps, so this happens a few times while they
  * settle).  A map that would outgrow its buffer keeps the old one. */
 int refresh_plan(vsa_ctx *c, const vsa_db *db, vsa_plan *p) {
-    static const bool refresh = env_int("VSA_FB_REFRESH", 1) != 0; /* A/B knob */
-    if (!refresh || !xcd_feedback_on() || p->grid < 64 || p->in[0].empty()) return VSA_OK;
+    if (!xcd_feedback_on() || p->grid < 64 || p->in[0].empty()) return VSA_OK;
     const int si = fb_set_of(db);
     if (!c->fb.set[si].known) return VSA_OK;
     const uint64_t key = fb_key_of(c, db);
@@ -3620,13 +3163,24 @@ int refresh_plan(vsa_ctx *c, const vsa_db *db, vsa_plan *p) {
                        (uint64_t)c->num_cus * (LIT_WAVES - 1), pl, nullptr, LIT_WAVES - 1,
                        c->fb.set[si].wg);
     if (r != VSA_OK) return r;
-    p->fb_key = key;
-    if (pl.segblk.size() > p->segblk_cap || pl.blocks.size() != p->nb) return VSA_OK;
+    if (pl.blocks.size() != p->nb) return VSA_E_INVALID;
+    const size_t bb = (size_t)p->nb * sizeof(VsaBlock);
+    if (pl.segblk.size() > p->segblk_cap) {
+        /* weighted shares cut more pieces than the map had room for: grow
+         * it (the context's previous scan, the only reader, is complete) */
+        const size_t cap = pl.segblk.size() + pl.segblk.size() / 4;
+        uint32_t *d = nullptr;
+        VSA_CHECK(hipMalloc(&d, cap * sizeof(uint32_t)));
+        VSA_CHECK(hipFree(p->d_segblk));
+        p->d_segblk = d;
+        p->segblk_cap = cap;
+        if (p->h_stage) VSA_CHECK(hipHostFree(p->h_stage));
+        p->h_stage = nullptr;
+    }
     /* through a pinned staging buffer, queued on the scan stream: no host
      * wait.  The staging is rewritten only at this plan's next refresh, by
      * then this context's next scan -- queued behind these copies -- has
      * completed (finish_pending), so the copies have run */
-    const size_t bb = (size_t)p->nb * sizeof(VsaBlock);
     if (!p->h_stage)
         VSA_CHECK(hipHostMalloc(&p->h_stage, bb + p->segblk_cap * sizeof(uint32_t),
                                 hipHostMallocDefault));
@@ -3645,8 +3199,14 @@ int refresh_plan(vsa_ctx *c, const vsa_db *db, vsa_plan *p) {
                              hipMemcpyHostToDevice, c->stream));
     p->segs = pl.nsegs;
     p->grid = pl.grid;
+    /* the weights it follows now (only once applied: a failed rebuild is
+     * tried again at the next scan) */
+    p->fb_key = key;
+    p->rebuilds++;
     return VSA_OK;
 }
+
+uint32_t vsa_plan_rebuilds(const vsa_plan_t *p) { return p ? p->rebuilds : 0u; }
 
 int vsa_scan_plan(vsa_ctx_t *c, const vsa_db_t *db, const vsa_plan_t *p, uint32_t flags,
                   uint64_t *n_matches) {
@@ -3655,7 +3215,7 @@ int vsa_scan_plan(vsa_ctx_t *c, const vsa_db_t *db, const vsa_plan_t *p, uint32_
     if (int r1 = refresh_plan(c, db, const_cast<vsa_plan *>(p))) return r1;
     uint64_t dummy;
     return launch_planned(c, db, p->d_data, p->d_blocks, p->d_segblk, p->nb, p->segs,
-                          p->seg_bytes, p->grid, p->end_bits, p->bytes, flags,
+                          p->grid, p->end_bits, p->bytes, flags,
                           n_matches ? n_matches : &dummy);
 }
 
