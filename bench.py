@@ -164,6 +164,11 @@ def main():
                     help="one scan context: each step completed before the next is queued")
     ap.add_argument("--no-settle", action="store_true",
                     help="skip the clock-settle launches before the warmup steps")
+    ap.add_argument("--dist", action="store_true",
+                    help="run the N > 1 exchange (process group, PackedGather collectives) "
+                         "even at N = 1: the RCCL path on a one-GPU box")
+    ap.add_argument("--no-ceiling", action="store_true",
+                    help="skip the streaming-read ceiling probe (roofline.peak_measured)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="host threads for the oracle / cpu_baseline (default min(16, cpus))")
     args = ap.parse_args()
@@ -196,8 +201,13 @@ def run(args):
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count())
                        if backend != "nccl" else local)
     torch.cuda.set_device(dev)
-    if world > 1:
+    if world > 1 or args.dist:
         import torch.distributed as dist
+        if world == 1:
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -314,6 +324,12 @@ def run(args):
             if settle_n >= 40 and max(hist[-8:]) <= 1.02 * min(hist[-8:]):
                 break
     t_settle = time.perf_counter() - t_settle
+    # the box's streaming-read ceiling over this rank's own corpus buffer
+    # (untimed; a plain 16-byte-load kernel, vsa_read_ceiling): the HBM rate
+    # a scan could reach here, beside the 8 TB/s spec peak
+    ceiling = None
+    if not args.no_ceiling:
+        ceiling = ctx.read_ceiling(data.data_ptr(), data.numel(), 5)
     if dist is not None:
         dist.barrier()
     run_steps(args.warmup)
@@ -487,7 +503,9 @@ def run(args):
             "config": {"workload": "cfg4: FDR %d literals len 4-8 (2%% nocase), one %.0f GiB "
                                    "corpus as %d blocks striped over %d GPU(s), engine id %s" %
                                    (args.lits, args.gib, nblocks, world, blob.engine_id),
-                       "global_bytes": total, "parallelism": "stripe%d" % world},
+                       "global_bytes": total, "parallelism": "stripe%d" % world,
+                       "exchange": ("rccl" if dist is not None and backend == "nccl" else
+                                    backend if dist is not None else None)},
             "matches": nm,
             "confirm_candidates": ncand,
             "parity": parity,
@@ -497,6 +515,11 @@ def run(args):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "kernel_ms": round(kavg, 4),
+                         "peak_measured": round(ceiling[0], 1) if ceiling else None,
+                         "frac_of_measured": round(achieved / ceiling[0], 4) if ceiling else None,
+                         "peak_measured_how": "vsa_read_ceiling: plain 16-byte-load read of "
+                                              "%d bytes of this rank's corpus buffer, best of 5, "
+                                              "untimed setup" % ceiling[2] if ceiling else None,
                          "scope": "rank 0 scan kernel (%d input bytes)" % local_bytes},
             "cpu_baseline": cpu,
             "pipeline": nslot,

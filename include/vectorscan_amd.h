@@ -325,6 +325,13 @@ uint64_t vsa_scan_candidates(vsa_ctx_t *ctx);
 int vsa_scan_debug_counters(vsa_ctx_t *ctx, uint64_t out[16]);
 /* Device time (ms, hipEvents on the scan stream) of the last scan kernel. */
 double vsa_scan_kernel_ms(vsa_ctx_t *ctx);
+/* Measurement helper, not a scan (no reference counterpart): the streaming-
+ * read ceiling of this device over d_data -- the first len rounded down to
+ * 64 KiB read once per run by a plain 16-byte-load kernel on the ctx stream,
+ * best of `runs` after one untimed run.  *bytes = the bytes read per run.
+ * Synchronous.  bench.py reports it as roofline.peak_measured. */
+int vsa_read_ceiling(vsa_ctx_t *ctx, const uint8_t *d_data, uint64_t len, uint32_t runs,
+                     double *best_ms, uint64_t *bytes);
 
 /* Byte-class scan over a device buffer: class = 256-bit membership bitmap
  * (bit c of byte c>>3).  class2 non-NULL: pair mode (class at i, class2 at

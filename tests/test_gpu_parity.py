@@ -262,6 +262,10 @@ def test_gpu_schedule_feedback_512mib(ctx):
                 assert oracle.digest_of(res["key"] >> np.uint64(24), res["id"]) == want
             else:
                 assert np.array_equal(cur[0], first[0]) and np.array_equal(cur[1], first[1]), k
+            if k == 7:
+                # the first complete feedback record always publishes weights
+                # (feedback_update), so the prebuilt plan was rebuilt for them
+                assert plan.rebuilds() >= 1
     finally:
         if plan is not None:
             plan.close()

@@ -145,6 +145,7 @@ _sig("vsa_plan_create", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c
      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
      ctypes.POINTER(ctypes.c_void_p))
 _sig("vsa_plan_free", ctypes.c_int, ctypes.c_void_p)
+_sig("vsa_plan_rebuilds", ctypes.c_uint32, ctypes.c_void_p)
 _sig("vsa_scan_plan", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_uint32, _u64p)
 _sig("vsa_scan_wait", ctypes.c_int, ctypes.c_void_p, _u64p)
@@ -160,6 +161,8 @@ _sig("vsa_scan_debug_counters", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)
 _sig("vsa_derive_first_stage", ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
      ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32))
 _sig("vsa_scan_kernel_ms", ctypes.c_double, ctypes.c_void_p)
+_sig("vsa_read_ceiling", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+     ctypes.c_uint32, ctypes.POINTER(ctypes.c_double), _u64p)
 _sig("vsa_class_scan", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, _u64p,
      _u64p, _u64p, ctypes.c_uint32)
@@ -785,6 +788,15 @@ class Context:
         """Device time of the last scan kernel (hipEvents on the scan stream)."""
         return lib.vsa_scan_kernel_ms(self.ptr)
 
+    def read_ceiling(self, d_data, length, runs=5):
+        """(GB/s, ms, bytes): this device's streaming-read ceiling over the
+        device buffer at d_data (vsa_read_ceiling), best of `runs`."""
+        ms = ctypes.c_double()
+        n = ctypes.c_uint64()
+        _check(lib.vsa_read_ceiling(self.ptr, d_data, length, runs, ctypes.byref(ms),
+                                    ctypes.byref(n)))
+        return n.value / (ms.value * 1e-3) / 1e9, ms.value, n.value
+
     def class_scan(self, cls, d_data, length, d_bitmap=None, cls2=None):
         cls = np.ascontiguousarray(cls, np.uint8)
         c2 = None if cls2 is None else np.ascontiguousarray(cls2, np.uint8)
@@ -824,6 +836,11 @@ class Plan:
     def __init__(self, ctx, ptr):
         self.ctx = ctx
         self.ptr = ptr
+
+    def rebuilds(self):
+        """how many times the plan's segment map was rebuilt for new XCD
+        feedback weights (vsa_plan_rebuilds)"""
+        return lib.vsa_plan_rebuilds(self.ptr)
 
     def close(self):
         if self.ptr:

@@ -642,8 +642,11 @@ __device__ __forceinline__ void fdr4_conf(const LitShared &L, const u32 (&d)[4],
     u64 m[5];
 #pragma unroll
     for (int k = 0; k < 4; k++) m[k] = __builtin_amdgcn_ballot_w64(U[k] != 0xffffffffu);
-    /* U[4]: ends 16..18 (the next lane's 0..2); its byte 3 is never set */
-    m[4] = __builtin_amdgcn_ballot_w64((U[4] | 0xff000000u) != 0xffffffffu);
+    /* ends 16..18 are the next lane's ends 0..2: live unless that lane's own
+     * level 1 already killed its ends 0..3 (bit l + 1 of m[0]; lane 63's next
+     * lane is the next chunk's lane 0, unknown here, so live).  U[4] itself
+     * always has end 18 live: level 1 never reaches it. */
+    m[4] = (m[0] >> 1) | (1ull << 63);
 #pragma unroll
     for (int w = 0; w < 4; w++)
         lds_ld32x2_masked(m[w] | m[w + 1], tab_addr16x4<0>(ko[w], L.tab_lds),
@@ -2513,4 +2516,37 @@ __global__ void __launch_bounds__(1024) vsa_class_scan_lut(VsaClassParams P, u64
         if (last) atomicMax(P.last + sl, last);
         if (cnt) atomicAdd(P.count + sl, cnt);
     }
+}
+
+/* Read-ceiling probe (bench.py's roofline.peak_measured; not a scan): every
+ * byte of [A, A + n) read once with 16-byte non-temporal loads, one 1024-
+ * thread workgroup per CU, wave w reading static 64 KiB segments w, w + W, ..
+ * through a 4-deep 1 KiB ring -- the fastest of the schedules
+ * tools/probe_stream.hip measured (6.6 TB/s).  n is a multiple of 64 KiB
+ * (the caller rounds down).  The sink store is data-dependent so the loads
+ * are kept; it lands in a scratch word, never in scan state. */
+__global__ void __launch_bounds__(1024) vsa_read_probe(const uint8_t *A, u64 n, u32 *sink) {
+    typedef u32 v4u __attribute__((ext_vector_type(4)));
+    const u32 lane = threadIdx.x & 63;
+    const u64 W = (u64)gridDim.x * 16;
+    const u64 w = (u64)blockIdx.x * 16 + (threadIdx.x >> 6);
+    constexpr u64 SEG = 64 << 10;
+    constexpr u32 ITERS = SEG >> 10, DEPTH = 4;
+    u32 acc = 0;
+    for (u64 sg = w; sg * SEG < n; sg += W) {
+        const uint8_t *base = A + sg * SEG + 16 * lane;
+        v4u ring[DEPTH];
+#pragma unroll
+        for (u32 k = 0; k < DEPTH; k++) ring[k] = __builtin_nontemporal_load((const v4u *)(base + 1024 * k));
+        for (u32 g = 0; g < ITERS / DEPTH; g++) {
+#pragma unroll
+            for (u32 k = 0; k < DEPTH; k++) {
+                const v4u v = ring[k];
+                acc ^= v.x + v.y * 3 + v.z * 5 + v.w * 7;
+                const u32 it = g * DEPTH + k + DEPTH;
+                ring[k] = __builtin_nontemporal_load((const v4u *)(base + 1024 * (it < ITERS ? it : 0)));
+            }
+        }
+    }
+    if (acc == 0x9e3779b9u) sink[threadIdx.x & 15] = acc;
 }

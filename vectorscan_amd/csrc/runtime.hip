@@ -58,6 +58,7 @@ __global__ void vsa_publish(unsigned long long *ctr, unsigned long long *h, unsi
 __global__ void vsa_pack(const unsigned long long *saved, uint64_t out_cap, const uint64_t *keys,
                          const uint32_t *ids, uint64_t cap, uint64_t *dst);
 __global__ void vsa_pair_scan(VsaPairParams P);
+__global__ void vsa_read_probe(const uint8_t *A, uint64_t n, uint32_t *sink);
 
 #define VSA_CHECK(x)                                                          \
     do {                                                                      \
@@ -2313,6 +2314,46 @@ int vsa_scan_debug_counters(vsa_ctx_t *c, uint64_t out[16]) {
 }
 
 double vsa_scan_kernel_ms(vsa_ctx_t *c) { return c ? c->last_kernel_ms : 0.0; }
+
+/* The box's streaming-read ceiling over a device buffer (bench.py's
+ * roofline.peak_measured): vsa_read_probe reads the first len & ~64 KiB
+ * bytes once per run on the ctx stream; best of `runs` (hipEvents) after
+ * one untimed run.  Synchronous; not a scan, touches no scan state. */
+int vsa_read_ceiling(vsa_ctx_t *c, const uint8_t *d_data, uint64_t len, uint32_t runs,
+                     double *best_ms, uint64_t *bytes) {
+    if (!c || !d_data || !best_ms || !runs) return VSA_E_INVALID;
+    const uint64_t n = len & ~((uint64_t)(64 << 10) - 1);
+    if (!n) return VSA_E_INVALID;
+    uint32_t *sink = nullptr;
+    VSA_CHECK(hipMalloc(&sink, 64));
+    hipEvent_t e0, e1;
+    hipError_t e = hipEventCreate(&e0);
+    if (e == hipSuccess && (e = hipEventCreate(&e1)) != hipSuccess) (void)hipEventDestroy(e0);
+    if (e != hipSuccess) {
+        (void)hipFree(sink);
+        VSA_CHECK(e);
+    }
+    float best = 1e30f;
+    for (uint32_t r = 0; r <= runs && e == hipSuccess; r++) {
+        e = hipEventRecord(e0, c->stream);
+        if (e != hipSuccess) break;
+        hipLaunchKernelGGL(vsa_read_probe, dim3(c->num_cus), dim3(1024), 0, c->stream, d_data, n,
+                           sink);
+        if ((e = hipGetLastError()) != hipSuccess) break;
+        if ((e = hipEventRecord(e1, c->stream)) != hipSuccess) break;
+        if ((e = hipEventSynchronize(e1)) != hipSuccess) break;
+        float ms = 0.f;
+        if ((e = hipEventElapsedTime(&ms, e0, e1)) != hipSuccess) break;
+        if (r > 0 && ms < best) best = ms;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(sink);
+    VSA_CHECK(e);
+    *best_ms = best;
+    if (bytes) *bytes = n;
+    return VSA_OK;
+}
 
 /* The shufti / truffle bytecode (masks, shufticompile.cpp:54 /
  * trufflecompile.cpp:60) over a device buffer: the class the masks accept,
