@@ -1125,7 +1125,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                                              const uint4 *rings, u32 lg, u32 *tails,
                                              const u32 *heads, const u32 *q_done, u32 mis,
                                              const u32 *slots, QEnt *pq, u32 cw, u32 nc,
-                                             u64 *pcl) {
+                                             u64 *pcl, u64 (&dg)[3]) {
     typedef LitTraits<MODE> T;
     constexpr int EW = XP ? 1 : T::EW; /* ring entry: chunk or QEnt (XP) */
     constexpr int CW = T::CW;
@@ -1162,7 +1162,15 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
         }
     };
     /* confirm k <= CONF_U * 64 queued candidates, CONF_U per lane */
+    /* diagnostic (dbg & 8192, wave log): when every scanning wave was first
+     * seen done, when the last batch started, batches after that */
+    const bool dlog = (P.dbg & 8192) != 0;
+    bool seen_done = false;
     auto confirm_batch = [&](u32 k) {
+        if (dlog) {
+            dg[1] = __builtin_amdgcn_s_memrealtime();
+            if (seen_done) dg[2]++;
+        }
         phase(1);
         asm volatile("" ::: "memory");
         QEnt q[CONF_U];
@@ -1183,6 +1191,10 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
     for (;;) {
         const bool all_done = lds_ld32(q_done) == nscan;
         asm volatile("" ::: "memory");
+        if (dlog && all_done && !seen_done) {
+            seen_done = true;
+            dg[0] = __builtin_amdgcn_s_memrealtime();
+        }
         /* poll: the served rings' heads in one read */
         const u32 avail = ring_lane ? lds_ld32(&heads[rr]) - tail : 0u;
         const bool valid = rk < avail;
@@ -1427,6 +1439,9 @@ vsa_lit_scan(VsaLitParams P) {
     /* diagnostic (dbg & 8192, wave log): the kernel's entry, before staging */
     const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
 
+    const u32 mis = (u32)((uintptr_t)P.data & 15);
+    const u8 *A = P.data - mis;
+
     /* ---- stage tables into LDS ---- */
     u32 tab_bytes = 0;
     const void *tab;
@@ -1491,21 +1506,22 @@ vsa_lit_scan(VsaLitParams P) {
     if (tid < 8 * MAX_CONF_WAVES) prof_lds[tid] = 0;
     __syncthreads();
 
-    const u32 mis = (u32)((uintptr_t)P.data & 15);
     if (wave >= NS) {
         const u32 cw = wave - NS;
+        u64 dg[3] = {0, 0, 0};
         if (NC == 1)
             confirm_wave<MODE, 4, XP>(P, cl, rings, 31 - __clz(P.qcap), q_tails, q_heads, &q_done,
-                                  mis, slots, pqx, 0, 1, prof_lds);
+                                  mis, slots, pqx, 0, 1, prof_lds, dg);
         else
             confirm_wave<MODE, 2, XP>(P, cl, rings, 31 - __clz(P.qcap), q_tails, q_heads, &q_done,
                                   mis, slots, pqx + (size_t)cw * PQ_ENTRIES(2), cw, NC,
-                                  prof_lds + 8 * cw);
+                                  prof_lds + 8 * cw, dg);
         if ((P.dbg & 8192) && P.wave_log && lane < 8) {
             /* diagnostic: a confirm wave's entry and end */
             const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
             P.wave_log[((size_t)blockIdx.x * LIT_WAVES + wave) * 8 + lane] =
-                lane == 0 ? t_entry : lane == 1 ? t_end : lane == 2 ? 1ull : 0ull;
+                lane == 0 ? t_entry : lane == 1 ? t_end : lane == 2 ? 1ull
+                : lane == 3 ? dg[0] : lane == 4 ? dg[1] : lane == 5 ? dg[2] : 0ull;
         }
         return;
     }
@@ -1538,7 +1554,6 @@ vsa_lit_scan(VsaLitParams P) {
     u32 n_seg = 0, n_iter = 0; /* diagnostic (wave_log) */
     if ((P.dbg & 2048) && lane == 0) /* diagnostic: first scanning-wave start */
         atomicMax(&P.counters[8], ~t_start);
-    const u8 *A = P.data - mis;
     u32 ncand_total = 0;
     u32 ring_tail_cache = 0, ring_head = 0;
     /* scanner expansion's batch (IterState xs / xn), carried across blocks
