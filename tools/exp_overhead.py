@@ -3,13 +3,16 @@
 the hipEvent kernel time against the waves' own timeline -- entry ->
 first scanning-wave start (table staging), start -> median / last wave end
 (the tail), and the streaming-read ceiling of the same bytes.  One JSON line
-per (workload, size).  Usage: python tools/exp_overhead.py [out.jsonl]"""
+per (workload, size).  Usage: python tools/exp_overhead.py [out.jsonl]
+Needs the diagnostic build: tools/build_variant.sh diag -DVSA_DIAG, then
+VSA_LIB_VARIANT=libvsa_diag.so (the product build compiles these counters
+out)."""
 import ctypes
 import json
 import os
 import sys
 
-os.environ["VSA_DEBUG_FLAGS"] = str(4096 | 8192)
+os.environ["VSA_DEBUG_FLAGS"] = str(4096 | 8192 | int(os.environ.get("EXTRA_DBG", "0")))
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -25,12 +28,26 @@ vsa.lib.vsa_set_wave_log(log.data_ptr())
 total = 4 << 30
 fdr_lits = bench.make_literals(5000, seed=12)
 data = bench.make_corpus_device(torch, 0, total, total, fdr_lits, 5, 64 << 10, dev)
-dbs = {"fdr5k": vsa.Database(ctx, vsa.hwlm_build(fdr_lits)),
-       "noodle": vsa.Database(ctx, vsa.hwlm_build([vsa.HwlmLiteral(b"abcde", False, 1)]))}
+# WL: which workloads (comma list); the *_p4k ones scan their own 1 GiB
+# corpus with a literal planted every 4 KiB (tools/bench_configs.py cfg 1 / 3)
+WL = os.environ.get("WL", "fdr5k,noodle").split(",")
+import tools.bench_configs as bc  # noqa: E402
+sets = {"fdr5k": (fdr_lits, -1, None), "noodle": ([vsa.HwlmLiteral(b"abcde", False, 1)], -1, None),
+        "noodle_p4k": ([vsa.HwlmLiteral(b"abcde", False, 1)], -1, 3),
+        "teddy48_p4k": (bc.lits_printable(48, 55), -1, 3),
+        "teddy48": (bc.lits_printable(48, 55), -1, None),
+        "teddy48e18_p4k": (bc.lits_printable(48, 55), 18, 3),
+        "teddy48e18": (bc.lits_printable(48, 55), 18, None)}
+dbs = {}
+for w in WL:
+    ls, hint, seed = sets[w]
+    dbs[w] = (vsa.Database(ctx, vsa.hwlm_build(ls, engine_hint=hint)),
+              None if seed is None else
+              bench.make_corpus_device(torch, 0, 1 << 30, 1 << 30, ls, seed, 4 << 10, dev))
 torch.cuda.synchronize()
-base = data.data_ptr()
-for name, db in dbs.items():
-    for mib, nb in ((512, 1), (1024, 1), (4096, 4)):
+for name, (db, own) in dbs.items():
+    base = data.data_ptr() if own is None else own.data_ptr()
+    for mib, nb in (((512, 1), (1024, 1), (4096, 4)) if own is None else ((1024, 1),)):
         n = mib << 20
         bl = n // nb
         offs = [i * bl for i in range(nb)]
@@ -82,7 +99,7 @@ for name, db in dbs.items():
         R = np.median(np.array(rows), axis=0)
         C = np.median(np.array(cgap), axis=0)
         _, ms, _ = ctx.read_ceiling(base, n, 5)
-        rec = {"workload": name, "mib": mib, "blocks": nb, "kernel_us": round(R[0], 1),
+        rec = {"workload": name, "engine": dbs[name][0].engine, "mib": mib, "blocks": nb, "kernel_us": round(R[0], 1),
                "start_us_p50": round(R[1], 2), "start_us_max": round(R[2], 2),
                "wave_end_us_min": round(R[3], 1), "wave_end_us_p50": round(R[4], 1),
                "wave_end_us_max": round(R[5], 1), "wg_done_us_p50": round(R[6], 1),

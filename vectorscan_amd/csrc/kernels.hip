@@ -43,6 +43,15 @@
 
 #define WAVE 64
 #define LIT_WAVES 16
+/* diagnostics that touch the hot loops (candidate-path cycles, the confirm
+ * wave's end phase) exist only in -DVSA_DIAG builds
+ * (tools/build_variant.sh diag -DVSA_DIAG): measured 1-2 % on the cfg-4
+ * scan even when off (profiles/r05/r05u_*) */
+#ifdef VSA_DIAG
+#define VSA_DIAG_ON 1
+#else
+#define VSA_DIAG_ON 0
+#endif
 #define LIT_THREADS (LIT_WAVES * WAVE)
 #define QCAP 256
 
@@ -149,10 +158,14 @@ struct LitTraits;
 template <>
 struct LitTraits<VSA_MODE_TEDDY> {
     static constexpr int LB = 8;
-    static constexpr int NL = 8;
+    /* 4 of the table's 8 positions (its low dword): a byte of each of the
+     * last 4 literal bytes, exact, passes ~48 / 95^4 of random positions at
+     * cfg 3 -- the u64 entries' other 4 fields bought no candidates worth
+     * their accumulate (39 VALU against 22 for u32 entries, fdr4_acc_*) */
+    static constexpr int NL = 4;
     static constexpr int CW = 4;
     static constexpr int EW = 3;
-    typedef u64 S_t;
+    typedef u32 S_t;
 };
 template <>
 struct LitTraits<VSA_MODE_NOOD> {
@@ -235,6 +248,7 @@ struct LitShared {
     u32 lg;          /* log2 ring entries (>= 2) */
     u32 dbg;         /* VsaLitParams.dbg */
     const u32 *slots; /* slot bitmaps (LDS; scanner expansion, XP) */
+    unsigned long long *diag; /* LDS: candidate-path cycles (dbg & 32768) */
 };
 
 __device__ __forceinline__ u32 lds_ld32(const u32 *p) {
@@ -377,6 +391,9 @@ __device__ __forceinline__ u64 lit_lookup(const void *tab, u32 key, u32 lane) {
     if constexpr (MODE == VSA_MODE_FDR4) {
         (void)lane;
         return ((const u32 *)tab)[key];
+    } else if constexpr (MODE == VSA_MODE_TEDDY) {
+        /* u32 rows of 256 B: the lane's copy at (lane & 31) * 4 */
+        return ((const u32 *)tab)[(key << 6) | (lane & 31)];
     } else {
         return ((const u64 *)tab)[(key << 5) | (lane & 31)];
     }
@@ -455,12 +472,23 @@ __device__ __forceinline__ void ring_push(const LitShared &L, ST &st, bool push,
  * group is then shifted into place once (alignbyte) — 39 VALU for FDR's 16
  * u64 entries against 64 for a per-position shift.  c = the conf fields of
  * the lane's own 16 ends, s_out = the fields spilling into ends 16.. */
+__device__ __forceinline__ void fdr4_acc_even(const u32 (&x)[16], u32 (&U)[5]);
+__device__ __forceinline__ void fdr4_acc_odd(const u32 (&x)[16], u32 (&U)[5]);
 template <int MODE>
 __device__ __forceinline__ void conf_accumulate(const typename LitTraits<MODE>::S_t (&x)[16],
                                                 u32 (&c)[LitTraits<MODE>::CW], u64 &s_out) {
     auto lo = [&](int j) { return (u32)(u64)x[j]; };
     auto hi = [&](int j) { return (u32)((u64)x[j] >> 32); };
-    if constexpr (LitTraits<MODE>::LB == 8) {
+    if constexpr (MODE == VSA_MODE_TEDDY) {
+        /* u32 entries, 4 fields: FDR4's OR-into-place (field f of x[p] onto
+         * end p + f; U[4] = ends 16..18, the next lane's 0..2) */
+        u32 U[5];
+        fdr4_acc_even(x, U);
+        fdr4_acc_odd(x, U);
+#pragma unroll
+        for (int i = 0; i < 4; i++) c[i] = U[i];
+        s_out = U[4];
+    } else if constexpr (LitTraits<MODE>::LB == 8) {
         /* A[r][w] = dword w of the group j = 4 w' + r (before its r-byte
          * shift); group 0 is folded straight into F */
         u32 A[4][5];
@@ -871,7 +899,8 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
         /* byte r of d[w] -> address byte 1, L.tsel = 0x10000 | lane slot */
         const u32 sel = 0x0c020000u | ((4u + (j & 3)) << 8);
         const u32 a = __builtin_amdgcn_perm(d[j >> 2], L.tsel, sel);
-        x[j] = lds_ld64(a);
+        if constexpr (MODE == VSA_MODE_TEDDY) x[j] = lds_ld32a(a);
+        else x[j] = lds_ld64(a);
         if (EDGE) {
             if (!((look_m >> j) & 1u)) x[j] = 0;
         }
@@ -925,6 +954,15 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
 #pragma unroll
     for (int i = 1; i < T::CW; i++) all &= c[i];
     if (!wave_any((all | ~bucket_mask) != 0xffffffffu)) return out;
+    /* diagnostic (dbg & 32768): cycles of the candidate path before the
+     * push -> counters[13], of the push (with any wait for ring room) ->
+     * [14], iterations taking it -> [15] */
+#ifdef VSA_DIAG
+    const bool tdiag = (P.dbg & 32768) != 0;
+#else
+    constexpr bool tdiag = false; /* diagnostic builds only (-DVSA_DIAG) */
+#endif
+    const u64 t_c0 = tdiag ? __builtin_amdgcn_s_memtime() : 0;
     u32 any = 0;
 #pragma unroll
     for (int i = 0; i < T::CW; i++) {
@@ -965,7 +1003,16 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
     w[3 + T::CW] = pv3;
 #pragma unroll
     for (int i = 0; i < 4; i++) w[4 + T::CW + i] = d[i];
+    const u64 t_c1 = tdiag ? __builtin_amdgcn_s_memtime() : 0;
     ring_push<T::EW>(L, out, any != 0, w);
+    if (tdiag && lane == 0) {
+        /* per workgroup in LDS (one global word per counter would
+         * serialize every wave's add chip-wide) */
+        const u64 t_c2 = __builtin_amdgcn_s_memtime();
+        atomicAdd(&L.diag[0], (unsigned long long)(t_c1 - t_c0));
+        atomicAdd(&L.diag[1], (unsigned long long)(t_c2 - t_c1));
+        atomicAdd(&L.diag[2], 1ull);
+    }
     return out;
 }
 
@@ -1115,6 +1162,9 @@ __device__ __forceinline__ uint4 load_wave_kib(const u8 *base, u32 off) {
  * pre-filter queue by their lanes, then filtered 64 at a time with every
  * lane busy -- measured slower: 10.4 vs 9.4 ms at 20k literals.) */
 #define MAX_CONF_WAVES 4
+#ifndef CONF_IDLE_SLEEP
+#define CONF_IDLE_SLEEP 8 /* s_sleep units (64 clocks) between idle polls */
+#endif
 #define EXP_U 1 /* candidate bits per lane per expansion round (2 and 4 measured
                    slower at 5k and at 20k literals) */
 /* confirm queue entries of a confirm wave confirming CU per lane per batch:
@@ -1164,7 +1214,11 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
     /* confirm k <= CONF_U * 64 queued candidates, CONF_U per lane */
     /* diagnostic (dbg & 8192, wave log): when every scanning wave was first
      * seen done, when the last batch started, batches after that */
+#ifdef VSA_DIAG
     const bool dlog = (P.dbg & 8192) != 0;
+#else
+    constexpr bool dlog = false; /* diagnostic builds only (-DVSA_DIAG) */
+#endif
     bool seen_done = false;
     auto confirm_batch = [&](u32 k) {
         if (dlog) {
@@ -1231,7 +1285,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
             if (all_done) break;
             /* idle: yield issue priority while polling */
             __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_s_sleep(8);
+            __builtin_amdgcn_s_sleep(CONF_IDLE_SLEEP);
             phase(3);
             continue;
         }
@@ -1275,8 +1329,20 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
              * wave prefix sum + one atomic per gather) */
             if (hits) {
                 const u32 n = (u32)__popc(hits);
+                /* the first hit's bin slot (staged binned sort) is reserved
+                 * before the output slots, so both returning atomics are in
+                 * flight together: one memory round trip per gather, not
+                 * two (under the scanners' streaming a round trip costs
+                 * microseconds, and this wave's rounds bound match-dense
+                 * scans: profiles/r05/r05r_*) */
+                u32 s_first = 0;
+                if (P.bin_slots)
+                    s_first = __hip_atomic_fetch_add(
+                        &P.bin_counts[(u32)((p0 + (__ffs(hits) - 1) - mis) >> P.bin_shift)], 1u,
+                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 unsigned long long slot = atomicAdd(&P.counters[0], (unsigned long long)n);
                 consumed += n;
+                bool first = true;
                 for (; hits; hits &= hits - 1, slot++) {
                     const u32 j = __ffs(hits) - 1;
                     const u64 key = (p0 + j - mis) << VSA_KEY_END_SHIFT;
@@ -1287,9 +1353,11 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                     if (P.bin_slots) {
                         /* staged binned sort (vsa_bin_finish) */
                         const u32 bin = (u32)((p0 + j - mis) >> P.bin_shift);
-                        const u32 s = __hip_atomic_fetch_add(&P.bin_counts[bin], 1u,
-                                                             __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT);
+                        const u32 s = first ? s_first
+                                            : __hip_atomic_fetch_add(&P.bin_counts[bin], 1u,
+                                                                     __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT);
+                        first = false;
                         if (s < VSA_SORT_BIN_MAX)
                             P.bin_slots[(size_t)bin * VSA_SORT_BIN_MAX + s] = (u32)slot;
                         else
@@ -1431,6 +1499,7 @@ vsa_lit_scan(VsaLitParams P) {
      * (groups of LIT_DEPTH iterations; cur = the next group to claim) */
     __shared__ unsigned long long rng[16];
     __shared__ u64 prof_lds[8 * MAX_CONF_WAVES]; /* confirm-wave profile (dbg & 64) */
+    __shared__ unsigned long long diag_lds[3];   /* candidate-path cycles (dbg & 32768) */
     const u32 tid = threadIdx.x;
     const u32 lane = lane_id();
     /* provably wave-uniform: the confirm wave's s_setprio is a scalar
@@ -1458,7 +1527,23 @@ vsa_lit_scan(VsaLitParams P) {
          * bank pairs and the address of byte c is 0x10000 | c << 8 |
          * (lane & 31) << 3: one v_perm (TEDDY_TAB_LDS) */
         u8 *tb = smem + (TEDDY_TAB_LDS - (u32)(uintptr_t)(lds_u8_t *)smem);
-        stage_lds<8>((u64 *)tb, 256 * 32, tid, [&](u32 i) { return P.table[i >> 5]; });
+        if constexpr (MODE == VSA_MODE_TEDDY) {
+            /* u32 entries (the low 4 fields), 32 copies in the first 128 B
+             * of a 256-B row per byte value: one v_perm builds the address */
+            u32 *t32 = (u32 *)tb;
+            for (u32 b0 = 0; b0 < 256 * 32; b0 += 8 * LIT_THREADS) {
+                u32 v[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) v[k] = (u32)P.table[(b0 + k * LIT_THREADS + tid) >> 5];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const u32 i = b0 + k * LIT_THREADS + tid;
+                    t32[((i >> 5) << 6) | (i & 31)] = v[k];
+                }
+            }
+        } else {
+            stage_lds<8>((u64 *)tb, 256 * 32, tid, [&](u32 i) { return P.table[i >> 5]; });
+        }
         tab = tb;
     }
     /* one ring of qcap entries per scanning wave, the slot bitmaps, then the
@@ -1504,6 +1589,7 @@ vsa_lit_scan(VsaLitParams P) {
         if (P.wg_time) P.wg_time[gridDim.x + blockIdx.x] = t_entry;
     }
     if (tid < 8 * MAX_CONF_WAVES) prof_lds[tid] = 0;
+    if (tid < 3) diag_lds[tid] = 0;
     __syncthreads();
 
     if (wave >= NS) {
@@ -1542,13 +1628,14 @@ vsa_lit_scan(VsaLitParams P) {
     LitShared L;
     L.tab = tab;
     L.tab_lds = (u32)(uintptr_t)(lds_u8_t *)smem;
-    L.tsel = TEDDY_TAB_LDS | ((lane & 31) << 3);
+    L.tsel = TEDDY_TAB_LDS | ((lane & 31) << (MODE == VSA_MODE_TEDDY ? 2 : 3));
     L.ring = rings + (size_t)wave * P.qcap * REW;
     L.slots = slots;
     L.tail = &q_tails[wave];
     L.head = &q_heads[wave];
     L.lg = 31 - __clz(P.qcap);
     L.dbg = P.dbg;
+    L.diag = diag_lds;
 
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     u32 n_seg = 0, n_iter = 0; /* diagnostic (wave_log) */
@@ -1997,6 +2084,10 @@ vsa_lit_scan(VsaLitParams P) {
     if (lane == 0) {
         const u32 prev = __hip_atomic_fetch_add(&q_done, 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (VSA_DIAG_ON && (P.dbg & 32768) && prev + 1 == NS) {
+            /* every scanning wave's adds precede its q_done add (LDS order) */
+            for (int k = 0; k < 3; k++) atomicAdd(&P.counters[13 + k], diag_lds[k]);
+        }
         if ((P.dbg & 2048) && prev + 1 == NS) /* diagnostic: earliest CU done */
             atomicMax(&P.counters[11], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
         if (P.wg_time && prev + 1 == NS) {

@@ -2308,8 +2308,11 @@ uint64_t vsa_scan_candidates(vsa_ctx_t *c) { return c ? c->last_cand : 0; }
 
 int vsa_scan_debug_counters(vsa_ctx_t *c, uint64_t out[16]) {
     if (!c || !out) return VSA_E_INVALID;
+    /* the completed scan's counters as published to the host (the device
+     * copies are zeroed for the next launch by the publish) */
+    if (int r = finish_pending(c)) return r;
     VSA_CHECK(hipStreamSynchronize(c->stream));
-    VSA_CHECK(hipMemcpy(out, c->ws.d_counters, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    memcpy(out, c->ws.h_counters, 16 * sizeof(uint64_t));
     return VSA_OK;
 }
 
