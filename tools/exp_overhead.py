@@ -31,6 +31,8 @@ data = bench.make_corpus_device(torch, 0, total, total, fdr_lits, 5, 64 << 10, d
 # WL: which workloads (comma list); the *_p4k ones scan their own 1 GiB
 # corpus with a literal planted every 4 KiB (tools/bench_configs.py cfg 1 / 3)
 WL = os.environ.get("WL", "fdr5k,noodle").split(",")
+# SORT=0: unsorted output (no binned-sort staging in the scan)
+SORT = os.environ.get("SORT", "1") != "0"
 import tools.bench_configs as bc  # noqa: E402
 sets = {"fdr5k": (fdr_lits, -1, None), "noodle": ([vsa.HwlmLiteral(b"abcde", False, 1)], -1, None),
         "noodle_p4k": ([vsa.HwlmLiteral(b"abcde", False, 1)], -1, 3),
@@ -52,12 +54,12 @@ for name, (db, own) in dbs.items():
         bl = n // nb
         offs = [i * bl for i in range(nb)]
         for _ in range(40):  # clock ramp
-            ctx.scan_blocks(db, base, offs, [bl] * nb)
+            ctx.scan_blocks(db, base, offs, [bl] * nb, sort=SORT)
         rows = []
         cgap = []
         for _ in range(8):
             log.zero_()
-            ctx.scan_blocks(db, base, offs, [bl] * nb)
+            ctx.scan_blocks(db, base, offs, [bl] * nb, sort=SORT)
             k = ctx.kernel_ms()
             L = log[:65536].view(-1, 8).cpu().numpy().astype(np.int64)
             # scanning waves log their entry in field 7; confirm waves log

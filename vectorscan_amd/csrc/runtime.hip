@@ -18,6 +18,7 @@
  *    end (program_runtime.c:2985-2997).
  */
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -173,6 +174,10 @@ struct vsa_ctx {
         uint64_t bytes = 0; /* scanned bytes (len - start summed) */
         const VsaBlock *d_blocks = nullptr;
         const uint32_t *d_segblk = nullptr;
+        /* the kernel-timing events the next literal-scan dispatch carries
+         * itself (launch_lit: start on the first kernel, stop on the last
+         * of split passes); null = untimed */
+        hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     } launch;
     /* kernel-only timing of the last scan (hipEvents on the scan stream) */
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -463,7 +468,15 @@ int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds) {
                 MODE, (int)XP, grid, (unsigned long long)P.nsegs, P.nblocks, lds, P.qcap, P.nconf,
                 P.end_par, (const void *)P.data, (const void *)P.blocks,
                 (const void *)P.seg_desc, (unsigned long long)P.out_cap, (void *)P.bin_counts);
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(LIT_THREADS), lds, c->stream, P);
+    /* the timing events ride on the dispatch packet itself
+     * (hipExtLaunchKernel): separate hipEventRecord markers before and after
+     * put two more packets between the scan and its sort on the stream */
+    hipEvent_t e0 = c->launch.ev_start;
+    hipEvent_t e1 = P.end_par == 1 ? nullptr : c->launch.ev_stop; /* split: the 2nd pass */
+    c->launch.ev_start = nullptr;
+    if (e1) c->launch.ev_stop = nullptr;
+    hipExtLaunchKernelGGL(fn, dim3(grid), dim3(LIT_THREADS), (uint32_t)lds, c->stream, e0, e1, 0u,
+                          P);
     VSA_CHECK(hipGetLastError());
     return VSA_OK;
 }
@@ -685,9 +698,11 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
     /* drop-in calls (a few records, sorted by the host) skip the kernel
      * timing and get their counters and records published (no copies) */
     const bool small = (c->launch.flags & SCAN_HOST_SORT_SMALL) != 0;
-    if (!small) VSA_CHECK(hipEventRecord(c->ev0, c->stream));
+    c->launch.ev_start = small ? nullptr : c->ev0;
+    c->launch.ev_stop = small ? nullptr : c->ev1;
     arm_feedback(c, fb_set_of(db), c->launch.grid, c->launch.bytes, small);
     int r = launch_scan_kernel(c, db, d_data, nb, nsegs);
+    c->launch.ev_start = c->launch.ev_stop = nullptr;
     if (r != VSA_OK) return r;
     if (small) {
         hipLaunchKernelGGL(vsa_publish, dim3(1), dim3(256), 0, c->stream, c->ws.d_counters,
@@ -700,7 +715,6 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
         c->ctr_clean = true;
         return VSA_OK;
     }
-    VSA_CHECK(hipEventRecord(c->ev1, c->stream));
     /* the binned sort queues behind the scan with no host round trip: its
      * kernels read the record count and the overflow flag on the device
      * (finish_scan falls back to the library sort if a bin overflowed) */
@@ -2416,21 +2430,23 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
      * no gain at 256 MiB (0.0592 / 0.0597 / 0.0566 ms against 0.0593 /
      * 0.0587 / 0.0580, profiles/r04p_configs.jsonl, r04p_cfg2_nofb.jsonl)
      * and was removed in round 5: equal spans. */
-    VSA_CHECK(hipEventRecord(c->ev0, c->stream));
+    /* timing events on the dispatch packet (hipExtLaunchKernel), as the
+     * literal scan's */
     if (lut) {
         /* large buffers: pair-LUT kernel, one 1024-thread workgroup per CU,
          * an equal 4 KiB-aligned share per workgroup, taken by its waves in
          * 4 KiB groups (kernels.hip vsa_class_scan_lut) */
-        hipLaunchKernelGGL(vsa_class_scan_lut, dim3(lgrid), dim3(1024), 0, c->stream, P, wspan);
+        hipExtLaunchKernelGGL(vsa_class_scan_lut, dim3(lgrid), dim3(1024), 0u, c->stream, c->ev0,
+                              c->ev1, 0u, P, wspan);
     } else {
         uint64_t chunks = (len + 15) / 16;
         uint64_t want = (chunks + 255) / 256;
         uint64_t cap = (uint64_t)c->num_cus * 8;
         uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
-        hipLaunchKernelGGL(vsa_class_scan, dim3(grid), dim3(256), 0, c->stream, P);
+        hipExtLaunchKernelGGL(vsa_class_scan, dim3(grid), dim3(256), 0u, c->stream, c->ev0, c->ev1,
+                              0u, P);
     }
     VSA_CHECK(hipGetLastError());
-    VSA_CHECK(hipEventRecord(c->ev1, c->stream));
     VSA_CHECK(hipMemcpyAsync(w.h_counters + CLASS_BASE, part, 16 * CLASS_SLOTS * 8,
                              hipMemcpyDeviceToHost, c->stream));
     VSA_CHECK(hipStreamSynchronize(c->stream));
