@@ -38,8 +38,31 @@ def describe(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000, weights=
                           ns, words.ctypes.data, w, ctypes.byref(n), ctypes.byref(g), wp)
     nseg, grid = n.value, g.value
     desc = words[:4 * nseg].reshape(-1, 4)
-    bounds = words[4 * nseg:] if grid else None
+    bounds = words[4 * nseg:4 * nseg + grid + 1] if grid else None
     return desc, bounds, grid
+
+
+def describe_bins(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000):
+    """(desc, bounds, grid, wg_bins): wg_bins[b] = the sort bins [lo, hi)
+    workgroup b counts alone (runtime.hip plan_wg_bins)"""
+    o = np.ascontiguousarray(offs, np.uint64)
+    ln = np.ascontiguousarray(lens, np.uint64)
+    st = None if starts is None else np.ascontiguousarray(starts, np.uint64)
+    n = ctypes.c_uint64()
+    g = ctypes.c_uint32()
+    w = lib.vsa_plan_describe(base, o.ctypes.data, ln.ctypes.data,
+                              None if st is None else st.ctypes.data, None, None, len(o),
+                              num_cus, ns, None, 0, ctypes.byref(n), ctypes.byref(g), None)
+    words = np.zeros(w, np.uint32)
+    lib.vsa_plan_describe(base, o.ctypes.data, ln.ctypes.data,
+                          None if st is None else st.ctypes.data, None, None, len(o), num_cus,
+                          ns, words.ctypes.data, w, ctypes.byref(n), ctypes.byref(g), None)
+    nseg, grid = n.value, g.value
+    desc = words[:4 * nseg].reshape(-1, 4)
+    bounds = words[4 * nseg:4 * nseg + grid + 1]
+    wg_bins = words[4 * nseg + grid + 1:4 * nseg + 3 * grid + 1].reshape(-1, 2)
+    assert len(words) == 4 * nseg + 3 * grid + 1
+    return desc, bounds, grid, wg_bins
 
 
 def spans(offs, lens, starts, base):
@@ -286,3 +309,55 @@ def test_plan_blocks_read_only_inside_the_buffer(seed):
             org = int(b["org"])
             assert org >= 0 and org % 1024 == 0, (i, org)  # chunk loads
             assert org <= blo + max(0, starts[i] - 16), (i, org, blo)
+
+
+def _bits_for(v):
+    """runtime.hip bits_for: the bit length of v"""
+    return int(v).bit_length()
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_plan_owned_bins_are_exclusive(seed):
+    """Sort bins a workgroup counts in LDS (plan_wg_bins, kernels.hip
+    bin_slot_take) hold only that workgroup's ends: every end a segment can
+    report lies in its block (a part: its KiB range of it), so every owned
+    bin must lie inside the owner's segments' hull and outside every other
+    workgroup's segments; overlapping blocks own none."""
+    rng = random.Random(9100 + seed)
+    base = 0x100000 + rng.choice([0, 1, 7, 15])
+    mis = base & 15
+    n = rng.choice([1, 4, 40, 700])
+    offs, lens, pos = [], [], 0
+    for _ in range(n):
+        ln = rng.choice([1, 100, 4096, 70000, 1 << 20, 64 << 20])
+        offs.append(pos)
+        lens.append(ln)
+        pos += ln + rng.choice([0, 0, 64, rng.randint(1, 5000)])
+    desc, bounds, grid, wb = describe_bins(offs, lens, base=base)
+    span = max(o + l for o, l in zip(offs, lens))
+    shift = max(0, _bits_for(span) - 14)
+    owner = {}
+    for b in range(grid):
+        for s in range(bounds[b], bounds[b + 1]):
+            first, cnt = int(desc[s][0]) & 0xffffff, int(desc[s][0]) >> 24
+            if cnt == 0:
+                blo = offs[first]
+                org = (blo + mis) & ~1023  # start 0: the block's origin
+                s0 = org - mis + (int(desc[s][1]) << 10)
+                lo, hi = max(blo, s0), min(blo + lens[first], s0 + (int(desc[s][2]) << 10))
+            else:
+                lo, hi = offs[first], offs[first + cnt - 1] + lens[first + cnt - 1]
+            for k in range(lo >> shift, ((hi - 1) >> shift) + 1 if hi > lo else lo >> shift):
+                owner.setdefault(k, set()).add(b)
+    owned = 0
+    for b in range(grid):
+        lo, hi = int(wb[b][0]), int(wb[b][1])
+        assert hi - lo <= 256
+        for k in range(lo, hi):
+            assert owner.get(k, {b}) == {b}, (b, k, owner.get(k))
+        owned += hi - lo
+    if n >= 4 and max(lens) >= (1 << 20):
+        assert owned > 0
+    # overlapping blocks (the same bytes scanned twice): nothing owned
+    desc, bounds, grid, wb = describe_bins([0, 0], [64 << 20, 64 << 20], base=base)
+    assert not wb.any()

@@ -81,6 +81,7 @@ enum VsaLitMode {
  * sorted by one wave when no bin holds more than VSA_SORT_BIN_MAX */
 #define VSA_SORT_BIN_BITS 14
 #define VSA_SORT_BINS (1u << VSA_SORT_BIN_BITS)
+#define VSA_LBINS 256u /* sort bins a workgroup may count in LDS */
 #define VSA_SORT_BIN_MAX 64
 #define VSA_CTR_BIN_OVERFLOW 12 /* counters[12]: some bin passed VSA_SORT_BIN_MAX */
 
@@ -94,6 +95,9 @@ struct VsaLitParams {
                                  origin (a part of one block), 0 */
     const uint32_t *wg_seg;   /* workgroup b's segments are [wg_seg[b],
                                  wg_seg[b + 1]), handed out in LDS */
+    const uint32_t *wg_bins;  /* [2b, 2b + 1]: the sort bins workgroup b owns
+                                 alone (runtime.hip plan_wg_bins), counted in
+                                 LDS; others with global atomics */
     uint32_t steal;           /* a wave out of segments steals sweep groups
                                  inside its workgroup when some wave has at
                                  least `steal` unclaimed (0: off) */

@@ -208,7 +208,23 @@ struct ConfLds {
     u32 nbits[16];
     u32 off[16];
     PfRec pf[16]; /* one 32-B record per bucket for the scanners' prefilter */
+    /* the sort bins this workgroup owns alone, [lb_lo, lb_lo + lb_n)
+     * (runtime.hip plan_wg_bins): their record counts, kept here and
+     * stored to bin_counts when the confirm waves are done */
+    u32 lb_lo, lb_n;
+    u32 lbins[VSA_LBINS];
 };
+
+/* a record's slot in its sort bin: an owned bin's from the workgroup's LDS
+ * count (no global round trip), any other bin's from the global one */
+__device__ __forceinline__ u32 bin_slot_take(const VsaLitParams &P, const ConfLds &cl, u32 bin) {
+    const u32 k = bin - cl.lb_lo;
+    if (k < cl.lb_n)
+        return __hip_atomic_fetch_add(const_cast<u32 *>(&cl.lbins[k]), 1u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __hip_atomic_fetch_add(&P.bin_counts[bin], 1u, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+}
 
 /* confirm-queue entry (the confirm wave's private queue): meta = aoff << 24 |
  * blk << 4 | bucket; key = 8 bytes ending at the candidate end (bytes
@@ -349,10 +365,7 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
 #pragma unroll
                 for (int i = 0; i < CONF_U; i++) {
                     bix[i] = (u32)((base[i] + (u64)e[i]) >> P.bin_shift);
-                    if (mt[i])
-                        bslot[i] = __hip_atomic_fetch_add(&P.bin_counts[bix[i]], 1u,
-                                                          __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
+                    if (mt[i]) bslot[i] = bin_slot_take(P, cl, bix[i]);
                 }
             }
             unsigned long long s0 = 0;
@@ -1337,9 +1350,8 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                  * scans: profiles/r05/r05r_*) */
                 u32 s_first = 0;
                 if (P.bin_slots)
-                    s_first = __hip_atomic_fetch_add(
-                        &P.bin_counts[(u32)((p0 + (__ffs(hits) - 1) - mis) >> P.bin_shift)], 1u,
-                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    s_first = bin_slot_take(P, cl,
+                                            (u32)((p0 + (__ffs(hits) - 1) - mis) >> P.bin_shift));
                 unsigned long long slot = atomicAdd(&P.counters[0], (unsigned long long)n);
                 consumed += n;
                 bool first = true;
@@ -1353,10 +1365,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                     if (P.bin_slots) {
                         /* staged binned sort (vsa_bin_finish) */
                         const u32 bin = (u32)((p0 + j - mis) >> P.bin_shift);
-                        const u32 s = first ? s_first
-                                            : __hip_atomic_fetch_add(&P.bin_counts[bin], 1u,
-                                                                     __ATOMIC_RELAXED,
-                                                                     __HIP_MEMORY_SCOPE_AGENT);
+                        const u32 s = first ? s_first : bin_slot_take(P, cl, bin);
                         first = false;
                         if (s < VSA_SORT_BIN_MAX)
                             P.bin_slots[(size_t)bin * VSA_SORT_BIN_MAX + s] = (u32)slot;
@@ -1493,7 +1502,7 @@ vsa_lit_scan(VsaLitParams P) {
     typedef typename T::S_t S_t;
     extern __shared__ __align__(16) u8 smem[];
     __shared__ ConfLds cl;
-    __shared__ u32 q_tails[16], q_heads[16], q_done, wg_ctr;
+    __shared__ u32 q_tails[16], q_heads[16], q_done, wg_ctr, conf_fin;
     /* work stealing (dynamic 2): per scanning wave, the sweep groups of its
      * current segment it has not claimed yet: seg << 40 | end << 20 | cur
      * (groups of LIT_DEPTH iterations; cur = the next group to claim) */
@@ -1576,6 +1585,21 @@ vsa_lit_scan(VsaLitParams P) {
         }
         cl.pf[tid] = pf;
     }
+    {
+        /* owned sort bins: their counts so far (0, or the first split
+         * pass's) into LDS */
+        u32 lo = 0, n = 0;
+        if (P.bin_slots && P.wg_bins) {
+            lo = P.wg_bins[2 * blockIdx.x];
+            n = P.wg_bins[2 * blockIdx.x + 1] - lo;
+        }
+        if (tid == 0) {
+            cl.lb_lo = lo;
+            cl.lb_n = n;
+            conf_fin = 0;
+        }
+        for (u32 i = tid; i < n; i += LIT_THREADS) cl.lbins[i] = P.bin_counts[lo + i];
+    }
     if (tid < 16) {
         q_tails[tid] = 0;
         q_heads[tid] = 0;
@@ -1602,6 +1626,18 @@ vsa_lit_scan(VsaLitParams P) {
             confirm_wave<MODE, 2, XP>(P, cl, rings, 31 - __clz(P.qcap), q_tails, q_heads, &q_done,
                                   mis, slots, pqx + (size_t)cw * PQ_ENTRIES(2), cw, NC,
                                   prof_lds + 8 * cw, dg);
+        {
+            /* the last confirm wave out stores the owned bins' counts (every
+             * confirm wave's LDS adds precede its own add here) */
+            u32 prev = 0;
+            if (lane == 0)
+                prev = __hip_atomic_fetch_add(&conf_fin, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (readfirstlane_u32(prev) + 1 == NC) {
+                const u32 lo = cl.lb_lo, n = cl.lb_n;
+                for (u32 i = lane; i < n; i += WAVE) P.bin_counts[lo + i] = cl.lbins[i];
+            }
+        }
         if ((P.dbg & 8192) && P.wave_log && lane < 8) {
             /* diagnostic: a confirm wave's entry and end */
             const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();

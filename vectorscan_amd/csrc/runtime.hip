@@ -738,6 +738,7 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.blocks = c->launch.d_blocks;
     P.seg_desc = c->launch.d_segblk;
     P.wg_seg = c->launch.d_segblk + 4 * nsegs;
+    P.wg_bins = c->launch.d_segblk + 4 * nsegs + c->launch.grid + 1; /* plan_wg_bins */
     P.nblocks = nb;
     P.steal = steal_min();
     P.nsegs = nsegs;
@@ -943,6 +944,68 @@ constexpr uint32_t SEG_GROUP_SHIFT = 24;
 constexpr uint32_t SEG_GROUP_MAX = 255;
 constexpr uint32_t PLAN_MAX_BLOCKS = VSA_MAX_BLOCKS; /* 20-bit block field of the keys */
 
+/* Sort bins a workgroup owns alone (kernels.hip counts their records in
+ * LDS: no global returning atomic per record).  Workgroup b may report ends
+ * only inside its segments; their hull [lo_b, hi_b) (data-relative, the
+ * coordinates the bins are cut in) is taken over its segments' end ranges
+ * (a part of a block: its KiB range cut to the block; a group: its blocks).
+ * When the hulls of different workgroups do not overlap -- shares are cut
+ * in block order, so they do not unless blocks overlap or come out of
+ * order -- every bin lying wholly inside hull b holds only workgroup b's
+ * records.  Appended to segblk after the list bounds: 2 words per
+ * workgroup, the bins [lo, hi) (hi - lo <= VSA_LBINS; 0, 0 = none). */
+void plan_wg_bins(BatchPlan &pl, const VsaBlock *blocks, int64_t mis) {
+    const uint32_t G = pl.grid;
+    const uint64_t base = 4 * pl.nsegs;
+    std::vector<int64_t> hlo(G, INT64_MAX), hhi(G, INT64_MIN);
+    for (uint32_t b = 0; b < G; b++) {
+        for (uint32_t sg = pl.segblk[base + b]; sg < pl.segblk[base + b + 1]; sg++) {
+            const uint32_t *d = &pl.segblk[4 * (uint64_t)sg];
+            const uint32_t first = d[0] & 0xffffffu, cnt = d[0] >> 24;
+            int64_t lo, hi;
+            if (cnt == 0) {
+                const VsaBlock &B = blocks[first];
+                const int64_t s0 = B.org - mis + ((int64_t)d[1] << 10);
+                lo = std::max<int64_t>((int64_t)B.base, s0);
+                hi = std::min<int64_t>((int64_t)(B.base + B.len), s0 + ((int64_t)d[2] << 10));
+            } else {
+                lo = INT64_MAX;
+                hi = INT64_MIN;
+                for (uint32_t k = 0; k < cnt; k++) {
+                    const VsaBlock &B = blocks[first + k];
+                    if (!B.len) continue;
+                    lo = std::min<int64_t>(lo, (int64_t)B.base);
+                    hi = std::max<int64_t>(hi, (int64_t)(B.base + B.len));
+                }
+            }
+            if (hi > lo) {
+                hlo[b] = std::min(hlo[b], lo);
+                hhi[b] = std::max(hhi[b], hi);
+            }
+        }
+    }
+    std::vector<uint32_t> order;
+    for (uint32_t b = 0; b < G; b++)
+        if (hhi[b] > hlo[b]) order.push_back(b);
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hlo[a] < hlo[b]; });
+    bool ok = true;
+    for (size_t i = 1; i < order.size() && ok; i++) ok = hhi[order[i - 1]] <= hlo[order[i]];
+    const uint32_t shift = bin_shift_for(pl.end_bits);
+    const int64_t bs = (int64_t)1 << shift;
+    for (uint32_t b = 0; b < G; b++) {
+        uint32_t lo = 0, hi = 0;
+        if (ok && hhi[b] > hlo[b]) {
+            const int64_t l = (hlo[b] + bs - 1) >> shift, h = hhi[b] >> shift;
+            if (h > l) {
+                lo = (uint32_t)l;
+                hi = (uint32_t)std::min<int64_t>(h, l + VSA_LBINS);
+            }
+        }
+        pl.segblk.push_back(lo);
+        pl.segblk.push_back(hi);
+    }
+}
+
 int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens,
                const uint64_t *starts, const uint64_t *hlens, const uint64_t *rlos,
                uint32_t nb, uint64_t waves, BatchPlan &pl, VsaBlock *out = nullptr,
@@ -1136,6 +1199,7 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
     pl.grid = (uint32_t)G;
     pl.segblk.insert(pl.segblk.end(), wg_first.begin(), wg_first.end());
     pl.end_bits = bits_for(span);
+    plan_wg_bins(pl, out, (int64_t)((uintptr_t)d_data & 15));
     return VSA_OK;
 }
 
