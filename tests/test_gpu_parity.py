@@ -543,6 +543,40 @@ def test_gpu_binned_sort(ctx):
         ctx.free(d)
 
 
+def test_gpu_overlapping_blocks_dense(ctx):
+    """Blocks that overlap each other (the runtime then owns no sort bin in
+    any workgroup, plan_wg_bins) and blocks that do not (bins counted in LDS),
+    with a match every few bytes: every block's records == the oracle's for
+    that block, and the sorted output is in key order."""
+    rng = random.Random(29)
+    lits = rand_lits(rng, 200, minlen=3, maxlen=7)
+    blob = vsa.hwlm_build(lits)
+    host = np.frombuffer(b"abcdefghABCDEFGH", np.uint8)[
+        np.random.default_rng(29).integers(0, 16, 3 << 20)]
+    for p in range(0, len(host) - 16, 97):
+        w = lits[rng.randrange(len(lits))].s
+        host[p:p + len(w)] = np.frombuffer(w, np.uint8)
+    d = ctx.malloc(len(host))
+    try:
+        ctx.h2d(d, host)
+        db = vsa.Database(ctx, blob)
+        for offs, lens in (([0, 1 << 20, (5 << 19) + 3], [2 << 20, 2 << 20, (1 << 19) - 9]),
+                           ([0, (1 << 20) + 5, 2 << 20], [(1 << 20) + 5, (1 << 20) - 5, 1 << 20])):
+            want = []
+            for o, ln in zip(offs, lens):
+                _, m = oracle.hwlm_exec(blob.ptr, host[o:o + ln].tobytes(), cap=1 << 21)
+                want += [(o + e, i) for e, i in m]
+            n = ctx.scan_blocks(db, d, offs, lens)
+            got = ctx.results(n)
+            assert n == len(want) and n > 20000
+            assert np.all(np.diff(got["key"].astype(np.int64)) >= 0)
+            ends = (got["key"] >> np.uint64(24)).tolist()
+            assert sorted(zip(ends, got["id"].tolist())) == sorted(want)
+        db.close()
+    finally:
+        ctx.free(d)
+
+
 def test_gpu_plan_memo(ctx):
     """A repeated block list reuses the device tables of the previous call;
     any change (an offset, a length, a start, the buffer) rebuilds them."""
