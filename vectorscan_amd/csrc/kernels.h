@@ -137,12 +137,16 @@ struct VsaLitParams {
                                     bin_shift, counted as they are emitted
                                     (nullptr: no binned sort) */
     uint32_t bin_shift;
-    uint32_t *bin_slots;         /* staged binned sort (vsa_bin_finish): the
-                                    output slot of record s of bin b goes to
-                                    [b * VSA_SORT_BIN_MAX + s] (s from the
-                                    returning count atomic; a bin past
+    uint64_t *bin_keys;          /* staged binned sort (vsa_bin_finish):
+                                    record s of bin b (its key here, its id
+                                    in bin_ids) goes to [b * VSA_SORT_BIN_MAX
+                                    + s] (s from the bin's count; a bin past
                                     VSA_SORT_BIN_MAX sets
-                                    counters[VSA_CTR_BIN_OVERFLOW]) */
+                                    counters[VSA_CTR_BIN_OVERFLOW]).  The
+                                    records then live only there: out_keys /
+                                    out_ids are not written and counters[0]
+                                    is only counted (no output slot) */
+    uint32_t *bin_ids;
     unsigned long long *wg_time;  /* schedule feedback (or null): [b] = xcc <<
                                      60 | end of workgroup b's scanning
                                      waves, [grid + b] = its entry (100 MHz) */

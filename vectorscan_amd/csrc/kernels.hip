@@ -213,6 +213,7 @@ struct ConfLds {
      * stored to bin_counts when the confirm waves are done */
     u32 lb_lo, lb_n;
     u32 lbins[VSA_LBINS];
+    u32 nrec; /* binned sort: records confirmed here (one global add at the end) */
 };
 
 /* a record's slot in its sort bin: an owned bin's from the workgroup's LDS
@@ -342,7 +343,8 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
             }
         }
         bool mt[CONF_U];
-        u32 rank[CONF_U], tot = 0;
+        u64 pm[CONF_U]; /* wave-uniform */
+        u32 tot = 0;
 #pragma unroll
         for (int i = 0; i < CONF_U; i++) {
             mt[i] = false;
@@ -352,41 +354,49 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
                 const u32 size = w1[i].w & 0xff;
                 mt[i] = (q[i].key & msk) == v && e[i] + 1 + hlen[i] >= (int64_t)size;
             }
-            const u64 pm = __ballot(mt[i]);
-            rank[i] = tot + __builtin_amdgcn_mbcnt_hi((u32)(pm >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((u32)pm, 0));
-            tot += (u32)__popcll(pm);
+            pm[i] = __ballot(mt[i]);
+            tot += (u32)__popcll(pm[i]);
         }
         if (tot) {
-            /* staged binned sort: every match's bin slot (returning atomics,
-             * issued with the output reservation: one round trip for both) */
-            u32 bslot[CONF_U], bix[CONF_U];
-            if (P.bin_slots) {
-#pragma unroll
-                for (int i = 0; i < CONF_U; i++) {
-                    bix[i] = (u32)((base[i] + (u64)e[i]) >> P.bin_shift);
-                    if (mt[i]) bslot[i] = bin_slot_take(P, cl, bix[i]);
-                }
-            }
+            /* binned sort on: each match goes straight into its sort bin (an
+             * owned bin's slot from LDS, others' from a returning atomic)
+             * and is counted in LDS (cl.nrec, added to counters[0] once per
+             * workgroup): a confirm step neither waits on an output
+             * reservation nor adds to the one word every workgroup shares
+             * (profiles/r05/r05zl_bin_records_ab.txt).  Off: output slots
+             * from one returning atomic per wave and step */
+            const bool bins = P.bin_keys != nullptr;
             unsigned long long s0 = 0;
-            if (lane_id() == 0) s0 = atomicAdd(&P.counters[0], (unsigned long long)tot);
+            if (lane_id() == 0) {
+                if (bins)
+                    __hip_atomic_fetch_add(const_cast<u32 *>(&cl.nrec), tot, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                else
+                    s0 = atomicAdd(&P.counters[0], (unsigned long long)tot);
+            }
             const u64 sb = ((u64)readlane_u32((u32)(s0 >> 32), 0) << 32) | readlane_u32((u32)s0, 0);
+            u32 bslot[CONF_U];
+#pragma unroll
+            for (int i = 0; i < CONF_U; i++)
+                if (bins && mt[i])
+                    bslot[i] = bin_slot_take(P, cl, (u32)((base[i] + (u64)e[i]) >> P.bin_shift));
 #pragma unroll
             for (int i = 0; i < CONF_U; i++) {
-                const u64 slot = sb + rank[i];
-                if (mt[i] && slot < P.out_cap) {
-                    const u64 lidx = ((u64)(li[i] - fc[i]) >> 3) & VSA_KEY_LI_MASK;
-                    P.out_keys[slot] = ((base[i] + (u64)e[i]) << VSA_KEY_END_SHIFT) |
-                                       ((u64)b[i] << VSA_KEY_BUCKET_SHIFT) | lidx;
-                    P.out_ids[slot] = w1[i].z;
-                }
-                if (mt[i] && P.bin_slots) {
-                    /* the record's output slot, staged in its bin (an
-                     * overflowed output or bin leaves the sort to the host) */
-                    if (bslot[i] < VSA_SORT_BIN_MAX)
-                        P.bin_slots[bix[i] * VSA_SORT_BIN_MAX + bslot[i]] = (u32)slot;
-                    else
-                        P.counters[VSA_CTR_BIN_OVERFLOW] = 1;
+                if (!mt[i]) continue;
+                const u64 end = base[i] + (u64)e[i];
+                const u64 lidx = ((u64)(li[i] - fc[i]) >> 3) & VSA_KEY_LI_MASK;
+                u32 before = 0; /* this lane's rank among the step's matches */
+#pragma unroll
+                for (int k = 0; k < i; k++) before += (u32)__popcll(pm[k]);
+                const u64 q = bins ? (u64)(end >> P.bin_shift) * VSA_SORT_BIN_MAX + bslot[i]
+                                   : sb + before + __builtin_amdgcn_mbcnt_hi(
+                                         (u32)(pm[i] >> 32), __builtin_amdgcn_mbcnt_lo((u32)pm[i], 0));
+                if (bins ? bslot[i] < VSA_SORT_BIN_MAX : q < P.out_cap) {
+                    (bins ? P.bin_keys : P.out_keys)[q] = (end << VSA_KEY_END_SHIFT) |
+                                                          ((u64)b[i] << VSA_KEY_BUCKET_SHIFT) | lidx;
+                    (bins ? P.bin_ids : P.out_ids)[q] = w1[i].z;
+                } else if (bins) {
+                    P.counters[VSA_CTR_BIN_OVERFLOW] = 1; /* crowded: the host rescans without bins */
                 }
             }
         }
@@ -1340,37 +1350,36 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
             u32 hits = e[4];
             /* one atomic per lane with hits (measured faster here than a
              * wave prefix sum + one atomic per gather) */
-            if (hits) {
+            if (hits && P.bin_keys) {
+                /* staged binned sort: the hits straight into their bins,
+                 * counted in LDS (no output slot, no shared global word) */
+                __hip_atomic_fetch_add(const_cast<u32 *>(&cl.nrec), (u32)__popc(hits),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                consumed += (u32)__popc(hits);
+                for (; hits; hits &= hits - 1) {
+                    const u32 j = __ffs(hits) - 1;
+                    const u64 end = p0 + j - mis;
+                    const u32 bin = (u32)(end >> P.bin_shift);
+                    const u32 s = bin_slot_take(P, cl, bin);
+                    if (s < VSA_SORT_BIN_MAX) {
+                        const size_t q = (size_t)bin * VSA_SORT_BIN_MAX + s;
+                        P.bin_keys[q] = end << VSA_KEY_END_SHIFT;
+                        P.bin_ids[q] = P.nood_id;
+                    } else {
+                        P.counters[VSA_CTR_BIN_OVERFLOW] = 1;
+                    }
+                }
+            } else if (hits) {
+                /* one atomic per lane with hits (measured faster here than
+                 * a wave prefix sum + one atomic per gather) */
                 const u32 n = (u32)__popc(hits);
-                /* the first hit's bin slot (staged binned sort) is reserved
-                 * before the output slots, so both returning atomics are in
-                 * flight together: one memory round trip per gather, not
-                 * two (under the scanners' streaming a round trip costs
-                 * microseconds, and this wave's rounds bound match-dense
-                 * scans: profiles/r05/r05r_*) */
-                u32 s_first = 0;
-                if (P.bin_slots)
-                    s_first = bin_slot_take(P, cl,
-                                            (u32)((p0 + (__ffs(hits) - 1) - mis) >> P.bin_shift));
                 unsigned long long slot = atomicAdd(&P.counters[0], (unsigned long long)n);
                 consumed += n;
-                bool first = true;
                 for (; hits; hits &= hits - 1, slot++) {
                     const u32 j = __ffs(hits) - 1;
-                    const u64 key = (p0 + j - mis) << VSA_KEY_END_SHIFT;
                     if (slot < P.out_cap) {
-                        P.out_keys[slot] = key;
+                        P.out_keys[slot] = (p0 + j - mis) << VSA_KEY_END_SHIFT;
                         P.out_ids[slot] = P.nood_id;
-                    }
-                    if (P.bin_slots) {
-                        /* staged binned sort (vsa_bin_finish) */
-                        const u32 bin = (u32)((p0 + j - mis) >> P.bin_shift);
-                        const u32 s = first ? s_first : bin_slot_take(P, cl, bin);
-                        first = false;
-                        if (s < VSA_SORT_BIN_MAX)
-                            P.bin_slots[(size_t)bin * VSA_SORT_BIN_MAX + s] = (u32)slot;
-                        else
-                            P.counters[VSA_CTR_BIN_OVERFLOW] = 1;
                     }
                 }
             }
@@ -1589,13 +1598,14 @@ vsa_lit_scan(VsaLitParams P) {
         /* owned sort bins: their counts so far (0, or the first split
          * pass's) into LDS */
         u32 lo = 0, n = 0;
-        if (P.bin_slots && P.wg_bins) {
+        if (P.bin_keys && P.wg_bins) {
             lo = P.wg_bins[2 * blockIdx.x];
             n = P.wg_bins[2 * blockIdx.x + 1] - lo;
         }
         if (tid == 0) {
             cl.lb_lo = lo;
             cl.lb_n = n;
+            cl.nrec = 0;
             conf_fin = 0;
         }
         for (u32 i = tid; i < n; i += LIT_THREADS) cl.lbins[i] = P.bin_counts[lo + i];
@@ -1636,6 +1646,10 @@ vsa_lit_scan(VsaLitParams P) {
             if (readfirstlane_u32(prev) + 1 == NC) {
                 const u32 lo = cl.lb_lo, n = cl.lb_n;
                 for (u32 i = lane; i < n; i += WAVE) P.bin_counts[lo + i] = cl.lbins[i];
+                /* the workgroup's record count: one add, not one per
+                 * confirm step on a word every workgroup shares */
+                if (lane == 0 && cl.nrec)
+                    atomicAdd(&P.counters[0], (unsigned long long)cl.nrec);
             }
         }
         if ((P.dbg & 8192) && P.wave_log && lane < 8) {
@@ -2151,7 +2165,7 @@ template __global__ void vsa_lit_scan<VSA_MODE_NOOD, false, false>(VsaLitParams)
 
 /* Match records sorted without a library sort (runtime.hip
  * queue_bin_sort): bins = VSA_SORT_BINS ranges of end positions; the scan
- * kernel stages each record's output slot in its bin as it emits it
+ * kernel stages each record (key and id) in its bin as it emits it
  * (confirm_multi), and one vsa_bin_finish launch sorts every bin (<= 64
  * records: a register bitonic sort on the full key) into place.  Keys are
  * unique (end, bucket, LitInfo), so the result equals the full sort. */
@@ -2230,9 +2244,9 @@ __global__ void __launch_bounds__(256) vsa_publish(unsigned long long *ctr,
 }
 
 /* Staged binned sort, the one launch behind a scan (runtime.hip
- * queue_bin_sort): the scan wrote every record's output slot into its bin's
- * staging slots (bin_slots, VSA_SORT_BIN_MAX per bin) as it counted it, so
- * no scatter pass is needed: the records are gathered through them.  Workgroup w owns bins [64 w, 64 w + 64): it
+ * queue_bin_sort): the scan wrote every record into its bin's staging
+ * slots (bin_keys / bin_ids, VSA_SORT_BIN_MAX per bin) as it counted it and
+ * nowhere else, so no scatter pass is needed: they are read from there.  Workgroup w owns bins [64 w, 64 w + 64): it
  * sums the counts of every earlier bin itself (<= 64 KiB of L2 reads; no
  * hand-off between workgroups, which on this chip costs an agent-scope
  * release per workgroup), scans its own 64 counts, and each of its 16 waves
@@ -2244,12 +2258,12 @@ __global__ void __launch_bounds__(256) vsa_publish(unsigned long long *ctr,
  * to the host (publish_body) at its start: the count and the overflow flags
  * are final when the scan ends, and everything that reads the sorted records
  * is queued on the stream behind this launch.  A bin past VSA_SORT_BIN_MAX
- * (flagged by the scan) or an output past out_cap leaves the output to the
- * host's library sort / rescan, which read the scan's unsorted records. */
+ * (flagged by the scan) or an output past out_cap makes the host rescan
+ * (without bins, or with a larger output). */
 #define FIN_BINS 64 /* bins per workgroup (1024 threads, 16 waves x 4) */
 __global__ void __launch_bounds__(1024) vsa_bin_finish(const uint32_t *counts, uint32_t *counts_next,
-                                                     const uint32_t *slots, const uint64_t *ikeys,
-                                                     const uint32_t *iids, uint64_t *okeys,
+                                                     const uint64_t *skeys, const uint32_t *sids,
+                                                     uint64_t *okeys,
                                                      uint32_t *oids,
                                                      uint64_t out_cap, unsigned long long *ctr,
                                                      unsigned long long *h,
@@ -2299,26 +2313,19 @@ __global__ void __launch_bounds__(1024) vsa_bin_finish(const uint32_t *counts, u
     u64 k[4];
     u32 id[4], jb[4];
     bool ok[4];
-    /* every pass's loads issued together: the staged output slots, then
-     * the records they point at (a slot past out_cap: the output overflowed,
-     * the host rescans) */
-    u32 at[4];
+    /* every pass's loads issued together: the records staged in the bins */
 #pragma unroll
     for (u32 p = 0; p < 4; p++) {
         const u32 j = p * per + j_l;
         jb[p] = j;
         const u32 mj = j == 0 ? m[0] : j == 1 ? m[1] : j == 2 ? m[2] : j == 3 ? m[3] : 0u;
         ok[p] = p * per < 4 && r < mj;
-        at[p] = ~0u;
-        if (ok[p]) at[p] = slots[(size_t)(b0 + lb + j) * VSA_SORT_BIN_MAX + r];
-    }
-#pragma unroll
-    for (u32 p = 0; p < 4; p++) {
         k[p] = ~0ULL;
         id[p] = 0;
-        if (ok[p] && at[p] < out_cap) {
-            k[p] = ikeys[at[p]];
-            id[p] = iids[at[p]];
+        if (ok[p]) {
+            const size_t q = (size_t)(b0 + lb + j) * VSA_SORT_BIN_MAX + r;
+            k[p] = skeys[q];
+            id[p] = sids[q];
         }
     }
 #pragma unroll

@@ -46,8 +46,7 @@ template <int MODE, bool XP, bool SPLIT>
 __global__ void vsa_lit_scan(VsaLitParams P);
 __global__ void vsa_class_scan(VsaClassParams P);
 __global__ void vsa_bin_finish(const uint32_t *counts, uint32_t *counts_next,
-                               const uint32_t *slots, const uint64_t *ikeys, const uint32_t *iids,
-                               uint64_t *okeys, uint32_t *oids, uint64_t out_cap,
+                               const uint64_t *skeys, const uint32_t *sids, uint64_t *okeys, uint32_t *oids, uint64_t out_cap,
                                unsigned long long *ctr,
                                unsigned long long *h, unsigned long long seq,
                                const unsigned long long *fb, unsigned long long *hfb,
@@ -108,8 +107,9 @@ struct Workspace {
     uint32_t *d_bins = nullptr; /* binned sort: two count buffers of
                                    VSA_SORT_BINS, used in turn (vsa_bin_finish
                                    reads one and clears the other) */
-    /* staged output slots of the binned sort: VSA_SORT_BIN_MAX per bin */
-    uint32_t *d_bslots = nullptr;
+    /* staged records of the binned sort: VSA_SORT_BIN_MAX per bin, keys
+     * (u64) then ids (u32) */
+    uint8_t *d_bstage = nullptr;
     unsigned long long *h_counters = nullptr; /* pinned mirror */
     /* fine-grained host memory the device publishes a binned scan's
      * counters into (vsa_publish): [0] = sequence, [1..16] = counters */
@@ -530,10 +530,15 @@ uint32_t bin_shift_for(int end_bits) {
     return end_bits > (int)VSA_SORT_BIN_BITS ? (uint32_t)end_bits - VSA_SORT_BIN_BITS : 0u;
 }
 
+uint64_t *bstage_keys(Workspace &w) { return (uint64_t *)w.d_bstage; }
+uint32_t *bstage_ids(Workspace &w) {
+    return (uint32_t *)(w.d_bstage + (size_t)VSA_SORT_BINS * VSA_SORT_BIN_MAX * sizeof(uint64_t));
+}
 uint32_t *bin_counts_of(vsa_ctx *c, uint32_t par) { return c->ws.d_bins + par * VSA_SORT_BINS; }
 
-/* The binned sort behind the scan: the scan kernel stages each record's
- * output slot in its bin as it emits it (VsaLitParams.bin_slots), and one
+/* The binned sort behind the scan: the scan kernel stages each record
+ * in its bin as it emits it (VsaLitParams.bin_keys / bin_ids; the records
+ * are written nowhere else), and one
  * vsa_bin_finish launch sorts the bins into place, clears the other count
  * buffer for the next launch and publishes the counters to the host.  It
  * reads the record count and the overflow flags from d_counters, so it is
@@ -549,8 +554,8 @@ int queue_bin_sort(vsa_ctx *c) {
     const uint32_t par = c->bin_par;
     const bool fbd = c->fb.armed >= 0 && c->fb.dev;
     hipLaunchKernelGGL(vsa_bin_finish, dim3(VSA_SORT_BINS / 64), dim3(1024), 0, c->stream,
-                       bin_counts_of(c, par), bin_counts_of(c, par ^ 1u), w.d_bslots,
-                       w.d_keys[0], w.d_ids[0], w.d_keys[1], w.d_ids[1], (uint64_t)w.out_cap,
+                       bin_counts_of(c, par), bin_counts_of(c, par ^ 1u), bstage_keys(w),
+                       bstage_ids(w), w.d_keys[1], w.d_ids[1], (uint64_t)w.out_cap,
                        c->ws.d_counters, c->ws.d_pub, (unsigned long long)++c->pub_seq,
                        fbd ? c->fb.d_rec : nullptr, fbd ? c->fb.d : nullptr,
                        fbd ? 2 * c->fb.grid : 0u);
@@ -687,9 +692,9 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
     /* not for the drop-in calls, whose few records the host sorts (a
      * larger result takes the library sort) */
     c->launch.bins = use_bins(c) && !(c->launch.flags & SCAN_HOST_SORT_SMALL);
-    if (c->launch.bins && !c->ws.d_bslots)
-        VSA_CHECK(hipMalloc(&c->ws.d_bslots,
-                            (size_t)VSA_SORT_BINS * VSA_SORT_BIN_MAX * sizeof(uint32_t)));
+    if (c->launch.bins && !c->ws.d_bstage)
+        VSA_CHECK(hipMalloc(&c->ws.d_bstage, (size_t)VSA_SORT_BINS * VSA_SORT_BIN_MAX *
+                                                 (sizeof(uint64_t) + sizeof(uint32_t))));
     const uint32_t par = c->bin_par;
     if (c->launch.bins && !c->bins_clean[par])
         VSA_CHECK(hipMemsetAsync(bin_counts_of(c, par), 0, VSA_SORT_BINS * sizeof(uint32_t),
@@ -747,7 +752,8 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.out_cap = w.out_cap;
     P.bin_counts = c->launch.bins ? bin_counts_of(c, c->bin_par) : nullptr;
     P.bin_shift = bin_shift_for(c->launch.end_bits);
-    P.bin_slots = c->launch.bins ? w.d_bslots : nullptr;
+    P.bin_keys = c->launch.bins ? bstage_keys(w) : nullptr;
+    P.bin_ids = c->launch.bins ? bstage_ids(w) : nullptr;
     P.counters = w.d_counters;
     P.wg_time = c->fb.armed >= 0 ? (c->fb.dev ? c->fb.d_rec : c->fb.d) : nullptr;
     P.wave_log = g_wave_log;
@@ -910,11 +916,16 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     /* a launch whose records crowd one bin sorts with the library; the next
      * few launches (likely as dense) skip the histogram */
     if (c->bin_skip) c->bin_skip--;
-    if (c->launch.dev_sort && w.h_counters[VSA_CTR_BIN_OVERFLOW]) c->bin_skip = 16;
-    if (n > 1 && !(flags & VSA_SCAN_UNSORTED) && !c->host_sort && c->launch.dev_sort &&
-        !w.h_counters[VSA_CTR_BIN_OVERFLOW]) {
-        /* sorted by the binned sort queued in launch_scan (its overflow
-         * flag, set by the scan, is in the counters just read) */
+    if (c->launch.dev_sort && w.h_counters[VSA_CTR_BIN_OVERFLOW]) {
+        /* a crowded bin: the launch's records exist only in the bins, so
+         * it runs again without them (complete_scan), and the next few
+         * launches (likely as dense) skip them too */
+        c->bin_skip = 16;
+        return VSA_E_OVERFLOW;
+    }
+    if (c->launch.dev_sort) {
+        /* sorted by the binned sort queued in launch_scan, into buffer 1
+         * (a single record too: buffer 0 is not written in this mode) */
         c->cur = 1;
     } else if (n > 1 && !(flags & VSA_SCAN_UNSORTED) && !c->host_sort) {
         hipcub::DoubleBuffer<uint64_t> kb(w.d_keys[0], w.d_keys[1]);
@@ -1817,7 +1828,7 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (w.d_in) (void)hipFree(w.d_in);
     if (w.d_counters) (void)hipFree(w.d_counters);
     if (w.d_bins) (void)hipFree(w.d_bins);
-    if (w.d_bslots) (void)hipFree(w.d_bslots);
+    if (w.d_bstage) (void)hipFree(w.d_bstage);
     if (w.h_counters) (void)hipHostFree(w.h_counters);
     if (w.h_pub) (void)hipHostFree(w.h_pub);
     if (c->fb.h) (void)hipHostFree(c->fb.h);
