@@ -543,6 +543,70 @@ def test_gpu_binned_sort(ctx):
         ctx.free(d)
 
 
+def test_gpu_crowded_bin_plans(ctx):
+    """A binned scan's records live only in its sort bins, so a crowded bin
+    (> VSA_SORT_BIN_MAX records) makes the scan run again without bins:
+    through a plan (sync and asynchronous + wait) and through the packed
+    collective buffer (header flagged not-ready until the host completes).
+    Every result == the unsorted scan's records sorted here."""
+    vsa_ctx = vsa.Context(0)  # a fresh context: no bin_skip carried over
+    try:
+        crowd = vsa.Database(vsa_ctx, vsa.hwlm_build(
+            [vsa.HwlmLiteral(b"ab", False, 10 + i) for i in range(80)] +
+            [vsa.HwlmLiteral(b"bab", False, 5)]))
+        rng = random.Random(41)
+        host = np.frombuffer(rand_data(rng, 2 << 20), np.uint8).copy()
+        host[5000:5400] = np.frombuffer(b"ab" * 200, np.uint8)
+        d = vsa_ctx.malloc(len(host))
+        try:
+            vsa_ctx.h2d(d, host)
+            offs, lens = [0, 1 << 20], [1 << 20, (1 << 20) - 3]
+            n0 = vsa_ctx.scan_blocks(crowd, d, offs, lens, sort=False)
+            raw = vsa_ctx.results(n0)
+            order = np.argsort(raw["key"], kind="stable")
+            want_k, want_i = raw["key"][order], raw["id"][order]
+
+            def check(n):
+                got = vsa_ctx.results(n)
+                assert n == n0
+                assert np.array_equal(got["key"], want_k) and np.array_equal(got["id"], want_i)
+
+            for mode in ("sync", "async", "pack"):
+                fresh = vsa.Context(0)
+                try:
+                    db = vsa.Database(fresh, vsa.hwlm_build(
+                        [vsa.HwlmLiteral(b"ab", False, 10 + i) for i in range(80)] +
+                        [vsa.HwlmLiteral(b"bab", False, 5)]))
+                    plan = fresh.plan(d, offs, lens)
+                    if mode == "sync":
+                        n = fresh.scan_plan(db, plan)
+                    else:
+                        fresh.scan_plan(db, plan, asynchronous=True)
+                        if mode == "pack":
+                            cap = n0 + 16
+                            buf = fresh.malloc(8 * (1 + cap) + 4 * cap)
+                            fresh.scan_pack(buf, cap)
+                            hdr = np.zeros(1, np.uint64)
+                            fresh.d2h(hdr, buf)
+                            fresh.free(buf)
+                            assert int(hdr[0]) >> 62 & 1  # not ready: the host completes
+                        n = fresh.scan_wait()
+                    got = fresh.results(n)
+                    assert n == n0, mode
+                    assert np.array_equal(got["key"], want_k), mode
+                    assert np.array_equal(got["id"], want_i), mode
+                    plan.close()
+                    db.close()
+                finally:
+                    fresh.close()
+            check(vsa_ctx.scan_blocks(crowd, d, offs, lens))
+        finally:
+            vsa_ctx.free(d)
+            crowd.close()
+    finally:
+        vsa_ctx.close()
+
+
 def test_gpu_overlapping_blocks_dense(ctx):
     """Blocks that overlap each other (the runtime then owns no sort bin in
     any workgroup, plan_wg_bins) and blocks that do not (bins counted in LDS),
