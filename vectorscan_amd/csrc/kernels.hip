@@ -289,7 +289,9 @@ template <int CONF_U>
 __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfLds &cl,
                                               const QEnt (&q)[CONF_U], const bool (&valid)[CONF_U],
                                               u32 mis) {
-    const u8 *fc[CONF_U], *li[CONF_U];
+    /* LitInfo addresses as u32 offsets from confBase (an SGPR base: one
+     * VGPR per candidate instead of two) */
+    u32 fc[CONF_U], li[CONF_U];
     u32 st[CONF_U], b[CONF_U];
     u64 base[CONF_U], blen[CONF_U];
     int64_t hlen[CONF_U], e[CONF_U];
@@ -297,14 +299,14 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
     for (int i = 0; i < CONF_U; i++) {
         b[i] = (u32)(q[i].meta & 15);
         const u32 blk = (u32)((q[i].meta >> 4) & 0xfffff);
-        fc[i] = P.conf_base + cl.off[b[i]];
+        fc[i] = cl.off[b[i]];
         st[i] = 0;
         base[i] = 0;
         blen[i] = ~0ULL;
         hlen[i] = 0;
         if (valid[i]) {
             const u32 c = conf_hash(q[i].key, cl.andmsk[b[i]], cl.mult[b[i]], cl.nbits[b[i]]);
-            st[i] = *((const u32 *)(fc[i] + 32) + c);
+            st[i] = *((const u32 *)(P.conf_base + fc[i] + 32) + c);
             base[i] = P.blocks[blk].base;
             blen[i] = P.blocks[blk].len;
             hlen[i] = (int64_t)P.blocks[blk].hlen;
@@ -338,8 +340,8 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
 #pragma unroll
         for (int i = 0; i < CONF_U; i++) {
             if (live[i]) {
-                w0[i] = *(const uint4 *)li[i];        /* v, msk */
-                w1[i] = *(const uint4 *)(li[i] + 16); /* groups | id,size,flags,next */
+                w0[i] = *(const uint4 *)(P.conf_base + li[i]);        /* v, msk */
+                w1[i] = *(const uint4 *)(P.conf_base + li[i] + 16); /* groups | id,size,flags,next */
             }
         }
         bool mt[CONF_U];
@@ -384,7 +386,7 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
             for (int i = 0; i < CONF_U; i++) {
                 if (!mt[i]) continue;
                 const u64 end = base[i] + (u64)e[i];
-                const u64 lidx = ((u64)(li[i] - fc[i]) >> 3) & VSA_KEY_LI_MASK;
+                const u64 lidx = (u64)((li[i] - fc[i]) >> 3) & VSA_KEY_LI_MASK;
                 u32 before = 0; /* this lane's rank among the step's matches */
 #pragma unroll
                 for (int k = 0; k < i; k++) before += (u32)__popcll(pm[k]);
