@@ -297,9 +297,10 @@ int vsa_scan_wait(vsa_ctx_t *ctx, uint64_t *n_matches);
 /* Pack the last scan's sorted records for a collective, into caller device
  * memory d_dst (u64 words): [header | keys (cap) | ids (cap x u32, i.e.
  * cap / 2 words)], header = record count, bit 62 set when the records are
- * not usable as packed (the scan overflowed its output or a crowded bin
- * needs the host sort: complete the scan with vsa_scan_wait and pack
- * again), then min(count, cap) records.  After an asynchronous binned scan
+ * not usable as packed (the scan overflowed its output, or a crowded sort
+ * bin means the scan runs again without bins: complete the scan with
+ * vsa_scan_wait, which does so, and pack again), then min(count, cap)
+ * records.  After an asynchronous binned scan
  * the pack is queued on the context's stream behind it with no host wait
  * (RCCL gathers of stripes, vectorscan_amd/stripe.py); otherwise the scan
  * is completed first. */
