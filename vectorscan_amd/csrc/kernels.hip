@@ -141,9 +141,17 @@ __device__ __forceinline__ u32 wave_excl_scan(u32 v, u32 *total) {
     return x - v;
 }
 
-__device__ __forceinline__ u8 load_byte_masked(const u8 *A, int64_t aoff,
-                                               int64_t lo, int64_t hi) {
-    return (aoff >= lo && aoff < hi) ? A[aoff] : (u8)0;
+/* A byte of A inside [lo, hi) when `want`, else 0.  Branch-free: the load
+ * always issues, from `safe` (any valid device byte) when the byte is not
+ * wanted, so several of these go out together -- as guarded loads, each
+ * in its own EXEC-masked block, the compiler waited for one before issuing
+ * the next (a segment start took 4 serial round trips for 4 bytes). */
+__device__ __forceinline__ u8 load_byte_masked(const u8 *A, int64_t aoff, int64_t lo, int64_t hi,
+                                               bool want, const u8 *safe) {
+    const bool ok = want && aoff >= lo && aoff < hi;
+    typedef const __attribute__((address_space(1))) u8 gu8;
+    const u8 v = *(gu8 *)(ok ? A + aoff : safe);
+    return ok ? v : (u8)0;
 }
 
 /* ===================================================== literal scan === */
@@ -1926,13 +1934,14 @@ vsa_lit_scan(VsaLitParams P) {
         const bool pro1 = lane < (u32)(T::NL - 1);
         const int64_t pp = pro_lo - (T::NL - 1) + (int64_t)lane;
         const bool pro1_in = pro1 && pp - S.blo >= zlo && pp - S.blo < S.len;
-        const u8 pb0 = pro1_in ? load_byte_masked(A, pp, S.vlo, S.bhi) : (u8)0;
+        const u8 *safe = (const u8 *)P.blocks;
+        const u8 pb0 = load_byte_masked(A, pp, S.vlo, S.bhi, pro1_in, safe);
         /* FDR4 keys also need the two bytes before each position: issued
          * with the others (one memory round trip for the whole prologue) */
         const bool F4P = MODE == VSA_MODE_FDR4;
-        const u8 pm2 = (F4P && pro1_in) ? load_byte_masked(A, pp - 2, S.vlo, S.bhi) : (u8)0;
-        const u8 pm1 = (F4P && pro1_in) ? load_byte_masked(A, pp - 1, S.vlo, S.bhi) : (u8)0;
-        const u32 pbb = lane < 8 ? load_byte_masked(A, pro_lo - 8 + (int64_t)lane, S.vlo, S.bhi) : 0u;
+        const u8 pm2 = F4P ? load_byte_masked(A, pp - 2, S.vlo, S.bhi, pro1_in, safe) : (u8)0;
+        const u8 pm1 = F4P ? load_byte_masked(A, pp - 1, S.vlo, S.bhi, pro1_in, safe) : (u8)0;
+        const u32 pbb = load_byte_masked(A, pro_lo - 8 + (int64_t)lane, S.vlo, S.bhi, lane < 8, safe);
         /* a range that starts with the sweep (a segment inside a block, the
          * common case of large blocks): its first LIT_DEPTH chunks go out
          * with the prologue bytes, so a segment start waits for one memory
