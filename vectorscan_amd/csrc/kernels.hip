@@ -154,6 +154,23 @@ __device__ __forceinline__ u8 load_byte_masked(const u8 *A, int64_t aoff, int64_
     return ok ? v : (u8)0;
 }
 
+/* A segment's block record (i wave-uniform), read as scalar loads: the
+ * table is written by the host before the launch and only read here.  As
+ * vector loads the record went through the few VGPRs free at a segment
+ * start, one load waited for before the next -- four serial round trips
+ * per segment; scalar loads all go out at once. */
+__device__ __forceinline__ VsaBlock load_block(const VsaBlock *blocks, u32 i) {
+    static_assert(sizeof(VsaBlock) == 9 * sizeof(u64), "VsaBlock: 9 words");
+    typedef const __attribute__((address_space(4))) u64 cu64;
+    cu64 *p = (cu64 *)(blocks + i);
+    u64 w[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) w[k] = p[k];
+    VsaBlock b;
+    __builtin_memcpy(&b, w, sizeof(b));
+    return b;
+}
+
 /* ===================================================== literal scan === */
 
 template <int MODE>
@@ -1820,9 +1837,13 @@ vsa_lit_scan(VsaLitParams P) {
          * first block | count << 24 (count 0: a part of one block, else
          * `count` whole consecutive blocks), and for a part its offset and
          * length in KiB from the block's origin */
-        const uint4 dsc = ((const uint4 *)P.seg_desc)[seg];
-        const u32 sbv = readfirstlane_u32(dsc.x);
-        const u32 d_off = readfirstlane_u32(dsc.y), d_len = readfirstlane_u32(dsc.z);
+        /* scalar loads (seg is wave-uniform; the plan's tables are written
+         * by the host before the launch and only read here) */
+        typedef const __attribute__((address_space(4))) u32 cu32;
+        const u32 segu = readfirstlane_u32(seg);
+        const u32 sbv = ((cu32 *)P.seg_desc)[4 * (size_t)segu];
+        const u32 d_off = ((cu32 *)P.seg_desc)[4 * (size_t)segu + 1];
+        const u32 d_len = ((cu32 *)P.seg_desc)[4 * (size_t)segu + 2];
         const u32 gcount = sbv >> 24;
         /* a run (VSA_BLK_RUN, FDR / Teddy): the segment's back-to-back
          * blocks are one range -- one prologue, one sweep, two checked
@@ -1840,13 +1861,15 @@ vsa_lit_scan(VsaLitParams P) {
         const u32 first = sbv & 0xffffffu;
         bool run = false;
         if constexpr (MODE != VSA_MODE_NOOD)
-            run = gcount > 1 && (P.blocks[first].flags & VSA_BLK_RUN);
+            run = gcount > 1 &&
+                  (((cu32 *)P.blocks)[(size_t)first * (sizeof(VsaBlock) / 4) +
+                                      offsetof(VsaBlock, flags) / 4] & VSA_BLK_RUN);
         u32 rend0 = 0xffffffffu, rend1 = 0xffffffffu;
         const u32 nblk = run ? 1u : (gcount ? gcount : 1u);
         for (u32 gi = 0; gi < nblk; gi++) {
         lastb = gi + 1 == nblk;
         const u32 blk = first + gi;
-        const VsaBlock B = P.blocks[blk];
+        const VsaBlock B = load_block(P.blocks, blk);
         SegCtx S;
         S.blk = blk;
         S.blo = (int64_t)B.base + mis;
