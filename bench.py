@@ -159,6 +159,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline timing")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end (matches delivered to the host) line")
+    ap.add_argument("--no-cfg5", action="store_true",
+                    help="skip the cfg-5-shaped hsbench pass (end_to_end_cfg5proxy)")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one scan context: each step completed before the next is queued")
@@ -278,9 +280,15 @@ def run(args):
 
     def issue(k):
         sl = slots[k % nslot]
-        sl["ctx"].scan_plan(db, sl["plan"], asynchronous=True)
-        if dist is not None:
-            sl["pg"].start(sl["pack"], sl["wait"])
+        if dist is None:
+            sl["ctx"].scan_plan(db, sl["plan"], asynchronous=True)
+        else:
+            # the scan's binned sort writes the records straight into this
+            # slot's collective buffer (vsa_scan_plan_pack: no pack launch);
+            # a rescan is repacked by finish() through scan_pack
+            pg = sl["pg"]
+            sl["ctx"].scan_plan_pack(db, sl["plan"], pg.pk_dev.data_ptr(), pg.cap)
+            pg.start(None, sl["wait"])
 
     def complete(k):
         sl = slots[k % nslot]
@@ -374,6 +382,13 @@ def run(args):
             e2e = {"error": repr(e)}
     del data
     torch.cuda.empty_cache()
+    cfg5 = None
+    if world == 1 and not args.no_cfg5:
+        try:
+            cfg5 = cfg5_proxy(torch, dev, args.steps, args.no_parity, args.cpu_threads)
+        except Exception as e:  # a side measurement never voids the bench line
+            cfg5 = {"error": repr(e)}
+        torch.cuda.empty_cache()
 
     out = None
     # the CPU baseline is timed at N = 1 only (on rank 0); N > 1 runs check
@@ -474,9 +489,11 @@ def run(args):
                        "cpus_visible": visible, "cpu_quota": quota,
                        "sample": "the whole %d-byte corpus, 4 x 1 GiB blocks: oracle/oracle.c "
                                  "SSE2 port of the reference FDR main loop (fdr.c:145-333, "
-                                 "m128 state, flood checks) on the reference bytecode's own "
-                                 "domain-%d table, %d threads over contiguous stripes (7-byte "
-                                 "halo); host: %s" % (parity_bytes, blob_domain(blob), threads,
+                                 "m128 state, flood checks) over the FDR bytecode this "
+                                 "repository builds (csrc/compile.cpp, the restated "
+                                 "fdr_compile.cpp; byte identity with a reference-built blob "
+                                 "unpinned), its own domain-%d table, %d threads over "
+                                 "contiguous stripes (7-byte halo); host: %s" % (parity_bytes, blob_domain(blob), threads,
                                                      _cpu_model())}
         alg_bytes = local_bytes + 16 * nm // world  # rank 0's input + its share of records
         achieved = alg_bytes / (kavg * 1e-3) / 1e9
@@ -524,6 +541,7 @@ def run(args):
             "cpu_baseline": cpu,
             "pipeline": nslot,
             "end_to_end": e2e,
+            "end_to_end_cfg5proxy": cfg5,
             "settle": {"launches": settle_n, "s": round(t_settle, 3),
                        "why": "GPU clock ramp after idle (profiles/r03_ramp.jsonl): untimed "
                               "scans until the kernel time is stable, before the warmup"},
@@ -582,6 +600,90 @@ def end_to_end(lits, d_data, bl, nblocks, total, hwlm_records, reps):
         corpus.close()
         scratch.close()
         db.close()
+
+
+def cfg5_proxy(torch, dev, reps, no_parity=False, cpu_threads=0):
+    """hsbench block mode at cfg 5's shape (BASELINE configs[4]), the part of
+    it this image can build: cfg 5 is a 10k mixed-REGEX database, whose
+    compile needs the reference's full compiler (Ragel / Boost, absent), so
+    the database here is its pure-literal proxy -- make_mixed_set(10000):
+    10k printable literals of length 4-16 (the ones past 8 bytes confirmed on
+    the host), 70 % plain / 10 % CASELESS / 10 % SINGLEMATCH / 10 %
+    SOM_LEFTMOST, unique ids as hsbench expression files have -- over 1 GiB
+    in HBM cut into hsbench's 16 KiB chunks (65,536 hs_scan blocks), a
+    literal planted per 64 KiB.  `reps` pipelined passes
+    (vsa_hs_corpus_scan_repeats: pass k + 1 scans on the GPU while the host
+    replays pass k through the report program, the host-side confirm of the
+    north star), after an untimed settle; every pass delivers every match to
+    a host callback.  Parity: every chunk's delivered (id, from, to) sequence
+    digest and count of the last pass vs oracle/hs_lit.py over the oracle's
+    own HWLM records of that chunk (oracle.records_blocks), all 65,536
+    chunks."""
+    import vectorscan_amd as vsa
+    from vectorscan_amd import hs
+    exprs, flags, ids = make_mixed_set(10000, shared_ids=False)
+    lits = [vsa.HwlmLiteral(e, False, i) for i, e in enumerate(exprs)]
+    n, chunk = 1 << 30, 16 << 10
+    data = make_corpus_device(torch, 0, n, n, lits, 9, 64 << 10, dev)
+    host = data.cpu().numpy()
+    db = hs.compile_lit_multi(exprs, flags, ids, hs.MODE_BLOCK)
+    scratch = hs.Scratch(db)
+    offs = np.arange(0, n, chunk, dtype=np.uint64)
+    lens = np.full(len(offs), chunk, np.uint64)
+    corpus = hs.Corpus(db, scratch, data.data_ptr(), offs, lens, h_data=host)
+    threads = 16
+    try:
+        for _ in range(2):  # settle (compiling idled the GPU), as end_to_end
+            rc, _, _, _ = corpus.scan_repeats(30, threads=threads)
+            if rc:
+                return {"error": rc}
+        t0 = time.perf_counter()
+        rc, tot, cnt, dg = corpus.scan_repeats(reps, counts=True, threads=threads, digests=True)
+        el = time.perf_counter() - t0
+        if rc:
+            return {"error": rc}
+        out = {"value": round(n * reps / el / 1e9, 3), "unit": "GB/s",
+               "ms_per_gib": round(el / reps * 1e3 * (1 << 30) / n, 4), "passes": reps,
+               "matches_per_pass": int(tot[-1]), "chunks": len(offs),
+               "live_chunks": int(np.count_nonzero(cnt)), "replay_threads": threads,
+               "what": "cfg-5-shaped hsbench block mode: pure-literal proxy of the 10k mixed-regex "
+                       "database (make_mixed_set(10000), mixed CASELESS / SINGLEMATCH / "
+                       "SOM_LEFTMOST, literals 4-16 B), 1 GiB as 16 KiB hs_scan chunks, pipelined "
+                       "passes, every match delivered to a host callback through the report "
+                       "program"}
+        if not no_parity:
+            import oracle
+            import oracle.hs_lit as ohl
+            odb = ohl.compile_lit_multi(exprs, flags, ids)
+            oblob = vsa.hwlm_build([vsa.HwlmLiteral(t, nc, f, noruns=nr)
+                                    for t, nc, f, nr in odb.hwlm_literals()])
+            e, i, b = oracle.records_blocks(vsa.engine_blob(oblob), host, chunk,
+                                            cpu_threads or min(16, os.cpu_count() or 1))
+            want_n = np.zeros(len(offs), np.uint64)
+            want_d = np.zeros(len(offs), np.uint64)
+            cuts = np.flatnonzero(np.diff(b.astype(np.int64))) + 1
+            for lo, hi in zip(np.r_[0, cuts], np.r_[cuts, len(b)]):
+                if hi <= lo:
+                    continue
+                k = int(b[lo])
+                seq = ohl.scan_records(odb, host[k * chunk:(k + 1) * chunk],
+                                       zip(e[lo:hi].tolist(), i[lo:hi].tolist()))
+                want_n[k] = len(seq)
+                want_d[k] = hs.seq_digest(seq)
+            bad = np.flatnonzero((want_n != cnt) | (want_d != dg))
+            out["parity"] = len(bad) == 0 and all(int(t) == int(want_n.sum()) for t in tot)
+            out["parity_kind"] = ("order-exact per chunk: digest of the delivered (id, from, to) "
+                                  "callback sequence and its count vs oracle/hs_lit.py over all "
+                                  "%d chunks; every pass's total equal" % len(offs))
+            if len(bad):
+                print("bench: CFG5 PROXY PARITY FAILURE in chunks %s" % bad[:8].tolist(),
+                      file=sys.stderr, flush=True)
+        return out
+    finally:
+        corpus.close()
+        scratch.close()
+        db.close()
+        del data
 
 
 def blob_domain(blob):

@@ -305,6 +305,15 @@ int vsa_scan_wait(vsa_ctx_t *ctx, uint64_t *n_matches);
  * (RCCL gathers of stripes, vectorscan_amd/stripe.py); otherwise the scan
  * is completed first. */
 int vsa_scan_pack(vsa_ctx_t *ctx, void *d_dst, uint64_t cap);
+/* vsa_scan_plan(..., VSA_SCAN_ASYNC) whose binned sort also writes the
+ * records into d_dst in vsa_scan_pack's layout, header included: the pack
+ * launch behind the sort is gone (one kernel boundary and one copy of the
+ * records less per multi-GPU step).  For this launch only: when it is not
+ * binned (or a crowded bin / output overflow makes the header NOT_READY)
+ * the caller completes the scan and repacks with vsa_scan_pack, as after a
+ * plain scan. */
+int vsa_scan_plan_pack(vsa_ctx_t *ctx, const vsa_db_t *db, const vsa_plan_t *plan, void *d_dst,
+                       uint64_t cap);
 int vsa_scan_results(vsa_ctx_t *ctx, const uint64_t **d_keys,
                      const uint32_t **d_ids);
 /* Copy up to cap results of the last scan to the host. */
@@ -326,6 +335,10 @@ uint64_t vsa_scan_candidates(vsa_ctx_t *ctx);
 int vsa_scan_debug_counters(vsa_ctx_t *ctx, uint64_t out[16]);
 /* Device time (ms, hipEvents on the scan stream) of the last scan kernel. */
 double vsa_scan_kernel_ms(vsa_ctx_t *ctx);
+/* Literal-scan launches this context has queued (every rescan of an
+ * output overflow or a crowded sort bin counts): a diagnostic of the rerun
+ * cost, no reference counterpart. */
+uint64_t vsa_scan_launches(vsa_ctx_t *ctx);
 /* Measurement helper, not a scan (no reference counterpart): the streaming-
  * read ceiling of this device over d_data -- the first len rounded down to
  * 64 KiB read once per run by a plain 16-byte-load kernel on the ctx stream,

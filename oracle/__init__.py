@@ -362,6 +362,32 @@ def records_mt(engine_ptr, data, nthreads, nood=False, cap=1 << 24):
     raise RuntimeError("orc_records_mt: record count changed between runs")
 
 
+_sig("orc_records_blocks", ctypes.c_long, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+     ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+     ctypes.c_void_p, ctypes.c_size_t)
+
+
+def records_blocks(engine_ptr, data, block_len, nthreads, nood=False, cap=1 << 22):
+    """(ends, ids, blocks) of every `block_len`-byte block of `data` scanned
+    as its own call (oracle.c orc_records_blocks: hsbench's fixed-size
+    chunks), in block order, each block's records in callback order, ends
+    relative to their block."""
+    buf = np.ascontiguousarray(data, dtype=np.uint8)
+    for _ in range(2):
+        ends = np.zeros(cap, np.uint64)
+        ids = np.zeros(cap, np.uint32)
+        blks = np.zeros(cap, np.uint32)
+        n = _lib.orc_records_blocks(engine_ptr, int(nood), buf.ctypes.data, len(buf),
+                                    int(block_len), int(nthreads), ends.ctypes.data,
+                                    ids.ctypes.data, blks.ctypes.data, cap)
+        if n < 0:
+            raise RuntimeError("orc_records_blocks failed")
+        if n <= cap:
+            return ends[:n], ids[:n], blks[:n]
+        cap = n
+    raise RuntimeError("orc_records_blocks: record count changed between runs")
+
+
 def mix64(x):
     """splitmix64 finalizer over a uint64 numpy array (oracle.c orc_mix64)."""
     with np.errstate(over="ignore"):

@@ -1239,6 +1239,82 @@ long orc_records_mt(const void *eng, int nood, const u8 *buf, size_t len, int nt
     return n;
 }
 
+/* Many equal blocks (hsbench's corpus of fixed-size chunks): block b =
+ * buf[b * blen, min(len, (b + 1) * blen)) scanned as its own hwlmExec call
+ * (start 0, no history), every record kept with its block index; blocks are
+ * dealt to `nthreads` threads in contiguous ranges and the records come out
+ * in block order, each block's in callback order (fdr.c:299-333).  Writes
+ * min(total, cap) records (end relative to the block) and returns the total
+ * (-1 on a failed block or allocation).  bench.py's cfg-5 proxy parity. */
+typedef struct {
+    const void *eng;
+    int nood;
+    const u8 *buf;
+    size_t len, blen, b0, b1;
+    orc_match *out;
+    u32 *blk;
+    size_t n, cap;
+    int status, t;
+} orc_blocks_job;
+
+static void *orc_blocks_run(void *p) {
+    orc_blocks_job *j = (orc_blocks_job *)p;
+    orc_pin_self(j->t);
+    for (size_t b = j->b0; b < j->b1 && j->status == 0; b++) {
+        const size_t lo = b * j->blen, hi = lo + j->blen < j->len ? lo + j->blen : j->len;
+        cbctx cb = {NULL, 0, 0, -1, ~0ULL, 2, 0, 0, 0, 0};
+        j->status = j->nood ? nood_run((const struct o_nood *)j->eng, j->buf + lo, hi - lo, 0, &cb)
+                            : fdr_dispatch_s(j->eng, j->buf + lo, hi - lo, 0, ~0ULL, &cb, 0);
+        if (j->n + cb.n > j->cap) {
+            const size_t nc = 2 * (j->n + cb.n) + 4096;
+            orc_match *o = (orc_match *)realloc(j->out, nc * sizeof(orc_match));
+            u32 *bk = (u32 *)realloc(j->blk, nc * sizeof(u32));
+            if (o) j->out = o;
+            if (bk) j->blk = bk;
+            if (!o || !bk) j->status = -1;
+            else j->cap = nc;
+        }
+        for (size_t i = 0; j->status == 0 && i < cb.n; i++) {
+            j->out[j->n] = cb.out[i];
+            j->blk[j->n++] = (u32)b;
+        }
+        free(cb.out);
+    }
+    return NULL;
+}
+
+long orc_records_blocks(const void *eng, int nood, const u8 *buf, size_t len, size_t blen,
+                        int nthreads, u64a *ends, u32 *ids, u32 *blks, size_t cap) {
+    if (!blen) return -1;
+    const size_t nb = (len + blen - 1) / blen;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    if ((size_t)nthreads > nb) nthreads = nb ? (int)nb : 1;
+    orc_blocks_job jobs[256];
+    pthread_t th[256];
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = (orc_blocks_job){eng, nood, buf, len, blen, nb * (size_t)t / (size_t)nthreads,
+                                   nb * (size_t)(t + 1) / (size_t)nthreads, NULL, NULL, 0, 0, 0, t};
+        if (pthread_create(&th[t], NULL, orc_blocks_run, &jobs[t]) != 0) return -1;
+    }
+    long n = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        if (jobs[t].status != 0) n = -1;
+        for (size_t i = 0; n >= 0 && i < jobs[t].n; i++) {
+            if ((size_t)n < cap) {
+                ends[n] = jobs[t].out[i].end;
+                ids[n] = jobs[t].out[i].id;
+                blks[n] = jobs[t].blk[i];
+            }
+            n++;
+        }
+        free(jobs[t].out);
+        free(jobs[t].blk);
+    }
+    return n;
+}
+
 long orc_fdr_count_mt(const void *eng, const u8 *buf, size_t len, int nthreads) {
     u64a d[2];
     return orc_digest_mt(eng, 0, buf, len, nthreads, d);

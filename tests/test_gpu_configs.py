@@ -179,3 +179,58 @@ def test_gpu_large_literal_sets(ctx, nlits, monkeypatch):
     finally:
         monkeypatch.delenv("VSA_SPLIT", raising=False)
         ctx.free(d)
+
+
+def big_corpus(n, lits, seed, plant_every):
+    """a printable corpus with `lits` planted every `plant_every` bytes,
+    generated in 64 MiB pieces (uint8 draws: no 8-byte index array of the
+    whole size) and planted as bench.plant_plan does"""
+    r = np.random.default_rng(seed)
+    data = np.empty(n, np.uint8)
+    for o in range(0, n, 64 << 20):
+        m = min(64 << 20, n - o)
+        data[o:o + m] = r.integers(0x20, 0x7F, m, dtype=np.uint8)
+    idx, val = bench.plant_plan(n, lits, seed, plant_every)
+    data[idx] = val
+    return data
+
+
+def test_gpu_full_size_cfg1_cfg3(ctx):
+    """cfg 1 and cfg 3 at their BASELINE size (1 GiB, the size the bench
+    lines are quoted at), order-exact against the oracle's callback sequence
+    (oracle.records_mt over 16 host stripes with a 7-byte halo): cfg 1 noodle
+    'abcde' caseful and nocase on one corpus (planted every 4 KiB, seed 1),
+    cfg 3 on the 48-literal set (default Fat Teddy engine 8 and the SSE
+    build's 8-bucket engine 18) and the 64-literal set (engine 8), one corpus
+    per set (planted every 4 KiB, seed 3)."""
+    n = 1 << 30
+    cases = [(1, [vsa.HwlmLiteral(b"abcde", False, 0)], [(-1, None)]),
+             (1, [vsa.HwlmLiteral(b"abcde", True, 0)], [(-1, None)]),
+             (3, cfg3_lits(48), [(-1, 8), (18, 18)]),
+             (3, cfg3_lits(64), [(-1, 8)])]
+    d = ctx.malloc(n + 64)
+    try:
+        cur = None
+        for seed, lits, engines in cases:
+            if cur != (seed, lits[0].s):
+                cur = (seed, lits[0].s)
+                host = big_corpus(n, lits, seed, 4096)
+                ctx.h2d(d, host)
+            for hint, engine in engines:
+                blob = vsa.hwlm_build(lits, engine_hint=hint)
+                if engine is not None:
+                    assert blob.engine_id == engine
+                db = vsa.Database(ctx, blob)
+                try:
+                    k = ctx.scan_blocks(db, d, [0], [n])
+                    res = ctx.results(k)
+                finally:
+                    db.close()
+                want_e, want_i = oracle.records_mt(vsa.engine_blob(blob), host, 16,
+                                                   nood=blob.is_noodle)
+                assert len(want_e) >= n // 4096, (seed, hint)
+                assert k == len(want_e), (seed, hint, k, len(want_e))
+                assert np.array_equal(res["key"] >> np.uint64(24), want_e), (seed, hint)
+                assert np.array_equal(res["id"], want_i), (seed, hint)
+    finally:
+        ctx.free(d)

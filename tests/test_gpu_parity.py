@@ -571,7 +571,7 @@ def test_gpu_crowded_bin_plans(ctx):
                 assert n == n0
                 assert np.array_equal(got["key"], want_k) and np.array_equal(got["id"], want_i)
 
-            for mode in ("sync", "async", "pack"):
+            for mode in ("sync", "async", "pack", "plan_pack"):
                 fresh = vsa.Context(0)
                 try:
                     db = vsa.Database(fresh, vsa.hwlm_build(
@@ -580,6 +580,24 @@ def test_gpu_crowded_bin_plans(ctx):
                     plan = fresh.plan(d, offs, lens)
                     if mode == "sync":
                         n = fresh.scan_plan(db, plan)
+                    elif mode == "plan_pack":
+                        # the fused pack of a crowded launch: header flagged
+                        # not ready; the host completes (rescan without
+                        # bins) and repacks
+                        cap = n0 + 16
+                        buf = fresh.malloc(8 * (1 + cap) + 4 * cap)
+                        fresh.scan_plan_pack(db, plan, buf, cap)
+                        n = fresh.scan_wait()
+                        hdr = np.zeros(1, np.uint64)
+                        fresh.d2h(hdr, buf)
+                        assert int(hdr[0]) >> 62 & 1
+                        fresh.scan_pack(buf, cap)
+                        pk = np.zeros(1 + cap + (cap + 1) // 2, np.uint64)
+                        fresh.d2h(pk, buf)
+                        fresh.free(buf)
+                        assert int(pk[0]) == n0
+                        assert np.array_equal(pk[1:1 + n0], want_k)
+                        assert np.array_equal(pk[1 + cap:].view(np.uint32)[:n0], want_i)
                     else:
                         fresh.scan_plan(db, plan, asynchronous=True)
                         if mode == "pack":
@@ -605,6 +623,102 @@ def test_gpu_crowded_bin_plans(ctx):
             crowd.close()
     finally:
         vsa_ctx.close()
+
+
+def test_gpu_plan_pack_fused(ctx):
+    """vsa_scan_plan_pack: the binned sort writes the records into the
+    collective buffer itself (no vsa_pack launch).  Over ragged blocks with
+    sparse records, pipelined over two contexts on one stream as bench.py
+    does: header = the count, keys and ids == the scan's own sorted results,
+    and a buffer too small keeps its first cap records with the full count
+    in the header (the caller regrows and repacks)."""
+    rng = random.Random(17)
+    blob = vsa.hwlm_build(rand_lits(rng, 400, minlen=3, maxlen=8))
+    host = np.frombuffer(rand_data(rng, 6 << 20), np.uint8).copy()
+    c2 = vsa.Context(share_stream_with=ctx)
+    d = ctx.malloc(len(host))
+    try:
+        ctx.h2d(d, host)
+        offs, lens = [0, 3 << 20, (5 << 20) + 5], [(3 << 20) - 1, 2 << 20, 777000]
+        dbs = [vsa.Database(ctx, blob), vsa.Database(c2, blob)]
+        plans = [ctx.plan(d, offs, lens), c2.plan(d, offs, lens)]
+        want = None
+        for k in range(6):
+            c, db, pl = (ctx, c2)[k % 2], dbs[k % 2], plans[k % 2]
+            n = c.scan_plan(db, pl)
+            got = c.results(n)
+            if want is None:
+                want = got
+            assert np.array_equal(got["key"], want["key"]) and n > 1000
+            for cap in (n + 5, n // 3):
+                buf = c.malloc(8 * (1 + cap) + 4 * cap)
+                c.scan_plan_pack(db, pl, buf, cap)
+                assert c.scan_wait() == n
+                pk = np.zeros(1 + cap + (cap + 1) // 2, np.uint64)
+                c.d2h(pk, buf)
+                c.free(buf)
+                m = min(n, cap)
+                assert int(pk[0]) == n, (k, cap)
+                assert np.array_equal(pk[1:1 + m], want["key"][:m]), (k, cap)
+                assert np.array_equal(pk[1 + cap:].view(np.uint32)[:m], want["id"][:m]), (k, cap)
+        for p_ in plans:
+            p_.close()
+        for db in dbs:
+            db.close()
+    finally:
+        ctx.free(d)
+        c2.close()
+
+
+def test_gpu_crowded_bin_rerun_count():
+    """a first dense scan on a fresh context outgrows the output
+    (out_cap starts at 64 K records) AND crowds a sort bin.  It must rerun
+    once, without bins (2 launches, not 3), and a persistently dense
+    workload backs off: after a crowded binned launch 16 launches (its rerun
+    included) skip the bins, after the next crowded one 64 (bin_backoff).  Every result equals
+    the unsorted scan's records sorted here."""
+    lits = [vsa.HwlmLiteral(b"ab", False, 10 + i) for i in range(80)] + \
+           [vsa.HwlmLiteral(b"bab", False, 5)]
+    rng = random.Random(43)
+    host = np.frombuffer(rand_data(rng, 2 << 20), np.uint8).copy()
+    host[9000:11000] = np.frombuffer(b"ab" * 1000, np.uint8)  # ~80 K records
+    ref = vsa.Context(0)
+    c = vsa.Context(0)
+    try:
+        rdb = vsa.Database(ref, vsa.hwlm_build(lits))
+        db = vsa.Database(c, vsa.hwlm_build(lits))
+        d = c.malloc(len(host))
+        try:
+            c.h2d(d, host)
+            offs, lens = [0, 1 << 20], [1 << 20, (1 << 20) - 5]
+            n0 = ref.scan_blocks(rdb, d, offs, lens, sort=False)
+            assert n0 > 65536
+            raw = ref.results(n0)
+            order = np.argsort(raw["key"], kind="stable")
+            want_k, want_i = raw["key"][order], raw["id"][order]
+            plan = c.plan(d, offs, lens)
+            launches = []
+            for k in range(18):
+                l0 = c.launches()
+                n = c.scan_plan(db, plan)
+                launches.append(c.launches() - l0)
+                got = c.results(n)
+                assert n == n0, k
+                assert np.array_equal(got["key"], want_k), k
+                assert np.array_equal(got["id"], want_i), k
+            # scan 0: binned, crowded + output overflow -> one rerun without
+            # bins (the first of the 16 launches that skip them); scans 1-15
+            # skip them; scan 16 is binned again and crowds again -> one
+            # rerun, and the next 64 launches skip (scan 17)
+            assert launches == [2] + [1] * 15 + [2, 1], launches
+            plan.close()
+        finally:
+            c.free(d)
+            db.close()
+            rdb.close()
+    finally:
+        c.close()
+        ref.close()
 
 
 def test_gpu_overlapping_blocks_dense(ctx):

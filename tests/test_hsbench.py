@@ -313,3 +313,58 @@ def test_cfg5_small_chunks_sequences():
         assert _check_sequences(g, exprs, flags, ids, blocks, hs.MODE_BLOCK) > 2000
     finally:
         g.close()
+
+
+@pytest.mark.gpu
+def test_block_replay_ragged_parallel(monkeypatch):
+    """The parallel block-mode replay (hs_lit.cpp corpus_replay_blocks: the
+    records cut into per-thread ranges at block boundaries, each thread
+    mapping and replaying its own) on ragged blocks -- lengths 0 to 64 KiB,
+    gaps between some, a dense planted set so >= 8 threads get records, the
+    cfg-5-shaped set with shared ids (dedupe and SOM-log paths): every
+    block's count and callback-sequence digest equal the unit path's
+    (VSA_REPLAY_UNITS=1, the round-5 replay) and, for every block, the
+    oracle's (oracle.hs_lit over its own HWLM records of that block)."""
+    import bench
+    exprs, flags, ids = bench.make_mixed_set(10000)
+    lits = [vsa.HwlmLiteral(e, False, i) for i, e in enumerate(exprs)]
+    data = bench.make_corpus(12 << 20, lits, seed=13, plant_every=128)
+    rng = random.Random(5)
+    offs, lens, pos = [], [], 0
+    while True:
+        ln = rng.choice([0, 1, 9, 100, 2048, 16384, 40000, rng.randint(1, 65536)])
+        if pos + ln > len(data):
+            break
+        offs.append(pos)
+        lens.append(ln)
+        pos += ln + rng.choice([0, 0, 0, 7, 1000])
+    db = hs.compile_lit_multi(exprs, flags, ids, hs.MODE_BLOCK)
+    scratch = hs.Scratch(db)
+    ctx = vsa.Context(0)
+    d = ctx.malloc(len(data))
+    try:
+        ctx.h2d(d, data)
+        corpus = hs.Corpus(db, scratch, d, offs, lens, h_data=data)
+        try:
+            rc, tot, cnt, dg = corpus.scan(True, 16, digests=True)
+            assert rc == hs.SUCCESS and tot > 8 * 2048
+            monkeypatch.setenv("VSA_REPLAY_UNITS", "1")
+            rc2, tot2, cnt2, dg2 = corpus.scan(True, 16, digests=True)
+            monkeypatch.delenv("VSA_REPLAY_UNITS")
+            assert rc2 == hs.SUCCESS and tot2 == tot
+            assert np.array_equal(cnt, cnt2) and np.array_equal(dg, dg2)
+            rc3, tot3, cnt3, dg3 = corpus.scan(True, 1, digests=True)
+            assert tot3 == tot and np.array_equal(dg3, dg)
+            odb = ohs.compile_lit_multi(exprs, flags, ids)
+            oblob = vsa.hwlm_build([vsa.HwlmLiteral(t, nc, f, noruns=nr)
+                                    for t, nc, f, nr in odb.hwlm_literals()])
+            for b, (o, ln) in enumerate(zip(offs, lens)):
+                seq = ohs.scan(odb, oblob.ptr, data[o:o + ln].copy()) if ln else []
+                assert (int(cnt[b]), int(dg[b])) == (len(seq), hs.seq_digest(seq)), b
+        finally:
+            corpus.close()
+    finally:
+        ctx.free(d)
+        ctx.close()
+        scratch.close()
+        db.close()

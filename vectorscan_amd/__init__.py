@@ -150,6 +150,8 @@ _sig("vsa_scan_plan", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_v
      ctypes.c_uint32, _u64p)
 _sig("vsa_scan_wait", ctypes.c_int, ctypes.c_void_p, _u64p)
 _sig("vsa_scan_pack", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
+_sig("vsa_scan_plan_pack", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+     ctypes.c_void_p, ctypes.c_uint64)
 _sig("vsa_scan_results", ctypes.c_int, ctypes.c_void_p,
      ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p))
 _sig("vsa_scan_copy", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -161,6 +163,7 @@ _sig("vsa_scan_debug_counters", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)
 _sig("vsa_derive_first_stage", ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
      ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32))
 _sig("vsa_scan_kernel_ms", ctypes.c_double, ctypes.c_void_p)
+_sig("vsa_scan_launches", ctypes.c_uint64, ctypes.c_void_p)
 _sig("vsa_read_ceiling", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
      ctypes.c_uint32, ctypes.POINTER(ctypes.c_double), _u64p)
 _sig("vsa_class_scan", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -761,6 +764,12 @@ class Context:
         collective (queued behind an asynchronous binned scan, no wait)."""
         _check(lib.vsa_scan_pack(self.ptr, d_dst, cap))
 
+    def scan_plan_pack(self, db, plan, d_dst, cap):
+        """vsa_scan_plan_pack: an asynchronous plan scan whose binned sort
+        also writes the records into d_dst in scan_pack's layout (no pack
+        launch); vsa_scan_pack still repacks after a rescan."""
+        _check(lib.vsa_scan_plan_pack(self.ptr, db.ptr, plan.ptr, d_dst, cap))
+
     def results(self, n):
         """Copy the last scan's sorted (key, id) records to the host."""
         out = np.zeros(n, dtype=[("key", np.uint64), ("id", np.uint32), ("pad", np.uint32)])
@@ -787,6 +796,10 @@ class Context:
     def kernel_ms(self):
         """Device time of the last scan kernel (hipEvents on the scan stream)."""
         return lib.vsa_scan_kernel_ms(self.ptr)
+
+    def launches(self):
+        """Literal-scan launches queued on this context (reruns included)."""
+        return lib.vsa_scan_launches(self.ptr)
 
     def read_ceiling(self, d_data, length, runs=5):
         """(GB/s, ms, bytes): this device's streaming-read ceiling over the

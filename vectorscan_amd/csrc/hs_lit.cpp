@@ -687,6 +687,12 @@ struct vsa_hs_corpus {
     std::vector<uint32_t> bstamp, ustamp;
     uint32_t gen = 0;
     vsa_plan_t *plan = nullptr;
+    /* block mode, every block the same length L (the last may be shorter)
+     * and laid back to back from off0 (hsbench's fixed-size chunks): the
+     * block of an end is (end - off0) / L, no search */
+    bool uniform = false;
+    uint64_t off0 = 0, ulen = 0;
+    std::vector<uint32_t> empty; /* zero-length blocks (not in `order`) */
 };
 
 int vsa_hs_corpus_prepare(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch,
@@ -757,6 +763,16 @@ int vsa_hs_corpus_prepare(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch
         c->so.push_back(offsets[b]);
         c->se.push_back(offsets[b] + lens[b]);
     }
+    if (!c->streams) {
+        for (uint32_t b = 0; b < nblocks; b++)
+            if (!lens[b]) c->empty.push_back(b);
+        c->uniform = nblocks > 0 && c->empty.empty() && lens[0] > 0;
+        for (uint32_t b = 0; c->uniform && b < nblocks; b++)
+            c->uniform = offsets[b] == offsets[0] + (uint64_t)b * lens[0] &&
+                         (lens[b] == lens[0] || (b + 1 == nblocks && lens[b] < lens[0]));
+        c->off0 = nblocks ? offsets[0] : 0;
+        c->ulen = nblocks ? lens[0] : 0;
+    }
     c->rb.assign(nblocks, 0);
     c->re.assign(nblocks, 0);
     c->bstamp.assign(nblocks, 0);
@@ -779,6 +795,163 @@ int vsa_hs_corpus_free(vsa_hs_corpus_t *c) {
     return VSA_HS_SUCCESS;
 }
 
+/* Block mode (a unit is one block): the records, sorted by end, are cut
+ * into T contiguous ranges at block boundaries and each thread maps AND
+ * replays its own range -- no serial record-to-block pass, and each thread
+ * zeroes the counts / digests of the blocks between its first and the next
+ * thread's first (positions in `order`), so blocks without records cost one
+ * store each, in parallel.  Same results as the unit path: every block is
+ * an independent hs_scan. */
+static int corpus_replay_blocks(vsa_hs_corpus *cp, uint64_t *keys, const uint32_t *ids,
+                                uint64_t nm, uint64_t *counts, uint64_t *digests,
+                                uint64_t *total, unsigned threads) {
+    const auto t_start = std::chrono::steady_clock::now();
+    const vsa_hs_database *db = cp->db;
+    vsa_db_t *ddb = device_db(cp->scratch, db);
+    const uint64_t *lens = cp->lens.data();
+    const auto &so = cp->so, &se = cp->se;
+    const size_t npos = so.size();
+    *total = 0;
+    for (uint32_t b : cp->empty) {
+        if (counts) counts[b] = 0;
+        if (digests) digests[b] = 0;
+    }
+    /* the position in `order` of the block holding end e, searching
+     * forward from `at` (the previous record's position); npos = none */
+    auto pos_of = [&](uint64_t e, size_t at) -> size_t {
+        if (cp->uniform) {
+            if (e < cp->off0) return npos;
+            const uint64_t p = (e - cp->off0) / cp->ulen;
+            return p < npos && e < se[p] ? (size_t)p : npos;
+        }
+        size_t lo = at, step = 1;
+        while (lo + step < npos && so[lo + step] <= e) {
+            lo += step;
+            step <<= 1;
+        }
+        const size_t oi = (size_t)(std::upper_bound(so.begin() + lo,
+                                                    so.begin() + std::min(npos, lo + step), e) -
+                                   so.begin());
+        return oi && e < se[oi - 1] ? oi - 1 : npos;
+    };
+    /* a thread per ~2k records (thread start-up costs more than replaying a
+     * few hundred) */
+    const unsigned T = (unsigned)std::max<uint64_t>(
+        1, std::min<uint64_t>({threads ? threads : 1u, 1 + nm / 2048, npos ? npos : 1}));
+    /* range t = records [kt[t], kt[t + 1]), block positions [pt[t], pt[t + 1]) */
+    std::vector<uint64_t> kt(T + 1, nm);
+    std::vector<size_t> pt(T + 1, npos);
+    kt[0] = 0;
+    pt[0] = 0;
+    for (unsigned t = 1; t < T; t++) {
+        uint64_t k = std::max(kt[t - 1], nm * t / T);
+        size_t p = npos;
+        for (; k < nm; k++) {
+            const uint64_t e = keys[k] >> KEY_END_SHIFT;
+            const size_t lo = (size_t)(std::upper_bound(so.begin(), so.end(), e) - so.begin());
+            p = lo && e < se[lo - 1] ? lo - 1 : npos;
+            if (p != npos) break;
+        }
+        if (p == npos || p < pt[t - 1]) { /* the rest belongs to range t - 1 */
+            for (unsigned u = t; u < T; u++) {
+                kt[u] = nm;
+                pt[u] = npos;
+            }
+            break;
+        }
+        /* back to the block's first record */
+        kt[t] = (uint64_t)(std::lower_bound(keys + kt[t - 1], keys + k,
+                                            (uint64_t)so[p] << KEY_END_SHIFT) - keys);
+        pt[t] = p;
+    }
+    std::vector<uint64_t> part(T, 0);
+    std::vector<int> status(T, VSA_HS_SUCCESS);
+    std::vector<double> busy(T, 0.0);
+    using clk = std::chrono::steady_clock;
+    const auto t_split = clk::now();
+    const uint8_t *h_data = cp->h_data;
+    auto work = [&](unsigned t) {
+        const auto w0 = clk::now();
+        for (size_t p = pt[t]; p < pt[t + 1]; p++) {
+            const uint32_t b = cp->order[p];
+            if (counts) counts[b] = 0;
+            if (digests) digests[b] = 0;
+        }
+        vsa_hs_stream st;
+        init_stream(&st, db);
+        std::vector<uint32_t> touched;
+        const uint8_t *buf = nullptr;
+        size_t blen = 0;
+        SeqDigest dg;
+        uint64_t &cnt = dg.cnt;
+        Run r{db, &st, digests ? digest_match : count_match, digests ? (void *)&dg : (void *)&cnt,
+              &buf, &blen, {0}, 0};
+        r.touched = &touched;
+        size_t at = pt[t];
+        uint64_t k = kt[t];
+        const uint64_t k_end = kt[t + 1];
+        while (k < k_end) {
+            const uint64_t e = keys[k] >> KEY_END_SHIFT;
+            const size_t p = pos_of(e, at);
+            if (p == npos) { /* outside every block: not reported */
+                k++;
+                continue;
+            }
+            at = p;
+            const uint32_t b = cp->order[p];
+            const uint64_t o = so[p], hi = se[p];
+            const uint64_t k0 = k;
+            while (k < k_end && (keys[k] >> KEY_END_SHIFT) < hi) {
+                keys[k] -= o << KEY_END_SHIFT;
+                k++;
+            }
+            /* a fresh hs_scan of block b: the previous block's exhaustion
+             * keys reset, nothing else carried */
+            for (uint32_t x : touched) st.exhausted[x] = 0;
+            touched.clear();
+            cnt = 0;
+            dg.h = 0;
+            buf = h_data ? h_data + o : nullptr;
+            blen = lens[b];
+            r.last_to = ~0ULL;
+            r.at_to.clear();
+            r.som_log.clear();
+            r.terminated = false;
+            if (vsa::replay_records(ddb, keys + k0, ids + k0, k - k0, on_fragment, &r) !=
+                HWLM_SUCCESS) {
+                status[t] = VSA_HS_UNKNOWN_ERROR;
+                return;
+            }
+            flush_som(r);
+            if (counts) counts[b] = cnt;
+            if (digests) digests[b] = dg.h;
+            part[t] += cnt;
+        }
+        busy[t] = std::chrono::duration<double, std::milli>(clk::now() - w0).count();
+    };
+    if (T == 1) work(0);
+    else replay_pool().run(T, work);
+    static const bool timing = getenv("VSA_HOST_TIMING") != nullptr;
+    if (timing) {
+        double mx = 0, sum = 0;
+        for (double x : busy) {
+            mx = std::max(mx, x);
+            sum += x;
+        }
+        fprintf(stderr, "corpus_replay_blocks: %u threads, %llu records, %zu blocks: split %.3f ms, "
+                "replay %.3f ms (thread busy max %.3f, mean %.3f ms)\n", T,
+                (unsigned long long)nm, npos,
+                std::chrono::duration<double, std::milli>(t_split - t_start).count(),
+                std::chrono::duration<double, std::milli>(clk::now() - t_split).count(), mx,
+                sum / T);
+    }
+    for (unsigned t = 0; t < T; t++) {
+        if (status[t] != VSA_HS_SUCCESS) return status[t];
+        *total += part[t];
+    }
+    return VSA_HS_SUCCESS;
+}
+
 /* The records of one corpus scan (sorted by d_data end offset; keys are
  * rebased to their block in place) through the report program on
  * `threads` host threads: per-block counts / sequence digests (optional)
@@ -786,6 +959,8 @@ int vsa_hs_corpus_free(vsa_hs_corpus_t *c) {
 static int corpus_replay(vsa_hs_corpus *cp, uint64_t *keys, const uint32_t *ids, uint64_t nm,
                          uint64_t *counts, uint64_t *digests, uint64_t *total,
                          unsigned threads) {
+    if (!cp->streams && !getenv("VSA_REPLAY_UNITS"))
+        return corpus_replay_blocks(cp, keys, ids, nm, counts, digests, total, threads);
     const auto t_start = std::chrono::steady_clock::now();
     const vsa_hs_database *db = cp->db;
     vsa_db_t *ddb = device_db(cp->scratch, db);

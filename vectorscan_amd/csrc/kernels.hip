@@ -1664,11 +1664,13 @@ vsa_lit_scan(VsaLitParams P) {
                                   mis, slots, pqx + (size_t)cw * PQ_ENTRIES(2), cw, NC,
                                   prof_lds + 8 * cw, dg);
         {
-            /* the last confirm wave out stores the owned bins' counts (every
-             * confirm wave's LDS adds precede its own add here) */
+            /* the last confirm wave out stores the owned bins' counts: the
+             * acq_rel add orders every confirm wave's LDS adds (lbins, nrec;
+             * nrec's add returns nothing and nothing else waits on it) before
+             * its own, and the last wave's reads after all of them */
             u32 prev = 0;
             if (lane == 0)
-                prev = __hip_atomic_fetch_add(&conf_fin, 1u, __ATOMIC_RELAXED,
+                prev = __hip_atomic_fetch_add(&conf_fin, 1u, __ATOMIC_ACQ_REL,
                                               __HIP_MEMORY_SCOPE_WORKGROUP);
             if (readfirstlane_u32(prev) + 1 == NC) {
                 const u32 lo = cl.lb_lo, n = cl.lb_n;
@@ -2248,9 +2250,17 @@ __device__ __forceinline__ void publish_body(unsigned long long *ctr, unsigned l
 __device__ __forceinline__ void publish_wave(unsigned long long *ctr, unsigned long long *h,
                                              unsigned long long seq, uint32_t nzero,
                                              const unsigned long long *fb = nullptr,
-                                             unsigned long long *hfb = nullptr, u32 nfb = 0) {
+                                             unsigned long long *hfb = nullptr, u32 nfb = 0,
+                                             uint64_t *pk = nullptr, uint64_t out_cap = 0) {
     const u32 l = lane_id();
     const unsigned long long v = l < 16 ? ctr[l] : 0ULL;
+    if (pk && l == 0) {
+        /* the packed collective buffer's header (vsa_pack's rule): the
+         * count, bit 62 when the records are not final -- the output
+         * overflowed or a crowded bin left them to a rescan */
+        const unsigned long long ovf = ctr[VSA_CTR_BIN_OVERFLOW];
+        pk[0] = v | ((v > out_cap || ovf) ? (1ULL << 62) : 0ULL);
+    }
     /* the scan's schedule-feedback record (device memory) rides along to
      * the host, before the sequence store releases it */
     for (u32 i = l; i < nfb; i += WAVE) hfb[i] = fb[i];
@@ -2303,7 +2313,8 @@ __global__ void __launch_bounds__(1024) vsa_bin_finish(const uint32_t *counts, u
                                                      unsigned long long *h,
                                                      unsigned long long seq,
                                                      const unsigned long long *fb,
-                                                     unsigned long long *hfb, uint32_t nfb) {
+                                                     unsigned long long *hfb, uint32_t nfb,
+                                                     uint64_t *pk, uint64_t pk_cap) {
     __shared__ u32 red[16], cnt[FIN_BINS], off[FIN_BINS];
     const u32 t = threadIdx.x, wv = t / WAVE, lane = lane_id();
     const u32 b0 = blockIdx.x * FIN_BINS;
@@ -2330,7 +2341,7 @@ __global__ void __launch_bounds__(1024) vsa_bin_finish(const uint32_t *counts, u
         off[lane] = base + e;
     }
     __syncthreads();
-    if (blockIdx.x == 0 && wv == 0) publish_wave(ctr, h, seq, 144u, fb, hfb, nfb);
+    if (blockIdx.x == 0 && wv == 0) publish_wave(ctr, h, seq, 144u, fb, hfb, nfb, pk, out_cap);
     /* this wave's 4 bins */
     const u32 lb = wv * 4;
     u32 m[4], mmax = 0;
@@ -2389,6 +2400,13 @@ __global__ void __launch_bounds__(1024) vsa_bin_finish(const uint32_t *counts, u
             if (o < out_cap) {
                 okeys[o] = kk;
                 oids[o] = ii;
+            }
+            /* fused vsa_pack (vsa_scan_plan_pack): the records also go
+             * straight into the collective's buffer [header | keys (pk_cap)
+             * | ids (pk_cap x u32)], no pack launch behind this one */
+            if (pk && o < pk_cap) {
+                pk[1 + o] = kk;
+                ((uint32_t *)(pk + 1 + pk_cap))[o] = ii;
             }
         }
     }

@@ -50,7 +50,7 @@ __global__ void vsa_bin_finish(const uint32_t *counts, uint32_t *counts_next,
                                unsigned long long *ctr,
                                unsigned long long *h, unsigned long long seq,
                                const unsigned long long *fb, unsigned long long *hfb,
-                               uint32_t nfb);
+                               uint32_t nfb, uint64_t *pk, uint64_t pk_cap);
 __global__ void vsa_class_scan_lut(VsaClassParams P, uint64_t span);
 __global__ void vsa_publish(unsigned long long *ctr, unsigned long long *h, unsigned long long seq,
                             uint32_t nzero, const uint64_t *keys, const uint32_t *ids,
@@ -178,6 +178,11 @@ struct vsa_ctx {
          * itself (launch_lit: start on the first kernel, stop on the last
          * of split passes); null = untimed */
         hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+        /* vsa_scan_plan_pack: the binned sort also writes the records into
+         * this collective buffer (vsa_pack's layout), for the next launch
+         * only */
+        void *pack_dst = nullptr;
+        uint64_t pack_cap = 0;
     } launch;
     /* kernel-only timing of the last scan (hipEvents on the scan stream) */
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -185,6 +190,12 @@ struct vsa_ctx {
     hipEvent_t ev_rec = nullptr;  /* records_fetch_async's copies done */
     double last_kernel_ms = 0.0;
     uint32_t bin_skip = 0;   /* launches left without the binned sort */
+    /* the bin_skip a crowded bin sets: 16, x4 for every crowded binned
+     * launch in a row (up to 4096), back to 16 after a binned launch that
+     * fit: a persistently dense workload pays the rerun (finish_scan) about
+     * once per 4096 launches instead of once per 17 */
+    uint32_t bin_backoff = 16;
+    uint64_t lit_launches = 0; /* literal-scan launches queued (vsa_scan_launches) */
     bool bins_clean[2] = {false, false}; /* bin count buffer b is zero (no memset) */
     uint32_t bin_par = 0;                /* the count buffer the next binned scan uses */
     /* host bytes already in ws.d_in (set only inside one drop-in call, so the
@@ -419,6 +430,13 @@ int ensure_tables(vsa_ctx *c, uint32_t nb, uint64_t nsegs, bool keep_blocks = fa
     return VSA_OK;
 }
 
+/* Each launch is checked with hipGetLastError() right after it.  That call
+ * returns (and clears) the thread's last error from ANY earlier HIP call,
+ * including ignored statuses of free / destroy paths or another library's
+ * calls on this thread, so the stale value is dropped immediately before the
+ * launch: the check after it then sees this launch's error only. */
+inline void drop_stale_error() { (void)hipGetLastError(); }
+
 int env_int(const char *name, int dflt) {
     const char *e = getenv(name);
     return e ? atoi(e) : dflt;
@@ -475,6 +493,7 @@ int launch_lit(vsa_ctx *c, const VsaLitParams &P, size_t lds) {
     hipEvent_t e1 = P.end_par == 1 ? nullptr : c->launch.ev_stop; /* split: the 2nd pass */
     c->launch.ev_start = nullptr;
     if (e1) c->launch.ev_stop = nullptr;
+    drop_stale_error();
     hipExtLaunchKernelGGL(fn, dim3(grid), dim3(LIT_THREADS), (uint32_t)lds, c->stream, e0, e1, 0u,
                           P);
     VSA_CHECK(hipGetLastError());
@@ -553,12 +572,18 @@ int queue_bin_sort(vsa_ctx *c) {
     Workspace &w = c->ws;
     const uint32_t par = c->bin_par;
     const bool fbd = c->fb.armed >= 0 && c->fb.dev;
+    drop_stale_error();
     hipLaunchKernelGGL(vsa_bin_finish, dim3(VSA_SORT_BINS / 64), dim3(1024), 0, c->stream,
                        bin_counts_of(c, par), bin_counts_of(c, par ^ 1u), bstage_keys(w),
                        bstage_ids(w), w.d_keys[1], w.d_ids[1], (uint64_t)w.out_cap,
                        c->ws.d_counters, c->ws.d_pub, (unsigned long long)++c->pub_seq,
                        fbd ? c->fb.d_rec : nullptr, fbd ? c->fb.d : nullptr,
-                       fbd ? 2 * c->fb.grid : 0u);
+                       fbd ? 2 * c->fb.grid : 0u, (uint64_t *)c->launch.pack_dst,
+                       c->launch.pack_cap);
+    /* the pack buffer is filled by this launch only: a rescan (complete_scan)
+     * must not write into a buffer a collective may be reading; the caller
+     * repacks after it (vsa_scan_pack) */
+    c->launch.pack_dst = nullptr;
     VSA_CHECK(hipGetLastError());
     c->bins_clean[par ^ 1u] = true;
     c->bin_par = par ^ 1u;
@@ -706,10 +731,12 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
     c->launch.ev_start = small ? nullptr : c->ev0;
     c->launch.ev_stop = small ? nullptr : c->ev1;
     arm_feedback(c, fb_set_of(db), c->launch.grid, c->launch.bytes, small);
+    c->lit_launches++;
     int r = launch_scan_kernel(c, db, d_data, nb, nsegs);
     c->launch.ev_start = c->launch.ev_stop = nullptr;
     if (r != VSA_OK) return r;
     if (small) {
+        drop_stale_error();
         hipLaunchKernelGGL(vsa_publish, dim3(1), dim3(256), 0, c->stream, c->ws.d_counters,
                            c->ws.d_pub, (unsigned long long)++c->pub_seq, 144u,
                            (const uint64_t *)c->ws.d_keys[0], (const uint32_t *)c->ws.d_ids[0],
@@ -908,21 +935,26 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
          * thread's last error for the next launch check */
         (void)hipGetLastError();
     }
-    if (n > w.out_cap) return VSA_E_OVERFLOW;
+    if (c->bin_skip) c->bin_skip--;
+    /* A crowded bin (> VSA_SORT_BIN_MAX records): the launch's records exist
+     * only in the bins, so it runs again without them (complete_scan), and
+     * the next launches (likely as dense) skip them too, for longer after
+     * each crowded binned launch in a row (bin_backoff).  Checked before the
+     * output overflow, so a launch that both crowded a bin and outgrew the
+     * output (a first dense scan on a fresh context: out_cap starts at 64 K)
+     * runs once more, without bins, not twice. */
+    const bool crowded = c->launch.dev_sort && w.h_counters[VSA_CTR_BIN_OVERFLOW];
+    if (crowded) {
+        c->bin_skip = c->bin_backoff;
+        c->bin_backoff = std::min<uint32_t>(4096u, c->bin_backoff * 4u);
+    } else if (c->launch.dev_sort) {
+        c->bin_backoff = 16;
+    }
+    if (crowded || n > w.out_cap) return VSA_E_OVERFLOW;
     c->cur = 0;
     /* internal: a few records are sorted by the host caller after its copy
      * (the device sort's launches cost more than sorting them there) */
     c->host_sort = (flags & SCAN_HOST_SORT_SMALL) && n <= HOST_SORT_MAX;
-    /* a launch whose records crowd one bin sorts with the library; the next
-     * few launches (likely as dense) skip the histogram */
-    if (c->bin_skip) c->bin_skip--;
-    if (c->launch.dev_sort && w.h_counters[VSA_CTR_BIN_OVERFLOW]) {
-        /* a crowded bin: the launch's records exist only in the bins, so
-         * it runs again without them (complete_scan), and the next few
-         * launches (likely as dense) skip them too */
-        c->bin_skip = 16;
-        return VSA_E_OVERFLOW;
-    }
     if (c->launch.dev_sort) {
         /* sorted by the binned sort queued in launch_scan, into buffer 1
          * (a single record too: buffer 0 is not written in this mode) */
@@ -1727,6 +1759,7 @@ int64_t pair_host(const uint8_t *lo1, const uint8_t *hi1, const uint8_t *lo2,
     P.first = first;
     uint64_t want = (len + 255) / 256;
     uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * 4));
+    drop_stale_error();
     hipLaunchKernelGGL(vsa_pair_scan, dim3(grid), dim3(256), 0, c->stream, P);
     if (hipGetLastError() != hipSuccess) return -2;
     if (hipMemcpyAsync(w.h_counters + PAIR_BASE, first, 48 * 8, hipMemcpyDeviceToHost,
@@ -1842,6 +1875,8 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (c->ev_rec) (void)hipEventDestroy(c->ev_rec);
     if (t_ctx == c) t_ctx = nullptr;
     delete c; /* drops its hold on the stream */
+    /* the statuses ignored above must not fail a later launch check */
+    (void)hipGetLastError();
     return VSA_OK;
 }
 
@@ -2334,6 +2369,7 @@ int vsa_scan_pack(vsa_ctx_t *c, void *d_dst, uint64_t cap) {
     if (c->pending && c->launch.published && c->launch.dev_sort) {
         /* the async binned scan's sorted records (buffer 1) and the counters
          * vsa_publish keeps on the device: queued behind it, no wait */
+        drop_stale_error();
         hipLaunchKernelGGL(vsa_pack, dim3(grid), dim3(256), 0, c->stream,
                            (const unsigned long long *)c->ws.d_counters + 144,
                            (uint64_t)c->ws.out_cap, (const uint64_t *)c->ws.d_keys[1],
@@ -2347,6 +2383,7 @@ int vsa_scan_pack(vsa_ctx_t *c, void *d_dst, uint64_t cap) {
     unsigned long long *save = c->ws.d_counters + 144;
     unsigned long long hv[16] = {c->last_n, 0};
     VSA_CHECK(hipMemcpyAsync(save, hv, sizeof(hv), hipMemcpyHostToDevice, c->stream));
+    drop_stale_error();
     hipLaunchKernelGGL(vsa_pack, dim3(grid), dim3(256), 0, c->stream,
                        (const unsigned long long *)save, (uint64_t)c->ws.out_cap,
                        (const uint64_t *)c->ws.d_keys[c->cur], (const uint32_t *)c->ws.d_ids[c->cur],
@@ -2407,6 +2444,8 @@ int vsa_scan_debug_counters(vsa_ctx_t *c, uint64_t out[16]) {
 
 double vsa_scan_kernel_ms(vsa_ctx_t *c) { return c ? c->last_kernel_ms : 0.0; }
 
+uint64_t vsa_scan_launches(vsa_ctx_t *c) { return c ? c->lit_launches : 0; }
+
 /* The box's streaming-read ceiling over a device buffer (bench.py's
  * roofline.peak_measured): vsa_read_probe reads the first len & ~64 KiB
  * bytes once per run on the ctx stream; best of `runs` (hipEvents) after
@@ -2414,8 +2453,11 @@ double vsa_scan_kernel_ms(vsa_ctx_t *c) { return c ? c->last_kernel_ms : 0.0; }
 int vsa_read_ceiling(vsa_ctx_t *c, const uint8_t *d_data, uint64_t len, uint32_t runs,
                      double *best_ms, uint64_t *bytes) {
     if (!c || !d_data || !best_ms || !runs) return VSA_E_INVALID;
+    /* the probe reads 16-byte words (vsa_class_scan checks the same) */
+    if ((uintptr_t)d_data & 15) return VSA_E_INVALID;
     const uint64_t n = len & ~((uint64_t)(64 << 10) - 1);
     if (!n) return VSA_E_INVALID;
+    VSA_CHECK(hipSetDevice(c->device)); /* the sink goes on the context's device */
     uint32_t *sink = nullptr;
     VSA_CHECK(hipMalloc(&sink, 64));
     hipEvent_t e0, e1;
@@ -2429,6 +2471,7 @@ int vsa_read_ceiling(vsa_ctx_t *c, const uint8_t *d_data, uint64_t len, uint32_t
     for (uint32_t r = 0; r <= runs && e == hipSuccess; r++) {
         e = hipEventRecord(e0, c->stream);
         if (e != hipSuccess) break;
+        drop_stale_error();
         hipLaunchKernelGGL(vsa_read_probe, dim3(c->num_cus), dim3(1024), 0, c->stream, d_data, n,
                            sink);
         if ((e = hipGetLastError()) != hipSuccess) break;
@@ -2511,6 +2554,7 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
         /* large buffers: pair-LUT kernel, one 1024-thread workgroup per CU,
          * an equal 4 KiB-aligned share per workgroup, taken by its waves in
          * 4 KiB groups (kernels.hip vsa_class_scan_lut) */
+        drop_stale_error();
         hipExtLaunchKernelGGL(vsa_class_scan_lut, dim3(lgrid), dim3(1024), 0u, c->stream, c->ev0,
                               c->ev1, 0u, P, wspan);
     } else {
@@ -2518,6 +2562,7 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
         uint64_t want = (chunks + 255) / 256;
         uint64_t cap = (uint64_t)c->num_cus * 8;
         uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
+        drop_stale_error();
         hipExtLaunchKernelGGL(vsa_class_scan, dim3(grid), dim3(256), 0u, c->stream, c->ev0, c->ev1,
                               0u, P);
     }
@@ -3352,6 +3397,24 @@ int vsa_scan_plan(vsa_ctx_t *c, const vsa_db_t *db, const vsa_plan_t *p, uint32_
     return launch_planned(c, db, p->d_data, p->d_blocks, p->d_segblk, p->nb, p->segs,
                           p->grid, p->end_bits, p->bytes, flags,
                           n_matches ? n_matches : &dummy);
+}
+
+int vsa_scan_plan_pack(vsa_ctx_t *c, const vsa_db_t *db, const vsa_plan_t *p, void *d_dst,
+                       uint64_t cap) {
+    if (!c || !db || !p || !d_dst || p->ctx != c) return VSA_E_INVALID;
+    if (int r0 = finish_pending(c)) return r0;
+    if (int r1 = refresh_plan(c, db, const_cast<vsa_plan *>(p))) return r1;
+    c->launch.pack_dst = d_dst;
+    c->launch.pack_cap = cap;
+    uint64_t n = 0;
+    int r = launch_planned(c, db, p->d_data, p->d_blocks, p->d_segblk, p->nb, p->segs, p->grid,
+                           p->end_bits, p->bytes, VSA_SCAN_ASYNC, &n);
+    /* not consumed (no segments, or a launch without the binned sort): the
+     * records are packed the separate way, after the host completes it */
+    const bool fused = c->launch.pack_dst == nullptr && c->pending;
+    c->launch.pack_dst = nullptr;
+    if (r != VSA_OK) return r;
+    return fused ? VSA_OK : vsa_scan_pack(c, d_dst, cap);
 }
 
 void vsa_get_scratch_core_info(long *buf_off, long *hbuf_off, long *hlen_off) {

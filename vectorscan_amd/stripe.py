@@ -214,7 +214,8 @@ class PackedGather:
                       for _ in range(self.world)] if self.rank == self.root else None)
 
     def _once(self, pack, wait):
-        pack(self.pk_dev, self.cap)
+        if pack is not None:  # None: the scan filled pk_dev itself (scan_plan_pack)
+            pack(self.pk_dev, self.cap)
         if wait is not None:
             wait()
         if self.stage:
@@ -228,7 +229,9 @@ class PackedGather:
         return self.finish(pack, wait, complete)
 
     def start(self, pack, wait=None):
-        """queue the pack and both collectives (nothing is read on the host)"""
+        """queue the pack and both collectives (nothing is read on the host);
+        pack None: the buffer (pk_dev, cap) is already being filled on the
+        device stream `wait` orders the collectives after"""
         self._once(pack, wait)
 
     def finish(self, pack, wait=None, complete=None):
