@@ -25,11 +25,25 @@ $(CSRC)/hs_lit.o: $(CSRC)/hs_lit.cpp $(CSRC)/hs_layout.h $(CSRC)/vsa_internal.h 
 $(CSRC)/kernels.o: $(CSRC)/kernels.hip $(CSRC)/kernels.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(CSRC)/runtime.o: $(CSRC)/runtime.hip $(CSRC)/kernels.h $(CSRC)/hs_layout.h \
-                   $(CSRC)/vsa_internal.h include/vectorscan_amd.h
+RT_DEPS := $(CSRC)/runtime_internal.h $(CSRC)/kernels.h $(CSRC)/hs_layout.h \
+           $(CSRC)/vsa_internal.h include/vectorscan_amd.h
+
+# the host runtime: core, launch plans, drop-ins, batcher (runtime_internal.h)
+$(CSRC)/runtime.o: $(CSRC)/runtime.hip $(RT_DEPS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(CSRC)/compile.o $(CSRC)/flood.o $(CSRC)/hs_lit.o $(CSRC)/kernels.o $(CSRC)/runtime.o
+$(CSRC)/plan.o: $(CSRC)/plan.hip $(RT_DEPS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/dropin.o: $(CSRC)/dropin.hip $(RT_DEPS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/batcher.o: $(CSRC)/batcher.hip $(RT_DEPS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+RT_OBJS := $(CSRC)/runtime.o $(CSRC)/plan.o $(CSRC)/dropin.o $(CSRC)/batcher.o
+
+$(LIB): $(CSRC)/compile.o $(CSRC)/flood.o $(CSRC)/hs_lit.o $(CSRC)/kernels.o $(RT_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
 
 $(ORACLE): oracle/oracle.c

@@ -585,7 +585,7 @@ def test_gpu_crowded_bin_plans(ctx):
                         # not ready; the host completes (rescan without
                         # bins) and repacks
                         cap = n0 + 16
-                        buf = fresh.malloc(8 * (1 + cap) + 4 * cap)
+                        buf = fresh.malloc(8 * (1 + cap + (cap + 1) // 2))
                         fresh.scan_plan_pack(db, plan, buf, cap)
                         n = fresh.scan_wait()
                         hdr = np.zeros(1, np.uint64)
@@ -651,7 +651,7 @@ def test_gpu_plan_pack_fused(ctx):
                 want = got
             assert np.array_equal(got["key"], want["key"]) and n > 1000
             for cap in (n + 5, n // 3):
-                buf = c.malloc(8 * (1 + cap) + 4 * cap)
+                buf = c.malloc(8 * (1 + cap + (cap + 1) // 2))
                 c.scan_plan_pack(db, pl, buf, cap)
                 assert c.scan_wait() == n
                 pk = np.zeros(1 + cap + (cap + 1) // 2, np.uint64)

@@ -5,7 +5,9 @@ report_lo, sorted records, count read back), after a clock settle, then K
 timed steps, both one step at a time ("sync") and pipelined over two
 contexts as bench.py does ("pipe").  One JSON line per N and mode: step ms,
 kernel ms, step - kernel.  The collectives are not part of this (one GPU):
-they are what an N-rank run adds.
+they are what an N-rank run adds.  Modes pack2 / pack1: the pipelined step
+with the records packed into the collective buffer by a separate vsa_pack
+launch / by the sort launch itself (vsa_scan_plan_pack).
   python tools/exp_stripes.py [steps] [warmup]"""
 import json
 import os
@@ -39,7 +41,9 @@ for n in (1, 2, 4, 8):
     plans = [c.plan(dptr, offs, lens, None, None, rlos) for c in ctxs]
     for _ in range(60):  # clock settle + warm
         ctxs[0].scan_plan(db, plans[0])
-    for mode in ("sync", "pipe"):
+    cap = 1 << 16
+    bufs = [torch.zeros(1 + cap + (cap + 1) // 2, dtype=torch.int64, device=dev) for _ in ctxs]
+    for mode in ("sync", "pipe", "pack2", "pack1"):
         ks, counts = [], []
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -47,6 +51,26 @@ for n in (1, 2, 4, 8):
             for _ in range(steps):
                 counts.append(ctxs[0].scan_plan(db, plans[0]))
                 ks.append(ctxs[0].kernel_ms())
+        elif mode.startswith("pack"):
+            # a rank's step as bench.py's N > 1 path queues it, minus the
+            # collectives: pipelined scans whose records go into the
+            # collective buffer -- pack2 by a vsa_pack launch behind the
+            # sort (scan_plan + scan_pack, round 5), pack1 by the sort itself
+            # (scan_plan_pack)
+            for k in range(steps):
+                c, pl, bf = ctxs[k % 2], plans[k % 2], bufs[k % 2]
+                if mode == "pack2":
+                    c.scan_plan(db, pl, asynchronous=True)
+                    c.scan_pack(bf.data_ptr(), cap)
+                else:
+                    c.scan_plan_pack(db, pl, bf.data_ptr(), cap)
+                if k:
+                    counts.append(ctxs[(k - 1) % 2].scan_wait())
+                    ks.append(ctxs[(k - 1) % 2].kernel_ms())
+            counts.append(ctxs[(steps - 1) % 2].scan_wait())
+            ks.append(ctxs[(steps - 1) % 2].kernel_ms())
+            hdr = [int(b[0].item()) for b in bufs]
+            assert all(h == counts[-1] for h in hdr), (hdr, counts[-1])
         else:
             for k in range(steps):
                 ctxs[k % 2].scan_plan(db, plans[k % 2], asynchronous=True)
