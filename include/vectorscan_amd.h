@@ -198,6 +198,14 @@ int vsa_ctx_destroy(vsa_ctx_t *ctx);
  * using it is destroyed. */
 int vsa_ctx_create_shared(vsa_ctx_t *base, vsa_ctx_t **ctx);
 void *vsa_ctx_stream(vsa_ctx_t *ctx);
+/* Leave n CUs free of the literal scan's persistent grid (one 1024-thread
+ * workgroup per CU that fills the register file): plans built afterwards on
+ * this context (per-call ones, and vsa_plan_create's) use num_cus - n
+ * workgroups, so a kernel on another stream -- a multi-GPU step's RCCL
+ * collective of the previous step -- finds a CU while the next scan runs
+ * instead of queueing behind it.  Shared contexts inherit the value of the
+ * context they are made from.  0 (default) uses every CU. */
+int vsa_ctx_set_reserved_cus(vsa_ctx_t *ctx, int n);
 
 /* Upload an HWLM blob (reference layout, 64-byte aligned host copy). */
 int vsa_db_load(vsa_ctx_t *ctx, const void *hwlm, size_t size, vsa_db_t **db);

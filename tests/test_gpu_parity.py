@@ -670,6 +670,47 @@ def test_gpu_plan_pack_fused(ctx):
         c2.close()
 
 
+def test_gpu_reserved_cus_same_records():
+    """vsa_ctx_set_reserved_cus (bench.py's multi-GPU steps leave CUs free
+    for the collectives): plans on a context with 1 or 7 CUs reserved --
+    per-call and prebuilt, and a shared context inheriting the reserve --
+    give the same sorted records as the full grid."""
+    rng = random.Random(23)
+    blob = vsa.hwlm_build(rand_lits(rng, 700, minlen=3, maxlen=8))
+    host = np.frombuffer(rand_data(rng, 9 << 20), np.uint8).copy()
+    full = vsa.Context(0)
+    try:
+        d = full.malloc(len(host))
+        try:
+            full.h2d(d, host)
+            offs, lens = [0, 5 << 20, (7 << 20) + 3], [5 << 20, 2 << 20, (2 << 20) - 9]
+            db = vsa.Database(full, blob)
+            want = full.results(full.scan_blocks(db, d, offs, lens))
+            assert len(want) > 1000
+            for r in (1, 7):
+                c = vsa.Context(0)
+                c.reserve_cus(r)
+                c2 = vsa.Context(share_stream_with=c)
+                try:
+                    cdb = vsa.Database(c, blob)
+                    got = c.results(c.scan_blocks(cdb, d, offs, lens))
+                    assert np.array_equal(got["key"], want["key"]), r
+                    assert np.array_equal(got["id"], want["id"]), r
+                    pl = c2.plan(d, offs, lens)
+                    got2 = c2.results(c2.scan_plan(cdb, pl))
+                    assert np.array_equal(got2["key"], want["key"]), r
+                    pl.close()
+                    cdb.close()
+                finally:
+                    c2.close()
+                    c.close()
+            db.close()
+        finally:
+            full.free(d)
+    finally:
+        full.close()
+
+
 def test_gpu_crowded_bin_rerun_count():
     """a first dense scan on a fresh context outgrows the output
     (out_cap starts at 64 K records) AND crowds a sort bin.  It must rerun

@@ -7,7 +7,10 @@ contexts as bench.py does ("pipe").  One JSON line per N and mode: step ms,
 kernel ms, step - kernel.  The collectives are not part of this (one GPU):
 they are what an N-rank run adds.  Modes pack2 / pack1: the pipelined step
 with the records packed into the collective buffer by a separate vsa_pack
-launch / by the sort launch itself (vsa_scan_plan_pack).
+launch / by the sort launch itself (vsa_scan_plan_pack); "side" adds a
+stand-in for the collective (a one-workgroup copy of the packed buffer's
+header on another stream, after the scan) to show what the persistent grid does to it, with
+EXP_RESERVE=n CUs left free (vsa_ctx_set_reserved_cus).
   python tools/exp_stripes.py [steps] [warmup]"""
 import json
 import os
@@ -24,6 +27,8 @@ steps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
 warm = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 dev = torch.device("cuda", 0)
 ctxs = [vsa.Context(0)]
+# EXP_RESERVE=n: the grid leaves n CUs free, as bench.py's multi-GPU steps do
+ctxs[0].reserve_cus(int(os.environ.get("EXP_RESERVE", "0")))
 ctxs.append(vsa.Context(share_stream_with=ctxs[0]))
 lits = bench.make_literals(5000, seed=12)
 db = vsa.Database(ctxs[0], vsa.hwlm_build(lits))
@@ -43,7 +48,11 @@ for n in (1, 2, 4, 8):
         ctxs[0].scan_plan(db, plans[0])
     cap = 1 << 16
     bufs = [torch.zeros(1 + cap + (cap + 1) // 2, dtype=torch.int64, device=dev) for _ in ctxs]
-    for mode in ("sync", "pipe", "pack2", "pack1"):
+    side = torch.cuda.Stream()
+    cstreams = [torch.cuda.ExternalStream(c.stream, device=dev) for c in ctxs]
+    dsts = [torch.zeros_like(b) for b in bufs]
+    evs = [torch.cuda.Event() for _ in ctxs]
+    for mode in ("sync", "pipe", "pack2", "pack1", "side"):
         ks, counts = [], []
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -51,6 +60,29 @@ for n in (1, 2, 4, 8):
             for _ in range(steps):
                 counts.append(ctxs[0].scan_plan(db, plans[0]))
                 ks.append(ctxs[0].kernel_ms())
+        elif mode == "side":
+            # pack1 plus a stand-in for the collective: a copy of the packed
+            # buffer on another stream that waits for the scan stream (as
+            # RCCL's kernels wait on bench.py's), completed with the step;
+            # with EXP_RESERVE=0 it queues behind the next scan's persistent
+            # grid, with free CUs it runs beside it
+            for k in range(steps):
+                c, pl, bf = ctxs[k % 2], plans[k % 2], bufs[k % 2]
+                c.scan_plan_pack(db, pl, bf.data_ptr(), cap)
+                side.wait_stream(cstreams[k % 2])
+                with torch.cuda.stream(side):
+                    # one 64-byte copy: a one-workgroup kernel, the size of
+                    # RCCL's small-message collective kernels
+                    dsts[k % 2][:8].copy_(bf[:8])
+                evs[k % 2].record(side)
+                if k:
+                    counts.append(ctxs[(k - 1) % 2].scan_wait())
+                    evs[(k - 1) % 2].synchronize()
+                    ks.append(ctxs[(k - 1) % 2].kernel_ms())
+            counts.append(ctxs[(steps - 1) % 2].scan_wait())
+            evs[(steps - 1) % 2].synchronize()
+            ks.append(ctxs[(steps - 1) % 2].kernel_ms())
+            assert int(dsts[(steps - 1) % 2][0].item()) == counts[-1]  # the header
         elif mode.startswith("pack"):
             # a rank's step as bench.py's N > 1 path queues it, minus the
             # collectives: pipelined scans whose records go into the

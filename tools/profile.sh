@@ -9,7 +9,7 @@ TAG=${1:-r02}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="python3 bench.py --steps 3 --warmup 2 --no-cpu --no-parity"
+B="python3 bench.py --steps 3 --warmup 2 --no-cpu --no-parity --no-e2e --no-cfg5 --no-ceiling"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- \
     python3 bench.py > $OUT/bench_trace.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/fetch -o run -- $B > $OUT/bench_fetch.log 2>&1

@@ -164,6 +164,7 @@ _sig("vsa_derive_first_stage", ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, c
      ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32))
 _sig("vsa_scan_kernel_ms", ctypes.c_double, ctypes.c_void_p)
 _sig("vsa_scan_launches", ctypes.c_uint64, ctypes.c_void_p)
+_sig("vsa_ctx_set_reserved_cus", ctypes.c_int, ctypes.c_void_p, ctypes.c_int)
 _sig("vsa_read_ceiling", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
      ctypes.c_uint32, ctypes.POINTER(ctypes.c_double), _u64p)
 _sig("vsa_class_scan", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -796,6 +797,11 @@ class Context:
     def kernel_ms(self):
         """Device time of the last scan kernel (hipEvents on the scan stream)."""
         return lib.vsa_scan_kernel_ms(self.ptr)
+
+    def reserve_cus(self, n):
+        """vsa_ctx_set_reserved_cus: plans built afterwards leave n CUs free
+        of the scan's persistent grid (for a concurrent collective)."""
+        _check(lib.vsa_ctx_set_reserved_cus(self.ptr, n))
 
     def launches(self):
         """Literal-scan launches queued on this context (reruns included)."""

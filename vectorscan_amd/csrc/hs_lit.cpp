@@ -693,6 +693,12 @@ struct vsa_hs_corpus {
     bool uniform = false;
     uint64_t off0 = 0, ulen = 0;
     std::vector<uint32_t> empty; /* zero-length blocks (not in `order`) */
+    /* the plan's inputs (non-empty blocks), and the second context (on the
+     * scratch context's stream) with its own plan of them that the
+     * pipelined repeat loop alternates with: made at its first use */
+    std::vector<uint64_t> p_off, p_len, p_hist;
+    vsa_ctx_t *ctx2 = nullptr;
+    vsa_plan_t *plan2 = nullptr;
 };
 
 int vsa_hs_corpus_prepare(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch,
@@ -784,6 +790,9 @@ int vsa_hs_corpus_prepare(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch
         delete c;
         return VSA_HS_NOMEM;
     }
+    c->p_off = std::move(lo);
+    c->p_len = std::move(ln);
+    c->p_hist = std::move(lh);
     *out = c;
     return VSA_HS_SUCCESS;
 }
@@ -791,6 +800,8 @@ int vsa_hs_corpus_prepare(const vsa_hs_database_t *db, vsa_hs_scratch_t *scratch
 int vsa_hs_corpus_free(vsa_hs_corpus_t *c) {
     if (!c) return VSA_HS_SUCCESS;
     vsa_plan_free(c->plan);
+    vsa_plan_free(c->plan2);
+    if (c->ctx2) vsa_ctx_destroy(c->ctx2);
     delete c;
     return VSA_HS_SUCCESS;
 }
@@ -1192,12 +1203,14 @@ int vsa_hs_corpus_scan_ex(vsa_hs_corpus_t *cp, uint64_t *counts, uint64_t *diges
 }
 
 /* hsbench's repeat loop (main.cpp:487-511, `repeats` passes over the
- * corpus) pipelined: pass k + 1's scan is queued on the GPU behind the copy
- * of pass k's records, and runs while the host replays pass k through the
- * report program, so a pass costs max(scan, replay) instead of their sum.
- * totals[k] = the matches of pass k; counts / digests (optional) are those
- * of the last pass.  Every pass scans the whole corpus and replays all its
- * records. */
+ * corpus) pipelined two passes deep over two contexts on one stream: while
+ * the host replays pass k through the report program, passes k + 1 and
+ * k + 2 are already queued on the GPU, so a pass costs max(scan + copy,
+ * replay) and the GPU does not wait for the host between passes (one pass
+ * ahead, as in round 5, left it idle for the host's turnaround: 1.0 against
+ * 0.82 ms per 4 GiB pass end to end).  totals[k] = the matches of pass k;
+ * counts / digests (optional) are those of the last pass.  Every pass scans
+ * the whole corpus and replays all its records. */
 int vsa_hs_corpus_scan_repeats(vsa_hs_corpus_t *cp, uint32_t repeats, uint64_t *totals,
                                uint64_t *counts, uint64_t *digests, unsigned threads) {
     if (!cp || !totals || !repeats || !valid_db(cp->db)) return VSA_HS_INVALID;
@@ -1214,11 +1227,32 @@ int vsa_hs_corpus_scan_repeats(vsa_hs_corpus_t *cp, uint32_t repeats, uint64_t *
     int rc = enter(db, scratch);
     if (rc != VSA_HS_SUCCESS) return rc;
     vsa_db_t *ddb = device_db(scratch, db);
-    vsa_ctx_t *ctx = scratch->ctx;
+    if (!cp->plan) {
+        std::fill(totals, totals + repeats, 0);
+        if (counts) std::fill(counts, counts + cp->offsets.size(), 0);
+        if (digests) std::fill(digests, digests + cp->offsets.size(), 0);
+        leave(scratch);
+        return VSA_HS_SUCCESS;
+    }
+    /* two contexts on the scratch context's stream, each with its own plan,
+     * results and counters: pass k runs on cx[k & 1] */
+    if (repeats > 1 && !cp->ctx2) {
+        if (vsa_ctx_create_shared(scratch->ctx, &cp->ctx2) != VSA_OK ||
+            vsa_plan_create(cp->ctx2, cp->d_data, cp->p_off.data(), cp->p_len.data(), nullptr,
+                            cp->streams ? cp->p_hist.data() : nullptr, nullptr,
+                            (uint32_t)cp->p_off.size(), &cp->plan2) != VSA_OK) {
+            if (cp->ctx2) vsa_ctx_destroy(cp->ctx2);
+            cp->ctx2 = nullptr;
+            leave(scratch);
+            return VSA_HS_NOMEM;
+        }
+    }
+    vsa_ctx_t *cx[2] = {scratch->ctx, cp->ctx2 ? cp->ctx2 : scratch->ctx};
+    const vsa_plan_t *pl[2] = {cp->plan, cp->plan2 ? cp->plan2 : cp->plan};
     struct Buf {
         uint64_t *k = nullptr;
         uint32_t *i = nullptr;
-        uint64_t cap = 0, n = 0;
+        uint64_t cap = 0;
     } buf[2];
     auto grow = [&](Buf &b, uint64_t n) -> bool {
         if (n <= b.cap) return true;
@@ -1234,52 +1268,49 @@ int vsa_hs_corpus_scan_repeats(vsa_hs_corpus_t *cp, uint32_t repeats, uint64_t *
     auto ms = [](clk::time_point a, clk::time_point b) {
         return std::chrono::duration<double, std::milli>(b - a).count();
     };
-    rc = VSA_HS_SUCCESS;
-    uint64_t nm = 0;
-    if (!cp->plan) {
-        std::fill(totals, totals + repeats, 0);
-        if (counts) std::fill(counts, counts + cp->offsets.size(), 0);
-        if (digests) std::fill(digests, digests + cp->offsets.size(), 0);
-        leave(scratch);
-        return VSA_HS_SUCCESS;
-    }
-    /* pass 0: scanned, its records on their way to the host */
-    if (vsa_scan_plan(ctx, ddb, cp->plan, 0, &nm) != VSA_OK || !grow(buf[0], nm) ||
-        vsa::records_fetch_async(ctx, nm, buf[0].k, buf[0].i) != VSA_OK)
-        rc = VSA_HS_UNKNOWN_ERROR;
-    buf[0].n = nm;
+    /* hsbench's repeat loop, pipelined two passes deep: the scans of passes
+     * k + 1 and k + 2 are queued on the GPU before the host replays pass k.
+     * Stream order on the shared stream: ... scan k + 1 | copy of k's
+     * records | scan k + 2 | copy of k + 1's | ...: each copy reads its
+     * context's results before that context's next scan rewrites them, and
+     * the GPU never waits for the host while a pass is queued ahead. */
+    auto queue = [&](uint32_t k) -> int {
+        uint64_t dummy = 0;
+        return vsa_scan_plan(cx[k & 1], ddb, pl[k & 1], VSA_SCAN_ASYNC, &dummy) == VSA_OK
+                   ? VSA_HS_SUCCESS : VSA_HS_UNKNOWN_ERROR;
+    };
+    rc = queue(0);
+    if (rc == VSA_HS_SUCCESS && repeats > 1) rc = queue(1);
     for (uint32_t k = 0; k < repeats && rc == VSA_HS_SUCCESS; k++) {
-        Buf &cur = buf[k & 1], &nxt = buf[(k + 1) & 1];
-        const bool more = k + 1 < repeats;
-        /* pass k + 1 queued behind pass k's copy (the copy read the sorted
-         * records before the scan rewrites them) */
-        if (more && vsa_scan_plan(ctx, ddb, cp->plan, VSA_SCAN_ASYNC, &nm) != VSA_OK) {
+        vsa_ctx_t *c = cx[k & 1];
+        Buf &b = buf[k & 1];
+        const auto t0 = clk::now();
+        uint64_t nm = 0;
+        /* pass k complete (its count published; an overflow rescans here),
+         * its records copied behind the scan queued after it, then pass
+         * k + 2 on the same context behind that copy */
+        if (vsa_scan_wait(c, &nm) != VSA_OK || !grow(b, nm) ||
+            vsa::records_fetch_async(c, nm, b.k, b.i) != VSA_OK) {
             rc = VSA_HS_UNKNOWN_ERROR;
             break;
         }
-        const auto t0 = clk::now();
-        if (vsa::records_wait(ctx) != VSA_OK) {
+        if (k + 2 < repeats && (rc = queue(k + 2)) != VSA_HS_SUCCESS) break;
+        if (vsa::records_wait(c) != VSA_OK) {
             rc = VSA_HS_UNKNOWN_ERROR;
             break;
         }
         const auto t1 = clk::now();
-        const bool last = !more;
-        rc = corpus_replay(cp, cur.k, cur.i, cur.n, last ? counts : nullptr,
-                           last ? digests : nullptr, &totals[k], threads);
-        const auto t2 = clk::now();
-        if (rc != VSA_HS_SUCCESS || !more) break;
-        if (vsa_scan_wait(ctx, &nm) != VSA_OK || !grow(nxt, nm) ||
-            vsa::records_fetch_async(ctx, nm, nxt.k, nxt.i) != VSA_OK) {
-            rc = VSA_HS_UNKNOWN_ERROR;
-            break;
-        }
+        const bool last = k + 1 == repeats;
+        rc = corpus_replay(cp, b.k, b.i, nm, last ? counts : nullptr, last ? digests : nullptr,
+                           &totals[k], threads);
         if (timing)
-            fprintf(stderr, "vsa_hs_corpus_scan_repeats: pass %u copy wait %.3f ms, replay %.3f ms, "
-                    "next scan wait %.3f ms (%llu records)\n", k, ms(t0, t1), ms(t1, t2),
-                    ms(t2, clk::now()), (unsigned long long)cur.n);
-        nxt.n = nm;
+            fprintf(stderr, "vsa_hs_corpus_scan_repeats: pass %u wait+copy %.3f ms, replay %.3f ms "
+                    "(%llu records)\n", k, ms(t0, t1), ms(t1, clk::now()),
+                    (unsigned long long)nm);
     }
-    (void)vsa_sync(ctx);
+    /* passes still queued after a failure complete before the buffers go */
+    for (vsa_ctx_t *c : cx) (void)vsa_scan_wait(c, nullptr);
+    for (vsa_ctx_t *c : cx) (void)vsa_sync(c);
     for (Buf &b : buf) {
         vsa::host_pinned_free(b.k);
         vsa::host_pinned_free(b.i);

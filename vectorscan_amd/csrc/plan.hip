@@ -371,7 +371,7 @@ int vsa_plan_create(vsa_ctx_t *c, const uint8_t *d_data, const uint64_t *offsets
     if (!c || !d_data || !offsets || !lens || !nblocks || !out) return VSA_E_INVALID;
     BatchPlan pl;
     int r = build_plan(d_data, offsets, lens, starts, hlens, report_lo, nblocks,
-                       (uint64_t)c->num_cus * (LIT_WAVES - 1), pl);
+                       (uint64_t)c->plan_cus() * (LIT_WAVES - 1), pl);
     if (r != VSA_OK) return r;
     vsa_plan *p = new (std::nothrow) vsa_plan;
     if (!p) return VSA_E_NOMEM;
@@ -438,7 +438,7 @@ int refresh_plan(vsa_ctx *c, const vsa_db *db, vsa_plan *p) {
     BatchPlan pl;
     auto in = [&](int k) { return p->in[k].empty() ? nullptr : p->in[k].data(); };
     int r = build_plan(p->d_data, in(0), in(1), in(2), in(3), in(4), p->nb,
-                       (uint64_t)c->num_cus * (LIT_WAVES - 1), pl, nullptr, LIT_WAVES - 1,
+                       (uint64_t)c->plan_cus() * (LIT_WAVES - 1), pl, nullptr, LIT_WAVES - 1,
                        c->fb.set[si].wg);
     if (r != VSA_OK) return r;
     if (pl.blocks.size() != p->nb) return VSA_E_INVALID;

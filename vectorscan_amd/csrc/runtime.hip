@@ -711,7 +711,7 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
      * the plan's waves and scanning waves per workgroup must agree, or its
      * workgroup count would exceed the CUs */
     const uint64_t ns_plan = LIT_WAVES - db->nconf.load();
-    const uint64_t waves = (uint64_t)c->num_cus * ns_plan;
+    const uint64_t waves = (uint64_t)c->plan_cus() * ns_plan;
     const uint64_t *in[5] = {offs, lens, starts, hlens, rlos};
     auto &M = c->memo;
     bool same = M.valid && M.d_data == d_data && M.nb == nb && M.waves == waves &&
@@ -871,12 +871,20 @@ int vsa_ctx_create_shared(vsa_ctx_t *base, vsa_ctx_t **out) {
     if (rc != VSA_OK) return rc;
     (void)hipStreamSynchronize(c->stream);
     c->stream_ref = base->stream_ref; /* releases the stream it made */
+    c->reserved_cus = base->reserved_cus;
     c->stream = base->stream;
     *out = c;
     return VSA_OK;
 }
 
 void *vsa_ctx_stream(vsa_ctx_t *c) { return c ? (void *)c->stream : nullptr; }
+
+int vsa_ctx_set_reserved_cus(vsa_ctx_t *c, int n) {
+    if (!c || n < 0 || n >= c->num_cus) return VSA_E_INVALID;
+    c->reserved_cus = n;
+    c->memo.valid = false; /* per-call plans are rebuilt for the new grid */
+    return VSA_OK;
+}
 
 /* ------------------------------------------- derived FDR first stage -- */
 

@@ -149,6 +149,10 @@ struct vsa_plan;
 struct vsa_ctx {
     int device = 0;
     int num_cus = 256;
+    /* CUs the literal scan's persistent grid leaves free
+     * (vsa_ctx_set_reserved_cus): plans use num_cus - reserved_cus */
+    int reserved_cus = 0;
+    int plan_cus() const { return std::max(1, num_cus - reserved_cus); }
     hipStream_t stream = nullptr;
     /* the stream's owner: shared by contexts made with vsa_ctx_create_shared,
      * destroyed with the last of them */
