@@ -52,6 +52,13 @@
 #else
 #define VSA_DIAG_ON 0
 #endif
+/* an experiment hook of the candidate / confirm paths (VSA_DEBUG_FLAGS
+ * bits: 8 filter only, 16 drop expanded candidates, 32 count first-stage
+ * candidates, 64 confirm-wave phase profile, 128 drop gathered entries, 256
+ * short ring entries, 1024 no confirm-wave priority): compiled out of
+ * product builds, so the hot paths test no flag word (tools/build_variant.sh
+ * diag -DVSA_DIAG builds the library with them) */
+#define VSA_DBG(flags, bits) (VSA_DIAG_ON && ((flags) & (bits)))
 #define LIT_THREADS (LIT_WAVES * WAVE)
 #define QCAP 256
 
@@ -504,7 +511,7 @@ __device__ __forceinline__ void ring_push(const LitShared &L, ST &st, bool push,
             uint4 *q = L.ring + (size_t)(slot & (cap - 1)) * EW;
 #pragma unroll
             for (int k = 0; k < EW; k++)
-                if (k < 2 || !(L.dbg & 256)) /* experiment: short entries */
+                if (k < 2 || !VSA_DBG(L.dbg, 256)) /* experiment: short entries */
                     q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
         }
         st.head = pos + m;
@@ -1019,7 +1026,7 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
         c[i] = ~c[i] & bucket_mask;
         any |= c[i];
     }
-    if (P.dbg & 32) {
+    if (VSA_DBG(P.dbg, 32)) {
         /* diagnostic first-stage candidate count */
         u32 pc = 0;
 #pragma unroll
@@ -1028,7 +1035,7 @@ __device__ __forceinline__ IterState lit_iter(const VsaLitParams &P, const ConfL
         for (int dd = 32; dd >= 1; dd >>= 1) pc += shfl_xor_u32(pc, dd);
         out.ncand += readfirstlane_u32(pc);
     }
-    if (P.dbg & 8) return out;
+    if (VSA_DBG(P.dbg, 8)) return out;
 
     /* bytes p0-8 .. p0+15 for the 8-byte confirm keys */
     u32 pv2 = lane_up1(d[2]);
@@ -1249,7 +1256,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
     u32 pq_head = 0, pq_tail = 0; /* confirm queue cursors (wave-uniform) */
     /* VSA_DEBUG_FLAGS bit 6: cycles per phase + counts -> counters[4..11],
      * kept in LDS (pcl, this wave's 8 slots) so they hold no registers */
-    const bool prof = (P.dbg & 64) != 0;
+    const bool prof = VSA_DBG(P.dbg, 64);
     u64 tmark = prof ? __builtin_amdgcn_s_memtime() : 0;
     auto pcount = [&](int i, u64 v) {
         if (prof && lane == 0) pcl[i] += v;
@@ -1339,7 +1346,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
             phase(3);
             continue;
         }
-        if (P.dbg & 128) continue; /* experiment: drop gathered entries */
+        if (VSA_DBG(P.dbg, 128)) continue; /* experiment: drop gathered entries */
         if constexpr (XP) {
             /* QEnt entries (scanner expansion): queue them and confirm */
             const u64 pm = __ballot(valid);
@@ -1353,7 +1360,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
             pq_head += filled;
             /* < CONF_U * 64 queued before, <= 64 added */
             if (pq_head - pq_tail >= (u32)WAVE * CONF_U) {
-                if (filled >= 16 && !(P.dbg & 1024)) __builtin_amdgcn_s_setprio(2);
+                if (filled >= 16 && !VSA_DBG(P.dbg, 1024)) __builtin_amdgcn_s_setprio(2);
                 else __builtin_amdgcn_s_setprio(0);
                 confirm_batch(WAVE * CONF_U);
             }
@@ -1366,7 +1373,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
          * entries are final matches, where priority measured slower. */
         if constexpr (MODE != VSA_MODE_NOOD)
         {
-            if (filled >= 16 && !(P.dbg & 1024)) __builtin_amdgcn_s_setprio(2);
+            if (filled >= 16 && !VSA_DBG(P.dbg, 1024)) __builtin_amdgcn_s_setprio(2);
             else __builtin_amdgcn_s_setprio(0);
         }
         const u64 meta0 = ((u64)e[1] << 32) | e[0];
@@ -1479,7 +1486,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
 #pragma unroll
                 for (int u = 0; u < EXP_U; u++) {
                     push[u] = have[u] && ((sw[u] >> sh[u]) & 1u);
-                    if (P.dbg & 16) push[u] = false;
+                    if (VSA_DBG(P.dbg, 16)) push[u] = false;
                 }
 #pragma unroll
                 for (int u = 0; u < EXP_U; u++) {
@@ -1501,7 +1508,7 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
         }
     }
     /* confirm-stage candidates (first-stage count instead under dbg & 32) */
-    if (P.counters && lane == 0 && consumed && !(P.dbg & 32))
+    if (P.counters && lane == 0 && consumed && !VSA_DBG(P.dbg, 32))
         atomicAdd(&P.counters[2], (unsigned long long)consumed);
     if (prof && lane == 0) {
         phase(1);
