@@ -36,6 +36,7 @@ for threads in [int(t) for t in os.environ.get("EXP_THREADS", "16,8,4").split(",
         tots.append(g.scan(threads=threads)[0])
         each.append(time.perf_counter() - t1)
     one = (time.perf_counter() - t0) / reps
+    g.scan_repeats(reps, threads)  # untimed: the first call sets up its second context
     t0 = time.perf_counter()
     pt = g.scan_repeats(reps, threads)
     pipe = (time.perf_counter() - t0) / reps

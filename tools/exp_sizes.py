@@ -1,7 +1,7 @@
 """Median kernel time (hipEvents, clock-settled) of the cfg-4 FDR scan at
 several sizes: 512 MiB (the N = 8 rank stripe), 1 GiB, 4 GiB as 4 blocks.
 One JSON line; the library is the one VSA_LIB_VARIANT names (A/B builds,
-tools/build_variant.sh, tools/gpu_ab_sizes.sh)."""
+tools/archive/build_variant.sh)."""
 import json
 import os
 import sys

@@ -11,6 +11,7 @@ launch / by the sort launch itself (vsa_scan_plan_pack); "side" adds a
 stand-in for the collective (a one-workgroup copy of the packed buffer's
 header on another stream, after the scan) to show what the persistent grid does to it, with
 EXP_RESERVE=n CUs left free (vsa_ctx_set_reserved_cus).
+EXP_RANKS / EXP_MODES (comma lists) limit the rows.
   python tools/exp_stripes.py [steps] [warmup]"""
 import json
 import os
@@ -27,7 +28,7 @@ steps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
 warm = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 dev = torch.device("cuda", 0)
 ctxs = [vsa.Context(0)]
-# EXP_RESERVE=n: the grid leaves n CUs free, as bench.py's multi-GPU steps do
+# EXP_RESERVE=n: the grid leaves n CUs free (measured, not used by bench.py)
 ctxs[0].reserve_cus(int(os.environ.get("EXP_RESERVE", "0")))
 ctxs.append(vsa.Context(share_stream_with=ctxs[0]))
 lits = bench.make_literals(5000, seed=12)
@@ -37,7 +38,9 @@ bl = total // 4
 data = bench.make_corpus_device(torch, 0, total, total, lits, 5, 64 << 10, dev)
 torch.cuda.synchronize()
 dptr = data.data_ptr()
-for n in (1, 2, 4, 8):
+ranks = [int(x) for x in os.environ.get("EXP_RANKS", "1,2,4,8").split(",")]
+modes = os.environ.get("EXP_MODES", "sync,pipe,pack2,pack1,side").split(",")
+for n in ranks:
     cuts, plan = stripe.plan_corpus_stripes(total, bl, n)
     wins = plan[0]
     offs = [w.wlo for w in wins]
@@ -52,7 +55,7 @@ for n in (1, 2, 4, 8):
     cstreams = [torch.cuda.ExternalStream(c.stream, device=dev) for c in ctxs]
     dsts = [torch.zeros_like(b) for b in bufs]
     evs = [torch.cuda.Event() for _ in ctxs]
-    for mode in ("sync", "pipe", "pack2", "pack1", "side"):
+    for mode in modes:
         ks, counts = [], []
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -114,7 +117,7 @@ for n in (1, 2, 4, 8):
         torch.cuda.synchronize()
         st = (time.perf_counter() - t0) / steps * 1e3
         k = sum(ks) / len(ks)
-        print(json.dumps({"ranks": n, "mode": mode, "rank_bytes": cuts[1] - cuts[0],
+        print(json.dumps({"lib": os.environ.get("VSA_LIB_VARIANT", ""), "ranks": n, "mode": mode, "rank_bytes": cuts[1] - cuts[0],
                           "windows": len(wins), "step_ms": round(st, 4),
                           "kernel_ms": round(k, 4), "overhead_us": round((st - k) * 1e3, 1),
                           "matches": counts[-1], "counts_equal": len(set(counts)) == 1}),

@@ -2323,68 +2323,82 @@ __global__ void __launch_bounds__(1024) vsa_bin_finish(const uint32_t *counts, u
                                                      unsigned long long *hfb, uint32_t nfb,
                                                      uint64_t *pk, uint64_t pk_cap) {
     __shared__ u32 red[16], cnt[FIN_BINS], off[FIN_BINS];
+    static_assert(VSA_SORT_BINS / 4 <= 4 * 1024, "the prefix is 4 uint4 loads per thread");
     const u32 t = threadIdx.x, wv = t / WAVE, lane = lane_id();
     const u32 b0 = blockIdx.x * FIN_BINS;
-    /* the records of every bin before b0 */
+    const u32 lb = wv * 4; /* this wave's 4 bins */
+    /* Two dependent round trips to memory, not four: every count this
+     * workgroup needs -- the 64 it owns, this wave's 4 (read directly, to
+     * size its sort), and those of every bin before b0 (the prefix) -- is
+     * loaded at once; then each wave loads its bins' records before the
+     * prefix is reduced, so those loads are in flight across the reduction
+     * and both barriers. */
+    /* unconditional loads (clamped indices, masked after), in the order they
+     * are used, so the compiler can wait for each by count */
+    const uint4 mc = *(const uint4 *)(counts + b0 + lb);
+    const u32 c64 = counts[b0 + (t & (FIN_BINS - 1))];
+    uint4 pv[4];
+#pragma unroll
+    for (u32 q = 0; q < 4; q++) {
+        const u32 i = t + q * 1024;
+        pv[q] = ((const uint4 *)counts)[i < b0 / 4 ? i : 0u];
+    }
+    /* the records of every bin before b0 (this thread's part) */
     u32 s = 0;
-    for (u32 i = t; i < b0 / 4; i += 1024) {
-        const uint4 v = ((const uint4 *)counts)[i];
-        s += v.x + v.y + v.z + v.w;
+#pragma unroll
+    for (u32 q = 0; q < 4; q++)
+        if (t + q * 1024 < b0 / 4) s += pv[q].x + pv[q].y + pv[q].z + pv[q].w;
+    const u32 m[4] = {mc.x, mc.y, mc.z, mc.w};
+    u32 mmax = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) mmax = m[j] > mmax ? m[j] : mmax;
+    /* empty, or left to the library sort (a crowd: the host reruns) */
+    const bool sorting = mmax != 0 && mmax <= VSA_SORT_BIN_MAX;
+    u32 S = 2;
+    while (S < mmax && S < WAVE) S <<= 1;
+    const u32 per = WAVE / S; /* bins per pass (1..32; >= 4 covers all 4 in one) */
+    const u32 j_l = lane / S, r = lane % S;
+    u64 k[4];
+    u32 id[4], jb[4];
+    bool ok[4];
+    /* every pass's loads issued together: the records staged in the bins.
+     * Unconditional (an address inside this wave's 4 bins for every lane,
+     * the unused ones masked at the sort): a load under a divergent branch
+     * makes the compiler wait for it before the prefix reduction below */
+#pragma unroll
+    for (u32 p = 0; p < 4; p++) {
+        const u32 j = p * per + j_l;
+        jb[p] = j;
+        const u32 mj = j == 0 ? m[0] : j == 1 ? m[1] : j == 2 ? m[2] : j == 3 ? m[3] : 0u;
+        ok[p] = sorting && p * per < 4 && r < mj;
+        const size_t q = (size_t)(b0 + lb + (j & 3)) * VSA_SORT_BIN_MAX + r;
+        k[p] = skeys[q];
+        id[p] = sids[q];
     }
 #pragma unroll
     for (int dd = 32; dd >= 1; dd >>= 1) s += shfl_xor_u32(s, dd);
     if (lane == 0) red[wv] = s;
     if (t < FIN_BINS) {
-        cnt[t] = counts[b0 + t];
+        cnt[t] = c64;
         counts_next[b0 + t] = 0;
     }
     __syncthreads();
     if (wv == 0) {
         u32 base = 0;
 #pragma unroll
-        for (int k = 0; k < 16; k++) base += red[k];
+        for (int kk = 0; kk < 16; kk++) base += red[kk];
         u32 tot;
         const u32 e = wave_excl_scan(cnt[lane], &tot);
         off[lane] = base + e;
     }
     __syncthreads();
     if (blockIdx.x == 0 && wv == 0) publish_wave(ctr, h, seq, 144u, fb, hfb, nfb, pk, out_cap);
-    /* this wave's 4 bins */
-    const u32 lb = wv * 4;
-    u32 m[4], mmax = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        m[j] = cnt[lb + j];
-        mmax = m[j] > mmax ? m[j] : mmax;
-    }
-    if (mmax == 0 || mmax > VSA_SORT_BIN_MAX) return; /* empty, or left to the library sort */
-    u32 S = 2;
-    while (S < mmax) S <<= 1;
-    const u32 per = WAVE / S; /* bins per pass (1..32; >= 4 covers all 4 in one) */
-    const u32 j_l = lane / S, r = lane % S;
-    u64 k[4];
-    u32 id[4], jb[4];
-    bool ok[4];
-    /* every pass's loads issued together: the records staged in the bins */
-#pragma unroll
-    for (u32 p = 0; p < 4; p++) {
-        const u32 j = p * per + j_l;
-        jb[p] = j;
-        const u32 mj = j == 0 ? m[0] : j == 1 ? m[1] : j == 2 ? m[2] : j == 3 ? m[3] : 0u;
-        ok[p] = p * per < 4 && r < mj;
-        k[p] = ~0ULL;
-        id[p] = 0;
-        if (ok[p]) {
-            const size_t q = (size_t)(b0 + lb + j) * VSA_SORT_BIN_MAX + r;
-            k[p] = skeys[q];
-            id[p] = sids[q];
-        }
-    }
+    if (!sorting) return;
 #pragma unroll
     for (u32 p = 0; p < 4; p++) {
         if (p * per >= 4) break; /* wave-uniform */
-        u64 kk = k[p];
-        u32 ii = id[p];
+        u64 kk = ok[p] ? k[p] : ~0ULL;
+        u32 ii = ok[p] ? id[p] : 0u;
         for (u32 size = 2; size <= S; size <<= 1) {
             for (u32 jj = size >> 1; jj > 0; jj >>= 1) {
                 const u32 plo = shfl_xor_u32((u32)kk, (int)jj);
