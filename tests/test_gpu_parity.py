@@ -543,6 +543,47 @@ def test_gpu_binned_sort(ctx):
         ctx.free(d)
 
 
+def test_gpu_binned_sort_every_fill():
+    """vsa_bin_finish at every bin fill 1..64 (every sorting network size,
+    S = 2..64, and every mix of sizes among a wave's 4 bins): a block just
+    under 2 MiB has 128-byte bins (bin_shift_for); 1,500 bins get f back-to-back "zq"
+    (f random, ends inside the bin) over filler without 'z' / 'q', scanned
+    with databases of one, two and three literals "zq" (1 / 2 / 3 records
+    per occurrence, every bin <= 64 records: no crowd, one launch each).
+    The binned result == the unsorted scan's records sorted here.  A fresh
+    context: no bin_skip carried over from a crowded test."""
+    ctx = vsa.Context(0)
+    rng = random.Random(23)
+    nprng = np.random.default_rng(23)
+    # span < 2^21: end_bits 21, 128-byte bins (2^21 itself needs 22 bits)
+    host = nprng.integers(ord("a"), ord("p") + 1, (2 << 20) - 64, dtype=np.uint8)
+    d = ctx.malloc(len(host))
+    try:
+        for reps, fmax in ((1, 59), (2, 32), (3, 21)):
+            buf = host.copy()
+            for b in range(40, 40 + 1500):
+                f = rng.randint(1, fmax)
+                o = b * 128 + rng.randint(0, 128 - 2 * f - 1)
+                buf[o:o + 2 * f] = np.frombuffer(b"zq" * f, np.uint8)
+            ctx.h2d(d, buf)
+            db = vsa.Database(ctx, vsa.hwlm_build(
+                [vsa.HwlmLiteral(b"zq", False, 7 + i) for i in range(reps)]))
+            n = ctx.scan_blocks(db, d, [0], [len(buf)], sort=False)
+            raw = ctx.results(n)
+            order = np.argsort(raw["key"], kind="stable")
+            l0 = ctx.launches()
+            m = ctx.scan_blocks(db, d, [0], [len(buf)])
+            assert ctx.launches() == l0 + 1  # binned, not rerun
+            got = ctx.results(m)
+            assert m == n and n >= reps * 1500
+            assert np.array_equal(got["key"], raw["key"][order])
+            assert np.array_equal(got["id"], raw["id"][order])
+            db.close()
+    finally:
+        ctx.free(d)
+        ctx.close()
+
+
 def test_gpu_crowded_bin_plans(ctx):
     """A binned scan's records live only in its sort bins, so a crowded bin
     (> VSA_SORT_BIN_MAX records) makes the scan run again without bins:
