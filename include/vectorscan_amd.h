@@ -347,6 +347,16 @@ double vsa_scan_kernel_ms(vsa_ctx_t *ctx);
  * output overflow or a crowded sort bin counts): a diagnostic of the rerun
  * cost, no reference counterpart. */
 uint64_t vsa_scan_launches(vsa_ctx_t *ctx);
+/* 1 when the context's last literal-scan launch sorted its records inside
+ * the scan kernel (the fused finish: no vsa_bin_finish launch behind it),
+ * else 0.  A diagnostic, no reference counterpart. */
+int vsa_scan_last_fused(vsa_ctx_t *ctx);
+/* Sort inside the scan kernel when the plan allows it (the fused finish:
+ * no vsa_bin_finish launch behind the scan, the scan's workgroups sort
+ * their own records and the last one publishes the count), on = 1; off = 0
+ * (the default, or VSA_FUSED_FINISH=1 at start-up).  Results are identical
+ * either way; no reference counterpart. */
+int vsa_ctx_set_fused_finish(vsa_ctx_t *ctx, int on);
 /* Measurement helper, not a scan (no reference counterpart): the streaming-
  * read ceiling of this device over d_data -- the first len rounded down to
  * 64 KiB read once per run by a plain 16-byte-load kernel on the ctx stream,

@@ -232,13 +232,16 @@ def test_gpu_fdr_5k_64mib(ctx):
     assert len(m) >= (64 << 20) // (64 << 10)
 
 
-def test_gpu_schedule_feedback_512mib(ctx):
+@pytest.mark.parametrize("fused", [False, True])
+def test_gpu_schedule_feedback_512mib(ctx, fused):
     """Schedule feedback (runtime.hip take_feedback / refresh_plan): 512 MiB
     in 4 blocks scanned 8 times through one prebuilt plan and 8 times per
     call (scan_blocks), so the XCD weights are learned and the plans rebuilt
     with weighted shares between launches: every launch's records equal the
-    first one's, and that one's digest equals the oracle's."""
+    first one's, and that one's digest equals the oracle's.  With the fused
+    finish too (its last workgroup publishes the feedback record)."""
     import bench
+    ctx.fused_finish(fused)
     lits = bench.make_literals(5000, seed=12)
     blob = vsa.hwlm_build(lits)
     db = vsa.Database(ctx, blob)
@@ -249,6 +252,7 @@ def test_gpu_schedule_feedback_512mib(ctx):
     d = ctx.malloc(n + 64)
     first = None
     plan = None
+    fused_seen = []
     try:
         ctx.h2d(d, host)
         plan = ctx.plan(d, offs, [bl] * 4)
@@ -262,11 +266,14 @@ def test_gpu_schedule_feedback_512mib(ctx):
                 assert oracle.digest_of(res["key"] >> np.uint64(24), res["id"]) == want
             else:
                 assert np.array_equal(cur[0], first[0]) and np.array_equal(cur[1], first[1]), k
+            fused_seen.append(ctx.last_fused())
             if k == 7:
                 # the first complete feedback record always publishes weights
                 # (feedback_update), so the prebuilt plan was rebuilt for them
                 assert plan.rebuilds() >= 1
+        assert any(fused_seen) == fused
     finally:
+        ctx.fused_finish(False)
         if plan is not None:
             plan.close()
         db.close()
@@ -666,14 +673,17 @@ def test_gpu_crowded_bin_plans(ctx):
         vsa_ctx.close()
 
 
-def test_gpu_plan_pack_fused(ctx):
+@pytest.mark.parametrize("fused", [False, True])
+def test_gpu_plan_pack_fused(ctx, fused):
     """vsa_scan_plan_pack: the binned sort writes the records into the
     collective buffer itself (no vsa_pack launch).  Over ragged blocks with
     sparse records, pipelined over two contexts on one stream as bench.py
     does: header = the count, keys and ids == the scan's own sorted results,
     and a buffer too small keeps its first cap records with the full count
-    in the header (the caller regrows and repacks)."""
+    in the header (the caller regrows and repacks).  With the binned sort
+    launch and with the fused finish (the scan packs itself)."""
     rng = random.Random(17)
+    ctx.fused_finish(fused)
     blob = vsa.hwlm_build(rand_lits(rng, 400, minlen=3, maxlen=8))
     host = np.frombuffer(rand_data(rng, 6 << 20), np.uint8).copy()
     c2 = vsa.Context(share_stream_with=ctx)
@@ -681,6 +691,8 @@ def test_gpu_plan_pack_fused(ctx):
     try:
         ctx.h2d(d, host)
         offs, lens = [0, 3 << 20, (5 << 20) + 5], [(3 << 20) - 1, 2 << 20, 777000]
+        assert c2.last_fused() is False
+        fused_seen = []
         dbs = [vsa.Database(ctx, blob), vsa.Database(c2, blob)]
         plans = [ctx.plan(d, offs, lens), c2.plan(d, offs, lens)]
         want = None
@@ -702,18 +714,84 @@ def test_gpu_plan_pack_fused(ctx):
                 assert int(pk[0]) == n, (k, cap)
                 assert np.array_equal(pk[1:1 + m], want["key"][:m]), (k, cap)
                 assert np.array_equal(pk[1 + cap:].view(np.uint32)[:m], want["id"][:m]), (k, cap)
+                fused_seen.append(c.last_fused())
+        # (the shared fixture context may still skip bins after an earlier
+        # test's crowd: then some launches take the library sort)
+        assert any(fused_seen) == fused
         for p_ in plans:
             p_.close()
         for db in dbs:
             db.close()
     finally:
+        ctx.fused_finish(False)
         ctx.free(d)
         c2.close()
 
 
+def test_gpu_fused_finish():
+    """The fused finish (kernels.hip fused_finish, plan.hip plan_fused): a
+    plan of >= 64 workgroups whose end ranges ascend is sorted by the scan
+    kernel itself -- local bins counted in LDS, a look-back over the lower
+    workgroups' totals, the last workgroup publishing -- with no
+    vsa_bin_finish launch (vsa_ctx_set_fused_finish; off by default).  On a
+    fresh context per case with it on: last_fused() is set
+    and the records equal the unsorted scan's sorted here, for FDR over 4
+    blocks, a stripe window with report_lo, 16 KiB back-to-back blocks
+    (runs), noodle and Teddy databases, 30 launches in a row (one epoch
+    each), a first launch that outgrows the output (rerun, fused again) and
+    a crowded local bin (rerun without bins)."""
+    rng = random.Random(31)
+    host = np.frombuffer(rand_data(rng, 24 << 20), np.uint8).copy()
+    host[(9 << 20) + 100:(9 << 20) + 700] = np.frombuffer(b"ab" * 300, np.uint8)
+    dbs = {
+        "fdr": vsa.hwlm_build(rand_lits(rng, 300, minlen=3, maxlen=8)),
+        "noodle": vsa.hwlm_build([vsa.HwlmLiteral(b"q\x01", False, 3)]),
+        "teddy": vsa.hwlm_build(rand_lits(rng, 20, minlen=3, maxlen=6)),
+        "crowd": vsa.hwlm_build([vsa.HwlmLiteral(b"ab", False, 10 + i) for i in range(40)]),
+    }
+    q = 6 << 20
+    layouts = {
+        "blocks": ([0, q, 2 * q, 3 * q], [q, q, q, q - 5], None),
+        "window": ([(8 << 20) - 7], [(12 << 20) + 7], [7]),
+        "runs": ([i << 14 for i in range(1024)], [1 << 14] * 1024, None),
+    }
+    c0 = vsa.Context(0)
+    d = c0.malloc(len(host))
+    try:
+        c0.h2d(d, host)
+        for name, blob in dbs.items():
+            for lname, (offs, lens, rlo) in layouts.items():
+                c = vsa.Context(0)
+                c.fused_finish(True)
+                try:
+                    db = vsa.Database(c, blob)
+                    n0 = c.scan_blocks_ex(db, d, offs, lens, report_lo=rlo, sort=False)
+                    raw = c.results(n0)
+                    order = np.argsort(raw["key"], kind="stable")
+                    for k in range(30 if (name, lname) == ("fdr", "blocks") else 3):
+                        l0 = c.launches()
+                        n = c.scan_blocks_ex(db, d, offs, lens, report_lo=rlo)
+                        got = c.results(n)
+                        assert n == n0, (name, lname, k)
+                        assert np.array_equal(got["key"], raw["key"][order]), (name, lname, k)
+                        assert np.array_equal(got["id"], raw["id"][order]), (name, lname, k)
+                        if name == "crowd" and k == 0:
+                            # crowded: rerun without bins, then bins skipped
+                            assert c.launches() == l0 + 2 and not c.last_fused()
+                        elif name != "crowd":
+                            assert c.last_fused(), (name, lname, k)
+                            assert c.launches() == l0 + 1 or (k == 0 and n > 65536)
+                    db.close()
+                finally:
+                    c.close()
+    finally:
+        c0.free(d)
+        c0.close()
+
+
 def test_gpu_reserved_cus_same_records():
-    """vsa_ctx_set_reserved_cus (bench.py's multi-GPU steps leave CUs free
-    for the collectives): plans on a context with 1 or 7 CUs reserved --
+    """vsa_ctx_set_reserved_cus (CUs left free beside the scan's persistent
+    grid; measured, not used by bench.py): plans on a context with 1 or 7 CUs reserved --
     per-call and prebuilt, and a shared context inheriting the reserve --
     give the same sorted records as the full grid."""
     rng = random.Random(23)

@@ -61,7 +61,8 @@ def describe_bins(offs, lens, starts=None, num_cus=256, ns=15, base=0x10000):
     desc = words[:4 * nseg].reshape(-1, 4)
     bounds = words[4 * nseg:4 * nseg + grid + 1]
     wg_bins = words[4 * nseg + grid + 1:4 * nseg + 3 * grid + 1].reshape(-1, 2)
-    assert len(words) == 4 * nseg + 3 * grid + 1
+    # then the fused finish's local-bin table (plan_fused), 4 words each
+    assert len(words) == 4 * nseg + 7 * grid + 1
     return desc, bounds, grid, wg_bins
 
 
@@ -361,3 +362,90 @@ def test_plan_owned_bins_are_exclusive(seed):
     # overlapping blocks (the same bytes scanned twice): nothing owned
     desc, bounds, grid, wb = describe_bins([0, 0], [64 << 20, 64 << 20], base=base)
     assert not wb.any()
+
+
+def describe_fused(offs, lens, starts=None, rlos=None, num_cus=256, ns=15, base=0x10000):
+    """(desc, bounds, grid, fin): fin[b] = (lowest end, local bin shift,
+    local bins) of workgroup b's fused-finish bins (plan.hip plan_fused)"""
+    o = np.ascontiguousarray(offs, np.uint64)
+    ln = np.ascontiguousarray(lens, np.uint64)
+    st = None if starts is None else np.ascontiguousarray(starts, np.uint64)
+    rl = None if rlos is None else np.ascontiguousarray(rlos, np.uint64)
+    n = ctypes.c_uint64()
+    g = ctypes.c_uint32()
+    args = [base, o.ctypes.data, ln.ctypes.data, None if st is None else st.ctypes.data, None,
+            None if rl is None else rl.ctypes.data, len(o), num_cus, ns]
+    w = lib.vsa_plan_describe(*args, None, 0, ctypes.byref(n), ctypes.byref(g), None)
+    words = np.zeros(w, np.uint32)
+    lib.vsa_plan_describe(*args, words.ctypes.data, w, ctypes.byref(n), ctypes.byref(g), None)
+    nseg, grid = n.value, g.value
+    assert len(words) == 4 * nseg + 7 * grid + 1
+    f = words[4 * nseg + 3 * grid + 1:].reshape(-1, 4).astype(np.int64)
+    fin = [(int(a) | (int(b) << 32), int(c), int(d)) for a, b, c, d in f]
+    return words[:4 * nseg].reshape(-1, 4), words[4 * nseg:4 * nseg + grid + 1], grid, fin
+
+
+def _end_range(row, offs, lens, starts, rlos, mis):
+    """the ends a segment can report: [base + max(start, rlo), base + len)
+    of each of its blocks, a part cut to its KiB range"""
+    first, cnt = int(row[0]) & 0xffffff, int(row[0]) >> 24
+    lo, hi = None, None
+    for b in (range(first, first + cnt) if cnt else [first]):
+        l, h = offs[b] + max(starts[b], rlos[b]), offs[b] + lens[b]
+        if not cnt:
+            org = (offs[b] + mis + max(0, starts[b] - 16)) & ~1023
+            s0 = org - mis + (int(row[1]) << 10)
+            l, h = max(l, s0), min(h, s0 + (int(row[2]) << 10))
+        if h > l:
+            lo = l if lo is None else min(lo, l)
+            hi = h if hi is None else max(hi, h)
+    return lo, hi
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_plan_fused_local_bins(seed):
+    """The fused finish's local bins (plan_fused, kernels.hip fused_finish):
+    every end a workgroup's segments can report falls in its local bins
+    [lo, lo + bins << shift), at most VSA_LBINS (256) of them with the
+    smallest shift that fits, lo its lowest reportable end; on the layouts the bench
+    and the stripes use (blocks in address order) the workgroups' end
+    ranges ascend with the workgroup index, which makes the plan eligible."""
+    rng = random.Random(9300 + seed)
+    base = 0x100000 + rng.choice([0, 0, 1, 15])
+    mis = base & 15
+    kind = seed % 5
+    if kind == 0:  # the bench: 4 GiB as 4 blocks
+        offs, lens = [i << 30 for i in range(4)], [1 << 30] * 4
+    elif kind == 1:  # an N = 8 stripe window: [lo - 7, hi), ends >= 7 of it
+        lo = rng.choice([1, 3, 5]) << 29
+        offs, lens = [lo - 7], [(1 << 29) + 7]
+    elif kind == 2:  # hsbench chunks: 1 GiB of 16 KiB blocks (runs)
+        offs, lens = [i << 14 for i in range(1 << 16)], [1 << 14] * (1 << 16)
+    else:
+        n = rng.choice([3, 40, 500])
+        offs, lens, pos = [], [], 0
+        for _ in range(n):
+            ln = rng.choice([100, 4096, 70000, 1 << 20, 16 << 20])
+            offs.append(pos)
+            lens.append(ln)
+            pos += ln + rng.choice([0, 64, rng.randint(1, 5000)])
+    starts = [rng.choice([0, 0, 3, 100]) if kind >= 3 else 0 for _ in offs]
+    rlos = [7 if kind == 1 else 0 for _ in offs]
+    desc, bounds, grid, fin = describe_fused(offs, lens, starts, rlos, base=base)
+    prev_hi, ascending = -1, True
+    for b in range(grid):
+        rs = [_end_range(desc[s], offs, lens, starts, rlos, mis)
+              for s in range(bounds[b], bounds[b + 1])]
+        rs = [r for r in rs if r[0] is not None]
+        lo, shift, nb = fin[b]
+        if not rs:
+            assert (lo, shift, nb) == (0, 0, 0)
+            continue
+        hlo, hhi = min(r[0] for r in rs), max(r[1] for r in rs)
+        assert lo == hlo, (b, lo, hlo)
+        assert 1 <= nb <= 256 and hhi - hlo <= nb << shift, (b, nb, shift, hhi - hlo)
+        assert shift == 0 or (((hhi - hlo - 1) >> (shift - 1)) + 1) > 256  # the smallest
+        ascending = ascending and hlo >= prev_hi
+        prev_hi = hhi
+    if kind <= 2:
+        assert grid >= 64 and ascending

@@ -164,6 +164,8 @@ _sig("vsa_derive_first_stage", ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, c
      ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32))
 _sig("vsa_scan_kernel_ms", ctypes.c_double, ctypes.c_void_p)
 _sig("vsa_scan_launches", ctypes.c_uint64, ctypes.c_void_p)
+_sig("vsa_scan_last_fused", ctypes.c_int, ctypes.c_void_p)
+_sig("vsa_ctx_set_fused_finish", ctypes.c_int, ctypes.c_void_p, ctypes.c_int)
 _sig("vsa_ctx_set_reserved_cus", ctypes.c_int, ctypes.c_void_p, ctypes.c_int)
 _sig("vsa_read_ceiling", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
      ctypes.c_uint32, ctypes.POINTER(ctypes.c_double), _u64p)
@@ -806,6 +808,16 @@ class Context:
     def launches(self):
         """Literal-scan launches queued on this context (reruns included)."""
         return lib.vsa_scan_launches(self.ptr)
+
+    def fused_finish(self, on=True):
+        """Sort inside the scan kernel when the plan allows it
+        (vsa_ctx_set_fused_finish; results are identical either way)."""
+        _check(lib.vsa_ctx_set_fused_finish(self.ptr, 1 if on else 0))
+
+    def last_fused(self):
+        """True when the last literal-scan launch sorted its records inside
+        the scan (the fused finish, no vsa_bin_finish launch)."""
+        return lib.vsa_scan_last_fused(self.ptr) == 1
 
     def read_ceiling(self, d_data, length, runs=5):
         """(GB/s, ms, bytes): this device's streaming-read ceiling over the

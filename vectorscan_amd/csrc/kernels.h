@@ -84,6 +84,7 @@ enum VsaLitMode {
 #define VSA_LBINS 256u /* sort bins a workgroup may count in LDS */
 #define VSA_SORT_BIN_MAX 64
 #define VSA_CTR_BIN_OVERFLOW 12 /* counters[12]: some bin passed VSA_SORT_BIN_MAX */
+#define VSA_FIN_MAX_GRID 1024u /* workgroups of a fused-finish launch, at most */
 
 struct VsaLitParams {
     const uint8_t *data;
@@ -156,6 +157,26 @@ struct VsaLitParams {
     unsigned long long *counters; /* [0] matches, [2] candidates handed to
                                      confirm (after the slot prefilter;
                                      diagnostic) */
+    /* Fused finish (kernels.hip fused_finish; fin_keys null = off): each
+     * workgroup bins its records over its own end range in LDS-counted local
+     * bins (staging row blockIdx.x * VSA_LBINS + bin of bin_keys / bin_ids),
+     * sorts them at its end and writes them at its offset, found by a
+     * look-back over the lower workgroups' totals; the last workgroup out
+     * publishes the counters.  No vsa_bin_finish launch. */
+    const uint32_t *fin_wg;       /* 4 words per workgroup: lowest end (lo,
+                                     hi word), local bin shift, local bins */
+    uint64_t *fin_keys;           /* the sorted records (out_cap) */
+    uint32_t *fin_ids;
+    unsigned long long *fin_agg;  /* [b] = epoch << 32 | crowded << 31 |
+                                     workgroup b's records */
+    uint32_t *fin_ticket;         /* workgroups finished (the last resets it) */
+    uint32_t fin_epoch;           /* this launch's tag in fin_agg (nonzero) */
+    uint32_t fin_nfb;             /* feedback words published (2 x grid, or 0) */
+    unsigned long long *fin_pub;  /* host publish block (vsa_publish layout) */
+    unsigned long long fin_seq;
+    unsigned long long *fin_hfb;  /* feedback records' host copy */
+    uint64_t *fin_pk;             /* packed collective buffer (or null) */
+    uint64_t fin_pk_cap;
 };
 
 

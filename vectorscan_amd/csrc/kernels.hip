@@ -130,6 +130,159 @@ __device__ __forceinline__ u32 shfl_xor_u32(u32 v, int m) {
 __device__ __forceinline__ u32 shfl_down_u32(u32 v, unsigned d) {
     return (u32)__shfl_down((int)v, d, WAVE);
 }
+/* lane l gets lane l ^ M's v for a constant M, without the LDS crossbar
+ * where CDNA's DPP reaches: xor 1 / 2 are quad permutes, xor 4 = the
+ * half-row mirror (l ^ 7) then the quad reverse (^ 3), xor 8 = the row
+ * mirror (^ 15) then the half-row mirror (^ 7); xor 16 a ds_swizzle in
+ * bit mode (32-lane groups, no address VGPR); xor 32 a bpermute */
+template <int M>
+__device__ __forceinline__ u32 lane_xor(u32 v) {
+    static_assert(M == 1 || M == 2 || M == 4 || M == 8 || M == 16 || M == 32, "lane_xor");
+    if constexpr (M == 1) {
+        return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);
+    } else if constexpr (M == 2) {
+        return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);
+    } else if constexpr (M == 4) {
+        const int h = __builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);
+        return (u32)__builtin_amdgcn_update_dpp(0, h, 0x1B, 0xf, 0xf, false);
+    } else if constexpr (M == 8) {
+        const int h = __builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false);
+        return (u32)__builtin_amdgcn_update_dpp(0, h, 0x141, 0xf, 0xf, false);
+    } else if constexpr (M == 16) {
+        return (u32)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);
+    } else {
+        return shfl_xor_u32(v, 32);
+    }
+}
+
+/* A wave's 4 sort bins (the binned sort's unit, vsa_bin_finish and the
+ * fused finish): bin j holds m[j] <= VSA_SORT_BIN_MAX records at staging row
+ * row0 + j.  One register bitonic network of S lanes per bin (S = the next
+ * power of two >= the largest count, 2..64), 64 / S bins per pass, npass
+ * passes run in lockstep.  Lane r of a bin's S lanes ends up with the bin's
+ * r-th smallest key (keys are unique: end, bucket, LitInfo -- the full
+ * sort's order); ok[p] says it is a record. */
+struct Bins4 {
+    u64 k[4];
+    u32 id[4], jb[4];
+    bool ok[4];
+    u32 S, npass, r;
+};
+/* every pass's loads issued together.  Unconditional (an address inside
+ * the wave's 4 bins for every lane, the unused ones masked at the sort): a
+ * load under a divergent branch makes the compiler wait for it early */
+__device__ __forceinline__ void bins4_load(Bins4 &B, const uint64_t *skeys, const uint32_t *sids,
+                                           size_t row0, const u32 (&m)[4], bool sorting,
+                                           u32 lane) {
+    u32 mmax = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) mmax = m[j] > mmax ? m[j] : mmax;
+    B.S = 2;
+    while (B.S < mmax && B.S < WAVE) B.S <<= 1;
+    const u32 per = WAVE / B.S; /* bins per pass (1..32; >= 4 covers all 4 in one) */
+    B.npass = (4 + per - 1) / per; /* wave-uniform, 1..4 */
+    const u32 j_l = lane / B.S;
+    B.r = lane % B.S;
+#pragma unroll
+    for (u32 p = 0; p < 4; p++) {
+        const u32 j = p * per + j_l;
+        B.jb[p] = j;
+        const u32 mj = j == 0 ? m[0] : j == 1 ? m[1] : j == 2 ? m[2] : j == 3 ? m[3] : 0u;
+        B.ok[p] = sorting && p * per < 4 && B.r < mj;
+        const size_t q = (row0 + (j & 3)) * VSA_SORT_BIN_MAX + B.r;
+        B.k[p] = skeys[q];
+        B.id[p] = sids[q];
+    }
+}
+/* the passes' networks in lockstep (independent exchanges issued together),
+ * each step's partner fetched with lane_xor at a constant stride: DPP for
+ * strides <= 8, a swizzle for 16, a bpermute only for 32 (S = 64).  Empty
+ * slots hold ~0 and sort to the end of their bin. */
+__device__ __forceinline__ void bins4_sort(Bins4 &B, u32 lane) {
+#pragma unroll
+    for (u32 p = 0; p < 4; p++) {
+        if (!B.ok[p]) {
+            B.k[p] = ~0ULL;
+            B.id[p] = 0u;
+        }
+    }
+    const u32 S = B.S, npass = B.npass;
+    auto step = [&](auto jc, u32 size) {
+        constexpr int JJ = decltype(jc)::value;
+        /* ascending within each S-lane segment: the last merge is ascending
+         * everywhere, earlier ones alternate */
+        const bool up = size == S || (lane & size) == 0;
+        const bool lower = (lane & JJ) == 0;
+#pragma unroll
+        for (u32 p = 0; p < 4; p++) {
+            if (p >= npass) break; /* wave-uniform */
+            const u32 plo = lane_xor<JJ>((u32)B.k[p]);
+            const u32 phi = lane_xor<JJ>((u32)(B.k[p] >> 32));
+            const u32 pid = lane_xor<JJ>(B.id[p]);
+            const u64 pkk = ((u64)phi << 32) | plo;
+            const bool take = (lower == up) ? (pkk < B.k[p]) : (pkk > B.k[p]);
+            if (take) {
+                B.k[p] = pkk;
+                B.id[p] = pid;
+            }
+        }
+    };
+    using std::integral_constant;
+    for (u32 size = 2; size <= S; size <<= 1) {
+        /* a merge of `size`: strides size / 2 .. 1 (wave-uniform branches) */
+        if (size >= 64) step(integral_constant<int, 32>(), size);
+        if (size >= 32) step(integral_constant<int, 16>(), size);
+        if (size >= 16) step(integral_constant<int, 8>(), size);
+        if (size >= 8) step(integral_constant<int, 4>(), size);
+        if (size >= 4) step(integral_constant<int, 2>(), size);
+        step(integral_constant<int, 1>(), size);
+    }
+}
+/* The fused finish's form of bins4_load: a wave's nbins <= 16 consecutive
+ * bins (counts cnt[0..nbins) in LDS, all <= S <= 64), 64 / S bins per pass;
+ * this loads passes [pass0, pass0 + 4) of them (B.npass of which exist). */
+__device__ __forceinline__ void bins16_load(Bins4 &B, const uint64_t *skeys, const uint32_t *sids,
+                                            size_t row0, const u32 *cnt, u32 nbins, u32 S,
+                                            u32 pass0, u32 lane) {
+    B.S = S;
+    const u32 per = WAVE / S;
+    const u32 np = (nbins + per - 1) / per; /* passes in all (wave-uniform) */
+    B.npass = np > pass0 ? (np - pass0 < 4 ? np - pass0 : 4u) : 0u;
+    const u32 j_l = lane / S;
+    B.r = lane % S;
+#pragma unroll
+    for (u32 p = 0; p < 4; p++) {
+        const u32 j = (pass0 + p) * per + j_l;
+        const u32 jc = j < nbins ? j : nbins - 1;
+        B.jb[p] = j;
+        B.ok[p] = p < B.npass && j < nbins && B.r < cnt[jc];
+        const size_t q = (row0 + jc) * VSA_SORT_BIN_MAX + B.r;
+        B.k[p] = skeys[q];
+        B.id[p] = sids[q];
+    }
+}
+
+/* the sorted records to their positions: bin j's first at off[j] (and into
+ * the packed collective buffer [header | keys (pk_cap) | ids], if any) */
+__device__ __forceinline__ void bins4_write(const Bins4 &B, const u32 (&off)[4], uint64_t *okeys,
+                                            uint32_t *oids, uint64_t out_cap, uint64_t *pk,
+                                            uint64_t pk_cap) {
+#pragma unroll
+    for (u32 p = 0; p < 4; p++) {
+        if (p >= B.npass) break; /* wave-uniform */
+        if (!B.ok[p]) continue;
+        const u32 j = B.jb[p];
+        const u64 o = (u64)(j == 0 ? off[0] : j == 1 ? off[1] : j == 2 ? off[2] : off[3]) + B.r;
+        if (o < out_cap) {
+            okeys[o] = B.k[p];
+            oids[o] = B.id[p];
+        }
+        if (pk && o < pk_cap) {
+            pk[1 + o] = B.k[p];
+            ((uint32_t *)(pk + 1 + pk_cap))[o] = B.id[p];
+        }
+    }
+}
 
 /* any lane's c: one v_cmp into a scalar mask and a scalar test (__any's
  * lowering re-materialized the mask as a lane value and compared again) */
@@ -246,17 +399,45 @@ struct ConfLds {
     u32 lb_lo, lb_n;
     u32 lbins[VSA_LBINS];
     u32 nrec; /* binned sort: records confirmed here (one global add at the end) */
+    /* fused finish: the local bins cover ends [f_lo, f_lo + lb_n << f_shift)
+     * (lb_lo = 0) */
+    u64 f_lo;
+    u32 f_shift;
 };
 
+/* a record's sort bin: the end's global bin, or under the fused finish its
+ * local bin (end - f_lo) >> f_shift, whose staging row is the workgroup's
+ * own (bin_row) */
+__device__ __forceinline__ u32 rec_bin(const VsaLitParams &P, const ConfLds &cl, u64 end) {
+    if (P.fin_keys) {
+        const u64 d = (end - cl.f_lo) >> cl.f_shift; /* an end below f_lo wraps: out of range */
+        return d < VSA_LBINS ? (u32)d : 0xffffffffu;
+    }
+    return (u32)(end >> P.bin_shift);
+}
+__device__ __forceinline__ size_t bin_row(const VsaLitParams &P, u32 bin) {
+    return P.fin_keys ? (size_t)blockIdx.x * VSA_LBINS + bin : (size_t)bin;
+}
+
 /* a record's slot in its sort bin: an owned bin's from the workgroup's LDS
- * count (no global round trip), any other bin's from the global one */
+ * count (no global round trip), any other bin's from the global one.  Under
+ * the fused finish every record's bin is local; one outside the local range
+ * (the plan guarantees none) counts as a crowd, so the host rescans */
 __device__ __forceinline__ u32 bin_slot_take(const VsaLitParams &P, const ConfLds &cl, u32 bin) {
     const u32 k = bin - cl.lb_lo;
     if (k < cl.lb_n)
         return __hip_atomic_fetch_add(const_cast<u32 *>(&cl.lbins[k]), 1u, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (P.fin_keys) return VSA_SORT_BIN_MAX;
     return __hip_atomic_fetch_add(&P.bin_counts[bin], 1u, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
+}
+
+/* counters[VSA_CTR_BIN_OVERFLOW] = 1 as an agent-scope atomic store: the
+ * fused finish's last workgroup reads it from another XCD */
+__device__ __forceinline__ void flag_crowd(const VsaLitParams &P) {
+    __hip_atomic_store(&P.counters[VSA_CTR_BIN_OVERFLOW], 1ULL, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
 /* confirm-queue entry (the confirm wave's private queue): meta = aoff << 24 |
@@ -409,11 +590,13 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
                     s0 = atomicAdd(&P.counters[0], (unsigned long long)tot);
             }
             const u64 sb = ((u64)readlane_u32((u32)(s0 >> 32), 0) << 32) | readlane_u32((u32)s0, 0);
-            u32 bslot[CONF_U];
+            u32 bslot[CONF_U], bbin[CONF_U];
 #pragma unroll
             for (int i = 0; i < CONF_U; i++)
-                if (bins && mt[i])
-                    bslot[i] = bin_slot_take(P, cl, (u32)((base[i] + (u64)e[i]) >> P.bin_shift));
+                if (bins && mt[i]) {
+                    bbin[i] = rec_bin(P, cl, base[i] + (u64)e[i]);
+                    bslot[i] = bin_slot_take(P, cl, bbin[i]);
+                }
 #pragma unroll
             for (int i = 0; i < CONF_U; i++) {
                 if (!mt[i]) continue;
@@ -422,7 +605,7 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
                 u32 before = 0; /* this lane's rank among the step's matches */
 #pragma unroll
                 for (int k = 0; k < i; k++) before += (u32)__popcll(pm[k]);
-                const u64 q = bins ? (u64)(end >> P.bin_shift) * VSA_SORT_BIN_MAX + bslot[i]
+                const u64 q = bins ? (u64)bin_row(P, bbin[i]) * VSA_SORT_BIN_MAX + bslot[i]
                                    : sb + before + __builtin_amdgcn_mbcnt_hi(
                                          (u32)(pm[i] >> 32), __builtin_amdgcn_mbcnt_lo((u32)pm[i], 0));
                 if (bins ? bslot[i] < VSA_SORT_BIN_MAX : q < P.out_cap) {
@@ -430,7 +613,7 @@ __device__ __forceinline__ void confirm_multi(const VsaLitParams &P, const ConfL
                                                           ((u64)b[i] << VSA_KEY_BUCKET_SHIFT) | lidx;
                     (bins ? P.bin_ids : P.out_ids)[q] = w1[i].z;
                 } else if (bins) {
-                    P.counters[VSA_CTR_BIN_OVERFLOW] = 1; /* crowded: the host rescans without bins */
+                    flag_crowd(P); /* crowded: the host rescans without bins */
                 }
             }
         }
@@ -1393,14 +1576,14 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
                 for (; hits; hits &= hits - 1) {
                     const u32 j = __ffs(hits) - 1;
                     const u64 end = p0 + j - mis;
-                    const u32 bin = (u32)(end >> P.bin_shift);
+                    const u32 bin = rec_bin(P, cl, end);
                     const u32 s = bin_slot_take(P, cl, bin);
                     if (s < VSA_SORT_BIN_MAX) {
-                        const size_t q = (size_t)bin * VSA_SORT_BIN_MAX + s;
+                        const size_t q = bin_row(P, bin) * VSA_SORT_BIN_MAX + s;
                         P.bin_keys[q] = end << VSA_KEY_END_SHIFT;
                         P.bin_ids[q] = P.nood_id;
                     } else {
-                        P.counters[VSA_CTR_BIN_OVERFLOW] = 1;
+                        flag_crowd(P);
                     }
                 }
             } else if (hits) {
@@ -1536,6 +1719,8 @@ __device__ __forceinline__ void stage_lds(TV *dst, u32 n, u32 tid, F &&src) {
     for (u32 i = base + tid; i < n; i += LIT_THREADS) dst[i] = src(i);
 }
 
+__device__ __forceinline__ void fused_finish(const VsaLitParams &P, const ConfLds &cl, u32 *sc);
+
 template <int MODE, bool XP, bool SPLIT>
 __global__ void __launch_bounds__(LIT_THREADS)
 vsa_lit_scan(VsaLitParams P) {
@@ -1632,9 +1817,19 @@ vsa_lit_scan(VsaLitParams P) {
         /* owned sort bins: their counts so far (0, or the first split
          * pass's) into LDS */
         u32 lo = 0, n = 0;
-        if (P.bin_keys && P.wg_bins) {
+        if (P.fin_keys) {
+            /* fused finish: local bins over this workgroup's ends, from 0 */
+            const uint32_t *f = P.fin_wg + 4 * (size_t)blockIdx.x;
+            n = f[3];
+            if (tid == 0) {
+                cl.f_lo = ((u64)f[1] << 32) | f[0];
+                cl.f_shift = f[2];
+            }
+            for (u32 i = tid; i < n; i += LIT_THREADS) cl.lbins[i] = 0;
+        } else if (P.bin_keys && P.wg_bins) {
             lo = P.wg_bins[2 * blockIdx.x];
             n = P.wg_bins[2 * blockIdx.x + 1] - lo;
+            for (u32 i = tid; i < n; i += LIT_THREADS) cl.lbins[i] = P.bin_counts[lo + i];
         }
         if (tid == 0) {
             cl.lb_lo = lo;
@@ -1642,7 +1837,6 @@ vsa_lit_scan(VsaLitParams P) {
             cl.nrec = 0;
             conf_fin = 0;
         }
-        for (u32 i = tid; i < n; i += LIT_THREADS) cl.lbins[i] = P.bin_counts[lo + i];
     }
     if (tid < 16) {
         q_tails[tid] = 0;
@@ -1654,7 +1848,9 @@ vsa_lit_scan(VsaLitParams P) {
         wg_ctr = 0;
         /* the schedule's feedback (runtime.hip xcd_feedback): this
          * workgroup's entry time */
-        if (P.wg_time) P.wg_time[gridDim.x + blockIdx.x] = t_entry;
+        if (P.wg_time) /* atomic: the fused finish's publisher reads it */
+            __hip_atomic_store(&P.wg_time[gridDim.x + blockIdx.x], t_entry, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
     if (tid < 8 * MAX_CONF_WAVES) prof_lds[tid] = 0;
     if (tid < 3) diag_lds[tid] = 0;
@@ -1680,7 +1876,7 @@ vsa_lit_scan(VsaLitParams P) {
                 prev = __hip_atomic_fetch_add(&conf_fin, 1u, __ATOMIC_ACQ_REL,
                                               __HIP_MEMORY_SCOPE_WORKGROUP);
             if (readfirstlane_u32(prev) + 1 == NC) {
-                const u32 lo = cl.lb_lo, n = cl.lb_n;
+                const u32 lo = cl.lb_lo, n = P.fin_keys ? 0u : cl.lb_n; /* fused: kept in LDS */
                 for (u32 i = lane; i < n; i += WAVE) P.bin_counts[lo + i] = cl.lbins[i];
                 /* the workgroup's record count: one add, not one per
                  * confirm step on a word every workgroup shares */
@@ -1695,8 +1891,9 @@ vsa_lit_scan(VsaLitParams P) {
                 lane == 0 ? t_entry : lane == 1 ? t_end : lane == 2 ? 1ull
                 : lane == 3 ? dg[0] : lane == 4 ? dg[1] : lane == 5 ? dg[2] : 0ull;
         }
-        return;
+        goto finish; /* the fused finish: one inlined copy for every wave */
     }
+    { /* the scanning waves */
 
     u32 bucket_mask = 0;
     if (!(P.dbg & 2)) {
@@ -2188,12 +2385,20 @@ vsa_lit_scan(VsaLitParams P) {
              * wave finished, and on which XCD (bits 60..63) */
             u32 xcc;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            P.wg_time[blockIdx.x] = ((unsigned long long)(xcc & 15u) << 60) |
-                                    (__builtin_amdgcn_s_memrealtime() & ((1ULL << 60) - 1));
+            __hip_atomic_store(&P.wg_time[blockIdx.x],
+                               ((unsigned long long)(xcc & 15u) << 60) |
+                                   (__builtin_amdgcn_s_memrealtime() & ((1ULL << 60) - 1)),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     if (P.counters && lane_id() == 0 && ncand_total)
         atomicAdd(&P.counters[2], (unsigned long long)ncand_total);
+    } /* the scanning waves */
+finish:
+    /* not Fat Teddy: at 128 VGPRs its scan has no room for the epilogue's
+     * registers (it spills); its launches keep vsa_bin_finish */
+    if constexpr (MODE != VSA_MODE_FAT)
+        if (P.fin_keys) fused_finish(P, cl, (u32 *)smem); /* every wave of the workgroup */
 }
 
 template __global__ void vsa_lit_scan<VSA_MODE_FDR4, false, false>(VsaLitParams);
@@ -2253,24 +2458,34 @@ __device__ __forceinline__ void publish_body(unsigned long long *ctr, unsigned l
 }
 
 /* publish_body for one wave (no workgroup barrier): wave 0 of
- * vsa_bin_finish's first workgroup publishes while its other waves sort */
+ * vsa_bin_finish's first workgroup publishes while its other waves sort.
+ * COH: the counters and feedback records are read with agent-scope atomic
+ * loads -- the fused finish publishes from inside the scan, whose other
+ * workgroups (on other XCDs) added them with agent-scope atomics */
+template <bool COH = false>
 __device__ __forceinline__ void publish_wave(unsigned long long *ctr, unsigned long long *h,
                                              unsigned long long seq, uint32_t nzero,
                                              const unsigned long long *fb = nullptr,
                                              unsigned long long *hfb = nullptr, u32 nfb = 0,
                                              uint64_t *pk = nullptr, uint64_t out_cap = 0) {
+    auto ld = [](const unsigned long long *p) -> unsigned long long {
+        if constexpr (COH)
+            return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            return *p;
+    };
     const u32 l = lane_id();
-    const unsigned long long v = l < 16 ? ctr[l] : 0ULL;
+    const unsigned long long v = l < 16 ? ld(&ctr[l]) : 0ULL;
     if (pk && l == 0) {
         /* the packed collective buffer's header (vsa_pack's rule): the
          * count, bit 62 when the records are not final -- the output
          * overflowed or a crowded bin left them to a rescan */
-        const unsigned long long ovf = ctr[VSA_CTR_BIN_OVERFLOW];
+        const unsigned long long ovf = ld(&ctr[VSA_CTR_BIN_OVERFLOW]);
         pk[0] = v | ((v > out_cap || ovf) ? (1ULL << 62) : 0ULL);
     }
     /* the scan's schedule-feedback record (device memory) rides along to
      * the host, before the sequence store releases it */
-    for (u32 i = l; i < nfb; i += WAVE) hfb[i] = fb[i];
+    for (u32 i = l; i < nfb; i += WAVE) hfb[i] = ld(&fb[i]);
     /* every read above before any zeroing below (one wave: program order
      * and a wait for the loads) */
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2284,6 +2499,145 @@ __device__ __forceinline__ void publish_wave(unsigned long long *ctr, unsigned l
         __threadfence_system();
         __hip_atomic_store(&h[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+/* The fused finish (VsaLitParams.fin_keys): the binned sort done by the
+ * scan's own workgroups at their end, instead of a vsa_bin_finish launch
+ * behind the scan (one kernel boundary and launch less per step).  The plan
+ * (plan.hip plan_fused) gives every workgroup its own local bins over the
+ * ends it reports (its segments' hull, disjoint from the others' and in
+ * workgroup order), so each record's bin is counted in LDS and every bin
+ * holds one workgroup's records only: no record crosses workgroups.  What
+ * does cross them is one word per workgroup, its record total tagged with
+ * the launch's epoch -- an agent-scope atomic, coherent across XCDs without
+ * the agent-scope release per workgroup a plain-store hand-off needs
+ * (round 3: step 1.42 ms, profiles/r03_sort_fused_trace.csv).
+ *   B1  every wave's records staged and counted, its counter adds done (the
+ *       barrier's release waits for them);
+ *   then every wave loads and sorts its 16 local bins in registers (when
+ *   sparse: below), while wave 0 first takes the local bins' prefix and
+ *   stores the total to fin_agg[w], then, after its own sort, looks back:
+ *   the totals of workgroups 0..w-1 (each dispatched before this one, so it
+ *   runs or has run and the wait ends);
+ *   B2  every wave writes its records at base + offset.  The last workgroup
+ *       publishes the counters (publish_wave<true>, agent-scope loads): when
+ *       its look-back is complete every other workgroup has passed B1, so
+ *       every counter add is done.
+ * A crowded local bin (> VSA_SORT_BIN_MAX) was flagged by the scan: its
+ * records are skipped here and the host rescans without bins. */
+__device__ __forceinline__ void fused_finish(const VsaLitParams &P, const ConfLds &cl, u32 *sc) {
+    __syncthreads();
+    const u32 tid = threadIdx.x, wave = tid / WAVE, lane = lane_id();
+    const u32 w = blockIdx.x, nb = cl.lb_n;
+    u32 *loff = sc;             /* [VSA_LBINS] each local bin's first position */
+    u32 *misc = sc + VSA_LBINS; /* [0] the workgroup's first output position */
+    static_assert(VSA_LBINS == 4 * WAVE, "one wave scans the local bins, 4 per lane");
+    if (wave == 0) {
+        u32 c[4], t4 = 0;
+        bool crowd = false;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const u32 i = 4 * lane + k;
+            const u32 v = i < nb ? cl.lbins[i] : 0u;
+            crowd |= v > VSA_SORT_BIN_MAX;
+            c[k] = v < VSA_SORT_BIN_MAX ? v : VSA_SORT_BIN_MAX;
+            t4 += c[k];
+        }
+        u32 tot;
+        u32 e = wave_excl_scan(t4, &tot);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            loff[4 * lane + k] = e;
+            e += c[k];
+        }
+        const bool cr = wave_any(crowd);
+        if (lane == 0)
+            __hip_atomic_store(&P.fin_agg[w],
+                               ((unsigned long long)P.fin_epoch << 32) |
+                                   (cr ? (1ULL << 31) : 0ULL) | tot,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    /* this wave's bins: [16 wave, 16 wave + 16) of the local bins.  When
+     * none holds more than 16 records (sparse records: the common case) they
+     * take one register sort of <= 4 passes, done before the look-back; a
+     * denser wave sorts after it, 4 bins at a time.  A crowded bin (flagged:
+     * the host rescans) leaves the wave's bins unsorted. */
+    const u32 lb = 16 * wave;
+    const u32 nbw = nb > lb ? (nb - lb < 16 ? nb - lb : 16u) : 0u;
+    u32 mmax = 0;
+    for (u32 j = 0; j < nbw; j++) mmax = cl.lbins[lb + j] > mmax ? cl.lbins[lb + j] : mmax;
+    const bool live = mmax != 0 && mmax <= VSA_SORT_BIN_MAX; /* wave-uniform */
+    u32 S = 2;
+    while (S < mmax && S < WAVE) S <<= 1;
+    const u32 per = WAVE / S;
+    const u32 np = (nbw + per - 1) / per; /* passes over the 16 bins */
+    const bool early = live && np <= 4;   /* every bin <= 16 records: one round */
+    const size_t row0 = (size_t)w * VSA_LBINS + lb;
+    Bins4 B0;
+    if (early) {
+        bins16_load(B0, P.bin_keys, P.bin_ids, row0, &cl.lbins[lb], nbw, S, 0, lane);
+        bins4_sort(B0, lane);
+    }
+    /* a round's records to base + their bin's offset + their rank; which bin
+     * and slot each lane holds is recomputed (fewer registers live across
+     * the look-back: the keys and ids only) */
+    auto put = [&](const Bins4 &B, u32 pass0, u32 base) {
+        const u32 j_l = lane / S;
+#pragma unroll
+        for (u32 p = 0; p < 4; p++) {
+            if (p >= B.npass) break; /* wave-uniform */
+            const u32 j = (pass0 + p) * per + j_l;
+            if (j >= nbw || B.r >= cl.lbins[lb + j]) continue;
+            const u64 o = (u64)base + loff[lb + j] + B.r;
+            if (o < P.out_cap) {
+                P.fin_keys[o] = B.k[p];
+                P.fin_ids[o] = B.id[p];
+            }
+            if (P.fin_pk && o < P.fin_pk_cap) {
+                P.fin_pk[1 + o] = B.k[p];
+                ((uint32_t *)(P.fin_pk + 1 + P.fin_pk_cap))[o] = B.id[p];
+            }
+        }
+    };
+    if (wave == 0) {
+        /* a bound on the wait (~1 s; never reached when the lower
+         * workgroups run): past it the launch is flagged as crowded, so the
+         * host discards its records and rescans without bins, instead of
+         * the grid never draining */
+        u32 base = 0, polls = 0;
+        for (u32 v0 = 0; v0 < w; v0 += WAVE) {
+            const u32 v = v0 + lane;
+            if (v < w) {
+                unsigned long long a = 0;
+                for (; polls < (1u << 20); polls++) {
+                    a = __hip_atomic_load(&P.fin_agg[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((u32)(a >> 32) == P.fin_epoch) break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                base += (u32)a & 0x7fffffffu;
+            }
+        }
+        if (wave_any(polls >= (1u << 20)) && lane == 0) flag_crowd(P);
+#pragma unroll
+        for (int dd = 32; dd >= 1; dd >>= 1) base += shfl_xor_u32(base, dd);
+        if (lane == 0) misc[0] = base;
+    }
+    __syncthreads();
+    const u32 base = misc[0];
+    if (early) {
+        put(B0, 0, base);
+    } else if (live) {
+        /* denser bins: rounds of 4 passes after the look-back */
+        for (u32 pass0 = 0; pass0 < np; pass0 += 4) {
+            Bins4 B;
+            bins16_load(B, P.bin_keys, P.bin_ids, row0, &cl.lbins[lb], nbw, S, pass0, lane);
+            bins4_sort(B, lane);
+            put(B, pass0, base);
+        }
+    }
+    if (w + 1 == gridDim.x && wave == 0)
+        publish_wave<true>(P.counters, P.fin_pub, P.fin_seq, 144u, P.wg_time, P.fin_hfb,
+                           P.fin_nfb, P.fin_pk, P.out_cap);
 }
 
 __global__ void __launch_bounds__(256) vsa_publish(unsigned long long *ctr,
@@ -2354,27 +2708,8 @@ __global__ void __launch_bounds__(1024) vsa_bin_finish(const uint32_t *counts, u
     for (int j = 0; j < 4; j++) mmax = m[j] > mmax ? m[j] : mmax;
     /* empty, or left to the library sort (a crowd: the host reruns) */
     const bool sorting = mmax != 0 && mmax <= VSA_SORT_BIN_MAX;
-    u32 S = 2;
-    while (S < mmax && S < WAVE) S <<= 1;
-    const u32 per = WAVE / S; /* bins per pass (1..32; >= 4 covers all 4 in one) */
-    const u32 j_l = lane / S, r = lane % S;
-    u64 k[4];
-    u32 id[4], jb[4];
-    bool ok[4];
-    /* every pass's loads issued together: the records staged in the bins.
-     * Unconditional (an address inside this wave's 4 bins for every lane,
-     * the unused ones masked at the sort): a load under a divergent branch
-     * makes the compiler wait for it before the prefix reduction below */
-#pragma unroll
-    for (u32 p = 0; p < 4; p++) {
-        const u32 j = p * per + j_l;
-        jb[p] = j;
-        const u32 mj = j == 0 ? m[0] : j == 1 ? m[1] : j == 2 ? m[2] : j == 3 ? m[3] : 0u;
-        ok[p] = sorting && p * per < 4 && r < mj;
-        const size_t q = (size_t)(b0 + lb + (j & 3)) * VSA_SORT_BIN_MAX + r;
-        k[p] = skeys[q];
-        id[p] = sids[q];
-    }
+    Bins4 B;
+    bins4_load(B, skeys, sids, (size_t)(b0 + lb), m, sorting, lane);
 #pragma unroll
     for (int dd = 32; dd >= 1; dd >>= 1) s += shfl_xor_u32(s, dd);
     if (lane == 0) red[wv] = s;
@@ -2394,43 +2729,11 @@ __global__ void __launch_bounds__(1024) vsa_bin_finish(const uint32_t *counts, u
     __syncthreads();
     if (blockIdx.x == 0 && wv == 0) publish_wave(ctr, h, seq, 144u, fb, hfb, nfb, pk, out_cap);
     if (!sorting) return;
-#pragma unroll
-    for (u32 p = 0; p < 4; p++) {
-        if (p * per >= 4) break; /* wave-uniform */
-        u64 kk = ok[p] ? k[p] : ~0ULL;
-        u32 ii = ok[p] ? id[p] : 0u;
-        for (u32 size = 2; size <= S; size <<= 1) {
-            for (u32 jj = size >> 1; jj > 0; jj >>= 1) {
-                const u32 plo = shfl_xor_u32((u32)kk, (int)jj);
-                const u32 phi = shfl_xor_u32((u32)(kk >> 32), (int)jj);
-                const u32 pid = shfl_xor_u32(ii, (int)jj);
-                const u64 pk = ((u64)phi << 32) | plo;
-                /* ascending within each S-lane segment: the last merge is
-                 * ascending everywhere, earlier ones alternate */
-                const bool up = size == S || (lane & size) == 0;
-                const bool lower = (lane & jj) == 0;
-                const bool take = (lower == up) ? (pk < kk) : (pk > kk);
-                if (take) {
-                    kk = pk;
-                    ii = pid;
-                }
-            }
-        }
-        if (ok[p]) {
-            const u64 o = (u64)off[lb + jb[p]] + r;
-            if (o < out_cap) {
-                okeys[o] = kk;
-                oids[o] = ii;
-            }
-            /* fused vsa_pack (vsa_scan_plan_pack): the records also go
-             * straight into the collective's buffer [header | keys (pk_cap)
-             * | ids (pk_cap x u32)], no pack launch behind this one */
-            if (pk && o < pk_cap) {
-                pk[1 + o] = kk;
-                ((uint32_t *)(pk + 1 + pk_cap))[o] = ii;
-            }
-        }
-    }
+    bins4_sort(B, lane);
+    /* fused vsa_pack (vsa_scan_plan_pack): the records also go straight into
+     * the collective's buffer, no pack launch behind this one */
+    const u32 o4[4] = {off[lb], off[lb + 1], off[lb + 2], off[lb + 3]};
+    bins4_write(B, o4, okeys, oids, out_cap, pk, pk_cap);
 }
 
 /* A binned scan's sorted records packed for a collective, on the device

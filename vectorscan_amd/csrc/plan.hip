@@ -26,6 +26,8 @@ constexpr uint32_t PLAN_MAX_BLOCKS = VSA_MAX_BLOCKS; /* 20-bit block field of th
  * order -- every bin lying wholly inside hull b holds only workgroup b's
  * records.  Appended to segblk after the list bounds: 2 words per
  * workgroup, the bins [lo, hi) (hi - lo <= VSA_LBINS; 0, 0 = none). */
+void plan_fused(BatchPlan &pl, const VsaBlock *blocks, int64_t mis);
+
 void plan_wg_bins(BatchPlan &pl, const VsaBlock *blocks, int64_t mis) {
     const uint32_t G = pl.grid;
     const uint64_t base = 4 * pl.nsegs;
@@ -75,6 +77,66 @@ void plan_wg_bins(BatchPlan &pl, const VsaBlock *blocks, int64_t mis) {
         }
         pl.segblk.push_back(lo);
         pl.segblk.push_back(hi);
+    }
+    plan_fused(pl, blocks, mis);
+}
+
+/* The fused finish's local bins (kernels.hip fused_finish), appended to
+ * segblk after the owned bins: 4 words per workgroup -- the lowest end it
+ * can report (lo, hi word), the local bin shift, the local bins (<=
+ * VSA_LBINS) -- over the ends its segments report: [base + max(start, rlo),
+ * base + len) of each block, cut to a part's KiB range: 256 local bins
+ * per workgroup, 4x finer than the global bins at 256 workgroups (fewer
+ * crowds; a wave sorts its 16 bins in one pass when they are sparse).
+ * Eligible (fin_ok)
+ * when these hulls are disjoint and ascend with the workgroup index -- then
+ * every record's bin is its own workgroup's, the workgroups' records follow
+ * each other in workgroup order in the sorted output, and a workgroup's
+ * look-back waits only for workgroups dispatched before it -- and the grid
+ * has >= 64 workgroups (local bins then at least as fine as the global
+ * ones). */
+void plan_fused(BatchPlan &pl, const VsaBlock *blocks, int64_t mis) {
+    const uint32_t G = pl.grid;
+    const uint64_t base = 4 * pl.nsegs;
+    pl.fin_ok = G >= 64 && G <= VSA_FIN_MAX_GRID;
+    int64_t prev_hi = INT64_MIN;
+    for (uint32_t b = 0; b < G; b++) {
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        auto add = [&](const VsaBlock &B, int64_t l, int64_t h) {
+            l = std::max<int64_t>(l, (int64_t)(B.base + std::max<uint64_t>(B.start, (uint64_t)B.rlo)));
+            h = std::min<int64_t>(h, (int64_t)(B.base + B.len));
+            if (h > l) {
+                lo = std::min(lo, l);
+                hi = std::max(hi, h);
+            }
+        };
+        for (uint32_t sg = pl.segblk[base + b]; sg < pl.segblk[base + b + 1]; sg++) {
+            const uint32_t *d = &pl.segblk[4 * (uint64_t)sg];
+            const uint32_t first = d[0] & 0xffffffu, cnt = d[0] >> 24;
+            if (cnt == 0) {
+                const VsaBlock &B = blocks[first];
+                const int64_t s0 = B.org - mis + ((int64_t)d[1] << 10);
+                add(B, s0, s0 + ((int64_t)d[2] << 10));
+            } else {
+                for (uint32_t k = 0; k < cnt; k++) {
+                    const VsaBlock &B = blocks[first + k];
+                    add(B, INT64_MIN, INT64_MAX);
+                }
+            }
+        }
+        uint32_t w[4] = {0, 0, 0, 0};
+        if (hi > lo) {
+            if (lo < prev_hi) pl.fin_ok = false;
+            prev_hi = hi;
+            const uint64_t span = (uint64_t)(hi - lo);
+            uint32_t s = 0;
+            while (((span - 1) >> s) + 1 > VSA_LBINS) s++;
+            w[0] = (uint32_t)(uint64_t)lo;
+            w[1] = (uint32_t)((uint64_t)lo >> 32);
+            w[2] = s;
+            w[3] = (uint32_t)(((span - 1) >> s) + 1);
+        }
+        pl.segblk.insert(pl.segblk.end(), w, w + 4);
     }
 }
 
@@ -383,6 +445,7 @@ int vsa_plan_create(vsa_ctx_t *c, const uint8_t *d_data, const uint64_t *offsets
     p->grid = pl.grid;
     p->end_bits = pl.end_bits;
     p->bytes = pl.bytes;
+    p->fin_ok = pl.fin_ok;
     const uint64_t *ins[5] = {offsets, lens, starts, hlens, report_lo};
     for (int k = 0; k < 5; k++)
         if (ins[k]) p->in[k].assign(ins[k], ins[k] + nblocks);
@@ -477,6 +540,7 @@ int refresh_plan(vsa_ctx *c, const vsa_db *db, vsa_plan *p) {
                              hipMemcpyHostToDevice, c->stream));
     p->segs = pl.nsegs;
     p->grid = pl.grid;
+    p->fin_ok = pl.fin_ok;
     /* the weights it follows now (only once applied: a failed rebuild is
      * tried again at the next scan) */
     p->fb_key = key;
@@ -494,7 +558,7 @@ int vsa_scan_plan(vsa_ctx_t *c, const vsa_db_t *db, const vsa_plan_t *p, uint32_
     uint64_t dummy;
     return launch_planned(c, db, p->d_data, p->d_blocks, p->d_segblk, p->nb, p->segs,
                           p->grid, p->end_bits, p->bytes, flags,
-                          n_matches ? n_matches : &dummy);
+                          n_matches ? n_matches : &dummy, p->fin_ok);
 }
 
 int vsa_scan_plan_pack(vsa_ctx_t *c, const vsa_db_t *db, const vsa_plan_t *p, void *d_dst,
@@ -506,7 +570,7 @@ int vsa_scan_plan_pack(vsa_ctx_t *c, const vsa_db_t *db, const vsa_plan_t *p, vo
     c->launch.pack_cap = cap;
     uint64_t n = 0;
     int r = launch_planned(c, db, p->d_data, p->d_blocks, p->d_segblk, p->nb, p->segs, p->grid,
-                           p->end_bits, p->bytes, VSA_SCAN_ASYNC, &n);
+                           p->end_bits, p->bytes, VSA_SCAN_ASYNC, &n, p->fin_ok);
     /* not consumed (no segments, or a launch without the binned sort): the
      * records are packed the separate way, after the host completes it */
     const bool fused = c->launch.pack_dst == nullptr && c->pending;

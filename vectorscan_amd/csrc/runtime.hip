@@ -386,6 +386,43 @@ void take_feedback(vsa_ctx *c) {
 
 unsigned long long *g_wave_log = nullptr;
 
+/* the fused finish's default for new contexts: VSA_FUSED_FINISH=1 turns
+ * it on (vsa_ctx_set_fused_finish per context).  Off by default: measured
+ * against the vsa_bin_finish launch it shortens the pipelined step by 1-2
+ * us (0.2-0.9 %) but lengthens the scan kernel by 4-5 us
+ * (profiles/r06/r06l_fused_finish_ab3.jsonl) */
+bool fused_finish_default() {
+    static const bool v = env_int("VSA_FUSED_FINISH", 0) != 0;
+    return v;
+}
+
+/* the fused finish's buffers: local-bin staging for `grid` workgroups
+ * (grown, never shrunk), the totals (zero: no epoch matches) and the ticket */
+int ensure_fstage(vsa_ctx *c, uint32_t grid) {
+    Workspace &w = c->ws;
+    if (grid > VSA_FIN_MAX_GRID) return VSA_E_INVALID;
+    if (!w.d_fagg) {
+        VSA_CHECK(hipMalloc(&w.d_fagg, VSA_FIN_MAX_GRID * sizeof(unsigned long long)));
+        VSA_CHECK(hipMalloc(&w.d_fticket, 64));
+        VSA_CHECK(hipMemsetAsync(w.d_fagg, 0, VSA_FIN_MAX_GRID * sizeof(unsigned long long),
+                                 c->stream));
+        VSA_CHECK(hipMemsetAsync(w.d_fticket, 0, 64, c->stream));
+    }
+    if (grid > w.fstage_grid) {
+        if (w.d_fstage) {
+            /* the previous launch may still read the old staging */
+            VSA_CHECK(hipStreamSynchronize(c->stream));
+            VSA_CHECK(hipFree(w.d_fstage));
+            w.d_fstage = nullptr;
+            w.fstage_grid = 0;
+        }
+        VSA_CHECK(hipMalloc(&w.d_fstage, (size_t)grid * VSA_LBINS * VSA_SORT_BIN_MAX *
+                                             (sizeof(uint64_t) + sizeof(uint32_t))));
+        w.fstage_grid = grid;
+    }
+    return VSA_OK;
+}
+
 int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb,
                        uint64_t nsegs);
 
@@ -398,14 +435,23 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
     /* not for the drop-in calls, whose few records the host sorts (a
      * larger result takes the library sort) */
     c->launch.bins = use_bins(c) && !(c->launch.flags & SCAN_HOST_SORT_SMALL);
-    if (c->launch.bins && !c->ws.d_bstage)
-        VSA_CHECK(hipMalloc(&c->ws.d_bstage, (size_t)VSA_SORT_BINS * VSA_SORT_BIN_MAX *
-                                                 (sizeof(uint64_t) + sizeof(uint32_t))));
-    const uint32_t par = c->bin_par;
-    if (c->launch.bins && !c->bins_clean[par])
-        VSA_CHECK(hipMemsetAsync(bin_counts_of(c, par), 0, VSA_SORT_BINS * sizeof(uint32_t),
-                                 c->stream));
-    c->bins_clean[par] = false;
+    /* the fused finish: the scan sorts its records itself (kernels.hip
+     * fused_finish) when the plan's local bins allow it (plan_fused) */
+    c->launch.fused = c->launch.bins && c->launch.fin_ok && c->launch.db &&
+                      !c->launch.db->split && c->launch.db->mode != VSA_MODE_FAT &&
+                      c->fused_finish;
+    if (c->launch.fused) {
+        if (int r = ensure_fstage(c, c->launch.grid)) return r;
+    } else {
+        if (c->launch.bins && !c->ws.d_bstage)
+            VSA_CHECK(hipMalloc(&c->ws.d_bstage, (size_t)VSA_SORT_BINS * VSA_SORT_BIN_MAX *
+                                                     (sizeof(uint64_t) + sizeof(uint32_t))));
+        const uint32_t par = c->bin_par;
+        if (c->launch.bins && !c->bins_clean[par])
+            VSA_CHECK(hipMemsetAsync(bin_counts_of(c, par), 0, VSA_SORT_BINS * sizeof(uint32_t),
+                                     c->stream));
+        c->bins_clean[par] = false;
+    }
     /* drop-in calls (a few records, sorted by the host) skip the kernel
      * timing and get their counters and records published (no copies) */
     const bool small = (c->launch.flags & SCAN_HOST_SORT_SMALL) != 0;
@@ -425,6 +471,14 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
         VSA_CHECK(hipGetLastError());
         c->launch.published = true;
         c->launch.dev_sort = false;
+        c->ctr_clean = true;
+        return VSA_OK;
+    }
+    if (c->launch.fused) {
+        /* sorted, packed and published by the scan itself */
+        c->launch.pack_dst = nullptr;
+        c->launch.dev_sort = true;
+        c->launch.published = true;
         c->ctr_clean = true;
         return VSA_OK;
     }
@@ -465,6 +519,30 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.counters = w.d_counters;
     P.wg_time = c->fb.armed >= 0 ? (c->fb.dev ? c->fb.d_rec : c->fb.d) : nullptr;
     P.wave_log = g_wave_log;
+    if (c->launch.fused) {
+        /* the fused finish (kernels.hip fused_finish): local bins in the
+         * fused staging, the plan's local-bin table after its owned bins,
+         * sorted records into buffer 1 (as vsa_bin_finish), published by the
+         * last workgroup out with this launch's sequence */
+        const uint32_t G = c->launch.grid;
+        P.bin_keys = (uint64_t *)w.d_fstage;
+        P.bin_ids = (uint32_t *)(w.d_fstage + (size_t)w.fstage_grid * VSA_LBINS *
+                                                  VSA_SORT_BIN_MAX * sizeof(uint64_t));
+        P.bin_counts = nullptr;
+        P.fin_wg = c->launch.d_segblk + 4 * nsegs + G + 1 + 2 * (size_t)G;
+        P.fin_keys = w.d_keys[1];
+        P.fin_ids = w.d_ids[1];
+        P.fin_agg = w.d_fagg;
+        P.fin_ticket = w.d_fticket;
+        P.fin_seq = ++c->pub_seq;
+        P.fin_epoch = (uint32_t)(P.fin_seq % 0xfffffffeULL) + 1u;
+        P.fin_pub = w.d_pub;
+        const bool fbd = c->fb.armed >= 0 && c->fb.dev;
+        P.fin_hfb = fbd ? c->fb.d : nullptr;
+        P.fin_nfb = fbd ? 2 * G : 0u;
+        P.fin_pk = (uint64_t *)c->launch.pack_dst;
+        P.fin_pk_cap = c->launch.pack_cap;
+    }
     {
         const char *e = getenv("VSA_DEBUG_FLAGS");
         P.dbg = e ? (uint32_t)atoi(e) : 0u;
@@ -608,7 +686,13 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
         fprintf(stderr, "vsa: %llu queued confirm keys differ from HBM\n",
                 (unsigned long long)w.h_counters[3]);
     }
-    if (!(flags & SCAN_HOST_SORT_SMALL)) {
+    if (c->launch.fused) {
+        /* the scan published from inside itself: its end event may not be
+         * written yet, so the kernel time is read when asked for
+         * (vsa_scan_kernel_ms) */
+        c->kms_stale = true;
+    } else if (!(flags & SCAN_HOST_SORT_SMALL)) {
+        c->kms_stale = false;
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_kernel_ms = ms;
         /* a not-yet-observed event (the published path completes on the
@@ -668,7 +752,8 @@ int finish_pending(vsa_ctx *c) {
 /* launch a planned batch whose tables are on the device */
 int launch_planned(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, const VsaBlock *d_blocks,
                    const uint32_t *d_segblk, uint32_t nb, uint64_t segs,
-                   uint32_t grid, int end_bits, uint64_t bytes, uint32_t flags, uint64_t *n_out) {
+                   uint32_t grid, int end_bits, uint64_t bytes, uint32_t flags, uint64_t *n_out,
+                   bool fin_ok) {
     int r;
     if ((r = ensure_out(c, 1)) != VSA_OK) return r;
     if (segs == 0) {
@@ -687,6 +772,7 @@ int launch_planned(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, const Vs
     c->launch.end_bits = end_bits;
     c->launch.bytes = bytes;
     c->launch.flags = flags;
+    c->launch.fin_ok = fin_ok;
     if ((r = launch_scan(c, db, d_data, nb, segs)) != VSA_OK) return r;
     if (flags & VSA_SCAN_ASYNC) {
         c->pending = true;
@@ -752,7 +838,7 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         M.valid = true;
     }
     int rr = launch_planned(c, db, d_data, c->ws.d_blocks, c->ws.d_segblk, nb, pl.nsegs,
-                          pl.grid, pl.end_bits, pl.bytes, flags, n_out);
+                          pl.grid, pl.end_bits, pl.bytes, flags, n_out, pl.fin_ok);
     auto T3 = std::chrono::steady_clock::now();
     /* diagnostic: host-side cost of a per-call plan (tools/exp_host.py) */
     static const bool timing = getenv("VSA_HOST_TIMING") != nullptr;
@@ -800,6 +886,7 @@ int vsa_ctx_create(int device, vsa_ctx_t **out) {
     if (!out) return VSA_E_INVALID;
     std::unique_ptr<vsa_ctx> c(new vsa_ctx());
     c->device = device;
+    c->fused_finish = fused_finish_default();
     VSA_CHECK(hipSetDevice(device));
     int cus = 0;
     VSA_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
@@ -846,6 +933,9 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (w.d_counters) (void)hipFree(w.d_counters);
     if (w.d_bins) (void)hipFree(w.d_bins);
     if (w.d_bstage) (void)hipFree(w.d_bstage);
+    if (w.d_fstage) (void)hipFree(w.d_fstage);
+    if (w.d_fagg) (void)hipFree(w.d_fagg);
+    if (w.d_fticket) (void)hipFree(w.d_fticket);
     if (w.h_counters) (void)hipHostFree(w.h_counters);
     if (w.h_pub) (void)hipHostFree(w.h_pub);
     if (c->fb.h) (void)hipHostFree(c->fb.h);
@@ -872,6 +962,7 @@ int vsa_ctx_create_shared(vsa_ctx_t *base, vsa_ctx_t **out) {
     (void)hipStreamSynchronize(c->stream);
     c->stream_ref = base->stream_ref; /* releases the stream it made */
     c->reserved_cus = base->reserved_cus;
+    c->fused_finish = base->fused_finish;
     c->stream = base->stream;
     *out = c;
     return VSA_OK;
@@ -1434,9 +1525,39 @@ int vsa_scan_debug_counters(vsa_ctx_t *c, uint64_t out[16]) {
     return VSA_OK;
 }
 
-double vsa_scan_kernel_ms(vsa_ctx_t *c) { return c ? c->last_kernel_ms : 0.0; }
+double vsa_scan_kernel_ms(vsa_ctx_t *c) {
+    if (!c) return 0.0;
+    if (c->kms_stale) {
+        /* the end event of a fused-finish scan: polled, as wait_stream (a
+         * blocking wait wakes late and would hold up the caller's next
+         * launch) */
+        c->kms_stale = false;
+        const auto t0 = std::chrono::steady_clock::now();
+        hipError_t e;
+        while ((e = hipEventQuery(c->ev1)) == hipErrorNotReady) {
+            (void)hipGetLastError();
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+                e = hipEventSynchronize(c->ev1);
+                break;
+            }
+        }
+        float ms = 0.f;
+        if (e == hipSuccess && hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess)
+            c->last_kernel_ms = ms;
+        (void)hipGetLastError();
+    }
+    return c->last_kernel_ms;
+}
 
 uint64_t vsa_scan_launches(vsa_ctx_t *c) { return c ? c->lit_launches : 0; }
+
+int vsa_scan_last_fused(vsa_ctx_t *c) { return c && c->launch.fused ? 1 : 0; }
+
+int vsa_ctx_set_fused_finish(vsa_ctx_t *c, int on) {
+    if (!c) return VSA_E_INVALID;
+    c->fused_finish = on != 0;
+    return VSA_OK;
+}
 
 /* The box's streaming-read ceiling over a device buffer (bench.py's
  * roofline.peak_measured): vsa_read_probe reads the first len & ~64 KiB
@@ -1563,6 +1684,7 @@ int vsa_class_scan(vsa_ctx_t *c, const uint8_t cls[32], const uint8_t *cls2,
                              hipMemcpyDeviceToHost, c->stream));
     VSA_CHECK(hipStreamSynchronize(c->stream));
     {
+        c->kms_stale = false;
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_kernel_ms = ms;
         /* a not-ready event status is not an error: it must not stay the

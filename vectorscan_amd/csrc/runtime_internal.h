@@ -118,6 +118,14 @@ struct Workspace {
     size_t tab_cap = 0;           /* bytes of both */
     uint32_t *d_segblk = nullptr; /* block of each segment (inside d_blocks) */
     uint32_t *h_segblk = nullptr;
+    /* the fused finish (kernels.hip fused_finish): staged records in local
+     * bins, VSA_LBINS x VSA_SORT_BIN_MAX per workgroup (keys, then ids), for
+     * fstage_grid workgroups; the workgroups' epoch-tagged totals; the
+     * finished-workgroup ticket (zero between launches) */
+    uint8_t *d_fstage = nullptr;
+    uint32_t fstage_grid = 0;
+    unsigned long long *d_fagg = nullptr; /* VSA_FIN_MAX_GRID words */
+    uint32_t *d_fticket = nullptr;
 };
 
 
@@ -141,6 +149,9 @@ struct BatchPlan {
     uint32_t grid = 0; /* workgroups (one segment list each) */
     int end_bits = 0;
     uint64_t bytes = 0; /* scanned bytes (len - start summed) */
+    /* the fused finish's local-bin table follows the owned bins in segblk
+     * and is usable (plan_fused) */
+    bool fin_ok = false;
     std::vector<int64_t> spans, live; /* build_plan scratch */
 };
 
@@ -177,6 +188,8 @@ struct vsa_ctx {
         bool dev_sort = false; /* ... and the binned sort is queued behind it */
         bool published = false; /* ... and vsa_publish after it (finish_scan
                                    polls h_pub instead of copying) */
+        bool fin_ok = false;    /* the plan allows the fused finish */
+        bool fused = false;     /* ... and this launch sorts inside the scan */
         uint64_t bytes = 0; /* scanned bytes (len - start summed) */
         const VsaBlock *d_blocks = nullptr;
         const uint32_t *d_segblk = nullptr;
@@ -195,6 +208,10 @@ struct vsa_ctx {
     hipEvent_t ev_done = nullptr; /* polled by wait_stream */
     hipEvent_t ev_rec = nullptr;  /* records_fetch_async's copies done */
     double last_kernel_ms = 0.0;
+    bool kms_stale = false; /* last_kernel_ms not yet read for the last scan */
+    /* eligible launches sort inside the scan kernel (kernels.hip
+     * fused_finish; vsa_ctx_set_fused_finish, default VSA_FUSED_FINISH) */
+    bool fused_finish = false;
     uint32_t bin_skip = 0;   /* launches left without the binned sort */
     /* the bin_skip a crowded bin sets: 16, x4 for every crowded binned
      * launch in a row (up to 4096), back to 16 after a binned launch that
@@ -267,6 +284,7 @@ struct vsa_plan {
     int end_bits = 0;
     uint64_t bytes = 0;
     uint32_t rebuilds = 0; /* segment maps rebuilt for the feedback weights */
+    bool fin_ok = false;   /* its map allows the fused finish (plan_fused) */
     VsaBlock *d_blocks = nullptr;
     uint32_t *d_segblk = nullptr;
     /* schedule feedback: the inputs (to rebuild the segment map with the
@@ -362,6 +380,7 @@ uint32_t steal_min();
 int bits_for(uint64_t v);
 uint32_t bin_shift_for(int end_bits);
 bool xcd_feedback_on();
+bool fused_finish_default();
 int fb_set_of(const vsa_db *db);
 uint64_t fb_key_of(const vsa_ctx *c, const vsa_db *db);
 bool feedback_update(vsa_ctx::FbSet &F, const volatile unsigned long long *h, uint32_t G);
@@ -370,7 +389,8 @@ int finish_pending(vsa_ctx *c);
 int complete_scan(vsa_ctx *c, uint64_t *n_out);
 int launch_planned(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, const VsaBlock *d_blocks,
                    const uint32_t *d_segblk, uint32_t nb, uint64_t segs, uint32_t grid,
-                   int end_bits, uint64_t bytes, uint32_t flags, uint64_t *n_out);
+                   int end_bits, uint64_t bytes, uint32_t flags, uint64_t *n_out,
+                   bool fin_ok = false);
 int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
                      const uint64_t *offs, const uint64_t *lens, const uint64_t *starts,
                      uint32_t nb, uint32_t flags, uint64_t *n_out,
