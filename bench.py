@@ -45,6 +45,13 @@ import time
 
 import numpy as np
 
+# Kernel arguments in device memory, not host memory: the scan kernel reads
+# its ~600-byte argument block at start, and from host memory that is a
+# PCIe round trip per dependent read (measured 2.6 us off the 512 MiB rank
+# step, profiles/r06/r06n_gap_knobs.jsonl).  A runtime setting read when
+# HIP initializes, so set before any GPU call; an explicit setting wins.
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -300,7 +307,9 @@ def run(args):
             if rank == 0:
                 st["keys"], st["ids"] = sl["pg"].merged(cl)
             n = int(sum(cl))
-        kms.append(c.kernel_ms())
+        km = c.kernel_ms()
+        if km >= 0:  # a timed launch (vsa_ctx_set_timing)
+            kms.append(km)
         return n
 
     def run_steps(k_steps):
@@ -340,6 +349,12 @@ def run(args):
         ceiling = ctx.read_ceiling(data.data_ptr(), data.numel(), 5)
     if dist is not None:
         dist.barrier()
+    # from here on only every 4th launch of a context carries the timing
+    # events (they cost ~4 us per dispatch at 512 MiB: a rank's step is
+    # timed by the wall clock, the kernel average by the sampled launches)
+    every = max(1, min(4, args.steps // 4))
+    for sl in slots:
+        sl["ctx"].timing(every)
     run_steps(args.warmup)
 
     def barrier():

@@ -341,8 +341,13 @@ uint64_t vsa_scan_candidates(vsa_ctx_t *ctx);
  * and counts: [8] gather rounds, [9] chunk entries, [10] expansion rounds,
  * [11] confirm batches. */
 int vsa_scan_debug_counters(vsa_ctx_t *ctx, uint64_t out[16]);
-/* Device time (ms, hipEvents on the scan stream) of the last scan kernel. */
+/* Device time (ms, hipEvents on the scan stream) of the last scan kernel;
+ * -1 when that launch carried no timing events (vsa_ctx_set_timing). */
 double vsa_scan_kernel_ms(vsa_ctx_t *ctx);
+/* Time every `every`-th literal-scan launch of this context (1, the default:
+ * all; 0: none).  The events ride on the dispatch and cost a few us per
+ * launch; a pipelined caller can sample.  No reference counterpart. */
+int vsa_ctx_set_timing(vsa_ctx_t *ctx, uint32_t every);
 /* Literal-scan launches this context has queued (every rescan of an
  * output overflow or a crowded sort bin counts): a diagnostic of the rerun
  * cost, no reference counterpart. */

@@ -789,6 +789,44 @@ def test_gpu_fused_finish():
         c0.close()
 
 
+def test_gpu_sampled_timing():
+    """vsa_ctx_set_timing: every 3rd launch carries the kernel-timing events
+    (kernel_ms > 0), the others report -1; 0 times none; results are the
+    same whatever is timed, with the binned sort and the fused finish."""
+    rng = random.Random(37)
+    blob = vsa.hwlm_build(rand_lits(rng, 200, minlen=4, maxlen=8))
+    host = np.frombuffer(rand_data(rng, 8 << 20), np.uint8).copy()
+    c = vsa.Context(0)
+    try:
+        d = c.malloc(len(host))
+        c.h2d(d, host)
+        db = vsa.Database(c, blob)
+        pl = c.plan(d, [0, 4 << 20], [4 << 20, 4 << 20])
+        want = c.results(c.scan_plan(db, pl))
+        assert c.kernel_ms() > 0
+        for fused in (False, True):
+            c.fused_finish(fused)
+            c.timing(3)
+            timed = []
+            for _ in range(9):
+                got = c.results(c.scan_plan(db, pl))
+                assert np.array_equal(got["key"], want["key"])
+                assert np.array_equal(got["id"], want["id"])
+                timed.append(c.kernel_ms() > 0)
+            assert sum(timed) == 3, timed
+            c.timing(0)
+            c.scan_plan(db, pl)
+            assert c.kernel_ms() == -1.0
+            c.timing(1)
+            c.scan_plan(db, pl)
+            assert c.kernel_ms() > 0
+        pl.close()
+        db.close()
+        c.free(d)
+    finally:
+        c.close()
+
+
 def test_gpu_reserved_cus_same_records():
     """vsa_ctx_set_reserved_cus (CUs left free beside the scan's persistent
     grid; measured, not used by bench.py): plans on a context with 1 or 7 CUs reserved --

@@ -25,6 +25,9 @@ import time
 
 import numpy as np
 
+# kernel arguments in device memory, as bench.py (read when HIP initializes)
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 

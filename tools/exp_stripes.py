@@ -11,7 +11,8 @@ launch / by the sort launch itself (vsa_scan_plan_pack); "side" adds a
 stand-in for the collective (a one-workgroup copy of the packed buffer's
 header on another stream, after the scan) to show what the persistent grid does to it, with
 EXP_RESERVE=n CUs left free (vsa_ctx_set_reserved_cus).
-EXP_RANKS / EXP_MODES (comma lists) limit the rows.
+EXP_RANKS / EXP_MODES (comma lists) limit the rows; EXP_TIMING=n times every
+n-th launch of the pipelined modes (bench.py uses 4).
   python tools/exp_stripes.py [steps] [warmup]"""
 import json
 import os
@@ -31,6 +32,9 @@ ctxs = [vsa.Context(0)]
 # EXP_RESERVE=n: the grid leaves n CUs free (measured, not used by bench.py)
 ctxs[0].reserve_cus(int(os.environ.get("EXP_RESERVE", "0")))
 ctxs.append(vsa.Context(share_stream_with=ctxs[0]))
+# EXP_TIMING=n: the pipelined modes time every n-th launch per context (as
+# bench.py); their kernel_ms averages the timed ones
+t_every = int(os.environ.get("EXP_TIMING", "1"))
 lits = bench.make_literals(5000, seed=12)
 db = vsa.Database(ctxs[0], vsa.hwlm_build(lits))
 total = 4 << 30
@@ -57,6 +61,8 @@ for n in ranks:
     evs = [torch.cuda.Event() for _ in ctxs]
     for mode in modes:
         ks, counts = [], []
+        for c in ctxs:
+            c.timing(1 if mode == "sync" else t_every)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         if mode == "sync":
@@ -116,6 +122,7 @@ for n in ranks:
             ks.append(ctxs[(steps - 1) % 2].kernel_ms())
         torch.cuda.synchronize()
         st = (time.perf_counter() - t0) / steps * 1e3
+        ks = [x for x in ks if x >= 0] or [float("nan")]
         k = sum(ks) / len(ks)
         print(json.dumps({"lib": os.environ.get("VSA_LIB_VARIANT", ""), "ranks": n, "mode": mode, "rank_bytes": cuts[1] - cuts[0],
                           "windows": len(wins), "step_ms": round(st, 4),

@@ -166,6 +166,7 @@ _sig("vsa_scan_kernel_ms", ctypes.c_double, ctypes.c_void_p)
 _sig("vsa_scan_launches", ctypes.c_uint64, ctypes.c_void_p)
 _sig("vsa_scan_last_fused", ctypes.c_int, ctypes.c_void_p)
 _sig("vsa_ctx_set_fused_finish", ctypes.c_int, ctypes.c_void_p, ctypes.c_int)
+_sig("vsa_ctx_set_timing", ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32)
 _sig("vsa_ctx_set_reserved_cus", ctypes.c_int, ctypes.c_void_p, ctypes.c_int)
 _sig("vsa_read_ceiling", ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
      ctypes.c_uint32, ctypes.POINTER(ctypes.c_double), _u64p)
@@ -808,6 +809,11 @@ class Context:
     def launches(self):
         """Literal-scan launches queued on this context (reruns included)."""
         return lib.vsa_scan_launches(self.ptr)
+
+    def timing(self, every=1):
+        """Time every `every`-th literal-scan launch (vsa_ctx_set_timing;
+        kernel_ms() is -1 after an untimed one)."""
+        _check(lib.vsa_ctx_set_timing(self.ptr, every))
 
     def fused_finish(self, on=True):
         """Sort inside the scan kernel when the plan allows it

@@ -167,14 +167,12 @@ struct VsaLitParams {
                                      hi word), local bin shift, local bins */
     uint64_t *fin_keys;           /* the sorted records (out_cap) */
     uint32_t *fin_ids;
-    unsigned long long *fin_agg;  /* [b] = epoch << 32 | crowded << 31 |
-                                     workgroup b's records */
-    uint32_t *fin_ticket;         /* workgroups finished (the last resets it) */
+    unsigned long long *fin_agg;  /* [2b] = epoch << 32 | crowded << 31 |
+                                     workgroup b's records, [2b + 1] = epoch
+                                     << 32 | its confirm candidates */
     uint32_t fin_epoch;           /* this launch's tag in fin_agg (nonzero) */
-    uint32_t fin_nfb;             /* feedback words published (2 x grid, or 0) */
     unsigned long long *fin_pub;  /* host publish block (vsa_publish layout) */
     unsigned long long fin_seq;
-    unsigned long long *fin_hfb;  /* feedback records' host copy */
     uint64_t *fin_pk;             /* packed collective buffer (or null) */
     uint64_t fin_pk_cap;
 };

@@ -403,6 +403,8 @@ struct ConfLds {
      * (lb_lo = 0) */
     u64 f_lo;
     u32 f_shift;
+    u32 f_bad;  /* a record outside the local bins (a crowd for the host) */
+    u32 f_cand; /* counters[2]'s part from this workgroup (the publisher sums) */
 };
 
 /* a record's sort bin: the end's global bin, or under the fused finish its
@@ -428,7 +430,11 @@ __device__ __forceinline__ u32 bin_slot_take(const VsaLitParams &P, const ConfLd
     if (k < cl.lb_n)
         return __hip_atomic_fetch_add(const_cast<u32 *>(&cl.lbins[k]), 1u, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (P.fin_keys) return VSA_SORT_BIN_MAX;
+    if (P.fin_keys) {
+        __hip_atomic_store(const_cast<u32 *>(&cl.f_bad), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+        return VSA_SORT_BIN_MAX;
+    }
     return __hip_atomic_fetch_add(&P.bin_counts[bin], 1u, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1691,8 +1697,12 @@ __device__ __forceinline__ void confirm_wave(const VsaLitParams &P, const ConfLd
         }
     }
     /* confirm-stage candidates (first-stage count instead under dbg & 32) */
-    if (P.counters && lane == 0 && consumed && !VSA_DBG(P.dbg, 32))
+    if (P.counters && lane == 0 && consumed && !VSA_DBG(P.dbg, 32)) {
         atomicAdd(&P.counters[2], (unsigned long long)consumed);
+        if (P.fin_keys)
+            __hip_atomic_fetch_add(const_cast<u32 *>(&cl.f_cand), consumed, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     if (prof && lane == 0) {
         phase(1);
         for (int i = 0; i < 8; i++) atomicAdd(&P.counters[4 + i], (unsigned long long)pcl[i]);
@@ -1824,6 +1834,8 @@ vsa_lit_scan(VsaLitParams P) {
             if (tid == 0) {
                 cl.f_lo = ((u64)f[1] << 32) | f[0];
                 cl.f_shift = f[2];
+                cl.f_bad = 0;
+                cl.f_cand = 0;
             }
             for (u32 i = tid; i < n; i += LIT_THREADS) cl.lbins[i] = 0;
         } else if (P.bin_keys && P.wg_bins) {
@@ -2391,8 +2403,12 @@ vsa_lit_scan(VsaLitParams P) {
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    if (P.counters && lane_id() == 0 && ncand_total)
+    if (P.counters && lane_id() == 0 && ncand_total) {
         atomicAdd(&P.counters[2], (unsigned long long)ncand_total);
+        if (P.fin_keys)
+            __hip_atomic_fetch_add(&cl.f_cand, ncand_total, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     } /* the scanning waves */
 finish:
     /* not Fat Teddy: at 128 VGPRs its scan has no room for the epilogue's
@@ -2501,6 +2517,34 @@ __device__ __forceinline__ void publish_wave(unsigned long long *ctr, unsigned l
     }
 }
 
+/* The fused finish's publish (its last workgroup's wave 0): the counters
+ * the host reads -- [0] records, [2] confirm candidates, [12] crowd --
+ * from the look-back's totals (the others only under debug flags, read
+ * back), to host memory and to the kept copy vsa_pack reads; the packed
+ * collective buffer's header; the scan counters zeroed for the next
+ * launch; then the sequence word with a system-scope release. */
+__device__ __forceinline__ void publish_fused(const VsaLitParams &P, unsigned long long n,
+                                              unsigned long long cand, bool crowded) {
+    const u32 l = lane_id();
+    unsigned long long v = 0;
+    if (l == 0) v = n;
+    else if (l == 2) v = cand;
+    else if (l == VSA_CTR_BIN_OVERFLOW) v = crowded ? 1ULL : 0ULL;
+    else if (P.dbg && l < 16)
+        v = __hip_atomic_load(&P.counters[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (P.fin_pk && l == 0)
+        P.fin_pk[0] = n | ((n > P.out_cap || crowded) ? (1ULL << 62) : 0ULL);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* debug reads before the zeroing */
+    if (l < 16) {
+        P.fin_pub[1 + l] = v;
+        P.counters[144 + l] = v; /* kept on the device too (vsa_pack) */
+    }
+    for (u32 i = l; i < 144; i += WAVE) P.counters[i] = 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (l == 0)
+        __hip_atomic_store(&P.fin_pub[0], P.fin_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 /* The fused finish (VsaLitParams.fin_keys): the binned sort done by the
  * scan's own workgroups at their end, instead of a vsa_bin_finish launch
  * behind the scan (one kernel boundary and launch less per step).  The plan
@@ -2509,7 +2553,7 @@ __device__ __forceinline__ void publish_wave(unsigned long long *ctr, unsigned l
  * workgroup order), so each record's bin is counted in LDS and every bin
  * holds one workgroup's records only: no record crosses workgroups.  What
  * does cross them is one word per workgroup, its record total tagged with
- * the launch's epoch -- an agent-scope atomic, coherent across XCDs without
+ * the launch's epoch -- agent-scope atomics, coherent across XCDs without
  * the agent-scope release per workgroup a plain-store hand-off needs
  * (round 3: step 1.42 ms, profiles/r03_sort_fused_trace.csv).
  *   B1  every wave's records staged and counted, its counter adds done (the
@@ -2520,9 +2564,12 @@ __device__ __forceinline__ void publish_wave(unsigned long long *ctr, unsigned l
  *   the totals of workgroups 0..w-1 (each dispatched before this one, so it
  *   runs or has run and the wait ends);
  *   B2  every wave writes its records at base + offset.  The last workgroup
- *       publishes the counters (publish_wave<true>, agent-scope loads): when
- *       its look-back is complete every other workgroup has passed B1, so
- *       every counter add is done.
+ *       publishes (publish_fused): its look-back has every other
+ *       workgroup's totals -- records, crowd flag, confirm candidates, two
+ *       epoch-tagged words each -- so the count the host reads needs no
+ *       further round trip.  (The schedule-feedback records go to host
+ *       memory from each workgroup; feedback_update skips an incomplete
+ *       one.)
  * A crowded local bin (> VSA_SORT_BIN_MAX) was flagged by the scan: its
  * records are skipped here and the host rescans without bins. */
 __device__ __forceinline__ void fused_finish(const VsaLitParams &P, const ConfLds &cl, u32 *sc) {
@@ -2530,7 +2577,9 @@ __device__ __forceinline__ void fused_finish(const VsaLitParams &P, const ConfLd
     const u32 tid = threadIdx.x, wave = tid / WAVE, lane = lane_id();
     const u32 w = blockIdx.x, nb = cl.lb_n;
     u32 *loff = sc;             /* [VSA_LBINS] each local bin's first position */
-    u32 *misc = sc + VSA_LBINS; /* [0] the workgroup's first output position */
+    u32 *misc = sc + VSA_LBINS; /* [0] the workgroup's first output position, [1] its
+                                   records, [2] its crowd, [3..5] the lower ones' crowd
+                                   and candidates (the publisher's) */
     static_assert(VSA_LBINS == 4 * WAVE, "one wave scans the local bins, 4 per lane");
     if (wave == 0) {
         u32 c[4], t4 = 0;
@@ -2550,12 +2599,16 @@ __device__ __forceinline__ void fused_finish(const VsaLitParams &P, const ConfLd
             loff[4 * lane + k] = e;
             e += c[k];
         }
-        const bool cr = wave_any(crowd);
-        if (lane == 0)
-            __hip_atomic_store(&P.fin_agg[w],
-                               ((unsigned long long)P.fin_epoch << 32) |
-                                   (cr ? (1ULL << 31) : 0ULL) | tot,
+        const bool cr = wave_any(crowd) || cl.f_bad != 0;
+        if (lane == 0) {
+            const unsigned long long ep = (unsigned long long)P.fin_epoch << 32;
+            __hip_atomic_store(&P.fin_agg[2 * w], ep | (cr ? (1ULL << 31) : 0ULL) | tot,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&P.fin_agg[2 * w + 1], ep | cl.f_cand, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        misc[1] = tot;
+        misc[2] = cr;
     }
     /* this wave's bins: [16 wave, 16 wave + 16) of the local bins.  When
      * none holds more than 16 records (sparse records: the common case) they
@@ -2604,23 +2657,41 @@ __device__ __forceinline__ void fused_finish(const VsaLitParams &P, const ConfLd
          * workgroups run): past it the launch is flagged as crowded, so the
          * host discards its records and rescans without bins, instead of
          * the grid never draining */
-        u32 base = 0, polls = 0;
+        u32 base = 0, polls = 0, crowd_lo = 0;
+        unsigned long long cand = 0;
         for (u32 v0 = 0; v0 < w; v0 += WAVE) {
             const u32 v = v0 + lane;
             if (v < w) {
-                unsigned long long a = 0;
+                unsigned long long a = 0, b = 0;
                 for (; polls < (1u << 20); polls++) {
-                    a = __hip_atomic_load(&P.fin_agg[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if ((u32)(a >> 32) == P.fin_epoch) break;
+                    a = __hip_atomic_load(&P.fin_agg[2 * v], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                    b = __hip_atomic_load(&P.fin_agg[2 * v + 1], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                    if ((u32)(a >> 32) == P.fin_epoch && (u32)(b >> 32) == P.fin_epoch) break;
                     __builtin_amdgcn_s_sleep(2);
                 }
                 base += (u32)a & 0x7fffffffu;
+                crowd_lo |= (u32)(a >> 31) & 1u;
+                cand += (u32)b;
             }
         }
-        if (wave_any(polls >= (1u << 20)) && lane == 0) flag_crowd(P);
+        const bool timeout = wave_any(polls >= (1u << 20));
+        if (timeout && lane == 0) flag_crowd(P);
 #pragma unroll
-        for (int dd = 32; dd >= 1; dd >>= 1) base += shfl_xor_u32(base, dd);
-        if (lane == 0) misc[0] = base;
+        for (int dd = 32; dd >= 1; dd >>= 1) {
+            base += shfl_xor_u32(base, dd);
+            crowd_lo |= shfl_xor_u32(crowd_lo, dd);
+            cand += ((unsigned long long)shfl_xor_u32((u32)(cand >> 32), dd) << 32) |
+                    shfl_xor_u32((u32)cand, dd);
+        }
+        if (lane == 0) {
+            misc[0] = base;
+            /* the last workgroup: the launch's totals for the publish */
+            misc[3] = crowd_lo | (timeout ? 1u : 0u);
+            misc[4] = (u32)cand;
+            misc[5] = (u32)(cand >> 32);
+        }
     }
     __syncthreads();
     const u32 base = misc[0];
@@ -2635,9 +2706,15 @@ __device__ __forceinline__ void fused_finish(const VsaLitParams &P, const ConfLd
             put(B, pass0, base);
         }
     }
-    if (w + 1 == gridDim.x && wave == 0)
-        publish_wave<true>(P.counters, P.fin_pub, P.fin_seq, 144u, P.wg_time, P.fin_hfb,
-                           P.fin_nfb, P.fin_pk, P.out_cap);
+    if (w + 1 == gridDim.x && wave == 0) {
+        /* every other workgroup's totals are in its look-back: the count,
+         * the crowd and the candidates need no further memory round trip */
+        const unsigned long long n = (unsigned long long)base + misc[1];
+        const bool crowded = misc[2] != 0 || misc[3] != 0;
+        const unsigned long long cand =
+            (((unsigned long long)misc[5] << 32) | misc[4]) + cl.f_cand;
+        publish_fused(P, n, cand, crowded);
+    }
 }
 
 __global__ void __launch_bounds__(256) vsa_publish(unsigned long long *ctr,

@@ -295,8 +295,12 @@ void arm_feedback(vsa_ctx *c, int set, uint32_t grid, uint64_t bytes, bool small
                   bytes >= (256u << 20) && !small ? set : -1;
     c->fb.grid = grid;
     /* a scan whose counters vsa_bin_finish publishes records in device
-     * memory and rides on the publish; otherwise host stores */
-    c->fb.dev = c->fb.armed >= 0 && c->fb.d_rec && c->launch.bins && !small;
+     * memory and rides on the publish; otherwise (and under the fused
+     * finish, whose publish would wait for them) host stores, a record
+     * not yet complete when the host reads it being skipped
+     * (feedback_update) */
+    c->fb.dev = c->fb.armed >= 0 && c->fb.d_rec && c->launch.bins && !small &&
+                !c->launch.fused;
     if (c->fb.armed >= 0) memset(c->fb.h, 0, 2 * grid * sizeof(unsigned long long));
 }
 
@@ -388,25 +392,23 @@ unsigned long long *g_wave_log = nullptr;
 
 /* the fused finish's default for new contexts: VSA_FUSED_FINISH=1 turns
  * it on (vsa_ctx_set_fused_finish per context).  Off by default: measured
- * against the vsa_bin_finish launch it shortens the pipelined step by 1-2
- * us (0.2-0.9 %) but lengthens the scan kernel by 4-5 us
- * (profiles/r06/r06l_fused_finish_ab3.jsonl) */
+ * against the vsa_bin_finish launch it shortens the pipelined step by 0.4-
+ * 2.5 us (0.3-0.8 %) but lengthens the scan kernel by 5-6 us
+ * (profiles/r06/r06q_fused_publish_ab.jsonl) */
 bool fused_finish_default() {
     static const bool v = env_int("VSA_FUSED_FINISH", 0) != 0;
     return v;
 }
 
 /* the fused finish's buffers: local-bin staging for `grid` workgroups
- * (grown, never shrunk), the totals (zero: no epoch matches) and the ticket */
+ * (grown, never shrunk) and the totals (zero: no epoch matches) */
 int ensure_fstage(vsa_ctx *c, uint32_t grid) {
     Workspace &w = c->ws;
     if (grid > VSA_FIN_MAX_GRID) return VSA_E_INVALID;
     if (!w.d_fagg) {
-        VSA_CHECK(hipMalloc(&w.d_fagg, VSA_FIN_MAX_GRID * sizeof(unsigned long long)));
-        VSA_CHECK(hipMalloc(&w.d_fticket, 64));
-        VSA_CHECK(hipMemsetAsync(w.d_fagg, 0, VSA_FIN_MAX_GRID * sizeof(unsigned long long),
+        VSA_CHECK(hipMalloc(&w.d_fagg, 2 * VSA_FIN_MAX_GRID * sizeof(unsigned long long)));
+        VSA_CHECK(hipMemsetAsync(w.d_fagg, 0, 2 * VSA_FIN_MAX_GRID * sizeof(unsigned long long),
                                  c->stream));
-        VSA_CHECK(hipMemsetAsync(w.d_fticket, 0, 64, c->stream));
     }
     if (grid > w.fstage_grid) {
         if (w.d_fstage) {
@@ -455,8 +457,13 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
     /* drop-in calls (a few records, sorted by the host) skip the kernel
      * timing and get their counters and records published (no copies) */
     const bool small = (c->launch.flags & SCAN_HOST_SORT_SMALL) != 0;
-    c->launch.ev_start = small ? nullptr : c->ev0;
-    c->launch.ev_stop = small ? nullptr : c->ev1;
+    /* the timing events ride on every timing_every-th dispatch only
+     * (vsa_ctx_set_timing: they cost ~4 us per step at 512 MiB,
+     * profiles/r06/r06n_gap_knobs.jsonl) */
+    c->launch.timed = !small && c->timing_every &&
+                      (c->lit_launches % (uint64_t)c->timing_every) == 0;
+    c->launch.ev_start = c->launch.timed ? c->ev0 : nullptr;
+    c->launch.ev_stop = c->launch.timed ? c->ev1 : nullptr;
     arm_feedback(c, fb_set_of(db), c->launch.grid, c->launch.bytes, small);
     c->lit_launches++;
     int r = launch_scan_kernel(c, db, d_data, nb, nsegs);
@@ -533,13 +540,9 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
         P.fin_keys = w.d_keys[1];
         P.fin_ids = w.d_ids[1];
         P.fin_agg = w.d_fagg;
-        P.fin_ticket = w.d_fticket;
         P.fin_seq = ++c->pub_seq;
         P.fin_epoch = (uint32_t)(P.fin_seq % 0xfffffffeULL) + 1u;
         P.fin_pub = w.d_pub;
-        const bool fbd = c->fb.armed >= 0 && c->fb.dev;
-        P.fin_hfb = fbd ? c->fb.d : nullptr;
-        P.fin_nfb = fbd ? 2 * G : 0u;
         P.fin_pk = (uint64_t *)c->launch.pack_dst;
         P.fin_pk_cap = c->launch.pack_cap;
     }
@@ -686,7 +689,10 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
         fprintf(stderr, "vsa: %llu queued confirm keys differ from HBM\n",
                 (unsigned long long)w.h_counters[3]);
     }
-    if (c->launch.fused) {
+    if (!c->launch.timed) {
+        c->kms_stale = false;
+        if (!(flags & SCAN_HOST_SORT_SMALL)) c->last_kernel_ms = -1.0; /* untimed */
+    } else if (c->launch.fused) {
         /* the scan published from inside itself: its end event may not be
          * written yet, so the kernel time is read when asked for
          * (vsa_scan_kernel_ms) */
@@ -935,7 +941,6 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (w.d_bstage) (void)hipFree(w.d_bstage);
     if (w.d_fstage) (void)hipFree(w.d_fstage);
     if (w.d_fagg) (void)hipFree(w.d_fagg);
-    if (w.d_fticket) (void)hipFree(w.d_fticket);
     if (w.h_counters) (void)hipHostFree(w.h_counters);
     if (w.h_pub) (void)hipHostFree(w.h_pub);
     if (c->fb.h) (void)hipHostFree(c->fb.h);
@@ -963,6 +968,7 @@ int vsa_ctx_create_shared(vsa_ctx_t *base, vsa_ctx_t **out) {
     c->stream_ref = base->stream_ref; /* releases the stream it made */
     c->reserved_cus = base->reserved_cus;
     c->fused_finish = base->fused_finish;
+    c->timing_every = base->timing_every;
     c->stream = base->stream;
     *out = c;
     return VSA_OK;
@@ -1552,6 +1558,12 @@ double vsa_scan_kernel_ms(vsa_ctx_t *c) {
 uint64_t vsa_scan_launches(vsa_ctx_t *c) { return c ? c->lit_launches : 0; }
 
 int vsa_scan_last_fused(vsa_ctx_t *c) { return c && c->launch.fused ? 1 : 0; }
+
+int vsa_ctx_set_timing(vsa_ctx_t *c, uint32_t every) {
+    if (!c) return VSA_E_INVALID;
+    c->timing_every = every;
+    return VSA_OK;
+}
 
 int vsa_ctx_set_fused_finish(vsa_ctx_t *c, int on) {
     if (!c) return VSA_E_INVALID;

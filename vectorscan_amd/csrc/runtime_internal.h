@@ -120,12 +120,10 @@ struct Workspace {
     uint32_t *h_segblk = nullptr;
     /* the fused finish (kernels.hip fused_finish): staged records in local
      * bins, VSA_LBINS x VSA_SORT_BIN_MAX per workgroup (keys, then ids), for
-     * fstage_grid workgroups; the workgroups' epoch-tagged totals; the
-     * finished-workgroup ticket (zero between launches) */
+     * fstage_grid workgroups; the workgroups' epoch-tagged totals */
     uint8_t *d_fstage = nullptr;
     uint32_t fstage_grid = 0;
-    unsigned long long *d_fagg = nullptr; /* VSA_FIN_MAX_GRID words */
-    uint32_t *d_fticket = nullptr;
+    unsigned long long *d_fagg = nullptr; /* 2 x VSA_FIN_MAX_GRID words */
 };
 
 
@@ -189,6 +187,7 @@ struct vsa_ctx {
         bool published = false; /* ... and vsa_publish after it (finish_scan
                                    polls h_pub instead of copying) */
         bool fin_ok = false;    /* the plan allows the fused finish */
+        bool timed = false;     /* the dispatch carries ev0 / ev1 */
         bool fused = false;     /* ... and this launch sorts inside the scan */
         uint64_t bytes = 0; /* scanned bytes (len - start summed) */
         const VsaBlock *d_blocks = nullptr;
@@ -212,6 +211,9 @@ struct vsa_ctx {
     /* eligible launches sort inside the scan kernel (kernels.hip
      * fused_finish; vsa_ctx_set_fused_finish, default VSA_FUSED_FINISH) */
     bool fused_finish = false;
+    /* every timing_every-th literal-scan launch carries the kernel-timing
+     * events (vsa_ctx_set_timing; 1 = all, 0 = none) */
+    uint32_t timing_every = 1;
     uint32_t bin_skip = 0;   /* launches left without the binned sort */
     /* the bin_skip a crowded bin sets: 16, x4 for every crowded binned
      * launch in a row (up to 4096), back to 16 after a binned launch that
