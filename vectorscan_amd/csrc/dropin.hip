@@ -770,15 +770,35 @@ int scan_records(vsa_ctx *c, const vsa_db *db, const u8 *d_data, const uint64_t 
     return VSA_OK;
 }
 
-int records_fetch_async(vsa_ctx *c, uint64_t n, uint64_t *h_keys, uint32_t *h_ids) {
+int records_mark(vsa_ctx *c) {
+    if (!c->ev_mark) VSA_CHECK(hipEventCreateWithFlags(&c->ev_mark, hipEventDisableTiming));
+    VSA_CHECK(hipEventRecord(c->ev_mark, c->stream));
+    c->marked = true;
+    return VSA_OK;
+}
+
+int records_fetch_async(vsa_ctx *c, uint64_t n, uint64_t *h_keys, uint32_t *h_ids,
+                        bool remark) {
     if (!c->ev_rec) VSA_CHECK(hipEventCreateWithFlags(&c->ev_rec, hipEventDisableTiming));
+    if (!c->copy_stream) {
+        VSA_CHECK(hipSetDevice(c->device));
+        VSA_CHECK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    }
+    /* the copy starts when the scan that made the records has ended: its
+     * mark, or (no mark, or a rescan since) everything queued so far */
+    if (!c->marked || remark) VSA_CHECK(records_mark(c) == VSA_OK ? hipSuccess : hipErrorUnknown);
+    c->marked = false;
+    VSA_CHECK(hipStreamWaitEvent(c->copy_stream, c->ev_mark, 0));
     if (n) {
         VSA_CHECK(hipMemcpyAsync(h_keys, c->ws.d_keys[c->cur], n * 8, hipMemcpyDeviceToHost,
-                                 c->stream));
+                                 c->copy_stream));
         VSA_CHECK(hipMemcpyAsync(h_ids, c->ws.d_ids[c->cur], n * 4, hipMemcpyDeviceToHost,
-                                 c->stream));
+                                 c->copy_stream));
     }
-    VSA_CHECK(hipEventRecord(c->ev_rec, c->stream));
+    VSA_CHECK(hipEventRecord(c->ev_rec, c->copy_stream));
+    /* the scan stream's next work (this context's next scan rewrites the
+     * records) waits for the copy, on the device */
+    VSA_CHECK(hipStreamWaitEvent(c->stream, c->ev_rec, 0));
     return VSA_OK;
 }
 

@@ -952,6 +952,8 @@ int vsa_ctx_destroy(vsa_ctx_t *c) {
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->ev_rec) (void)hipEventDestroy(c->ev_rec);
+    if (c->ev_mark) (void)hipEventDestroy(c->ev_mark);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (t_ctx == c) t_ctx = nullptr;
     delete c; /* drops its hold on the stream */
     /* the statuses ignored above must not fail a later launch check */

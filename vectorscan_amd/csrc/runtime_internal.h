@@ -206,6 +206,9 @@ struct vsa_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_done = nullptr; /* polled by wait_stream */
     hipEvent_t ev_rec = nullptr;  /* records_fetch_async's copies done */
+    hipEvent_t ev_mark = nullptr; /* records_mark: the end of a queued scan */
+    bool marked = false;
+    hipStream_t copy_stream = nullptr; /* records_fetch_async's copies */
     double last_kernel_ms = 0.0;
     bool kms_stale = false; /* last_kernel_ms not yet read for the last scan */
     /* eligible launches sort inside the scan kernel (kernels.hip

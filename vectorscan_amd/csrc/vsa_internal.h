@@ -78,10 +78,17 @@ int exec_pieces(vsa_ctx *c, const vsa_db *db, const u8 *hist, size_t hist_len,
 /* runtime.hip: one launch over device blocks (hlens NULL = block mode);
  * the sorted records to the host when keys != NULL, else only counted */
 /* pipelined corpus repeats (vsa_hs_corpus_scan_repeats): the last
- * completed scan's n records copied into host buffers asynchronously on the
- * scan stream (records_fetch_async, then records_wait), so the next scan can
- * be queued behind the copy while the host replays; pinned host buffers */
-int records_fetch_async(vsa_ctx *c, uint64_t n, uint64_t *h_keys, uint32_t *h_ids);
+ * completed scan's n records copied into host buffers asynchronously
+ * (records_fetch_async, then records_wait), so the next scan can be queued
+ * while the host replays; pinned host buffers.  records_mark after queuing
+ * a scan notes its end on the scan stream; records_fetch_async then copies
+ * on the context's copy stream after that mark (beside the scan queued
+ * after it) and holds the scan stream's next work until the copy is done
+ * (the context's next scan rewrites the records).  Without a mark (or
+ * remark, after a rescan) the copy follows everything queued so far. */
+int records_mark(vsa_ctx *c);
+int records_fetch_async(vsa_ctx *c, uint64_t n, uint64_t *h_keys, uint32_t *h_ids,
+                        bool remark = false);
 int records_wait(vsa_ctx *c);
 void *host_pinned_alloc(size_t bytes);
 void host_pinned_free(void *p);
