@@ -803,8 +803,24 @@ int records_fetch_async(vsa_ctx *c, uint64_t n, uint64_t *h_keys, uint32_t *h_id
 }
 
 int records_wait(vsa_ctx *c) {
-    if (c->ev_rec) VSA_CHECK(hipEventSynchronize(c->ev_rec));
-    return VSA_OK;
+    if (!c->ev_rec) return VSA_OK;
+    /* polled (a blocking wait wakes on a coarse tick, runtime.hip
+     * wait_stream): spin ~100 us, then yield; past 50 ms block */
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0;; i++) {
+        const hipError_t e = hipEventQuery(c->ev_rec);
+        if (e == hipSuccess) return VSA_OK;
+        if (e != hipErrorNotReady) VSA_CHECK(e);
+        (void)hipGetLastError();
+        if ((i & 15) == 15) {
+            const auto dt = std::chrono::steady_clock::now() - t0;
+            if (dt > std::chrono::milliseconds(50)) {
+                VSA_CHECK(hipEventSynchronize(c->ev_rec));
+                return VSA_OK;
+            }
+            if (dt > std::chrono::microseconds(100)) sched_yield();
+        }
+    }
 }
 
 void *host_pinned_alloc(size_t bytes) {

@@ -870,10 +870,23 @@ static int corpus_replay_blocks(vsa_hs_corpus *cp, uint64_t *keys, const uint32_
             }
             break;
         }
-        /* back to the block's first record */
-        kt[t] = (uint64_t)(std::lower_bound(keys + kt[t - 1], keys + k,
-                                            (uint64_t)so[p] << KEY_END_SHIFT) - keys);
-        pt[t] = p;
+        /* to the nearer block boundary: back to the block's first record,
+         * or on to the next block's (few large blocks: snapping back alone
+         * left one thread two blocks and another none) */
+        const uint64_t k_lo = (uint64_t)(std::lower_bound(keys + kt[t - 1], keys + k,
+                                                          (uint64_t)so[p] << KEY_END_SHIFT) - keys);
+        const uint64_t k_hi =
+            p + 1 < npos ? (uint64_t)(std::lower_bound(keys + k, keys + nm,
+                                                       (uint64_t)so[p + 1] << KEY_END_SHIFT) -
+                                      keys)
+                         : nm;
+        if ((k_lo <= kt[t - 1] || k - k_lo > k_hi - k) && p + 1 < npos) {
+            kt[t] = k_hi;
+            pt[t] = p + 1;
+        } else {
+            kt[t] = k_lo;
+            pt[t] = p;
+        }
     }
     std::vector<uint64_t> part(T, 0);
     std::vector<int> status(T, VSA_HS_SUCCESS);
