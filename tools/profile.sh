@@ -9,6 +9,7 @@ TAG=${1:-r02}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
+export HIP_FORCE_DEV_KERNARG=1  # as bench.py sets it for itself
 B="python3 bench.py --steps 3 --warmup 2 --no-cpu --no-parity --no-e2e --no-cfg5 --no-ceiling"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- \
     python3 bench.py > $OUT/bench_trace.log 2>&1
