@@ -368,3 +368,50 @@ def test_block_replay_ragged_parallel(monkeypatch):
         ctx.close()
         scratch.close()
         db.close()
+
+
+@pytest.mark.gpu
+def test_block_replay_few_large_blocks():
+    """Few large blocks (the end-to-end bench's shape: 4 blocks, 4-16
+    threads): the replay's thread ranges snap to the nearer block boundary,
+    so every thread count gives the one-thread counts and digests; and the
+    pipelined repeats on a fresh corpus -- whose first pass outgrows the
+    output and rescans inside its wait, so its record copy follows the
+    rescan, not the mark queued with the first launch -- give every pass the
+    same total and the same per-block sequences."""
+    import bench
+    exprs, flags, ids = bench.make_mixed_set(2000)
+    lits = [vsa.HwlmLiteral(e, False, i) for i, e in enumerate(exprs)]
+    data = bench.make_corpus(16 << 20, lits, seed=17, plant_every=96)
+    bl = 4 << 20
+    offs, lens = [i * bl for i in range(4)], [bl, bl, bl, bl - 3]
+    db = hs.compile_lit_multi(exprs, flags, ids, hs.MODE_BLOCK)
+    want = None
+    for threads in (1, 2, 3, 4, 5, 8, 16):
+        scratch = hs.Scratch(db)
+        ctx = vsa.Context(0)
+        d = ctx.malloc(len(data))
+        try:
+            ctx.h2d(d, data)
+            corpus = hs.Corpus(db, scratch, d, offs, lens, h_data=data)
+            try:
+                if threads in (4, 16):
+                    # a fresh corpus: pass 0 rescans (> 65,536 records)
+                    rc, tot, cnt, dg = corpus.scan_repeats(3, True, threads, True)
+                    assert rc == hs.SUCCESS and len(set(int(t) for t in tot)) == 1
+                    tot = int(tot[-1])
+                else:
+                    rc, tot, cnt, dg = corpus.scan(True, threads, digests=True)
+                    assert rc == hs.SUCCESS
+                if want is None:
+                    want = (tot, cnt.copy(), dg.copy())
+                    assert tot > 65536
+                assert tot == want[0], threads
+                assert np.array_equal(cnt, want[1]) and np.array_equal(dg, want[2]), threads
+            finally:
+                corpus.close()
+        finally:
+            ctx.free(d)
+            ctx.close()
+            scratch.close()
+    db.close()
