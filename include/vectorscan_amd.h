@@ -282,6 +282,15 @@ int vsa_plan_blocks(const uint8_t *d_data, const uint64_t *offsets, const uint64
                     const uint64_t *starts, const uint64_t *hlens, const uint64_t *report_lo,
                     uint32_t nblocks, void *out);
 
+/* Host-only (tests): the dynamic shares the planner grants a batch on
+ * num_cus CUs with ns scanning waves each (kernels.hip dyn_bounds: each
+ * launch cuts the live KiB at per-XCD weights it derives from the previous
+ * launch's end times): out[0] = the live KiB (0: static lists), out[1] = how
+ * far (KiB) a boundary may move from the equal-share one.  Returns VSA_OK
+ * or a VSA_E_* code. */
+int vsa_plan_dyn(const uint8_t *d_data, const uint64_t *offsets, const uint64_t *lens,
+                 const uint64_t *starts, const uint64_t *hlens, const uint64_t *report_lo,
+                 uint32_t nblocks, uint32_t num_cus, uint32_t ns, uint32_t *out);
 /* Host-only (tests): the schedule feedback's per-XCD weight updates over
  * `launches` synthetic launches of `grid` workgroups (b on XCD b % 8) whose
  * XCDs run at rate[0..7], with relative timing noise `jitter`; the applied
@@ -356,6 +365,17 @@ uint64_t vsa_scan_launches(vsa_ctx_t *ctx);
  * the scan kernel (the fused finish: no vsa_bin_finish launch behind it),
  * else 0.  A diagnostic, no reference counterpart. */
 int vsa_scan_last_fused(vsa_ctx_t *ctx);
+/* 1 when the context's last literal-scan launch set its workgroups' shares
+ * itself (dynamic shares: per-XCD weights from the previous launch's end
+ * times; VSA_DYN_SHARES=0 turns them off), else 0.  A diagnostic, no
+ * reference counterpart. */
+int vsa_scan_last_dyn(vsa_ctx_t *ctx);
+/* Dynamic shares for the context's FDR launches of at least min_bytes
+ * over eligible plans (>= 64 workgroups, >= 256 MiB of parts of blocks in
+ * address order): on = 1 (the default, min_bytes VSA_DYN_MIN_MIB = 2048
+ * MiB, unless VSA_DYN_SHARES=0), off = 0 (the host's static lists and its
+ * schedule feedback).  Results are identical either way. */
+int vsa_ctx_set_dyn_shares(vsa_ctx_t *ctx, int on, uint64_t min_bytes);
 /* Sort inside the scan kernel when the plan allows it (the fused finish:
  * no vsa_bin_finish launch behind the scan, the scan's workgroups sort
  * their own records and the last one publishes the count), on = 1; off = 0

@@ -232,16 +232,76 @@ def test_gpu_fdr_5k_64mib(ctx):
     assert len(m) >= (64 << 20) // (64 << 10)
 
 
-@pytest.mark.parametrize("fused", [False, True])
-def test_gpu_schedule_feedback_512mib(ctx, fused):
+@pytest.mark.parametrize("engine", ["fdr", "teddy", "noodle"])
+def test_gpu_dyn_shares_ragged(ctx, engine):
+    """Dynamic shares (kernels.hip dyn_bounds; on here from 256 MiB): ~400
+    MiB of 40 ragged blocks (4-16 MiB plus odd bytes, gaps between them, some
+    with a start) scanned 5 times through one prebuilt plan and 3 times per
+    call.  Each FDR launch after the first cuts the workgroups' KiB ranges at
+    the weights the previous launch's end times give, so every launch splits
+    the bytes differently, at arbitrary KiB inside segments: each launch's
+    records equal the oracle's, block by block, and every FDR launch used the
+    dynamic shares.  Teddy and noodle launches of the same plan keep the
+    static lists (and their owned bins)."""
+    import bench
+    ctx.dyn_shares(True, min_mib=256)
+    rng = random.Random(77)
+    if engine == "fdr":
+        lits = bench.make_literals(5000, seed=12)
+    elif engine == "teddy":
+        lits = bench.make_literals(24, seed=13)
+    else:
+        lits = [vsa.HwlmLiteral(b"needle", False, 7)]
+    blob = vsa.hwlm_build(lits)
+    offs, lens, starts, pos = [], [], [], 3
+    for i in range(40):
+        ln = rng.randint(4 << 20, 16 << 20) + rng.randint(0, 1023)
+        offs.append(pos)
+        lens.append(ln)
+        starts.append(rng.choice([0, 0, 0, 5, 1000]))
+        pos += ln + rng.choice([0, 64, rng.randint(1, 5000)])
+    host = bench.make_corpus(pos + 64, lits, seed=6, plant_every=64 << 10)
+    want = [oracle.hwlm_exec(blob.ptr, host[o:o + ln], start=s, cap=1 << 20)[1]
+            for o, ln, s in zip(offs, lens, starts)]
+    d = ctx.malloc(len(host))
+    db = vsa.Database(ctx, blob)
+    plan = None
+    try:
+        ctx.h2d(d, host)
+        plan = ctx.plan(d, offs, lens, starts)
+        for k in range(8):
+            m = (ctx.scan_plan(db, plan) if k < 5
+                 else ctx.scan_blocks(db, d, offs, lens, starts))
+            assert ctx.last_dyn() == (engine == "fdr"), k
+            res = ctx.results(m)
+            ends = res["key"] >> np.uint64(24)
+            bi = np.searchsorted(np.array(offs, np.uint64), ends, side="right") - 1
+            got = [[] for _ in offs]
+            for e, i, b in zip(ends.tolist(), res["id"].tolist(), bi.tolist()):
+                got[b].append((e - offs[b], i))
+            for b in range(len(offs)):
+                assert got[b] == want[b], (k, b)
+    finally:
+        ctx.dyn_shares(True)
+        if plan is not None:
+            plan.close()
+        db.close()
+        ctx.free(d)
+
+
+@pytest.mark.parametrize("fused,dyn", [(False, False), (True, False), (False, True)])
+def test_gpu_schedule_feedback_512mib(ctx, fused, dyn):
     """Schedule feedback (runtime.hip take_feedback / refresh_plan): 512 MiB
     in 4 blocks scanned 8 times through one prebuilt plan and 8 times per
     call (scan_blocks), so the XCD weights are learned and the plans rebuilt
     with weighted shares between launches: every launch's records equal the
     first one's, and that one's digest equals the oracle's.  With the fused
-    finish too (its last workgroup publishes the feedback record)."""
+    finish too (its last workgroup publishes the feedback record), and with
+    the dynamic shares instead of the host's feedback (each launch re-cuts
+    the shares from the previous launch's end times)."""
     import bench
     ctx.fused_finish(fused)
+    ctx.dyn_shares(dyn, min_mib=256)
     lits = bench.make_literals(5000, seed=12)
     blob = vsa.hwlm_build(lits)
     db = vsa.Database(ctx, blob)
@@ -267,13 +327,15 @@ def test_gpu_schedule_feedback_512mib(ctx, fused):
             else:
                 assert np.array_equal(cur[0], first[0]) and np.array_equal(cur[1], first[1]), k
             fused_seen.append(ctx.last_fused())
-            if k == 7:
+            assert ctx.last_dyn() == (dyn and not fused), k
+            if k == 7 and not dyn:
                 # the first complete feedback record always publishes weights
                 # (feedback_update), so the prebuilt plan was rebuilt for them
                 assert plan.rebuilds() >= 1
         assert any(fused_seen) == fused
     finally:
         ctx.fused_finish(False)
+        ctx.dyn_shares(True)
         if plan is not None:
             plan.close()
         db.close()

@@ -10,5 +10,6 @@ C=vectorscan_amd/csrc
 mkdir -p /tmp/vsa_variant_$name
 $H "$@" -I$C -c ${KSRC:-$C/kernels.hip} -o /tmp/vsa_variant_$name/kernels.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $C/compile.o $C/flood.o $C/hs_lit.o \
-    /tmp/vsa_variant_$name/kernels.o $C/runtime.o -o vectorscan_amd/libvsa_$name.so
+    /tmp/vsa_variant_$name/kernels.o $C/runtime.o $C/plan.o $C/dropin.o $C/batcher.o \
+    -o vectorscan_amd/libvsa_$name.so
 echo built vectorscan_amd/libvsa_$name.so

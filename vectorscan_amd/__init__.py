@@ -165,6 +165,8 @@ _sig("vsa_derive_first_stage", ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, c
 _sig("vsa_scan_kernel_ms", ctypes.c_double, ctypes.c_void_p)
 _sig("vsa_scan_launches", ctypes.c_uint64, ctypes.c_void_p)
 _sig("vsa_scan_last_fused", ctypes.c_int, ctypes.c_void_p)
+_sig("vsa_scan_last_dyn", ctypes.c_int, ctypes.c_void_p)
+_sig("vsa_ctx_set_dyn_shares", ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64)
 _sig("vsa_ctx_set_fused_finish", ctypes.c_int, ctypes.c_void_p, ctypes.c_int)
 _sig("vsa_ctx_set_timing", ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32)
 _sig("vsa_ctx_set_reserved_cus", ctypes.c_int, ctypes.c_void_p, ctypes.c_int)
@@ -824,6 +826,16 @@ class Context:
         """True when the last literal-scan launch sorted its records inside
         the scan (the fused finish, no vsa_bin_finish launch)."""
         return lib.vsa_scan_last_fused(self.ptr) == 1
+
+    def last_dyn(self):
+        """True when the last literal-scan launch set its workgroups' shares
+        itself (dynamic shares, kernels.hip dyn_bounds)."""
+        return lib.vsa_scan_last_dyn(self.ptr) == 1
+
+    def dyn_shares(self, on=True, min_mib=2048):
+        """Dynamic shares for the FDR launches of >= min_mib MiB over eligible
+        plans (vsa_ctx_set_dyn_shares)."""
+        _check(lib.vsa_ctx_set_dyn_shares(self.ptr, 1 if on else 0, int(min_mib) << 20))
 
     def read_ceiling(self, d_data, length, runs=5):
         """(GB/s, ms, bytes): this device's streaming-read ceiling over the

@@ -175,6 +175,17 @@ struct VsaLitParams {
     unsigned long long fin_seq;
     uint64_t *fin_pk;             /* packed collective buffer (or null) */
     uint64_t fin_pk_cap;
+    /* Dynamic shares (kernels.hip dyn_bounds; dyn_kib 0 = off): workgroup
+     * b scans the KiB range [L_b, L_b+1) of the plan's live KiB (descriptor
+     * word 3 = a segment's KiB position), L from per-XCD weights it derives
+     * at its start from the previous launch's end times, each L held within
+     * dyn_margin KiB of the equal-share boundary floor(dyn_kib * b / grid) */
+    const unsigned long long *dyn_prev; /* the previous such launch's records
+                                           (wg_time's layout) or null: equal */
+    const uint32_t *dyn_wprev;          /* ... its weights (8, 16.16) */
+    uint32_t *dyn_wout;                 /* this launch's (workgroup 0 writes) */
+    uint32_t dyn_kib;
+    uint32_t dyn_margin;
 };
 
 

@@ -1731,6 +1731,211 @@ __device__ __forceinline__ void stage_lds(TV *dst, u32 n, u32 tid, F &&src) {
 
 __device__ __forceinline__ void fused_finish(const VsaLitParams &P, const ConfLds &cl, u32 *sc);
 
+/* ---- dynamic shares (VsaLitParams.dyn_kib) ----
+ * The XCDs of a box drift apart and back over a few launches (XCD pairs
+ * 20-40 us apart on a 4 GiB scan, the deviation's correlation 0.92 from one
+ * launch to the next and 0.6 four launches later:
+ * profiles/r06/r06y_fb_trace_*.txt), faster than host-side feedback, which
+ * rebuilds the plan, can follow.  So each launch sets its own shares: wave
+ * 0 of every workgroup reads the previous launch's end times and weights
+ * (one memory round trip, beside the table staging), derives per-XCD
+ * weights that would have ended its XCDs together, and cuts the plan's
+ * live KiB at the weighted prefix sums.  Every workgroup computes the same
+ * boundaries from the same inputs with the same instructions (integer
+ * prefix sums and division; the float part runs on wave-uniform values in
+ * one order), so workgroup b's upper boundary is b + 1's lower one and
+ * every KiB is scanned exactly once.  Each boundary stays within dyn_margin
+ * KiB of the equal-share one, which the host's owned sort bins exclude
+ * (plan.hip plan_wg_bins).  The segments are the host list's (parts of
+ * large blocks only); a workgroup takes those overlapping its range,
+ * clipped to it. */
+struct DynB {
+    u32 s_lo, s_hi; /* the workgroup's segments [s_lo, s_hi) */
+    u32 lk, hk;     /* its KiB range */
+};
+
+__device__ __forceinline__ u32 wave_sum_u32(u32 v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += shfl_xor_u32(v, m);
+    return readfirstlane_u32(v);
+}
+
+/* segments whose KiB position (descriptor word 3, ascending) is <= L (or <
+ * L): a 64-entry window from `near`, else a 64-way search of the list */
+__device__ __forceinline__ u32 dyn_count(const VsaLitParams &P, u32 lane, u32 near, u32 L, bool strict) {
+    const u32 n = (u32)P.nsegs;
+    const u32 *pos = P.seg_desc + 3;
+    auto pred = [&](u32 s, u32 end) -> bool {
+        if (s >= end) return false;
+        const u32 v = pos[4 * (size_t)s];
+        return strict ? v < L : v <= L;
+    };
+    u32 base = near > 32 ? near - 32 : 0;
+    if (base + 64 > n) base = n > 64 ? n - 64 : 0;
+    {
+        const u32 c = (u32)__popcll(__ballot(pred(base + lane, n)));
+        if ((c > 0 || base == 0) && (c < 64 || base + 64 >= n)) return base + c;
+    }
+    /* the count A lies in [lo, hi]: elements below lo hold, from hi on not */
+    u32 lo = 0, hi = n;
+    while (hi - lo > 64) {
+        const u32 step = (hi - lo + 63) / 64;
+        const u32 c = (u32)__popcll(__ballot(pred(lo + lane * step, hi)));
+        if (c == 0) return lo;
+        const u32 nhi = min(hi, lo + c * step);
+        lo = lo + (c - 1) * step + 1;
+        hi = nhi;
+    }
+    return lo + (u32)__popcll(__ballot(pred(lo + lane, hi)));
+}
+
+/* the previous launch's records and weights, loaded by wave 0 at the
+ * kernel's entry so their round trip overlaps the table staging */
+struct DynPre {
+    unsigned long long en[4], ex[4];
+    u32 wp;
+};
+
+__device__ __forceinline__ void dyn_load(const VsaLitParams &P, u32 lane, DynPre &d) {
+    const u32 G = gridDim.x;
+    constexpr unsigned long long M60 = (1ull << 60) - 1;
+    d.wp = 65536;
+    if (!P.dyn_prev) return;
+    if (lane < 8 && P.dyn_wprev) d.wp = P.dyn_wprev[lane];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const u32 k = lane + 64 * j;
+        d.en[j] = ~0ull; /* past the grid: no part in the minimum */
+        d.ex[j] = M60;
+        if (k < G) {
+            d.ex[j] = P.dyn_prev[k];
+            d.en[j] = P.dyn_prev[G + k];
+        }
+    }
+}
+
+/* wave 0 of each workgroup: its range and segments (grid <= 256) */
+__device__ __forceinline__ void dyn_bounds(const VsaLitParams &P, u32 lane, const DynPre &dp,
+                                           DynB &o) {
+    const u32 G = gridDim.x, b = blockIdx.x;
+    constexpr u32 ONE = 65536;
+    constexpr unsigned long long M60 = (1ull << 60) - 1;
+    u32 wq[8];
+#pragma unroll
+    for (int x = 0; x < 8; x++) wq[x] = ONE;
+    u32 xk[4] = {0, 0, 0, 0};
+    if (P.dyn_prev) {
+        const unsigned long long *en = dp.en, *ex = dp.ex;
+        const u32 wp = dp.wp;
+        unsigned long long t0 = ~0ull;
+        bool bad = false; /* a workgroup without a complete record */
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            bad = bad || !en[j] || !(ex[j] & M60);
+            t0 = en[j] < t0 ? en[j] : t0;
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            const unsigned long long o2 = ((unsigned long long)shfl_xor_u32((u32)(t0 >> 32), m) << 32) |
+                                          shfl_xor_u32((u32)t0, m);
+            t0 = o2 < t0 ? o2 : t0;
+        }
+        u32 s[8], c[8];
+#pragma unroll
+        for (int x = 0; x < 8; x++) s[x] = c[x] = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const u32 k = lane + 64 * j;
+            const u32 x = (u32)(ex[j] >> 60) & 7u;
+            const unsigned long long e = ex[j] & M60;
+            bad = bad || (k < G && e <= t0);
+            const unsigned long long dt = e > t0 ? e - t0 : 0ull;
+            const u32 d = dt < 0xffffffull ? (u32)dt : 0xffffffu;
+            xk[j] = x;
+#pragma unroll
+            for (int xx = 0; xx < 8; xx++)
+                if (k < G && x == (u32)xx) {
+                    s[xx] += d;
+                    c[xx] += 1;
+                }
+        }
+        if (!__ballot(bad)) {
+            float tx[8], tm = 0.f, np = 0.f;
+#pragma unroll
+            for (int x = 0; x < 8; x++) {
+                s[x] = wave_sum_u32(s[x]);
+                c[x] = wave_sum_u32(c[x]);
+                tx[x] = c[x] ? (float)s[x] / (float)c[x] : 0.f;
+                if (c[x]) {
+                    tm += tx[x];
+                    np += 1.f;
+                }
+            }
+            tm /= np;
+            /* the weights that would have ended every XCD together (time
+             * per XCD ~ weight / rate), normalized to mean 1, held in
+             * 0.9-1.1 */
+            float tw[8], tsum = 0.f;
+#pragma unroll
+            for (int x = 0; x < 8; x++) {
+                const float w0 = (float)readlane_u32(wp, x) * (1.f / 65536.f);
+                tw[x] = c[x] ? w0 * tm / fmaxf(tx[x], 1.f) : 0.f;
+                tsum += tw[x];
+            }
+            const float mean = tsum / np;
+#pragma unroll
+            for (int x = 0; x < 8; x++)
+                if (c[x]) wq[x] = (u32)(fminf(1.1f, fmaxf(0.9f, tw[x] / mean)) * 65536.f + 0.5f);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) xk[j] = 0;
+        }
+    }
+    if (b == 0 && lane < 8 && P.dyn_wout) {
+        u32 w = wq[0];
+#pragma unroll
+        for (int x = 1; x < 8; x++) w = lane == (u32)x ? wq[x] : w;
+        P.dyn_wout[lane] = w;
+    }
+    /* integer prefix sums of the workgroups' weights */
+    u32 pre = 0, mine = 0, tot = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const u32 k = lane + 64 * j;
+        u32 w = wq[0];
+#pragma unroll
+        for (int x = 1; x < 8; x++) w = xk[j] == (u32)x ? wq[x] : w;
+        if (k < G) {
+            tot += w;
+            if (k < b) pre += w;
+            if (k == b) mine = w;
+        }
+    }
+    pre = wave_sum_u32(pre);
+    mine = wave_sum_u32(mine);
+    tot = wave_sum_u32(tot);
+    const unsigned long long T = P.dyn_kib, M = P.dyn_margin;
+    auto bound = [&](u32 i, u32 S) -> u32 {
+        if (i == 0) return 0u;
+        if (i >= G) return (u32)T;
+        const unsigned long long nom = T * i / G;
+        unsigned long long L = T * S / tot;
+        const unsigned long long lo = nom > M ? nom - M : 0ull, hi = min(nom + M, T);
+        L = L < lo ? lo : L > hi ? hi : L;
+        return (u32)L;
+    };
+    o.lk = bound(b, pre);
+    o.hk = bound(b + 1, pre + mine);
+    o.s_lo = o.s_hi = 0;
+    if (o.lk < o.hk) {
+        /* the window's guess: the segments' KiB in proportion (the plan's
+         * parts are near-equal within a block) */
+        const u32 n = (u32)P.nsegs;
+        o.s_lo = dyn_count(P, lane, (u32)((unsigned long long)n * o.lk / T), o.lk, false) - 1;
+        o.s_hi = dyn_count(P, lane, (u32)((unsigned long long)n * o.hk / T), o.hk, true);
+    }
+}
+
 template <int MODE, bool XP, bool SPLIT>
 __global__ void __launch_bounds__(LIT_THREADS)
 vsa_lit_scan(VsaLitParams P) {
@@ -1741,6 +1946,7 @@ vsa_lit_scan(VsaLitParams P) {
     extern __shared__ __align__(16) u8 smem[];
     __shared__ ConfLds cl;
     __shared__ u32 q_tails[16], q_heads[16], q_done, wg_ctr, conf_fin;
+    __shared__ u32 dyn_s[4]; /* dynamic shares: DynB of this workgroup */
     /* work stealing (dynamic 2): per scanning wave, the sweep groups of its
      * current segment it has not claimed yet: seg << 40 | end << 20 | cur
      * (groups of LIT_DEPTH iterations; cur = the next group to claim) */
@@ -1754,6 +1960,8 @@ vsa_lit_scan(VsaLitParams P) {
     const u32 wave = readfirstlane_u32(tid / WAVE);
     /* diagnostic (dbg & 8192, wave log): the kernel's entry, before staging */
     const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
+    DynPre dpre;
+    if (P.dyn_kib && wave == 0) dyn_load(P, lane, dpre);
 
     const u32 mis = (u32)((uintptr_t)P.data & 15);
     const u8 *A = P.data - mis;
@@ -1866,6 +2074,17 @@ vsa_lit_scan(VsaLitParams P) {
     }
     if (tid < 8 * MAX_CONF_WAVES) prof_lds[tid] = 0;
     if (tid < 3) diag_lds[tid] = 0;
+    if (P.dyn_kib && wave == 0) {
+        /* dynamic shares: this workgroup's range and segments */
+        DynB d;
+        dyn_bounds(P, lane, dpre, d);
+        if (lane == 0) {
+            dyn_s[0] = d.s_lo;
+            dyn_s[1] = d.s_hi;
+            dyn_s[2] = d.lk;
+            dyn_s[3] = d.hk;
+        }
+    }
     __syncthreads();
 
     if (wave >= NS) {
@@ -1967,8 +2186,8 @@ vsa_lit_scan(VsaLitParams P) {
         const u32 t = readlane_u32(t0, 0);
         /* reloaded per segment (scalar loads) rather than held: the sweep
          * needs the SGPRs */
-        const u32 wg_lo = readfirstlane_u32(P.wg_seg[blockIdx.x]);
-        const u32 wg_hi = readfirstlane_u32(P.wg_seg[blockIdx.x + 1]);
+        const u32 wg_lo = readfirstlane_u32(P.dyn_kib ? dyn_s[0] : P.wg_seg[blockIdx.x]);
+        const u32 wg_hi = readfirstlane_u32(P.dyn_kib ? dyn_s[1] : P.wg_seg[blockIdx.x + 1]);
         return wg_lo + t < wg_hi ? wg_lo + t : (u32)P.nsegs;
     };
     /* Work stealing inside the workgroup (P.steal): a wave whose
@@ -2060,8 +2279,18 @@ vsa_lit_scan(VsaLitParams P) {
         typedef const __attribute__((address_space(4))) u32 cu32;
         const u32 segu = readfirstlane_u32(seg);
         const u32 sbv = ((cu32 *)P.seg_desc)[4 * (size_t)segu];
-        const u32 d_off = ((cu32 *)P.seg_desc)[4 * (size_t)segu + 1];
-        const u32 d_len = ((cu32 *)P.seg_desc)[4 * (size_t)segu + 2];
+        u32 d_off = ((cu32 *)P.seg_desc)[4 * (size_t)segu + 1];
+        u32 d_len = ((cu32 *)P.seg_desc)[4 * (size_t)segu + 2];
+        if (P.dyn_kib) {
+            /* dynamic shares: the part of the segment (a part of one block)
+             * inside this workgroup's KiB range */
+            const u32 d_pos = ((cu32 *)P.seg_desc)[4 * (size_t)segu + 3];
+            const u32 lk = readfirstlane_u32(dyn_s[2]), hk = readfirstlane_u32(dyn_s[3]);
+            const u32 a = d_pos > lk ? d_pos : lk;
+            const u32 e = d_pos + d_len < hk ? d_pos + d_len : hk;
+            d_off += a - d_pos;
+            d_len = e > a ? e - a : 0u;
+        }
         const u32 gcount = sbv >> 24;
         /* a run (VSA_BLK_RUN, FDR / Teddy): the segment's back-to-back
          * blocks are one range -- one prologue, one sweep, two checked

@@ -25,23 +25,64 @@ constexpr uint32_t PLAN_MAX_BLOCKS = VSA_MAX_BLOCKS; /* 20-bit block field of th
  * in block order, so they do not unless blocks overlap or come out of
  * order -- every bin lying wholly inside hull b holds only workgroup b's
  * records.  Appended to segblk after the list bounds: 2 words per
- * workgroup, the bins [lo, hi) (hi - lo <= VSA_LBINS; 0, 0 = none). */
+ * workgroup, the bins [lo, hi) (hi - lo <= VSA_LBINS; 0, 0 = none); a
+ * dynamic-share plan appends a second such table after the fused finish's,
+ * for its dynamic launches. */
 void plan_fused(BatchPlan &pl, const VsaBlock *blocks, int64_t mis);
 
-void plan_wg_bins(BatchPlan &pl, const VsaBlock *blocks, int64_t mis) {
+static void owned_bins(BatchPlan &pl, const VsaBlock *blocks, int64_t mis, bool dyn) {
     const uint32_t G = pl.grid;
     const uint64_t base = 4 * pl.nsegs;
     std::vector<int64_t> hlo(G, INT64_MAX), hhi(G, INT64_MIN);
+    /* dynamic shares: workgroup b's range moves within dyn_margin KiB of
+     * the equal-share boundaries, so it owns bins only inside its sure range
+     * [nom_b + margin, nom_b+1 - margin) of the live KiB (the first and last
+     * boundaries are fixed) */
+    const uint64_t TK = dyn ? pl.dyn_kib : 0, MK = pl.dyn_margin;
+    auto sure = [&](uint32_t i, bool upper) -> uint64_t {
+        if (i == 0) return 0;
+        if (i >= G) return TK;
+        const uint64_t nom = TK * i / G;
+        return upper ? (nom > MK ? nom - MK : 0) : std::min(nom + MK, TK);
+    };
     for (uint32_t b = 0; b < G; b++) {
-        for (uint32_t sg = pl.segblk[base + b]; sg < pl.segblk[base + b + 1]; sg++) {
+        uint32_t s0g = pl.segblk[base + b], s1g = pl.segblk[base + b + 1];
+        uint64_t klo = 0, khi = 0;
+        if (TK) {
+            klo = sure(b, false);
+            khi = sure(b + 1, true);
+            /* the segments overlapping [klo, khi): word 3 ascends */
+            s0g = s1g = 0;
+            if (khi > klo) {
+                uint32_t a = 0, e = (uint32_t)pl.nsegs;
+                while (a < e) { /* first segment ending after klo */
+                    const uint32_t m = (a + e) / 2;
+                    const uint64_t end = (uint64_t)pl.segblk[4 * (uint64_t)m + 3] +
+                                         pl.segblk[4 * (uint64_t)m + 2];
+                    if (end > klo) e = m;
+                    else a = m + 1;
+                }
+                s0g = s1g = a;
+                while (s1g < pl.nsegs && pl.segblk[4 * (uint64_t)s1g + 3] < khi) s1g++;
+            }
+        }
+        for (uint32_t sg = s0g; sg < s1g; sg++) {
             const uint32_t *d = &pl.segblk[4 * (uint64_t)sg];
             const uint32_t first = d[0] & 0xffffffu, cnt = d[0] >> 24;
             int64_t lo, hi;
             if (cnt == 0) {
                 const VsaBlock &B = blocks[first];
-                const int64_t s0 = B.org - mis + ((int64_t)d[1] << 10);
+                uint64_t off = d[1], len = d[2];
+                if (TK) {
+                    /* the part inside the sure range (kernels.hip's clip) */
+                    const uint64_t a = std::max<uint64_t>(d[3], klo);
+                    const uint64_t e = std::min<uint64_t>((uint64_t)d[3] + d[2], khi);
+                    off += a - d[3];
+                    len = e - a;
+                }
+                const int64_t s0 = B.org - mis + ((int64_t)off << 10);
                 lo = std::max<int64_t>((int64_t)B.base, s0);
-                hi = std::min<int64_t>((int64_t)(B.base + B.len), s0 + ((int64_t)d[2] << 10));
+                hi = std::min<int64_t>((int64_t)(B.base + B.len), s0 + ((int64_t)len << 10));
             } else {
                 lo = INT64_MAX;
                 hi = INT64_MIN;
@@ -78,7 +119,14 @@ void plan_wg_bins(BatchPlan &pl, const VsaBlock *blocks, int64_t mis) {
         pl.segblk.push_back(lo);
         pl.segblk.push_back(hi);
     }
+}
+
+/* the owned bins of the static lists, the fused finish's local bins, then
+ * (dynamic-share plans) the owned bins of the sure ranges */
+void plan_wg_bins(BatchPlan &pl, const VsaBlock *blocks, int64_t mis) {
+    owned_bins(pl, blocks, mis, false);
     plan_fused(pl, blocks, mis);
+    if (pl.dyn_kib) owned_bins(pl, blocks, mis, true);
 }
 
 /* The fused finish's local bins (kernels.hip fused_finish), appended to
@@ -200,12 +248,16 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
     int64_t g_span = 0;
     pl.nsegs = 0;
     pl.grid = 0;
-    /* one 16-byte descriptor per segment (kernels.h VsaLitParams.seg_desc) */
+    /* one 16-byte descriptor per segment (kernels.h VsaLitParams.seg_desc);
+     * word 3: the segment's position in the plan's live KiB (dynamic
+     * shares) */
+    uint64_t kib_pos = 0;
     auto push_desc = [&](uint32_t info, uint64_t off, uint64_t len) {
         pl.segblk.push_back(info);
         pl.segblk.push_back((uint32_t)(off >> 10));
         pl.segblk.push_back((uint32_t)((len + 1023) >> 10));
-        pl.segblk.push_back(0u);
+        pl.segblk.push_back((uint32_t)kib_pos);
+        kib_pos += (len + 1023) >> 10;
         pl.nsegs++;
     };
     /* a packed segment of back-to-back blocks >= 1 KiB scanned from their
@@ -333,6 +385,29 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
     pl.grid = (uint32_t)G;
     pl.segblk.insert(pl.segblk.end(), wg_first.begin(), wg_first.end());
     pl.end_bits = bits_for(span);
+    /* dynamic shares (kernels.hip dyn_bounds): large launches whose
+     * segments are all parts of blocks, the blocks in ascending,
+     * non-overlapping order (so the live KiB ascend with the addresses and
+     * a bin inside one workgroup's sure range is its own) */
+    pl.dyn_kib = pl.dyn_margin = 0;
+    if (dyn_shares_on() && G >= 64 && G <= 256 && pl.bytes >= (256ull << 20) &&
+        kib_pos < (1ull << 32) && kib_pos >= 16 * G) {
+        bool ok = true;
+        for (uint64_t s = 0; s < pl.nsegs && ok; s++) ok = (pl.segblk[4 * s] >> 24) == 0;
+        int64_t prev_end = INT64_MIN;
+        for (uint32_t i = 0; i < nb && ok; i++) {
+            if (spans[i] < 0) continue;
+            ok = (int64_t)out[i].base >= prev_end;
+            prev_end = (int64_t)(out[i].base + out[i].len);
+        }
+        if (ok) {
+            pl.dyn_kib = (uint32_t)kib_pos;
+            /* a boundary moves at most 1/6 of a share: per-XCD weights in
+             * 0.9-1.1 move the b % 8 interleave's boundaries less, and the
+             * owned bins keep 2/3 of each share */
+            pl.dyn_margin = (uint32_t)(kib_pos / G / 6);
+        }
+    }
     plan_wg_bins(pl, out, (int64_t)((uintptr_t)d_data & 15));
     return VSA_OK;
 }
@@ -377,6 +452,19 @@ int vsa_plan_describe(const uint8_t *d_data, const uint64_t *offsets, const uint
     return (int)pl.segblk.size();
 }
 
+int vsa_plan_dyn(const uint8_t *d_data, const uint64_t *offsets, const uint64_t *lens,
+                 const uint64_t *starts, const uint64_t *hlens, const uint64_t *report_lo,
+                 uint32_t nblocks, uint32_t num_cus, uint32_t ns, uint32_t *out) {
+    if (!offsets || !lens || !nblocks || !ns || !num_cus || !out) return VSA_E_INVALID;
+    BatchPlan pl;
+    int r = build_plan(d_data, offsets, lens, starts, hlens, report_lo, nblocks,
+                       (uint64_t)num_cus * ns, pl, nullptr, ns);
+    if (r != VSA_OK) return r;
+    out[0] = pl.dyn_kib;
+    out[1] = pl.dyn_margin;
+    return VSA_OK;
+}
+
 int vsa_plan_blocks(const uint8_t *d_data, const uint64_t *offsets, const uint64_t *lens,
                     const uint64_t *starts, const uint64_t *hlens, const uint64_t *report_lo,
                     uint32_t nblocks, void *out) {
@@ -419,7 +507,10 @@ int vsa_feedback_simulate(const double *rate, uint32_t grid, uint32_t launches, 
             const double share = F.wg[b] / tw;
             const double t = share / rate[b & 7] * (1.0 + jitter * rnd());
             h[grid + b] = 1000;
-            h[b] = ((unsigned long long)(b & 7) << 60) | (1000 + (unsigned long long)(t * 1e9));
+            /* ~800 us launches (100 MHz ticks): a 4 GiB scan's length, which
+             * the gain rule (fb_gain_us) weighs */
+            h[b] = ((unsigned long long)(b & 7) << 60) |
+                   (1000 + (unsigned long long)(t * 8e4 * grid));
         }
         (void)feedback_update(F, h.data(), grid);
     }
@@ -446,6 +537,8 @@ int vsa_plan_create(vsa_ctx_t *c, const uint8_t *d_data, const uint64_t *offsets
     p->end_bits = pl.end_bits;
     p->bytes = pl.bytes;
     p->fin_ok = pl.fin_ok;
+    p->dyn_kib = pl.dyn_kib;
+    p->dyn_margin = pl.dyn_margin;
     const uint64_t *ins[5] = {offsets, lens, starts, hlens, report_lo};
     for (int k = 0; k < 5; k++)
         if (ins[k]) p->in[k].assign(ins[k], ins[k] + nblocks);
@@ -541,6 +634,8 @@ int refresh_plan(vsa_ctx *c, const vsa_db *db, vsa_plan *p) {
     p->segs = pl.nsegs;
     p->grid = pl.grid;
     p->fin_ok = pl.fin_ok;
+    p->dyn_kib = pl.dyn_kib;
+    p->dyn_margin = pl.dyn_margin;
     /* the weights it follows now (only once applied: a failed rebuild is
      * tried again at the next scan) */
     p->fb_key = key;
@@ -558,7 +653,7 @@ int vsa_scan_plan(vsa_ctx_t *c, const vsa_db_t *db, const vsa_plan_t *p, uint32_
     uint64_t dummy;
     return launch_planned(c, db, p->d_data, p->d_blocks, p->d_segblk, p->nb, p->segs,
                           p->grid, p->end_bits, p->bytes, flags,
-                          n_matches ? n_matches : &dummy, p->fin_ok);
+                          n_matches ? n_matches : &dummy, p->fin_ok, p->dyn_kib, p->dyn_margin);
 }
 
 int vsa_scan_plan_pack(vsa_ctx_t *c, const vsa_db_t *db, const vsa_plan_t *p, void *d_dst,
@@ -570,7 +665,8 @@ int vsa_scan_plan_pack(vsa_ctx_t *c, const vsa_db_t *db, const vsa_plan_t *p, vo
     c->launch.pack_cap = cap;
     uint64_t n = 0;
     int r = launch_planned(c, db, p->d_data, p->d_blocks, p->d_segblk, p->nb, p->segs, p->grid,
-                           p->end_bits, p->bytes, VSA_SCAN_ASYNC, &n, p->fin_ok);
+                           p->end_bits, p->bytes, VSA_SCAN_ASYNC, &n, p->fin_ok, p->dyn_kib,
+                           p->dyn_margin);
     /* not consumed (no segments, or a launch without the binned sort): the
      * records are packed the separate way, after the host completes it */
     const bool fused = c->launch.pack_dst == nullptr && c->pending;

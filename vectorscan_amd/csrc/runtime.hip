@@ -289,6 +289,38 @@ bool xcd_feedback_on() {
     return v;
 }
 
+/* the least gain (us of kernel time) that applies new weights;
+ * VSA_FB_GAIN_US=-1 restores the earlier rule (any weight moved by 2 %) */
+int fb_gain_us() {
+    static const int v = env_int("VSA_FB_GAIN_US", 4);
+    return v;
+}
+
+/* Dynamic shares (kernels.hip dyn_bounds): on for the FDR launches of at
+ * least VSA_DYN_MIN_MIB (default 2048) MiB over eligible plans (build_plan:
+ * >= 256 MiB of parts of blocks in address order); VSA_DYN_SHARES=0 keeps
+ * the host's static lists (with the host-side feedback) everywhere;
+ * vsa_ctx_set_dyn_shares per context.  Measured: the
+ * FDR scan is LDS-bound per CU, so an XCD's rate is its own and following it
+ * pays (4 GiB: XCD spread 17 -> 5 us, kernel 791 -> 773 us in synchronous
+ * scans); the streaming scans (noodle, Teddy) share HBM bandwidth, their
+ * XCD deviations do not follow a launch's weights, and the start cost made
+ * them 3-4 % slower at 1 GiB; FDR at 1 GiB is even. */
+bool dyn_shares_on() {
+    static const bool v = env_int("VSA_DYN_SHARES", 1) != 0;
+    return v;
+}
+
+uint64_t dyn_min_bytes() {
+    static const uint64_t v = (uint64_t)std::max(0, env_int("VSA_DYN_MIN_MIB", 2048)) << 20;
+    return v;
+}
+
+static bool fb_trace() {
+    static const bool v = env_int("VSA_FB_TRACE", 0) != 0;
+    return v;
+}
+
 /* arm the feedback record of the next launch (set: FbSet kind) */
 void arm_feedback(vsa_ctx *c, int set, uint32_t grid, uint64_t bytes, bool small) {
     c->fb.armed = xcd_feedback_on() && c->fb.h && grid >= 64 && grid <= 1024 &&
@@ -367,6 +399,33 @@ bool feedback_update(vsa_ctx::FbSet &F, const volatile unsigned long long *h, ui
     for (int x = 0; x < 8; x++) {
         nw[x] = std::min(1.3f, std::max(0.7f, (float)(nw[x] / mean)));
         moved = moved || std::fabs(nw[x] - F.wa[x]) > 0.02f;
+    }
+    if (const int gus = fb_gain_us(); gus >= 0) {
+        /* the rule in time: with shares wa an XCD ends in proportion to
+         * wa / nw (nw estimates its rate), with nw all together, so the
+         * launch would end (max r / mean r - 1) of its length earlier.
+         * The 2 % rule above left XCDs up to 11-20 us apart on a 4 GiB
+         * scan (1.4 % moves, never applied: profiles/r06/r06w_wg_spread.jsonl,
+         * whose per-XCD spread is all of the workgroups' persistent spread);
+         * apply when the gain is worth the refresh (~10-20 us, at most once
+         * per 16 launches) */
+        double rmax = 0, rsum = 0, rn = 0;
+        for (int x = 0; x < 8; x++)
+            if (cnt[x]) {
+                const double r = F.wa[x] / nw[x];
+                rmax = std::max(rmax, r);
+                rsum += r;
+                rn += 1;
+            }
+        moved = (rmax * rn / rsum - 1.0) * tm / 100.0 > (double)gus;
+    }
+    if (fb_trace()) {
+        /* diagnostic (VSA_FB_TRACE=1): one line per record to stderr */
+        fprintf(stderr, "fb v%u tm_us %.1f", F.version, tm / 100.0);
+        for (int x = 0; x < 8; x++)
+            fprintf(stderr, " x%d %+.2f/%.4f/%.4f", x,
+                    cnt[x] ? (sum[x] / cnt[x] - tm) / 100.0 : 0.0, F.wa[x], nw[x]);
+        fprintf(stderr, " moved %d\n", (int)moved);
     }
     memcpy(F.w, nw, sizeof(nw));
     const bool first = !F.known;
@@ -464,7 +523,13 @@ int launch_scan(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint32_t nb
                       (c->lit_launches % (uint64_t)c->timing_every) == 0;
     c->launch.ev_start = c->launch.timed ? c->ev0 : nullptr;
     c->launch.ev_stop = c->launch.timed ? c->ev1 : nullptr;
-    arm_feedback(c, fb_set_of(db), c->launch.grid, c->launch.bytes, small);
+    /* dynamic shares: the launch balances its XCDs itself (its records go
+     * to the stream's state, not to the host feedback) */
+    c->launch.dyn = c->launch.dyn_kib && c->dyn_shares && !c->launch.fused && !small &&
+                    db->mode == VSA_MODE_FDR4 && c->launch.bytes >= c->dyn_min &&
+                    c->launch.grid >= 64 && c->launch.grid <= 256 && c->dyn;
+    if (c->launch.dyn) arm_feedback(c, 0, 0, 0, true); /* disarmed */
+    else arm_feedback(c, fb_set_of(db), c->launch.grid, c->launch.bytes, small);
     c->lit_launches++;
     int r = launch_scan_kernel(c, db, d_data, nb, nsegs);
     c->launch.ev_start = c->launch.ev_stop = nullptr;
@@ -525,6 +590,33 @@ int launch_scan_kernel(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, uint
     P.bin_ids = c->launch.bins ? bstage_ids(w) : nullptr;
     P.counters = w.d_counters;
     P.wg_time = c->fb.armed >= 0 ? (c->fb.dev ? c->fb.d_rec : c->fb.d) : nullptr;
+    if (c->launch.dyn) {
+        /* dynamic shares (kernels.hip dyn_bounds): this launch's records and
+         * weights in buffer epoch & 1, the previous dynamic launch's (same
+         * grid and mode, complete by stream order) in the other */
+        DynState &D = *c->dyn;
+        constexpr size_t REC = 512, WTS = 8;
+        if (!D.d) {
+            VSA_CHECK(hipMalloc(&D.d, (2 * REC + WTS) * sizeof(unsigned long long)));
+            VSA_CHECK(hipMemsetAsync(D.d, 0, (2 * REC + WTS) * sizeof(unsigned long long),
+                                     c->stream));
+        }
+        const uint64_t e = ++D.epoch;
+        c->launch.dyn_epoch = e;
+        const bool prev = D.grid == c->launch.grid && D.kind == db->mode;
+        uint32_t *wts = (uint32_t *)(D.d + 2 * REC);
+        P.wg_time = D.d + (e & 1) * REC;
+        P.dyn_prev = prev ? D.d + ((e - 1) & 1) * REC : nullptr;
+        P.dyn_wprev = prev ? wts + ((e - 1) & 1) * WTS : nullptr;
+        P.dyn_wout = wts + (e & 1) * WTS;
+        P.dyn_kib = c->launch.dyn_kib;
+        P.dyn_margin = c->launch.dyn_margin;
+        /* the plan's owned bins of the sure ranges (plan_wg_bins: after the
+         * static table and the fused finish's) */
+        P.wg_bins = c->launch.d_segblk + 4 * nsegs + 7 * (size_t)c->launch.grid + 1;
+        D.grid = c->launch.grid;
+        D.kind = db->mode;
+    }
     P.wave_log = g_wave_log;
     if (c->launch.fused) {
         /* the fused finish (kernels.hip fused_finish): local bins in the
@@ -673,6 +765,37 @@ int finish_scan(vsa_ctx *c, uint32_t flags, int end_bits, uint64_t *n_out) {
     uint64_t n = w.h_counters[0];
     c->last_cand = w.h_counters[2];
     take_feedback(c);
+    if (fb_trace() && c->launch.dyn) {
+        /* diagnostic (VSA_FB_TRACE=1): the dynamic shares' weights and the
+         * per-XCD end deviations of this launch (us), to stderr */
+        /* (the launch is complete; a later one writes the other buffer) */
+        const DynState &D = *c->dyn;
+        const uint64_t ep = c->launch.dyn_epoch;
+        unsigned long long rec[512 + 4];
+        const uint32_t G = c->launch.grid;
+        if (hipMemcpy(rec, D.d + (ep & 1) * 512, 2 * G * 8, hipMemcpyDeviceToHost) ==
+                hipSuccess &&
+            hipMemcpy(rec + 512, D.d + 1024 + (ep & 1) * 4, 32, hipMemcpyDeviceToHost) ==
+                hipSuccess) {
+            const uint32_t *wq = (const uint32_t *)(rec + 512);
+            double s[8] = {0}, k[8] = {0}, t0 = 1e300;
+            for (uint32_t b = 0; b < G; b++) t0 = std::min(t0, (double)rec[G + b]);
+            for (uint32_t b = 0; b < G; b++) {
+                const uint32_t x = (uint32_t)(rec[b] >> 60) & 7u;
+                s[x] += (double)(rec[b] & ((1ULL << 60) - 1)) - t0;
+                k[x] += 1;
+            }
+            double tm = 0, nx = 0;
+            for (int x = 0; x < 8; x++)
+                if (k[x]) tm += s[x] / k[x], nx += 1;
+            tm /= nx;
+            fprintf(stderr, "dyn e%llu tm_us %.1f", (unsigned long long)ep, tm / 100.0);
+            for (int x = 0; x < 8; x++)
+                fprintf(stderr, " x%d %+.2f/%.4f", x, k[x] ? (s[x] / k[x] - tm) / 100.0 : 0.0,
+                        wq[x] / 65536.0);
+            fprintf(stderr, "\n");
+        }
+    }
     /* adapt the db's confirm-wave count to the measured candidate rate
      * (over a representative launch; not under diagnostic flags) */
     if (c->launch.db && c->launch.bytes >= (16u << 20) && !getenv("VSA_DEBUG_FLAGS")) {
@@ -759,7 +882,7 @@ int finish_pending(vsa_ctx *c) {
 int launch_planned(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, const VsaBlock *d_blocks,
                    const uint32_t *d_segblk, uint32_t nb, uint64_t segs,
                    uint32_t grid, int end_bits, uint64_t bytes, uint32_t flags, uint64_t *n_out,
-                   bool fin_ok) {
+                   bool fin_ok, uint32_t dyn_kib, uint32_t dyn_margin) {
     int r;
     if ((r = ensure_out(c, 1)) != VSA_OK) return r;
     if (segs == 0) {
@@ -779,6 +902,8 @@ int launch_planned(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, const Vs
     c->launch.bytes = bytes;
     c->launch.flags = flags;
     c->launch.fin_ok = fin_ok;
+    c->launch.dyn_kib = dyn_kib;
+    c->launch.dyn_margin = dyn_margin;
     if ((r = launch_scan(c, db, d_data, nb, segs)) != VSA_OK) return r;
     if (flags & VSA_SCAN_ASYNC) {
         c->pending = true;
@@ -844,7 +969,8 @@ int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
         M.valid = true;
     }
     int rr = launch_planned(c, db, d_data, c->ws.d_blocks, c->ws.d_segblk, nb, pl.nsegs,
-                          pl.grid, pl.end_bits, pl.bytes, flags, n_out, pl.fin_ok);
+                          pl.grid, pl.end_bits, pl.bytes, flags, n_out, pl.fin_ok, pl.dyn_kib,
+                          pl.dyn_margin);
     auto T3 = std::chrono::steady_clock::now();
     /* diagnostic: host-side cost of a per-call plan (tools/exp_host.py) */
     static const bool timing = getenv("VSA_HOST_TIMING") != nullptr;
@@ -893,12 +1019,15 @@ int vsa_ctx_create(int device, vsa_ctx_t **out) {
     std::unique_ptr<vsa_ctx> c(new vsa_ctx());
     c->device = device;
     c->fused_finish = fused_finish_default();
+    c->dyn_shares = dyn_shares_on();
+    c->dyn_min = dyn_min_bytes();
     VSA_CHECK(hipSetDevice(device));
     int cus = 0;
     VSA_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     c->num_cus = cus > 0 ? cus : 256;
     VSA_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->stream_ref.reset((void *)c->stream, [](void *st) { (void)hipStreamDestroy((hipStream_t)st); });
+    c->dyn = std::make_shared<DynState>();
     VSA_CHECK(hipEventCreate(&c->ev0));
     VSA_CHECK(hipEventCreate(&c->ev1));
     VSA_CHECK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
@@ -968,9 +1097,12 @@ int vsa_ctx_create_shared(vsa_ctx_t *base, vsa_ctx_t **out) {
     if (rc != VSA_OK) return rc;
     (void)hipStreamSynchronize(c->stream);
     c->stream_ref = base->stream_ref; /* releases the stream it made */
+    c->dyn = base->dyn;               /* one dynamic-share state per stream */
     c->reserved_cus = base->reserved_cus;
     c->fused_finish = base->fused_finish;
     c->timing_every = base->timing_every;
+    c->dyn_shares = base->dyn_shares;
+    c->dyn_min = base->dyn_min;
     c->stream = base->stream;
     *out = c;
     return VSA_OK;
@@ -1560,6 +1692,15 @@ double vsa_scan_kernel_ms(vsa_ctx_t *c) {
 uint64_t vsa_scan_launches(vsa_ctx_t *c) { return c ? c->lit_launches : 0; }
 
 int vsa_scan_last_fused(vsa_ctx_t *c) { return c && c->launch.fused ? 1 : 0; }
+
+int vsa_scan_last_dyn(vsa_ctx_t *c) { return c && c->launch.dyn ? 1 : 0; }
+
+int vsa_ctx_set_dyn_shares(vsa_ctx_t *c, int on, uint64_t min_bytes) {
+    if (!c) return VSA_E_INVALID;
+    c->dyn_shares = on != 0;
+    c->dyn_min = min_bytes;
+    return VSA_OK;
+}
 
 int vsa_ctx_set_timing(vsa_ctx_t *c, uint32_t every) {
     if (!c) return VSA_E_INVALID;

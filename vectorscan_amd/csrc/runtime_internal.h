@@ -150,7 +150,24 @@ struct BatchPlan {
     /* the fused finish's local-bin table follows the owned bins in segblk
      * and is usable (plan_fused) */
     bool fin_ok = false;
+    /* dynamic shares (kernels.hip dyn_bounds): the live KiB the workgroups
+     * split at launch, 0 = the static lists; the boundaries' margin (KiB) */
+    uint32_t dyn_kib = 0, dyn_margin = 0;
     std::vector<int64_t> spans, live; /* build_plan scratch */
+};
+
+/* the dynamic shares' state of one stream (shared by the contexts on it):
+ * the launches' end-time records and weights, double-buffered by launch
+ * (a launch reads the previous one's, complete by stream order, and writes
+ * its own) */
+struct DynState {
+    unsigned long long *d = nullptr; /* [2][512] records, then [2][8] u32 weights */
+    uint64_t epoch = 0;              /* dynamic-share launches queued */
+    uint32_t grid = 0;               /* the last one's grid (0: none yet) */
+    int kind = -1;                   /* ... and its scan mode */
+    ~DynState() {
+        if (d) (void)hipFree(d);
+    }
 };
 
 struct vsa_plan;
@@ -166,6 +183,7 @@ struct vsa_ctx {
     /* the stream's owner: shared by contexts made with vsa_ctx_create_shared,
      * destroyed with the last of them */
     std::shared_ptr<void> stream_ref;
+    std::shared_ptr<DynState> dyn; /* the stream's dynamic-share state */
     Workspace ws;
     int cur = 0;          /* which key/id buffer holds the last results */
     uint64_t last_n = 0;
@@ -189,6 +207,9 @@ struct vsa_ctx {
         bool fin_ok = false;    /* the plan allows the fused finish */
         bool timed = false;     /* the dispatch carries ev0 / ev1 */
         bool fused = false;     /* ... and this launch sorts inside the scan */
+        uint32_t dyn_kib = 0, dyn_margin = 0; /* the plan's (BatchPlan) */
+        bool dyn = false;       /* this launch sets its shares (dyn_bounds) */
+        uint64_t dyn_epoch = 0; /* ... its DynState epoch */
         uint64_t bytes = 0; /* scanned bytes (len - start summed) */
         const VsaBlock *d_blocks = nullptr;
         const uint32_t *d_segblk = nullptr;
@@ -217,6 +238,10 @@ struct vsa_ctx {
     /* every timing_every-th literal-scan launch carries the kernel-timing
      * events (vsa_ctx_set_timing; 1 = all, 0 = none) */
     uint32_t timing_every = 1;
+    /* eligible plans' launches set their own shares (kernels.hip
+     * dyn_bounds; vsa_ctx_set_dyn_shares, default VSA_DYN_SHARES) */
+    bool dyn_shares = true;
+    uint64_t dyn_min = 0; /* ... of at least this many bytes */
     uint32_t bin_skip = 0;   /* launches left without the binned sort */
     /* the bin_skip a crowded bin sets: 16, x4 for every crowded binned
      * launch in a row (up to 4096), back to 16 after a binned launch that
@@ -290,6 +315,7 @@ struct vsa_plan {
     uint64_t bytes = 0;
     uint32_t rebuilds = 0; /* segment maps rebuilt for the feedback weights */
     bool fin_ok = false;   /* its map allows the fused finish (plan_fused) */
+    uint32_t dyn_kib = 0, dyn_margin = 0; /* dynamic shares (BatchPlan) */
     VsaBlock *d_blocks = nullptr;
     uint32_t *d_segblk = nullptr;
     /* schedule feedback: the inputs (to rebuild the segment map with the
@@ -395,7 +421,9 @@ int complete_scan(vsa_ctx *c, uint64_t *n_out);
 int launch_planned(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data, const VsaBlock *d_blocks,
                    const uint32_t *d_segblk, uint32_t nb, uint64_t segs, uint32_t grid,
                    int end_bits, uint64_t bytes, uint32_t flags, uint64_t *n_out,
-                   bool fin_ok = false);
+                   bool fin_ok = false, uint32_t dyn_kib = 0, uint32_t dyn_margin = 0);
+bool dyn_shares_on();
+uint64_t dyn_min_bytes();
 int scan_blocks_impl(vsa_ctx *c, const vsa_db *db, const uint8_t *d_data,
                      const uint64_t *offs, const uint64_t *lens, const uint64_t *starts,
                      uint32_t nb, uint32_t flags, uint64_t *n_out,
