@@ -370,11 +370,13 @@ int vsa_scan_last_fused(vsa_ctx_t *ctx);
  * times; VSA_DYN_SHARES=0 turns them off), else 0.  A diagnostic, no
  * reference counterpart. */
 int vsa_scan_last_dyn(vsa_ctx_t *ctx);
-/* Dynamic shares for the context's FDR launches of at least min_bytes
- * over eligible plans (>= 64 workgroups, >= 256 MiB of parts of blocks in
- * address order): on = 1 (the default, min_bytes VSA_DYN_MIN_MIB = 2048
- * MiB, unless VSA_DYN_SHARES=0), off = 0 (the host's static lists and its
- * schedule feedback).  Results are identical either way. */
+/* Dynamic shares (an option; measured even with the host's schedule
+ * feedback on the headline) for the context's FDR launches of at least
+ * min_bytes over eligible plans (>= 64 workgroups, >= 256 MiB of parts of
+ * blocks in address order): each launch cuts its workgroups' ranges from
+ * the previous launch's per-XCD end times.  on = 1, off = 0 (the default
+ * unless VSA_DYN_SHARES=1; VSA_DYN_MIN_MIB sets the default min_bytes,
+ * 2048 MiB).  Results are identical either way. */
 int vsa_ctx_set_dyn_shares(vsa_ctx_t *ctx, int on, uint64_t min_bytes);
 /* Sort inside the scan kernel when the plan allows it (the fused finish:
  * no vsa_bin_finish launch behind the scan, the scan's workgroups sort

@@ -282,7 +282,7 @@ def test_gpu_dyn_shares_ragged(ctx, engine):
             for b in range(len(offs)):
                 assert got[b] == want[b], (k, b)
     finally:
-        ctx.dyn_shares(True)
+        ctx.dyn_shares(False)
         if plan is not None:
             plan.close()
         db.close()
@@ -335,7 +335,7 @@ def test_gpu_schedule_feedback_512mib(ctx, fused, dyn):
         assert any(fused_seen) == fused
     finally:
         ctx.fused_finish(False)
-        ctx.dyn_shares(True)
+        ctx.dyn_shares(False)
         if plan is not None:
             plan.close()
         db.close()

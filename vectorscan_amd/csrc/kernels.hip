@@ -1760,20 +1760,28 @@ __device__ __forceinline__ u32 wave_sum_u32(u32 v) {
     return readfirstlane_u32(v);
 }
 
-/* segments whose KiB position (descriptor word 3, ascending) is <= L (or <
- * L): a 64-entry window from `near`, else a 64-way search of the list */
-__device__ __forceinline__ u32 dyn_count(const VsaLitParams &P, u32 lane, u32 near, u32 L, bool strict) {
+/* The segments whose KiB position (descriptor word 3, ascending) is <= L
+ * (or < L), counted over a 64-entry window loaded at the kernel's entry
+ * around the equal-share boundary's segment (the boundary moves at most
+ * 1/6 of a share, a few segments), else by a 64-way search of the list. */
+__device__ __forceinline__ u32 dyn_window_base(u32 n, u32 near) {
+    u32 base = near > 32 ? near - 32 : 0;
+    if (base + 64 > n) base = n > 64 ? n - 64 : 0;
+    return base;
+}
+
+__device__ __forceinline__ u32 dyn_count(const VsaLitParams &P, u32 lane, u32 base, u32 v, u32 L,
+                                         bool strict) {
     const u32 n = (u32)P.nsegs;
     const u32 *pos = P.seg_desc + 3;
     auto pred = [&](u32 s, u32 end) -> bool {
         if (s >= end) return false;
-        const u32 v = pos[4 * (size_t)s];
-        return strict ? v < L : v <= L;
+        const u32 x = pos[4 * (size_t)s];
+        return strict ? x < L : x <= L;
     };
-    u32 base = near > 32 ? near - 32 : 0;
-    if (base + 64 > n) base = n > 64 ? n - 64 : 0;
     {
-        const u32 c = (u32)__popcll(__ballot(pred(base + lane, n)));
+        const bool in = base + lane < n && (strict ? v < L : v <= L);
+        const u32 c = (u32)__popcll(__ballot(in));
         if ((c > 0 || base == 0) && (c < 64 || base + 64 >= n)) return base + c;
     }
     /* the count A lies in [lo, hi]: elements below lo hold, from hi on not */
@@ -1789,15 +1797,24 @@ __device__ __forceinline__ u32 dyn_count(const VsaLitParams &P, u32 lane, u32 ne
     return lo + (u32)__popcll(__ballot(pred(lo + lane, hi)));
 }
 
-/* the previous launch's records and weights, loaded by wave 0 at the
- * kernel's entry so their round trip overlaps the table staging */
+/* loaded by wave 0 at the kernel's entry, so the round trip overlaps the
+ * table staging: the previous launch's records and weights, and the
+ * segment positions around this workgroup's equal-share boundaries */
 struct DynPre {
     unsigned long long en[4], ex[4];
     u32 wp;
+    u32 base_lo, base_hi, v_lo, v_hi;
 };
 
 __device__ __forceinline__ void dyn_load(const VsaLitParams &P, u32 lane, DynPre &d) {
-    const u32 G = gridDim.x;
+    const u32 G = gridDim.x, b = blockIdx.x;
+    const u32 n = (u32)P.nsegs;
+    const unsigned long long T = P.dyn_kib;
+    const u32 *pos = P.seg_desc + 3;
+    d.base_lo = dyn_window_base(n, (u32)((unsigned long long)n * (T * b / G) / T));
+    d.base_hi = dyn_window_base(n, (u32)((unsigned long long)n * (T * (b + 1) / G) / T));
+    d.v_lo = d.base_lo + lane < n ? pos[4 * (size_t)(d.base_lo + lane)] : 0xffffffffu;
+    d.v_hi = d.base_hi + lane < n ? pos[4 * (size_t)(d.base_hi + lane)] : 0xffffffffu;
     constexpr unsigned long long M60 = (1ull << 60) - 1;
     d.wp = 65536;
     if (!P.dyn_prev) return;
@@ -1928,11 +1945,8 @@ __device__ __forceinline__ void dyn_bounds(const VsaLitParams &P, u32 lane, cons
     o.hk = bound(b + 1, pre + mine);
     o.s_lo = o.s_hi = 0;
     if (o.lk < o.hk) {
-        /* the window's guess: the segments' KiB in proportion (the plan's
-         * parts are near-equal within a block) */
-        const u32 n = (u32)P.nsegs;
-        o.s_lo = dyn_count(P, lane, (u32)((unsigned long long)n * o.lk / T), o.lk, false) - 1;
-        o.s_hi = dyn_count(P, lane, (u32)((unsigned long long)n * o.hk / T), o.hk, true);
+        o.s_lo = dyn_count(P, lane, dp.base_lo, dp.v_lo, o.lk, false) - 1;
+        o.s_hi = dyn_count(P, lane, dp.base_hi, dp.v_hi, o.hk, true);
     }
 }
 

@@ -390,7 +390,7 @@ int build_plan(const uint8_t *d_data, const uint64_t *offs, const uint64_t *lens
      * non-overlapping order (so the live KiB ascend with the addresses and
      * a bin inside one workgroup's sure range is its own) */
     pl.dyn_kib = pl.dyn_margin = 0;
-    if (dyn_shares_on() && G >= 64 && G <= 256 && pl.bytes >= (256ull << 20) &&
+    if (G >= 64 && G <= 256 && pl.bytes >= (256ull << 20) &&
         kib_pos < (1ull << 32) && kib_pos >= 16 * G) {
         bool ok = true;
         for (uint64_t s = 0; s < pl.nsegs && ok; s++) ok = (pl.segblk[4 * s] >> 24) == 0;

@@ -296,18 +296,17 @@ int fb_gain_us() {
     return v;
 }
 
-/* Dynamic shares (kernels.hip dyn_bounds): on for the FDR launches of at
- * least VSA_DYN_MIN_MIB (default 2048) MiB over eligible plans (build_plan:
- * >= 256 MiB of parts of blocks in address order); VSA_DYN_SHARES=0 keeps
- * the host's static lists (with the host-side feedback) everywhere;
- * vsa_ctx_set_dyn_shares per context.  Measured: the
- * FDR scan is LDS-bound per CU, so an XCD's rate is its own and following it
- * pays (4 GiB: XCD spread 17 -> 5 us, kernel 791 -> 773 us in synchronous
- * scans); the streaming scans (noodle, Teddy) share HBM bandwidth, their
- * XCD deviations do not follow a launch's weights, and the start cost made
- * them 3-4 % slower at 1 GiB; FDR at 1 GiB is even. */
+/* Dynamic shares (kernels.hip dyn_bounds): an option (VSA_DYN_SHARES=1, or
+ * vsa_ctx_set_dyn_shares per context) for the FDR launches of at least
+ * VSA_DYN_MIN_MIB (default 2048) MiB over eligible plans (build_plan: >=
+ * 256 MiB of parts of blocks in address order).  Off by default: measured
+ *  it takes the XCDs' spread at 4 GiB from 8-17 to 5
+ * us, but the kernel and the pipelined bench step come out even or 0.3 %
+ * slower on two of three boxes (791 -> 773 us synchronous on the third);
+ * the streaming scans (noodle, Teddy), whose XCDs share HBM bandwidth,
+ * were 3-4 % slower at 1 GiB, so they never take it. */
 bool dyn_shares_on() {
-    static const bool v = env_int("VSA_DYN_SHARES", 1) != 0;
+    static const bool v = env_int("VSA_DYN_SHARES", 0) != 0;
     return v;
 }
 
