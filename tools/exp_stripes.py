@@ -10,7 +10,8 @@ with the records packed into the collective buffer by a separate vsa_pack
 launch / by the sort launch itself (vsa_scan_plan_pack); "side" adds a
 stand-in for the collective (a one-workgroup copy of the packed buffer's
 header on another stream, after the scan) to show what the persistent grid does to it, with
-EXP_RESERVE=n CUs left free (vsa_ctx_set_reserved_cus).
+EXP_RESERVE=n CUs left free (vsa_ctx_set_reserved_cus); EXP_STREAMS=2 puts
+the second context on its own stream.
 EXP_RANKS / EXP_MODES (comma lists) limit the rows; EXP_TIMING=n times every
 n-th launch of the pipelined modes (bench.py uses 4).
   python tools/exp_stripes.py [steps] [warmup]"""
@@ -31,7 +32,10 @@ dev = torch.device("cuda", 0)
 ctxs = [vsa.Context(0)]
 # EXP_RESERVE=n: the grid leaves n CUs free (measured, not used by bench.py)
 ctxs[0].reserve_cus(int(os.environ.get("EXP_RESERVE", "0")))
-ctxs.append(vsa.Context(share_stream_with=ctxs[0]))
+# EXP_STREAMS=2: the second context on a stream of its own, so a scan can
+# start on the CUs the previous one's last workgroups leave (not bench.py's)
+ctxs.append(vsa.Context(0) if os.environ.get("EXP_STREAMS") == "2"
+            else vsa.Context(share_stream_with=ctxs[0]))
 # EXP_TIMING=n: the pipelined modes time every n-th launch per context (as
 # bench.py); their kernel_ms averages the timed ones
 t_every = int(os.environ.get("EXP_TIMING", "1"))
@@ -124,7 +128,8 @@ for n in ranks:
         st = (time.perf_counter() - t0) / steps * 1e3
         ks = [x for x in ks if x >= 0] or [float("nan")]
         k = sum(ks) / len(ks)
-        print(json.dumps({"lib": os.environ.get("VSA_LIB_VARIANT", ""), "ranks": n, "mode": mode, "rank_bytes": cuts[1] - cuts[0],
+        print(json.dumps({"lib": os.environ.get("VSA_LIB_VARIANT", ""),
+                          "streams": os.environ.get("EXP_STREAMS", "1"), "ranks": n, "mode": mode, "rank_bytes": cuts[1] - cuts[0],
                           "windows": len(wins), "step_ms": round(st, 4),
                           "kernel_ms": round(k, 4), "overhead_us": round((st - k) * 1e3, 1),
                           "matches": counts[-1], "counts_equal": len(set(counts)) == 1}),
