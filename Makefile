@@ -5,12 +5,13 @@ CSRC := vectorscan_amd/csrc
 LIB := vectorscan_amd/libvectorscan_amd.so
 ORACLE := oracle/_build/liboracle.so
 HARNESS := tests/c/abi_harness
+HSNAMES := tests/c/hs_names_demo
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
             -Wno-unused-parameter -Iinclude
 
 DROPIN := tools/dropin_threads
 
-all: $(LIB) $(ORACLE) $(HARNESS) $(DROPIN)
+all: $(LIB) $(ORACLE) $(HARNESS) $(HSNAMES) $(DROPIN)
 
 $(CSRC)/compile.o: $(CSRC)/compile.cpp $(CSRC)/hs_layout.h $(CSRC)/vsa_internal.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -57,6 +58,12 @@ $(HARNESS): tests/c/abi_harness.c include/vectorscan_amd.h $(LIB) $(ORACLE)
 	    -Loracle/_build -loracle -Wl,-rpath,'$$ORIGIN/../../vectorscan_amd' \
 	    -Wl,-rpath,'$$ORIGIN/../../oracle/_build'
 
+# test-only program written against the reference's hs names
+# (include/vectorscan_amd_hs_names.h), checked against its own brute force
+$(HSNAMES): tests/c/hs_names_demo.c include/vectorscan_amd_hs_names.h include/vectorscan_amd_hs.h $(LIB)
+	gcc -O2 -std=gnu11 -Wall -Iinclude $< -o $@ -Lvectorscan_amd -lvectorscan_amd \
+	    -Wl,-rpath,'$$ORIGIN/../../vectorscan_amd'
+
 # measurement tool: small drop-in calls from POSIX threads (GPU, batcher,
 # the oracle's SSE2 port as the CPU comparator)
 $(DROPIN): tools/dropin_threads.c include/vectorscan_amd.h $(LIB) $(ORACLE)
@@ -65,6 +72,6 @@ $(DROPIN): tools/dropin_threads.c include/vectorscan_amd.h $(LIB) $(ORACLE)
 	    -Wl,-rpath,'$$ORIGIN/../oracle/_build'
 
 clean:
-	rm -f $(CSRC)/*.o $(LIB) $(ORACLE) $(HARNESS) $(DROPIN)
+	rm -f $(CSRC)/*.o $(LIB) $(ORACLE) $(HARNESS) $(HSNAMES) $(DROPIN)
 
 .PHONY: all clean
